@@ -1,0 +1,127 @@
+/* ssbls.h -- C ABI of the MI355X threshold-BLS batch engine (libssbls.so, gfx950).
+ *
+ * This is the drop-in boundary for SafeStake's threshold-BLS hot path.  Each entry point names
+ * the reference interface it replaces (paths relative to the SafeStakeOperator repository):
+ *
+ *   ssb_threshold_aggregate_batch  <- GenericThresholdSignature::threshold_aggregate
+ *                                     (src/crypto/generic_threshold.rs:132-175), batched over
+ *                                     independent (validator, signing-root) jobs
+ *   ssb_unsafe_aggregate_batch     <- TThresholdSignature::unsafe_aggregate /
+ *                                     BlstThresholdSignature::unsafe_aggregate
+ *                                     (src/crypto/generic_threshold.rs:177-179,
+ *                                      src/crypto/impls/blst.rs:67-87)
+ *   ssb_verify_batch               <- bls::Signature::verify(pk, msg) as called per share at
+ *                                     src/crypto/generic_threshold.rs:156 (blst verify with
+ *                                     sig_groupcheck=true, pk_validate=false; same convention
+ *                                     as src/network/io_committee.rs:536-539)
+ *   ssb_hash_to_g2                 <- the hash_to_G2 blst runs inside verify/sign with the DST of
+ *                                     src/crypto/impls/blst.rs:11
+ *   ssb_lagrange_coeffs            <- lagrange_coeffs (src/crypto/impls/blst.rs:19-39)
+ *
+ * Conventions
+ *   - Signatures are 96-byte compressed G2 points, public keys 48-byte compressed G1 points
+ *     (ZCash encoding, as Signature::serialize / PublicKey::serialize).  Roots are 32 bytes.
+ *   - Public keys are PRE-VALIDATED by the caller (lighthouse PublicKey::deserialize does
+ *     key_validate; verify passes pk_validate=false).  A public key that does not decode, or
+ *     decodes to infinity, makes its share invalid (verdict 0).
+ *   - A signature that does not decode (blst BAD_ENCODING / POINT_NOT_ON_CURVE), is not in G2,
+ *     or is the point at infinity yields verdict 0, exactly as blst verify returns false.
+ *   - Verification is by random linear combination (64-bit non-zero scalars derived from
+ *     `rlc_seed`, one final exponentiation per batch); a failing batch falls back to exact
+ *     per-share verification, so every verdict equals the single-signature verify result.
+ *   - Host-pointer functions copy inputs to the device and results back; they are synchronous.
+ *     The *_dev variants take DEVICE pointers and a hipStream_t (as void*), enqueue everything
+ *     on that stream and return without synchronising.
+ *   - Return value of every function: SSB_OK or a negative SSB_E* code (ssb_last_error() has
+ *     the message).  No C++ exception crosses this ABI.  A context must not be used by two
+ *     threads at once (one context per thread, or an external mutex).
+ */
+#ifndef SSBLS_H
+#define SSBLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SSB_OK 0
+#define SSB_EINVAL (-1)  /* bad argument (null pointer, size, t == 0, dst too long) */
+#define SSB_EHIP (-2)    /* HIP runtime error (no device, launch failure, ...) */
+#define SSB_ENOMEM (-3)  /* device allocation failed */
+
+/* Per-job status tags (DvfError variants, src/utils/error.rs:12-60) */
+#define SSB_DVF_OK 0
+#define SSB_DVF_DIFFERENT_LENGTH 1            /* err = {x, y} (host-side wrapper only) */
+#define SSB_DVF_INSUFFICIENT_SIGNATURES 2     /* err = {got, expected} */
+#define SSB_DVF_INVALID_OPERATOR_ID 3         /* err = {id, 0} */
+#define SSB_DVF_INSUFFICIENT_VALID_SIGNATURES 4 /* err = {got, expected} */
+#define SSB_DVF_BAD_SIGNATURE_ENCODING 5      /* unsafe_aggregate only: a share does not decode
+                                                 (the reference's unwrap() would panic) */
+
+/* Maximum threshold t supported per job, and maximum DST length. */
+#define SSB_MAX_T 64
+#define SSB_MAX_DST 255
+
+typedef struct ssb_ctx ssb_ctx;
+
+int ssb_create(ssb_ctx** out, int device_ordinal);
+void ssb_destroy(ssb_ctx* ctx);
+const char* ssb_last_error(const ssb_ctx* ctx);
+/* Device-side timing of the dominant kernel of the last call on this context (ms, hipEvent). */
+int ssb_last_kernel_ms(const ssb_ctx* ctx, const char* kernel_name, float* ms);
+
+/* hash_to_G2 of n 32-byte messages; out: n x 192 bytes (blst_p2_serialize layout). */
+int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* dst, size_t dst_len,
+                   uint8_t* out192);
+
+/* verdicts[i] = Signature::verify(pk48[i], roots32[root_idx[i]]) for sig96[i]  (1/0). */
+int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t* sig96,
+                     const uint32_t* root_idx, size_t n_roots, const uint8_t* roots32,
+                     const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* verdicts);
+
+/* Batched threshold_aggregate.  Job j owns shares [share_off[j], share_off[j+1]) of sig96 /
+ * pk48 / ids (input order = the reference's scan order), threshold t[j], and signs
+ * roots32[job_root[j]].  Per job: out_status[j] (SSB_DVF_*), out_err[2j..2j+1] (error fields),
+ * out_sig96[j] (combined signature, on SSB_DVF_OK).  share_verdicts (may be NULL) receives the
+ * verify result of EVERY share (the reference stops verifying at the t-th valid share; the
+ * combined signature is identical because every valid share lies on the same polynomial). */
+int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off,
+                                  const uint32_t* t, const uint8_t* sig96, const uint8_t* pk48,
+                                  const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                                  const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                  uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
+                                  uint64_t* out_err, uint8_t* share_verdicts);
+
+/* Same, all array arguments are device pointers; `stream` is a hipStream_t (NULL = default). */
+int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares,
+                                      const uint32_t* share_off, const uint32_t* t,
+                                      const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids,
+                                      const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
+                                      const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
+                                      uint8_t* out_sig96, int32_t* out_status, uint64_t* out_err,
+                                      uint8_t* share_verdicts, void* stream);
+
+/* Batched unsafe_aggregate: job j combines ALL its shares [share_off[j], share_off[j+1]) with
+ * Lagrange coefficients of its ids (t = share count), starting from infinity. */
+int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off,
+                               const uint8_t* sig96, const uint64_t* ids, uint8_t* out_sig96,
+                               int32_t* out_status);
+
+/* Batched local partial signing (SecretKey::sign = H(m)*sk, src/node/dvfcore.rs:241-243):
+ * out_sig96[i] = compress(sk_i * hash_to_G2(roots32[root_idx[i]])), sk as 32-byte little-endian
+ * scalars (< r).  Also the synthetic-input generator of bench.py. */
+int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t* root_idx, size_t n_roots,
+                   const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint8_t* out_sig96);
+
+/* SecretKey::public_key: out_pk48[i] = compress(sk_i * g1). */
+int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* out_pk48);
+
+/* lagrange_coeffs for one id set: out 32-byte little-endian scalars (blst_scalar.b layout). */
+int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* out32);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SSBLS_H */

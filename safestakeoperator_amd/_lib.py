@@ -1,0 +1,68 @@
+"""ctypes binding of libssbls.so (include/ssbls.h).  There is no CPU fallback: if the library or
+a GPU is missing, every entry point raises."""
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libssbls.so")
+HEADER = os.path.join(HERE, "..", "include", "ssbls.h")
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_sz = ctypes.c_size_t
+_ctx = ctypes.c_void_p
+
+SIGNATURES = {
+    "ssb_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
+    "ssb_destroy": (None, [_ctx]),
+    "ssb_last_error": (ctypes.c_char_p, [_ctx]),
+    "ssb_last_kernel_ms": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float)]),
+    "ssb_hash_to_g2": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _sz, _u8p]),
+    "ssb_verify_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _u32p, _sz, _u8p, _u8p, _sz, ctypes.c_uint64, _u8p]),
+    "ssb_threshold_aggregate_batch": (ctypes.c_int, [_ctx, _sz, _u32p, _u32p, _u8p, _u8p, _u64p, _u32p, _sz, _u8p,
+                                                     _u8p, _sz, ctypes.c_uint64, _u8p, _i32p, _u64p, _u8p]),
+    "ssb_threshold_aggregate_batch_dev": (ctypes.c_int, [_ctx, _sz, _sz, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_void_p, _sz, ctypes.c_void_p, _u8p, _sz,
+                                                         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_unsafe_aggregate_batch": (ctypes.c_int, [_ctx, _sz, _u32p, _u8p, _u64p, _u8p, _i32p]),
+    "ssb_sign_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u32p, _sz, _u8p, _u8p, _sz, _u8p]),
+    "ssb_sk_to_pk_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p]),
+    "ssb_lagrange_coeffs": (ctypes.c_int, [_ctx, _sz, _u64p, _u8p]),
+}
+
+
+def header_symbols():
+    """Every function declared in include/ssbls.h."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ssb_\w+)\s*\(", txt, re.M)))
+
+
+_LIB = None
+
+
+def load():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libssbls.so is not built (run `python -m safestakeoperator_amd.build`); "
+                           "there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def buf(b):
+    """bytes/bytearray/numpy -> ctypes uint8 pointer (kept alive by the caller's object)."""
+    import numpy as np
+    a = np.ascontiguousarray(np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray)) else b)
+    return a, a.ctypes.data_as(_u8p)

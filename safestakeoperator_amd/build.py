@@ -1,0 +1,37 @@
+"""Build libssbls.so (gfx950) in-tree.  Used by __graft_entry__.build() and the tests.
+
+    python -m safestakeoperator_amd.build [--force]
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libssbls.so")
+SOURCES = ["ssbls.hip"]
+HEADERS = ["ssb_field.h", "ssb_curve.h", "ssb_pairing.h", "ssb_h2c.h", "ssb_consts.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SSB_OFFLOAD_ARCH", "gfx950")
+
+
+def _newest_input():
+    paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    paths.append(os.path.join(HERE, "..", "include", "ssbls.h"))
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input():
+        return LIB
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-Wno-unused-result", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print("[ssbls] building:", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

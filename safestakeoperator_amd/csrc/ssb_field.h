@@ -1,0 +1,533 @@
+// ssb_field.h -- BLS12-381 field tower for the MI355X threshold-BLS engine.
+//
+// Fp: 12 x 32-bit limbs, Montgomery form (R = 2^384), CIOS multiplication on v_mad_u64_u32
+// chains; every value is kept fully reduced (< p).  Fr: 8 x 32-bit limbs, R = 2^256.
+// Tower: Fp2 = Fp[u]/(u^2+1), Fp6 = Fp2[v]/(v^3 - (1+u)), Fp12 = Fp6[w]/(w^2 - v).
+//
+// These replace the blst 0.3.10 field layer the reference calls through lighthouse `bls`
+// (SURVEY.md §2, F2): blst_sk_* (src/crypto/impls/blst.rs:19-39) and the Fp/Fp2/Fp12 arithmetic
+// inside blst_p2_mult / verify.  The same source compiles for gfx950 (kernels) and, for the
+// host-side unit tests and op counter only, for the CPU.
+#pragma once
+#include <cstdint>
+#include "ssb_consts.h"
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define SSB_INL __host__ __device__ __forceinline__
+#define SSB_FN __host__ __device__ __noinline__
+#else
+#define SSB_INL inline
+#define SSB_FN inline
+#endif
+
+#ifdef SSB_OPCOUNT
+// Host-only instrumented build (tests/native): counts the algorithmic work per operation.
+struct ssb_opcounts { unsigned long long fp_mul, fp_sqr, fr_mul; };
+extern ssb_opcounts g_ssb_counts;
+#define SSB_CNT(f) (g_ssb_counts.f++)
+#else
+#define SSB_CNT(f) ((void)0)
+#endif
+
+namespace ssb {
+
+// ------------------------------------------------------------------------------------------
+// carry helpers (lower to v_add_co_u32 / v_addc_co_u32 / v_sub_co_u32 / v_subb_co_u32)
+// ------------------------------------------------------------------------------------------
+SSB_INL uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+  return __builtin_addc(a, b, cin, &cout);
+}
+SSB_INL uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+  return __builtin_subc(a, b, bin, &bout);
+}
+
+// ------------------------------------------------------------------------------------------
+// Generic N-limb Montgomery arithmetic (N = 12 for Fp, 8 for Fr)
+// ------------------------------------------------------------------------------------------
+template <int N>
+SSB_INL void mp_add_mod(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* m) {
+  uint32_t t[N], s[N];
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = addc(a[i], b[i], c, c);
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s[i] = subb(t[i], m[i], br, br);
+  // a + b < 2m < 2^(32N): no carry out; keep t if t < m (borrow), else s.
+  const bool keep = br != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s[i];
+}
+
+template <int N>
+SSB_INL void mp_sub_mod(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* m) {
+  uint32_t t[N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = subb(a[i], b[i], br, br);
+  const uint32_t mask = 0u - br;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = addc(t[i], m[i] & mask, c, c);
+}
+
+// CIOS Montgomery product r = a*b/2^(32N) mod m, for m < 2^(32N-2) (no top-word carry).
+// The outer loop is kept rolled (b is rotated so every access is a static register index):
+// the unrolled 12x12 body inlined at every call site made kernels ~12x larger.
+template <int N>
+SSB_INL void mp_mont_mul(uint32_t* r, const uint32_t* a, const uint32_t* b_in, const uint32_t* m,
+                         uint32_t minv) {
+  uint32_t t[N], b[N];
+  uint32_t tN = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) { t[j] = 0; b[j] = b_in[j]; }
+#pragma nounroll
+  for (int i = 0; i < N; ++i) {
+    uint32_t carry = 0;
+    const uint32_t bi = b[0];
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) b[j] = b[j + 1];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      uint64_t s = (uint64_t)a[j] * bi + t[j] + carry;
+      t[j] = (uint32_t)s;
+      carry = (uint32_t)(s >> 32);
+    }
+    tN += carry;  // t < 2^(32N) + m*2^32: never overflows 32 bits
+    const uint32_t q = t[0] * minv;
+    uint64_t s = (uint64_t)q * m[0] + t[0];
+    carry = (uint32_t)(s >> 32);
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+      s = (uint64_t)q * m[j] + t[j] + carry;
+      t[j - 1] = (uint32_t)s;
+      carry = (uint32_t)(s >> 32);
+    }
+    s = (uint64_t)tN + carry;
+    t[N - 1] = (uint32_t)s;
+    tN = (uint32_t)(s >> 32);
+  }
+  // t < 2m: conditional subtraction
+  uint32_t s2[N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s2[i] = subb(t[i], m[i], br, br);
+  const bool keep = (br != 0) && (tN == 0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
+}
+
+template <int N>
+SSB_INL bool mp_is_zero(const uint32_t* a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc |= a[i];
+  return acc == 0;
+}
+
+template <int N>
+SSB_INL bool mp_eq(const uint32_t* a, const uint32_t* b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc |= a[i] ^ b[i];
+  return acc == 0;
+}
+
+// a > b (canonical integers)
+template <int N>
+SSB_INL bool mp_gt(const uint32_t* a, const uint32_t* b) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) (void)subb(b[i], a[i], br, br);
+  return br != 0;  // b - a borrowed  <=>  a > b
+}
+
+// ------------------------------------------------------------------------------------------
+// Fp
+// ------------------------------------------------------------------------------------------
+struct fp { uint32_t l[12]; };
+
+SSB_INL fp fp_from_c(const fp_c& c) { fp r; for (int i = 0; i < 12; ++i) r.l[i] = c.l[i]; return r; }
+SSB_INL fp fp_zero() { fp r; for (int i = 0; i < 12; ++i) r.l[i] = 0; return r; }
+SSB_INL fp fp_one() { fp r; for (int i = 0; i < 12; ++i) r.l[i] = P_ONE[i]; return r; }
+SSB_INL bool fp_is_zero(const fp& a) { return mp_is_zero<12>(a.l); }
+SSB_INL bool fp_eq(const fp& a, const fp& b) { return mp_eq<12>(a.l, b.l); }
+SSB_INL void fp_add(fp& r, const fp& a, const fp& b) { mp_add_mod<12>(r.l, a.l, b.l, P_LIMBS); }
+SSB_INL void fp_sub(fp& r, const fp& a, const fp& b) { mp_sub_mod<12>(r.l, a.l, b.l, P_LIMBS); }
+SSB_INL void fp_dbl(fp& r, const fp& a) { mp_add_mod<12>(r.l, a.l, a.l, P_LIMBS); }
+SSB_INL void fp_neg(fp& r, const fp& a) { fp z = fp_zero(); fp_sub(r, z, a); }
+SSB_INL void fp_mul(fp& r, const fp& a, const fp& b) {
+  SSB_CNT(fp_mul);
+  mp_mont_mul<12>(r.l, a.l, b.l, P_LIMBS, P_INV32);
+}
+SSB_INL void fp_sqr(fp& r, const fp& a) {
+  SSB_CNT(fp_sqr);
+  mp_mont_mul<12>(r.l, a.l, a.l, P_LIMBS, P_INV32);
+}
+SSB_INL void fp_cmov(fp& r, const fp& a, bool c) {
+  for (int i = 0; i < 12; ++i) r.l[i] = c ? a.l[i] : r.l[i];
+}
+// canonical integer (< 2^384) -> Montgomery form (reduces mod p)
+SSB_INL void fp_to_mont(fp& r, const fp& a) { mp_mont_mul<12>(r.l, a.l, P_R2, P_LIMBS, P_INV32); }
+SSB_INL void fp_from_mont(fp& r, const fp& a) {
+  uint32_t one[12] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  mp_mont_mul<12>(r.l, a.l, one, P_LIMBS, P_INV32);
+}
+
+// a^e for a fixed (wave-uniform) exponent given as 12 LE limbs
+SSB_FN void fp_pow(fp& r, const fp& a, const uint32_t* e) {
+  fp acc = fp_one();
+  bool started = false;
+  for (int i = 383; i >= 0; --i) {
+    if (started) fp_sqr(acc, acc);
+    if ((e[i >> 5] >> (i & 31)) & 1u) {
+      if (started) fp_mul(acc, acc, a); else acc = a;
+      started = true;
+    }
+  }
+  r = acc;
+}
+SSB_INL void fp_inv(fp& r, const fp& a) { fp_pow(r, a, EXP_P_MINUS_2); }  // inv(0) = 0
+// returns true iff a is a square; r = a^((p+1)/4) (a root when it is)
+SSB_FN bool fp_sqrt(fp& r, const fp& a) {
+  fp s, s2;
+  fp_pow(s, a, EXP_P_PLUS_1_DIV_4);
+  fp_sqr(s2, s);
+  r = s;
+  return fp_eq(s2, a);
+}
+// ZCash sign: canonical(a) > (p-1)/2
+SSB_INL bool fp_lex_largest(const fp& a) {
+  fp c; fp_from_mont(c, a);
+  return mp_gt<12>(c.l, P_HALF_CANON);
+}
+SSB_INL uint32_t fp_parity(const fp& a) { fp c; fp_from_mont(c, a); return c.l[0] & 1u; }
+
+// big-endian 48 bytes -> canonical limbs (no reduction); returns true iff value < p
+SSB_INL bool fp_from_be48(fp& r, const uint8_t* b, uint8_t top_mask) {
+  for (int i = 0; i < 12; ++i) {
+    const uint8_t* q = b + 44 - 4 * i;
+    uint32_t v = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    r.l[i] = v;
+  }
+  r.l[11] &= ((uint32_t)top_mask << 24) | 0x00ffffffu;
+  return mp_gt<12>(P_LIMBS, r.l);
+}
+SSB_INL void fp_to_be48(uint8_t* b, const fp& canon) {
+  for (int i = 0; i < 12; ++i) {
+    uint32_t v = canon.l[i];
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(v >> 24); q[1] = (uint8_t)(v >> 16); q[2] = (uint8_t)(v >> 8); q[3] = (uint8_t)v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fr (scalar field), used for the Lagrange coefficients (src/crypto/impls/blst.rs:19-39)
+// ------------------------------------------------------------------------------------------
+struct fr { uint32_t l[8]; };
+
+SSB_INL fr fr_zero() { fr r; for (int i = 0; i < 8; ++i) r.l[i] = 0; return r; }
+SSB_INL fr fr_one() { fr r; for (int i = 0; i < 8; ++i) r.l[i] = R_ONE[i]; return r; }
+SSB_INL bool fr_is_zero(const fr& a) { return mp_is_zero<8>(a.l); }
+SSB_INL void fr_sub(fr& r, const fr& a, const fr& b) { mp_sub_mod<8>(r.l, a.l, b.l, R_LIMBS); }
+SSB_INL void fr_mul(fr& r, const fr& a, const fr& b) {
+  SSB_CNT(fr_mul);
+  mp_mont_mul<8>(r.l, a.l, b.l, R_LIMBS, R_INV32);
+}
+// u64 -> Montgomery Fr (blst_scalar_from_uint64, src/utils/blst_utils.rs:15-21); u64 < r always
+SSB_INL void fr_from_u64(fr& r, uint64_t v) {
+  uint32_t c[8] = {(uint32_t)v, (uint32_t)(v >> 32), 0, 0, 0, 0, 0, 0};
+  mp_mont_mul<8>(r.l, c, R_R2, R_LIMBS, R_INV32);
+}
+SSB_INL void fr_from_mont(fr& r, const fr& a) {
+  uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+  mp_mont_mul<8>(r.l, a.l, one, R_LIMBS, R_INV32);
+}
+SSB_FN void fr_inv(fr& r, const fr& a) {  // Fermat; inv(0) = 0 like blst_sk_inverse
+  fr acc = fr_one();
+  bool started = false;
+  for (int i = 255; i >= 0; --i) {
+    if (started) fr_mul(acc, acc, acc);
+    if ((EXP_R_MINUS_2[i >> 5] >> (i & 31)) & 1u) {
+      if (started) fr_mul(acc, acc, a); else acc = a;
+      started = true;
+    }
+  }
+  r = acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fp2
+// ------------------------------------------------------------------------------------------
+struct fp2 { fp c0, c1; };
+
+SSB_INL fp2 fp2_from_c(const fp2_c& c) { fp2 r; r.c0 = fp_from_c(c.c0); r.c1 = fp_from_c(c.c1); return r; }
+SSB_INL fp2 fp2_zero() { fp2 r; r.c0 = fp_zero(); r.c1 = fp_zero(); return r; }
+SSB_INL fp2 fp2_one() { fp2 r; r.c0 = fp_one(); r.c1 = fp_zero(); return r; }
+SSB_INL bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+SSB_INL bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+SSB_INL void fp2_add(fp2& r, const fp2& a, const fp2& b) { fp_add(r.c0, a.c0, b.c0); fp_add(r.c1, a.c1, b.c1); }
+SSB_INL void fp2_sub(fp2& r, const fp2& a, const fp2& b) { fp_sub(r.c0, a.c0, b.c0); fp_sub(r.c1, a.c1, b.c1); }
+SSB_INL void fp2_dbl(fp2& r, const fp2& a) { fp_dbl(r.c0, a.c0); fp_dbl(r.c1, a.c1); }
+SSB_INL void fp2_neg(fp2& r, const fp2& a) { fp_neg(r.c0, a.c0); fp_neg(r.c1, a.c1); }
+SSB_INL void fp2_conj(fp2& r, const fp2& a) { r.c0 = a.c0; fp_neg(r.c1, a.c1); }
+SSB_INL void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
+  fp t0, t1, s0, s1, t2;
+  fp_mul(t0, a.c0, b.c0);
+  fp_mul(t1, a.c1, b.c1);
+  fp_add(s0, a.c0, a.c1);
+  fp_add(s1, b.c0, b.c1);
+  fp_mul(t2, s0, s1);
+  fp_sub(r.c0, t0, t1);
+  fp_sub(t2, t2, t0);
+  fp_sub(r.c1, t2, t1);
+}
+SSB_INL void fp2_sqr(fp2& r, const fp2& a) {
+  fp s, d, m;
+  fp_add(s, a.c0, a.c1);
+  fp_sub(d, a.c0, a.c1);
+  fp_mul(m, a.c0, a.c1);
+  fp_mul(r.c0, s, d);
+  fp_dbl(r.c1, m);
+}
+SSB_INL void fp2_mul_fp(fp2& r, const fp2& a, const fp& b) { fp_mul(r.c0, a.c0, b); fp_mul(r.c1, a.c1, b); }
+// (a0 + a1 u)(1 + u)
+SSB_INL void fp2_mul_xi(fp2& r, const fp2& a) {
+  fp t0, t1;
+  fp_sub(t0, a.c0, a.c1);
+  fp_add(t1, a.c0, a.c1);
+  r.c0 = t0; r.c1 = t1;
+}
+SSB_INL void fp2_cmov(fp2& r, const fp2& a, bool c) { fp_cmov(r.c0, a.c0, c); fp_cmov(r.c1, a.c1, c); }
+SSB_FN void fp2_inv(fp2& r, const fp2& a) {
+  fp t0, t1;
+  fp_sqr(t0, a.c0);
+  fp_sqr(t1, a.c1);
+  fp_add(t0, t0, t1);
+  fp_inv(t1, t0);
+  fp_mul(r.c0, a.c0, t1);
+  fp_mul(t0, a.c1, t1);
+  fp_neg(r.c1, t0);
+}
+// Square root in Fp2 by the norm method (p = 3 mod 4).  Any root is returned; the caller fixes
+// the sign.  Returns false iff a is not a square.
+SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) {
+  if (fp_is_zero(a.c1)) {
+    fp s;
+    if (fp_sqrt(s, a.c0)) { r.c0 = s; r.c1 = fp_zero(); return true; }
+    fp na; fp_neg(na, a.c0);
+    bool ok = fp_sqrt(s, na);
+    r.c0 = fp_zero(); r.c1 = s;
+    return ok;
+  }
+  fp n, t, s;
+  fp_sqr(n, a.c0);
+  fp_sqr(t, a.c1);
+  fp_add(n, n, t);
+  if (!fp_sqrt(s, n)) return false;
+  fp c, half = fp_from_c(FP_HALF);
+  fp_add(c, a.c0, s);
+  fp_mul(c, c, half);                       // c = (a0 + s)/2  (nonzero since a1 != 0)
+  fp_pow(t, c, EXP_P_MINUS_3_DIV_4);        // t = c^((p-3)/4)
+  fp x, x2;
+  fp_mul(x, c, t);                          // x^2 = c if c is a square, else -c
+  fp_sqr(x2, x);
+  fp2 y;
+  if (fp_eq(x2, c)) {
+    y.c0 = x;                               // x0 = sqrt(c), 1/x0 = t
+    fp_mul(y.c1, a.c1, t);
+    fp_mul(y.c1, y.c1, half);               // x1 = a1 / (2 x0)
+  } else {
+    fp nt; fp_neg(nt, t);
+    fp_mul(y.c0, a.c1, nt);
+    fp_mul(y.c0, y.c0, half);               // x0 = a1 / (2 sqrt(-c)) = -a1 t / 2
+    y.c1 = x;                               // x1 = sqrt(-c)
+  }
+  fp2 chk; fp2_sqr(chk, y);
+  r = y;
+  return fp2_eq(chk, a);
+}
+// ZCash sign for Fp2: c1 > (p-1)/2, or c0 > (p-1)/2 when c1 == 0
+SSB_INL bool fp2_lex_largest(const fp2& a) {
+  if (!fp_is_zero(a.c1)) return fp_lex_largest(a.c1);
+  return fp_lex_largest(a.c0);
+}
+// RFC 9380 sgn0 for Fp2
+SSB_INL uint32_t fp2_sgn0(const fp2& a) {
+  fp c0, c1;
+  fp_from_mont(c0, a.c0);
+  fp_from_mont(c1, a.c1);
+  const uint32_t sign0 = c0.l[0] & 1u;
+  const uint32_t zero0 = mp_is_zero<12>(c0.l) ? 1u : 0u;
+  const uint32_t sign1 = c1.l[0] & 1u;
+  return sign0 | (zero0 & sign1);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fp6
+// ------------------------------------------------------------------------------------------
+struct fp6 { fp2 c0, c1, c2; };
+
+SSB_INL fp6 fp6_zero() { fp6 r; r.c0 = fp2_zero(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); return r; }
+SSB_INL fp6 fp6_one() { fp6 r; r.c0 = fp2_one(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); return r; }
+SSB_INL void fp6_add(fp6& r, const fp6& a, const fp6& b) { fp2_add(r.c0, a.c0, b.c0); fp2_add(r.c1, a.c1, b.c1); fp2_add(r.c2, a.c2, b.c2); }
+SSB_INL void fp6_sub(fp6& r, const fp6& a, const fp6& b) { fp2_sub(r.c0, a.c0, b.c0); fp2_sub(r.c1, a.c1, b.c1); fp2_sub(r.c2, a.c2, b.c2); }
+SSB_INL void fp6_neg(fp6& r, const fp6& a) { fp2_neg(r.c0, a.c0); fp2_neg(r.c1, a.c1); fp2_neg(r.c2, a.c2); }
+SSB_INL bool fp6_eq(const fp6& a, const fp6& b) { return fp2_eq(a.c0, b.c0) && fp2_eq(a.c1, b.c1) && fp2_eq(a.c2, b.c2); }
+SSB_FN void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
+  fp2 t0, t1, t2, s0, s1, u;
+  fp2_mul(t0, a.c0, b.c0);
+  fp2_mul(t1, a.c1, b.c1);
+  fp2_mul(t2, a.c2, b.c2);
+  fp6 o;
+  // c0 = ((a1+a2)(b1+b2) - t1 - t2) xi + t0
+  fp2_add(s0, a.c1, a.c2); fp2_add(s1, b.c1, b.c2); fp2_mul(u, s0, s1);
+  fp2_sub(u, u, t1); fp2_sub(u, u, t2); fp2_mul_xi(u, u); fp2_add(o.c0, u, t0);
+  // c1 = (a0+a1)(b0+b1) - t0 - t1 + xi t2
+  fp2_add(s0, a.c0, a.c1); fp2_add(s1, b.c0, b.c1); fp2_mul(u, s0, s1);
+  fp2_sub(u, u, t0); fp2_sub(u, u, t1); fp2 x2; fp2_mul_xi(x2, t2); fp2_add(o.c1, u, x2);
+  // c2 = (a0+a2)(b0+b2) - t0 - t2 + t1
+  fp2_add(s0, a.c0, a.c2); fp2_add(s1, b.c0, b.c2); fp2_mul(u, s0, s1);
+  fp2_sub(u, u, t0); fp2_sub(u, u, t2); fp2_add(o.c2, u, t1);
+  r = o;
+}
+SSB_INL void fp6_mul_v(fp6& r, const fp6& a) {  // * v
+  fp2 t; fp2_mul_xi(t, a.c2);
+  fp2 a0 = a.c0, a1 = a.c1;
+  r.c0 = t; r.c1 = a0; r.c2 = a1;
+}
+// a * (b0 + b1 v)
+SSB_FN void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {
+  fp2 aa, bb, t1, t2, t3, s0, s1;
+  fp2_mul(aa, a.c0, b0);
+  fp2_mul(bb, a.c1, b1);
+  fp2_mul(t1, a.c2, b1); fp2_mul_xi(t1, t1); fp2_add(t1, t1, aa);
+  fp2_add(s0, b0, b1); fp2_add(s1, a.c0, a.c1); fp2_mul(t2, s0, s1); fp2_sub(t2, t2, aa); fp2_sub(t2, t2, bb);
+  fp2_mul(t3, a.c2, b0); fp2_add(t3, t3, bb);
+  r.c0 = t1; r.c1 = t2; r.c2 = t3;
+}
+// a * (b1 v)
+SSB_FN void fp6_mul_1(fp6& r, const fp6& a, const fp2& b1) {
+  fp2 t0, t1, t2;
+  fp2_mul(t0, a.c2, b1); fp2_mul_xi(t0, t0);
+  fp2_mul(t1, a.c0, b1);
+  fp2_mul(t2, a.c1, b1);
+  r.c0 = t0; r.c1 = t1; r.c2 = t2;
+}
+SSB_FN void fp6_inv(fp6& r, const fp6& a) {
+  fp2 c0, c1, c2, t, u;
+  fp2_sqr(c0, a.c0); fp2_mul(t, a.c1, a.c2); fp2_mul_xi(t, t); fp2_sub(c0, c0, t);
+  fp2_sqr(c1, a.c2); fp2_mul_xi(c1, c1); fp2_mul(t, a.c0, a.c1); fp2_sub(c1, c1, t);
+  fp2_sqr(c2, a.c1); fp2_mul(t, a.c0, a.c2); fp2_sub(c2, c2, t);
+  fp2_mul(t, a.c2, c1); fp2_mul(u, a.c1, c2); fp2_add(t, t, u); fp2_mul_xi(t, t);
+  fp2_mul(u, a.c0, c0); fp2_add(t, t, u);
+  fp2_inv(t, t);
+  fp2_mul(r.c0, c0, t); fp2_mul(r.c1, c1, t); fp2_mul(r.c2, c2, t);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fp12
+// ------------------------------------------------------------------------------------------
+struct fp12 { fp6 c0, c1; };
+
+SSB_INL fp12 fp12_one() { fp12 r; r.c0 = fp6_one(); r.c1 = fp6_zero(); return r; }
+SSB_INL bool fp12_eq(const fp12& a, const fp12& b) { return fp6_eq(a.c0, b.c0) && fp6_eq(a.c1, b.c1); }
+SSB_INL bool fp12_is_one(const fp12& a) { fp12 o = fp12_one(); return fp12_eq(a, o); }
+SSB_INL void fp12_conj(fp12& r, const fp12& a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
+SSB_FN void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
+  fp6 t0, t1, s0, s1, c1;
+  fp6_mul(t0, a.c0, b.c0);
+  fp6_mul(t1, a.c1, b.c1);
+  fp6_add(s0, a.c0, a.c1);
+  fp6_add(s1, b.c0, b.c1);
+  fp6_mul(c1, s0, s1);
+  fp6_sub(c1, c1, t0);
+  fp6_sub(r.c1, c1, t1);
+  fp6_mul_v(t1, t1);
+  fp6_add(r.c0, t0, t1);
+}
+SSB_FN void fp12_sqr(fp12& r, const fp12& a) {
+  fp6 ab, s0, s1, t;
+  fp6_mul(ab, a.c0, a.c1);
+  fp6_add(s0, a.c0, a.c1);
+  fp6_mul_v(t, a.c1);
+  fp6_add(s1, a.c0, t);
+  fp6_mul(s0, s0, s1);
+  fp6_sub(s0, s0, ab);
+  fp6_mul_v(t, ab);
+  fp6_sub(r.c0, s0, t);
+  fp6_add(r.c1, ab, ab);
+}
+SSB_FN void fp12_inv(fp12& r, const fp12& a) {
+  fp6 t0, t1;
+  fp6_mul(t0, a.c0, a.c0);
+  fp6_mul(t1, a.c1, a.c1);
+  fp6_mul_v(t1, t1);
+  fp6_sub(t0, t0, t1);
+  fp6_inv(t1, t0);
+  fp6_mul(r.c0, a.c0, t1);
+  fp6_mul(t0, a.c1, t1);
+  fp6_neg(r.c1, t0);
+}
+// f * (o0 + o1 v + o4 v w): the sparse line value (positions 0, 1, 4)
+SSB_FN void fp12_mul_014(fp12& r, const fp12& f, const fp2& o0, const fp2& o1, const fp2& o4) {
+  fp6 aa, bb, s;
+  fp6_mul_01(aa, f.c0, o0, o1);
+  fp6_mul_1(bb, f.c1, o4);
+  fp2 o; fp2_add(o, o1, o4);
+  fp6_add(s, f.c1, f.c0);
+  fp6_mul_01(s, s, o0, o);
+  fp6_sub(s, s, aa);
+  fp6_sub(r.c1, s, bb);
+  fp6_mul_v(bb, bb);
+  fp6_add(r.c0, bb, aa);
+}
+// Frobenius^n, n = 1, 2, 3: coefficient of w^k -> (conj^n) * xi^(k (p^n-1)/6)
+SSB_FN void fp12_frob(fp12& r, const fp12& a, int n) {
+  const fp2_c* g = (n == 1) ? FROB1 : (n == 2) ? FROB2 : FROB3;
+  fp2 c[6] = {a.c0.c0, a.c1.c0, a.c0.c1, a.c1.c1, a.c0.c2, a.c1.c2};  // w^0..w^5
+  for (int k = 0; k < 6; ++k) {
+    if (n & 1) fp2_conj(c[k], c[k]);
+    if (k) { fp2 gk = fp2_from_c(g[k]); fp2_mul(c[k], c[k], gk); }
+  }
+  r.c0.c0 = c[0]; r.c1.c0 = c[1]; r.c0.c1 = c[2]; r.c1.c1 = c[3]; r.c0.c2 = c[4]; r.c1.c2 = c[5];
+}
+// Granger-Scott squaring in the cyclotomic subgroup
+SSB_INL void fp4_sqr(fp2& c0, fp2& c1, const fp2& a, const fp2& b) {
+  fp2 t0, t1, t2;
+  fp2_sqr(t0, a);
+  fp2_sqr(t1, b);
+  fp2_mul_xi(t2, t1);
+  fp2_add(c0, t2, t0);
+  fp2_add(t2, a, b);
+  fp2_sqr(t2, t2);
+  fp2_sub(t2, t2, t0);
+  fp2_sub(c1, t2, t1);
+}
+SSB_FN void fp12_cyc_sqr(fp12& r, const fp12& f) {
+  fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fp2 t0, t1, t2, t3;
+  fp4_sqr(t0, t1, z0, z1);
+  fp2_sub(z0, t0, z0); fp2_dbl(z0, z0); fp2_add(z0, z0, t0);
+  fp2_add(z1, t1, z1); fp2_dbl(z1, z1); fp2_add(z1, z1, t1);
+  fp4_sqr(t0, t1, z2, z3);
+  fp4_sqr(t2, t3, z4, z5);
+  fp2_sub(z4, t0, z4); fp2_dbl(z4, z4); fp2_add(z4, z4, t0);
+  fp2_add(z5, t1, z5); fp2_dbl(z5, z5); fp2_add(z5, z5, t1);
+  fp2_mul_xi(t0, t3);
+  fp2_add(z2, t0, z2); fp2_dbl(z2, z2); fp2_add(z2, z2, t0);
+  fp2_sub(z3, t2, z3); fp2_dbl(z3, z3); fp2_add(z3, z3, t2);
+  r.c0.c0 = z0; r.c0.c1 = z4; r.c0.c2 = z3; r.c1.c0 = z2; r.c1.c1 = z1; r.c1.c2 = z5;
+}
+// f^x for x = -0xd201000000010000 (f in the cyclotomic subgroup)
+SSB_FN void fp12_cyc_exp_x(fp12& r, const fp12& f) {
+  fp12 acc = f;
+  for (int i = 62; i >= 0; --i) {
+    fp12_cyc_sqr(acc, acc);
+    if ((BLS_X_ABS >> i) & 1ull) fp12_mul(acc, acc, f);
+  }
+  fp12_conj(r, acc);
+}
+
+}  // namespace ssb

@@ -1,0 +1,811 @@
+// ssbls.hip -- gfx950 kernels and the C ABI (include/ssbls.h) of the threshold-BLS engine.
+//
+// Pipeline of ssb_threshold_aggregate_batch_dev (one HIP stream, no host round trip):
+//   k_share_map       share -> job, share -> root                          (bookkeeping)
+//   k_hash_to_g2      H(root) once per distinct signing root               (a-3)
+//   k_decode          G2 decompress + subgroup check, G1 decompress        (a-2 steps 1/4)
+//   k_rlc_mul         r_i*sig_i (G2), r_i*pk_i (G1), 64-bit RLC scalars    (a-7)
+//   k_sum_g1_by_root  per-root sum of r_i*pk_i                              (a-7)
+//   k_sum_g2_*        sum of r_i*sig_i                                      (a-7)
+//   k_miller          one Miller loop per (root, sum) pair + (-g1, sum sig) (a-2 step 3)
+//   k_final           product + ONE final exponentiation -> batch verdict
+//   k_fallback_verify exact per-share verify, only if the batch failed
+//   k_select          reference scan order / error semantics per job      (a-1)
+//   k_lagrange        Lagrange coefficients, Montgomery batch inversion    (a-5)
+//   k_combine_terms   lambda_i * sig_i  (255-bit, 4-bit window)            (a-4)
+//   k_combine_sum     sum, affine, compress                                 (a-4)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <map>
+#include <mutex>
+
+#include "ssb_pairing.h"
+#include "ssb_h2c.h"
+#include "../../include/ssbls.h"
+
+using namespace ssb;
+
+namespace {
+
+struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
+
+enum : uint32_t { FLAG_CANDIDATE = 1u << 16 };
+
+__device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
+  // splitmix64(seed ^ golden*i), forced non-zero
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (i + 1));
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z ? z : 1ull;
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+__global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
+                            uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  const uint32_t r = job_root ? job_root[j] : 0u;
+  for (uint32_t s = off[j]; s < off[j + 1]; ++s) {
+    share_job[s] = (uint32_t)j;
+    if (share_root) share_root[s] = r;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
+                                                   g2_aff* __restrict__ out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t m[32];
+  for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
+  g2_aff h;
+  hash_to_g2(h, m, dst.b, dst.len);
+  out[i] = h;
+}
+
+// flags: bits 0..7 signature DEC_* bits, bits 8..15 public-key DEC_* bits, bit 16 candidate
+__global__ void __launch_bounds__(64) k_decode(int n, const uint8_t* __restrict__ sig96,
+                                               const uint8_t* __restrict__ pk48, int group_check,
+                                               g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
+                                               uint32_t* __restrict__ flags) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  uint8_t b[96];
+  for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
+  g2_aff sig;
+  uint32_t st = g2_decompress(sig, b);
+  if ((st & DEC_OK) && group_check && g2_in_subgroup(sig)) st |= DEC_IN_GROUP;
+  sig_aff[s] = sig;
+  uint32_t pst = 0;
+  if (pk48) {
+    for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
+    g1_aff pk;
+    pst = g1_decompress(pk, b);
+    pk_aff[s] = pk;
+  }
+  const bool cand = (st & DEC_OK) && !(st & DEC_INF) && (st & DEC_IN_GROUP) && (pst & DEC_OK) && !(pst & DEC_INF);
+  flags[s] = st | (pst << 8) | (cand ? FLAG_CANDIDATE : 0u);
+}
+
+__global__ void __launch_bounds__(64) k_rlc_mul(int n, uint64_t seed, const uint32_t* __restrict__ flags,
+                                                const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
+                                                g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  g2_jac a; g1_jac b;
+  if (flags[s] & FLAG_CANDIDATE) {
+    const uint64_t r = rlc_scalar(seed, (uint64_t)s);
+    const uint32_t k[2] = {(uint32_t)r, (uint32_t)(r >> 32)};
+    jac_mul_aff(a, sig_aff[s], k, 2);
+    jac_mul_aff(b, pk_aff[s], k, 2);
+  } else {
+    jac_set_inf(a); jac_set_inf(b);
+  }
+  rsig[s] = a;
+  rpk[s] = b;
+}
+
+// One block per root: sum r_i*pk_i over the candidate shares of that root.
+constexpr int SUM_THREADS = 128;
+__global__ void __launch_bounds__(SUM_THREADS) k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
+                                                                const uint32_t* __restrict__ flags,
+                                                                const g1_jac* __restrict__ rpk,
+                                                                g1_aff* __restrict__ root_sum) {
+  __shared__ g1_jac sh[SUM_THREADS];
+  const uint32_t b = blockIdx.x;
+  g1_jac acc; jac_set_inf(acc);
+  for (int s = threadIdx.x; s < n; s += SUM_THREADS)
+    if ((flags[s] & FLAG_CANDIDATE) && share_root[s] == b) jac_add(acc, acc, rpk[s]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { g1_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { g1_aff a; jac_to_aff(a, acc); root_sum[b] = a; }
+}
+
+__global__ void __launch_bounds__(SUM_THREADS) k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
+                                                                const g2_jac* __restrict__ rsig,
+                                                                g2_jac* __restrict__ part) {
+  __shared__ g2_jac sh[SUM_THREADS];
+  g2_jac acc; jac_set_inf(acc);
+  for (int s = blockIdx.x * SUM_THREADS + threadIdx.x; s < n; s += gridDim.x * SUM_THREADS)
+    if (flags[s] & FLAG_CANDIDATE) jac_add(acc, acc, rsig[s]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(64) k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
+                                                     g2_aff* __restrict__ out) {
+  __shared__ g2_jac sh[64];
+  g2_jac acc; jac_set_inf(acc);
+  for (int i = threadIdx.x; i < nparts; i += 64) jac_add(acc, acc, part[i]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { g2_aff a; jac_to_aff(a, acc); *out = a; }
+}
+
+// pairs 0..n_roots-1: (sum_root r_i pk_i, H(root));  pair n_roots: (-g1, sum r_i sig_i)
+__global__ void __launch_bounds__(64) k_miller(int n_roots, const g1_aff* __restrict__ root_sum,
+                                               const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
+                                               fp12* __restrict__ f) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > n_roots) return;
+  fp12 r;
+  if (p < n_roots) {
+    miller_loop(r, root_sum[p], H[p]);
+  } else {
+    g1_aff ng; ng.x = fp_from_c(G1_GEN_X); ng.y = fp_from_c(G1_GEN_NEG_Y); ng.inf = 0;
+    miller_loop(r, ng, *sig_sum);
+  }
+  f[p] = r;
+}
+
+__global__ void __launch_bounds__(64) k_final(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok) {
+  __shared__ fp12 sh[64];
+  fp12 acc = fp12_one();
+  for (int i = threadIdx.x; i < npairs; i += 64) fp12_mul(acc, acc, f[i]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { fp12 o = sh[threadIdx.x + w]; fp12_mul(acc, acc, o); sh[threadIdx.x] = acc; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    fp12 e;
+    final_exponentiation(e, acc);
+    *ok = fp12_is_one(e) ? 1u : 0u;
+  }
+}
+
+// Exact per-share verify, run only when the RLC batch check failed.
+__global__ void __launch_bounds__(64) k_fallback_verify(int n, const uint32_t* __restrict__ ok,
+                                                        const uint32_t* __restrict__ flags,
+                                                        const uint32_t* __restrict__ share_root,
+                                                        const g2_aff* __restrict__ H,
+                                                        const g2_aff* __restrict__ sig_aff,
+                                                        const g1_aff* __restrict__ pk_aff,
+                                                        uint8_t* __restrict__ verdict) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
+  if (*ok || !cand) { verdict[s] = cand ? 1 : 0; return; }
+  fp12 f1, f2;
+  miller_loop(f1, pk_aff[s], H[share_root[s]]);
+  g1_aff ng; ng.x = fp_from_c(G1_GEN_X); ng.y = fp_from_c(G1_GEN_NEG_Y); ng.inf = 0;
+  miller_loop(f2, ng, sig_aff[s]);
+  fp12_mul(f1, f1, f2);
+  fp12 e;
+  final_exponentiation(e, f1);
+  verdict[s] = fp12_is_one(e) ? 1 : 0;
+}
+
+// Reference scan (src/crypto/generic_threshold.rs:133-172) on the batch verdicts.
+__global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
+                         uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  const uint32_t b = off[j], e = off[j + 1], t = tt[j];
+  const uint32_t n = e - b;
+  if (n < t) { status[j] = SSB_DVF_INSUFFICIENT_SIGNATURES; err[2 * j] = n; err[2 * j + 1] = t; return; }
+  uint32_t cnt = 0;
+  for (uint32_t s = b; s < e; ++s) {
+    const uint64_t id = ids[s];
+    if (id == 0) { status[j] = SSB_DVF_INVALID_OPERATOR_ID; err[2 * j] = 0; err[2 * j + 1] = 0; return; }
+    bool dup = false;
+    for (uint32_t k = 0; k < cnt; ++k) dup = dup || (ids[sel[b + k]] == id);
+    if (dup) continue;
+    if (verdict[s]) {
+      sel[b + cnt] = s;
+      ++cnt;
+      if (cnt >= t) break;
+    }
+  }
+  if (cnt < t) { status[j] = SSB_DVF_INSUFFICIENT_VALID_SIGNATURES; err[2 * j] = cnt; err[2 * j + 1] = t; return; }
+  status[j] = SSB_DVF_OK; err[2 * j] = 0; err[2 * j + 1] = 0;
+}
+
+// unsafe_aggregate: every share of the job, in order; a share that does not decode -> error
+__global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ flags,
+                             uint32_t* __restrict__ sel, uint32_t* __restrict__ tt, int32_t* __restrict__ status,
+                             uint64_t* __restrict__ err) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  const uint32_t b = off[j], e = off[j + 1];
+  tt[j] = e - b;
+  int32_t st = SSB_DVF_OK;
+  for (uint32_t s = b; s < e; ++s) {
+    sel[s] = s;
+    if (!(flags[s] & DEC_OK)) st = SSB_DVF_BAD_SIGNATURE_ENCODING;
+  }
+  status[j] = st; err[2 * j] = 0; err[2 * j + 1] = 0;
+}
+
+// lambda_i = prod_{j!=i} x_j (x_j - x_i)^{-1} mod r (src/crypto/impls/blst.rs:19-39), with the
+// blst convention inverse(0) = 0; one Fr inversion per job (Montgomery's trick).
+__global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                           const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
+                           const int32_t* __restrict__ status, fr* __restrict__ lam) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs || status[j] != SSB_DVF_OK) return;
+  const uint32_t b = off[j], t = tt[j];
+  // pass 1: den_i (into lam slots), running prefix product of the non-zero ones
+  fr prefix = fr_one();
+  for (uint32_t i = 0; i < t; ++i) {
+    fr xi; fr_from_u64(xi, ids[sel[b + i]]);
+    fr den = fr_one();
+    for (uint32_t k = 0; k < t; ++k) {
+      if (k == i) continue;
+      fr xk, d; fr_from_u64(xk, ids[sel[b + k]]);
+      fr_sub(d, xk, xi);
+      fr_mul(den, den, d);
+    }
+    lam[b + i] = den;
+    if (!fr_is_zero(den)) fr_mul(prefix, prefix, den);
+  }
+  fr inv; fr_inv(inv, prefix);
+  // pass 2 (backwards): den_i^{-1}, then times num_i
+  for (int i = (int)t - 1; i >= 0; --i) {
+    fr den = lam[b + i];
+    fr out;
+    if (fr_is_zero(den)) {
+      out = fr_zero();
+    } else {
+      // pre = prod_{k<i, nz} den_k (recomputed; t is small)
+      fr pre = fr_one();
+      for (int k = 0; k < i; ++k) { fr dk = lam[b + k]; if (!fr_is_zero(dk)) fr_mul(pre, pre, dk); }
+      fr dinv; fr_mul(dinv, pre, inv);   // inv = 1/prod_{k<=i,nz} den_k, so pre*inv = 1/den_i
+      fr_mul(inv, inv, den);             // drop den_i from the running inverse
+      fr xi; fr_from_u64(xi, ids[sel[b + i]]);
+      fr num = fr_one();
+      for (uint32_t k = 0; k < t; ++k) {
+        if ((int)k == i) continue;
+        fr xk; fr_from_u64(xk, ids[sel[b + k]]);
+        fr_mul(num, num, xk);
+      }
+      fr_mul(out, num, dinv);
+    }
+    fr c; fr_from_mont(c, out);
+    lam[b + i] = c;  // canonical (blst_scalar little-endian limbs)
+  }
+}
+
+__global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
+                                                      const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                                                      const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                                                      const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
+                                                      g2_jac* __restrict__ term) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint32_t j = share_job[s];
+  const uint32_t k = (uint32_t)s - off[j];
+  if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
+  const fr l = lam[s];
+  g2_jac r;
+  jac_mul_w4(r, sig_aff[sel[s]], l.l, 8);  // blst_p2_mult(.., 255 bits)
+  term[s] = r;
+}
+
+__global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
+                                                    const g2_jac* __restrict__ term, uint8_t* __restrict__ out96) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  uint8_t o[96];
+  if (status[j] == SSB_DVF_OK) {
+    g2_jac acc; jac_set_inf(acc);  // infinity(t) start (src/crypto/impls/blst.rs:74)
+    for (uint32_t k = 0; k < tt[j]; ++k) jac_add(acc, acc, term[off[j] + k]);
+    g2_aff a; jac_to_aff(a, acc);
+    g2_compress(o, a);
+  } else {
+    for (int k = 0; k < 96; ++k) o[k] = 0;
+  }
+  for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
+}
+
+// Batched local partial signing H(root)*sk (SecretKey::sign, src/node/dvfcore.rs:241-243).
+__global__ void __launch_bounds__(64) k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
+                                             const g2_aff* __restrict__ H, uint8_t* __restrict__ out96) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* q = sk32le + 32 * (size_t)i + 4 * w;
+    k[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  g2_jac r;
+  jac_mul_w4(r, H[root_idx[i]], k, 8);
+  g2_aff a; jac_to_aff(a, r);
+  uint8_t o[96];
+  g2_compress(o, a);
+  for (int b = 0; b < 96; ++b) out96[96 * (size_t)i + b] = o[b];
+}
+
+// sk -> pk = sk*g1, compressed (SecretKey::public_key)
+__global__ void __launch_bounds__(64) k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* q = sk32le + 32 * (size_t)i + 4 * w;
+    k[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  g1_aff g; g.x = fp_from_c(G1_GEN_X); g.y = fp_from_c(G1_GEN_Y); g.inf = 0;
+  g1_jac r;
+  jac_mul_w4(r, g, k, 8);
+  g1_aff a; jac_to_aff(a, r);
+  uint8_t o[48];
+  g1_compress(o, a);
+  for (int b = 0; b < 48; ++b) out48[48 * (size_t)i + b] = o[b];
+}
+
+__global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* __restrict__ out192) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t o[192];
+  g2_serialize(o, pts[i]);
+  for (int k = 0; k < 192; ++k) out192[192 * (size_t)i + k] = o[k];
+}
+
+__global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+struct ssb_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // workspace arena (grown on demand, never shrunk)
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  // host staging arena
+  void* io = nullptr;
+  size_t io_bytes = 0;
+  struct evpair { hipEvent_t a = nullptr, b = nullptr; bool used = false; };
+  std::map<std::string, evpair> timers;
+};
+
+namespace {
+
+#define SSB_HIP(call)                                                                 \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess) {                                                           \
+      ctx->err = std::string(#call) + ": " + hipGetErrorString(e_);                  \
+      return SSB_EHIP;                                                                \
+    }                                                                                 \
+  } while (0)
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct carve {
+  char* base; size_t off = 0;
+  template <class T> T* take(size_t n) { T* p = (T*)(base + off); off += align_up(n * sizeof(T)); return p; }
+};
+
+int ensure_ws(ssb_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->ws_bytes) return SSB_OK;
+  if (ctx->ws) { hipStreamSynchronize(ctx->stream); hipFree(ctx->ws); ctx->ws = nullptr; ctx->ws_bytes = 0; }
+  size_t want = bytes + bytes / 4;
+  if (hipMalloc(&ctx->ws, want) != hipSuccess) { ctx->err = "hipMalloc workspace failed"; ctx->ws = nullptr; return SSB_ENOMEM; }
+  ctx->ws_bytes = want;
+  return SSB_OK;
+}
+
+int ensure_io(ssb_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->io_bytes) return SSB_OK;
+  if (ctx->io) { hipFree(ctx->io); ctx->io = nullptr; ctx->io_bytes = 0; }
+  size_t want = bytes + bytes / 4;
+  if (hipMalloc(&ctx->io, want) != hipSuccess) { ctx->err = "hipMalloc io failed"; ctx->io = nullptr; return SSB_ENOMEM; }
+  ctx->io_bytes = want;
+  return SSB_OK;
+}
+
+inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+struct timed {
+  ssb_ctx* ctx; ssb_ctx::evpair* ev;
+  timed(ssb_ctx* c, const char* name) : ctx(c) {
+    ev = &ctx->timers[name];
+    if (!ev->a) { hipEventCreate(&ev->a); hipEventCreate(&ev->b); }
+    hipEventRecord(ev->a, ctx->stream);
+  }
+  ~timed() { hipEventRecord(ev->b, ctx->stream); ev->used = true; }
+};
+
+int fill_dst(ssb_ctx* ctx, dst_arg& d, const uint8_t* dst, size_t dst_len) {
+  if (dst_len > SSB_MAX_DST || (dst_len && !dst)) { ctx->err = "dst too long or null"; return SSB_EINVAL; }
+  memset(&d, 0, sizeof(d));
+  if (dst_len) memcpy(d.b, dst, dst_len);
+  d.len = (int)dst_len;
+  return SSB_OK;
+}
+
+// The verification stage shared by verify_batch and threshold_aggregate_batch.
+struct verify_ws {
+  g2_aff* H; g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags;
+  g2_jac* rsig; g1_jac* rpk; g1_aff* root_sum; g2_jac* part; g2_aff* sig_sum; fp12* f; uint32_t* ok;
+};
+constexpr int G2_PARTS = 64;
+
+size_t verify_ws_bytes(size_t n, size_t n_roots) {
+  return align_up(n_roots * sizeof(g2_aff)) + align_up(n * sizeof(g2_aff)) + align_up(n * sizeof(g1_aff)) +
+         align_up(n * 4) + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
+         align_up(n_roots * sizeof(g1_aff)) + align_up(G2_PARTS * sizeof(g2_jac)) + align_up(sizeof(g2_aff)) +
+         align_up((n_roots + 1) * sizeof(fp12)) + align_up(4);
+}
+
+verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
+  verify_ws w;
+  w.H = c.take<g2_aff>(n_roots); w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
+  w.flags = c.take<uint32_t>(n); w.rsig = c.take<g2_jac>(n); w.rpk = c.take<g1_jac>(n);
+  w.root_sum = c.take<g1_aff>(n_roots); w.part = c.take<g2_jac>(G2_PARTS); w.sig_sum = c.take<g2_aff>(1);
+  w.f = c.take<fp12>(n_roots + 1); w.ok = c.take<uint32_t>(1);
+  return w;
+}
+
+int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
+               const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t seed,
+               uint8_t* d_verdict) {
+  hipStream_t st = ctx->stream;
+  if (n_roots) { timed t(ctx, "k_hash_to_g2"); hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n_roots, 64)), dim3(64), 0, st, (int)n_roots, d_roots, dst, w.H); }
+  if (n) {
+    { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, 1, w.sig_aff, w.pk_aff, w.flags); }
+    { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_rlc_mul, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, seed, w.flags, w.sig_aff, w.pk_aff, w.rsig, w.rpk); }
+  }
+  { timed t(ctx, "k_sum");
+    if (n_roots) hipLaunchKernelGGL(k_sum_g1_by_root, dim3((unsigned)n_roots), dim3(SUM_THREADS), 0, st, (int)n, d_share_root, w.flags, w.rpk, w.root_sum);
+    hipLaunchKernelGGL(k_sum_g2_partial, dim3(G2_PARTS), dim3(SUM_THREADS), 0, st, (int)n, w.flags, w.rsig, w.part);
+    hipLaunchKernelGGL(k_sum_g2_final, dim3(1), dim3(64), 0, st, G2_PARTS, w.part, w.sig_sum); }
+  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller, dim3(nblk(n_roots + 1, 64)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.sig_sum, w.f); }
+  { timed t(ctx, "k_final"); hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, st, (int)(n_roots + 1), w.f, w.ok); }
+  if (n) { timed t(ctx, "k_fallback_verify"); hipLaunchKernelGGL(k_fallback_verify, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict); }
+  SSB_HIP(hipGetLastError());
+  return SSB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ssb_create(ssb_ctx** out, int device_ordinal) {
+  if (!out) return SSB_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SSB_EHIP;
+  if (device_ordinal < 0 || device_ordinal >= ndev) return SSB_EINVAL;
+  if (hipSetDevice(device_ordinal) != hipSuccess) return SSB_EHIP;
+  ssb_ctx* ctx = new (std::nothrow) ssb_ctx();
+  if (!ctx) return SSB_ENOMEM;
+  ctx->device = device_ordinal;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return SSB_EHIP; }
+  *out = ctx;
+  return SSB_OK;
+}
+
+void ssb_destroy(ssb_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->timers) { if (kv.second.a) hipEventDestroy(kv.second.a); if (kv.second.b) hipEventDestroy(kv.second.b); }
+  if (ctx->ws) hipFree(ctx->ws);
+  if (ctx->io) hipFree(ctx->io);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* ssb_last_error(const ssb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int ssb_last_kernel_ms(const ssb_ctx* ctx_c, const char* name, float* ms) {
+  ssb_ctx* ctx = const_cast<ssb_ctx*>(ctx_c);
+  if (!ctx || !name || !ms) return SSB_EINVAL;
+  auto it = ctx->timers.find(name);
+  if (it == ctx->timers.end() || !it->second.used) { ctx->err = "no timing for kernel"; return SSB_EINVAL; }
+  SSB_HIP(hipEventSynchronize(it->second.b));
+  SSB_HIP(hipEventElapsedTime(ms, it->second.a, it->second.b));
+  return SSB_OK;
+}
+
+int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* dst, size_t dst_len, uint8_t* out192) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!msgs32 || !out192) { ctx->err = "null pointer"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
+  size_t need = align_up(n * 32) + align_up(n * sizeof(g2_aff)) + align_up(n * 192);
+  if ((rc = ensure_ws(ctx, need))) return rc;
+  carve c{(char*)ctx->ws};
+  uint8_t* d_msg = c.take<uint8_t>(n * 32); g2_aff* d_h = c.take<g2_aff>(n); uint8_t* d_out = c.take<uint8_t>(n * 192);
+  SSB_HIP(hipMemcpyAsync(d_msg, msgs32, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  { timed t(ctx, "k_hash_to_g2"); hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->stream, (int)n, d_msg, d, d_h); }
+  hipLaunchKernelGGL(k_serialize_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->stream, (int)n, d_h, d_out);
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(out192, d_out, n * 192, hipMemcpyDeviceToHost, ctx->stream));
+  SSB_HIP(hipStreamSynchronize(ctx->stream));
+  return SSB_OK;
+}
+
+int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t* sig96, const uint32_t* root_idx,
+                     size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
+                     uint8_t* verdicts) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!pk48 || !sig96 || !root_idx || !roots32 || !verdicts || n_roots == 0) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
+  for (size_t i = 0; i < n; ++i) if (root_idx[i] >= n_roots) { ctx->err = "root_idx out of range"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
+  size_t io = align_up(n * 48) + align_up(n * 96) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n);
+  if ((rc = ensure_io(ctx, io))) return rc;
+  if ((rc = ensure_ws(ctx, verify_ws_bytes(n, n_roots)))) return rc;
+  carve ci{(char*)ctx->io};
+  uint8_t* d_pk = ci.take<uint8_t>(n * 48); uint8_t* d_sig = ci.take<uint8_t>(n * 96);
+  uint32_t* d_root = ci.take<uint32_t>(n); uint8_t* d_roots = ci.take<uint8_t>(n_roots * 32); uint8_t* d_v = ci.take<uint8_t>(n);
+  hipStream_t st = ctx->stream;
+  SSB_HIP(hipMemcpyAsync(d_pk, pk48, n * 48, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_sig, sig96, n * 96, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_root, root_idx, n * 4, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
+  carve c{(char*)ctx->ws};
+  verify_ws w = carve_verify(c, n, n_roots);
+  if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, d_root, d_roots, d, rlc_seed, d_v))) return rc;
+  SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
+int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* share_off,
+                                      const uint32_t* t, const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids,
+                                      const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
+                                      const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
+                                      int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, void* stream) {
+  if (!ctx) return SSB_EINVAL;
+  if (n_jobs == 0) return SSB_OK;
+  if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0 ||
+      (n_shares && (!sig96 || !pk48 || !ids))) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
+  const size_t n = n_shares;
+  size_t need = verify_ws_bytes(n, n_roots) + align_up(n * 4) * 3 + align_up(n) + align_up(n * sizeof(fr)) +
+                align_up(n * sizeof(g2_jac));
+  if ((rc = ensure_ws(ctx, need))) return rc;
+  hipStream_t user = (hipStream_t)stream;
+  hipStream_t st = ctx->stream;
+  // order the engine's private stream after the caller's stream, and back
+  hipEvent_t e_in, e_out;
+  SSB_HIP(hipEventCreateWithFlags(&e_in, hipEventDisableTiming));
+  SSB_HIP(hipEventCreateWithFlags(&e_out, hipEventDisableTiming));
+  SSB_HIP(hipEventRecord(e_in, user));
+  SSB_HIP(hipStreamWaitEvent(st, e_in, 0));
+  carve c{(char*)ctx->ws};
+  verify_ws w = carve_verify(c, n, n_roots);
+  uint32_t* share_job = c.take<uint32_t>(n);
+  uint32_t* share_root = c.take<uint32_t>(n);
+  uint32_t* sel = c.take<uint32_t>(n);
+  uint8_t* verdict = share_verdicts ? share_verdicts : c.take<uint8_t>(n);
+  fr* lam = c.take<fr>(n);
+  g2_jac* term = c.take<g2_jac>(n);
+  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, job_root, share_job, share_root);
+  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict))) return rc;
+  { timed tm(ctx, "k_select"); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, verdict, sel, out_status, out_err); }
+  { timed tm(ctx, "k_lagrange"); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, lam); }
+  if (n) { timed tm(ctx, "k_combine_terms"); hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, term); }
+  { timed tm(ctx, "k_combine_sum"); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, out_sig96); }
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipEventRecord(e_out, st));
+  SSB_HIP(hipStreamWaitEvent(user, e_out, 0));
+  hipEventDestroy(e_in);
+  hipEventDestroy(e_out);
+  return SSB_OK;
+}
+
+int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint32_t* t,
+                                  const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids, const uint32_t* job_root,
+                                  size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                  uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status, uint64_t* out_err,
+                                  uint8_t* share_verdicts) {
+  if (!ctx) return SSB_EINVAL;
+  if (n_jobs == 0) return SSB_OK;
+  if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0) {
+    ctx->err = "null pointer or no roots"; return SSB_EINVAL;
+  }
+  if (share_off[0] != 0) { ctx->err = "share_off[0] must be 0"; return SSB_EINVAL; }
+  for (size_t j = 0; j < n_jobs; ++j) {
+    if (share_off[j + 1] < share_off[j]) { ctx->err = "share_off not monotone"; return SSB_EINVAL; }
+    if (t[j] == 0 || t[j] > SSB_MAX_T) { ctx->err = "t out of range [1, SSB_MAX_T]"; return SSB_EINVAL; }
+    if (job_root[j] >= n_roots) { ctx->err = "job_root out of range"; return SSB_EINVAL; }
+  }
+  const size_t n = share_off[n_jobs];
+  if (n && (!sig96 || !pk48 || !ids)) { ctx->err = "null share arrays"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  size_t io = align_up(n * 96) + align_up(n * 48) + align_up(n * 8) + align_up((n_jobs + 1) * 4) + align_up(n_jobs * 4) * 2 +
+              align_up(n_roots * 32) + align_up(n_jobs * 96) + align_up(n_jobs * 4) + align_up(n_jobs * 16) + align_up(n);
+  int rc;
+  if ((rc = ensure_io(ctx, io))) return rc;
+  carve ci{(char*)ctx->io};
+  uint8_t* d_sig = ci.take<uint8_t>(n * 96); uint8_t* d_pk = ci.take<uint8_t>(n * 48); uint64_t* d_ids = ci.take<uint64_t>(n);
+  uint32_t* d_off = ci.take<uint32_t>(n_jobs + 1); uint32_t* d_t = ci.take<uint32_t>(n_jobs); uint32_t* d_jr = ci.take<uint32_t>(n_jobs);
+  uint8_t* d_roots = ci.take<uint8_t>(n_roots * 32); uint8_t* d_out = ci.take<uint8_t>(n_jobs * 96);
+  int32_t* d_st = ci.take<int32_t>(n_jobs); uint64_t* d_err = ci.take<uint64_t>(n_jobs * 2); uint8_t* d_v = ci.take<uint8_t>(n);
+  hipStream_t st = ctx->stream;
+  if (n) {
+    SSB_HIP(hipMemcpyAsync(d_sig, sig96, n * 96, hipMemcpyHostToDevice, st));
+    SSB_HIP(hipMemcpyAsync(d_pk, pk48, n * 48, hipMemcpyHostToDevice, st));
+    SSB_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, st));
+  }
+  SSB_HIP(hipMemcpyAsync(d_off, share_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_t, t, n_jobs * 4, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_jr, job_root, n_jobs * 4, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
+  if ((rc = ssb_threshold_aggregate_batch_dev(ctx, n_jobs, n, d_off, d_t, d_sig, d_pk, d_ids, d_jr, n_roots, d_roots, dst,
+                                              dst_len, rlc_seed, d_out, d_st, d_err, d_v, st)))
+    return rc;
+  SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipMemcpyAsync(out_err, d_err, n_jobs * 16, hipMemcpyDeviceToHost, st));
+  if (share_verdicts && n) SSB_HIP(hipMemcpyAsync(share_verdicts, d_v, n, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
+int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint8_t* sig96,
+                               const uint64_t* ids, uint8_t* out_sig96, int32_t* out_status) {
+  if (!ctx) return SSB_EINVAL;
+  if (n_jobs == 0) return SSB_OK;
+  if (!share_off || !out_sig96 || !out_status) { ctx->err = "null pointer"; return SSB_EINVAL; }
+  if (share_off[0] != 0) { ctx->err = "share_off[0] must be 0"; return SSB_EINVAL; }
+  for (size_t j = 0; j < n_jobs; ++j) {
+    if (share_off[j + 1] < share_off[j]) { ctx->err = "share_off not monotone"; return SSB_EINVAL; }
+    if (share_off[j + 1] - share_off[j] > SSB_MAX_T) { ctx->err = "more than SSB_MAX_T shares in a job"; return SSB_EINVAL; }
+  }
+  const size_t n = share_off[n_jobs];
+  if (n && (!sig96 || !ids)) { ctx->err = "null share arrays"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  int rc;
+  size_t io = align_up(n * 96) + align_up(n * 8) + align_up((n_jobs + 1) * 4) + align_up(n_jobs * 96) + align_up(n_jobs * 4);
+  if ((rc = ensure_io(ctx, io))) return rc;
+  size_t need = align_up(n * sizeof(g2_aff)) + align_up(n * 4) * 3 + align_up(n_jobs * 4) + align_up(n_jobs * 16) +
+                align_up(n * sizeof(fr)) + align_up(n * sizeof(g2_jac));
+  if ((rc = ensure_ws(ctx, need))) return rc;
+  carve ci{(char*)ctx->io};
+  uint8_t* d_sig = ci.take<uint8_t>(n * 96); uint64_t* d_ids = ci.take<uint64_t>(n); uint32_t* d_off = ci.take<uint32_t>(n_jobs + 1);
+  uint8_t* d_out = ci.take<uint8_t>(n_jobs * 96); int32_t* d_st = ci.take<int32_t>(n_jobs);
+  carve c{(char*)ctx->ws};
+  g2_aff* sig_aff = c.take<g2_aff>(n); uint32_t* flags = c.take<uint32_t>(n); uint32_t* share_job = c.take<uint32_t>(n);
+  uint32_t* sel = c.take<uint32_t>(n); uint32_t* tt = c.take<uint32_t>(n_jobs); uint64_t* err = c.take<uint64_t>(n_jobs * 2);
+  fr* lam = c.take<fr>(n); g2_jac* term = c.take<g2_jac>(n);
+  hipStream_t st = ctx->stream;
+  if (n) {
+    SSB_HIP(hipMemcpyAsync(d_sig, sig96, n * 96, hipMemcpyHostToDevice, st));
+    SSB_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, st));
+  }
+  SSB_HIP(hipMemcpyAsync(d_off, share_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, (const uint32_t*)nullptr, share_job, (uint32_t*)nullptr);
+  if (n) hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, (const uint8_t*)nullptr, 0, sig_aff, (g1_aff*)nullptr, flags);
+  hipLaunchKernelGGL(k_select_all, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, flags, sel, tt, d_st, err);
+  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, lam);
+  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, d_off, tt, d_st, sel, lam, sig_aff, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, d_out);
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
+int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t* root_idx, size_t n_roots,
+                   const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint8_t* out_sig96) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!sk32le || !root_idx || !roots32 || !out_sig96 || n_roots == 0) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
+  for (size_t i = 0; i < n; ++i) if (root_idx[i] >= n_roots) { ctx->err = "root_idx out of range"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
+  size_t need = align_up(n * 32) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n_roots * sizeof(g2_aff)) + align_up(n * 96);
+  if ((rc = ensure_ws(ctx, need))) return rc;
+  carve c{(char*)ctx->ws};
+  uint8_t* d_sk = c.take<uint8_t>(n * 32); uint32_t* d_ri = c.take<uint32_t>(n); uint8_t* d_roots = c.take<uint8_t>(n_roots * 32);
+  g2_aff* d_h = c.take<g2_aff>(n_roots); uint8_t* d_out = c.take<uint8_t>(n * 96);
+  hipStream_t st = ctx->stream;
+  SSB_HIP(hipMemcpyAsync(d_sk, sk32le, n * 32, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_ri, root_idx, n * 4, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n_roots, 64)), dim3(64), 0, st, (int)n_roots, d_roots, d, d_h);
+  { timed tm(ctx, "k_sign"); hipLaunchKernelGGL(k_sign, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sk, d_ri, d_h, d_out); }
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n * 96, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
+int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* out_pk48) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!sk32le || !out_pk48) { ctx->err = "null pointer"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  int rc;
+  size_t need = align_up(n * 32) + align_up(n * 48);
+  if ((rc = ensure_ws(ctx, need))) return rc;
+  carve c{(char*)ctx->ws};
+  uint8_t* d_sk = c.take<uint8_t>(n * 32); uint8_t* d_out = c.take<uint8_t>(n * 48);
+  hipStream_t st = ctx->stream;
+  SSB_HIP(hipMemcpyAsync(d_sk, sk32le, n * 32, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_sk_to_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sk, d_out);
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(out_pk48, d_out, n * 48, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
+int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* out32) {
+  if (!ctx) return SSB_EINVAL;
+  if (t == 0) return SSB_OK;
+  if (!ids || !out32 || t > SSB_MAX_T) { ctx->err = "bad arguments"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  int rc;
+  size_t need = align_up(8 * 4) + align_up(t * 8) + align_up(t * 4) + align_up(4) + align_up(t * sizeof(fr));
+  if ((rc = ensure_ws(ctx, need))) return rc;
+  carve c{(char*)ctx->ws};
+  uint32_t* d_off = c.take<uint32_t>(2); uint64_t* d_ids = c.take<uint64_t>(t); uint32_t* d_sel = c.take<uint32_t>(t);
+  uint32_t* d_t = c.take<uint32_t>(1); int32_t* d_st = c.take<int32_t>(1); fr* d_lam = c.take<fr>(t);
+  std::vector<uint32_t> sel(t); for (size_t i = 0; i < t; ++i) sel[i] = (uint32_t)i;
+  uint32_t off[2] = {0, (uint32_t)t}; uint32_t tt = (uint32_t)t; int32_t st0 = 0;
+  hipStream_t st = ctx->stream;
+  SSB_HIP(hipMemcpyAsync(d_off, off, 8, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_ids, ids, t * 8, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_sel, sel.data(), t * 4, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_t, &tt, 4, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_st, &st0, 4, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_lagrange, dim3(1), dim3(64), 0, st, 1, d_off, d_t, d_ids, d_sel, d_st, d_lam);
+  SSB_HIP(hipGetLastError());
+  std::vector<fr> lam(t);
+  SSB_HIP(hipMemcpyAsync(lam.data(), d_lam, t * sizeof(fr), hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  for (size_t i = 0; i < t; ++i)
+    for (int k = 0; k < 8; ++k)
+      for (int b = 0; b < 4; ++b) out32[32 * i + 4 * k + b] = (uint8_t)(lam[i].l[k] >> (8 * b));
+  return SSB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,355 @@
+"""Host-side mirror of SafeStake's threshold-signature API, backed by the MI355X engine.
+
+Reference interface (paths in the SafeStakeOperator repository):
+  * trait TThresholdSignature            src/crypto/generic_threshold.rs:15-23
+  * GenericThresholdSignature<T>         src/crypto/generic_threshold.rs:25-180
+      - new / infinity / threshold       :30-45
+      - threshold_aggregate              :132-175  (selection + error order reproduced exactly)
+      - unsafe_aggregate                 :177-179 -> src/crypto/impls/blst.rs:67-87
+  * DvfError                             src/utils/error.rs:12-60
+  * backend selection define_mod!        src/crypto/mod.rs:7-22  (here: the HIP engine)
+
+Added, as SURVEY.md §8b proposes: `threshold_aggregate_batch(jobs)`, the batched entry point a
+per-slot collector calls once for every (validator, signing-root) job of a slot.
+
+Every compute call goes through libssbls.so on the GPU; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import _lib
+
+DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"  # src/crypto/impls/blst.rs:11
+INFINITY_SIGNATURE = bytes([0xC0]) + bytes(95)          # bls::INFINITY_SIGNATURE
+
+SSB_OK = 0
+DVF_OK, DVF_DIFFERENT_LENGTH, DVF_INSUFFICIENT_SIGNATURES, DVF_INVALID_OPERATOR_ID, \
+    DVF_INSUFFICIENT_VALID_SIGNATURES, DVF_BAD_SIGNATURE_ENCODING = range(6)
+MAX_T = 64
+
+
+# ------------------------------------------------------------------------------------------
+# DvfError (src/utils/error.rs:12-60), the variants the threshold path can return
+# ------------------------------------------------------------------------------------------
+class DvfError(Exception):
+    tag = -1
+
+    def __eq__(self, other):
+        return type(self) is type(other) and self.args == other.args
+
+    def __hash__(self):
+        return hash((type(self).__name__, self.args))
+
+
+class DifferentLength(DvfError):
+    tag = DVF_DIFFERENT_LENGTH
+
+    def __init__(self, x, y):
+        super().__init__(int(x), int(y))
+        self.x, self.y = int(x), int(y)
+
+
+class InsufficientSignatures(DvfError):
+    tag = DVF_INSUFFICIENT_SIGNATURES
+
+    def __init__(self, got, expected):
+        super().__init__(int(got), int(expected))
+        self.got, self.expected = int(got), int(expected)
+
+
+class InvalidOperatorId(DvfError):
+    tag = DVF_INVALID_OPERATOR_ID
+
+    def __init__(self, id):  # noqa: A002 (reference field name)
+        super().__init__(int(id))
+        self.id = int(id)
+
+
+class InsufficientValidSignatures(DvfError):
+    tag = DVF_INSUFFICIENT_VALID_SIGNATURES
+
+    def __init__(self, got, expected):
+        super().__init__(int(got), int(expected))
+        self.got, self.expected = int(got), int(expected)
+
+
+class BadSignatureEncoding(DvfError):
+    """unsafe_aggregate on bytes that do not decode (the reference would panic in unwrap())."""
+    tag = DVF_BAD_SIGNATURE_ENCODING
+
+
+def _error_from(status: int, e0: int, e1: int) -> Optional[DvfError]:
+    if status == DVF_OK:
+        return None
+    if status == DVF_INSUFFICIENT_SIGNATURES:
+        return InsufficientSignatures(e0, e1)
+    if status == DVF_INVALID_OPERATOR_ID:
+        return InvalidOperatorId(e0)
+    if status == DVF_INSUFFICIENT_VALID_SIGNATURES:
+        return InsufficientValidSignatures(e0, e1)
+    if status == DVF_BAD_SIGNATURE_ENCODING:
+        return BadSignatureEncoding()
+    if status == DVF_DIFFERENT_LENGTH:
+        return DifferentLength(e0, e1)
+    raise RuntimeError("unknown status %d" % status)
+
+
+# ------------------------------------------------------------------------------------------
+# Engine: one ssb_ctx (device, stream, workspace)
+# ------------------------------------------------------------------------------------------
+class Engine:
+    def __init__(self, device: int = 0):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        rc = self._lib.ssb_create(ctypes.byref(h), int(device))
+        if rc != SSB_OK:
+            raise RuntimeError("ssb_create(device=%d) failed with %d (no usable GPU?)" % (device, rc))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.ssb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _check(self, rc, what):
+        if rc != SSB_OK:
+            msg = self._lib.ssb_last_error(self._h)
+            raise RuntimeError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def last_kernel_ms(self, name: str) -> float:
+        ms = ctypes.c_float()
+        self._check(self._lib.ssb_last_kernel_ms(self._h, name.encode(), ctypes.byref(ms)), "ssb_last_kernel_ms")
+        return float(ms.value)
+
+    # --- primitives -------------------------------------------------------------------------
+    def hash_to_g2(self, msgs: Sequence[bytes], dst: bytes = DST) -> List[bytes]:
+        n = len(msgs)
+        if n == 0:
+            return []
+        m = np.frombuffer(b"".join(msgs), dtype=np.uint8)
+        assert m.size == 32 * n
+        out = np.zeros(192 * n, dtype=np.uint8)
+        d, dp = _lib.buf(dst)
+        self._check(self._lib.ssb_hash_to_g2(self._h, n, m.ctypes.data_as(_lib._u8p), dp, len(dst),
+                                             out.ctypes.data_as(_lib._u8p)), "ssb_hash_to_g2")
+        return [out[192 * i:192 * (i + 1)].tobytes() for i in range(n)]
+
+    def verify_batch(self, pks: Sequence[bytes], sigs: Sequence[bytes], root_idx: Sequence[int],
+                     roots: Sequence[bytes], seed: int = 0x5AFE57A4E, dst: bytes = DST) -> np.ndarray:
+        n = len(sigs)
+        out = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return out
+        pk = np.frombuffer(b"".join(pks), dtype=np.uint8)
+        sg = np.frombuffer(b"".join(sigs), dtype=np.uint8)
+        ri = np.ascontiguousarray(np.asarray(root_idx, dtype=np.uint32))
+        rt = np.frombuffer(b"".join(roots), dtype=np.uint8)
+        d, dp = _lib.buf(dst)
+        self._check(self._lib.ssb_verify_batch(
+            self._h, n, pk.ctypes.data_as(_lib._u8p), sg.ctypes.data_as(_lib._u8p), ri.ctypes.data_as(_lib._u32p),
+            len(roots), rt.ctypes.data_as(_lib._u8p), dp, len(dst), seed & (2**64 - 1),
+            out.ctypes.data_as(_lib._u8p)), "ssb_verify_batch")
+        return out
+
+    def sign_batch(self, sks: Sequence[int], root_idx: Sequence[int], roots: Sequence[bytes],
+                   dst: bytes = DST) -> List[bytes]:
+        n = len(sks)
+        if n == 0:
+            return []
+        sk = np.frombuffer(b"".join(int(k).to_bytes(32, "little") for k in sks), dtype=np.uint8)
+        ri = np.ascontiguousarray(np.asarray(root_idx, dtype=np.uint32))
+        rt = np.frombuffer(b"".join(roots), dtype=np.uint8)
+        out = np.zeros(96 * n, dtype=np.uint8)
+        d, dp = _lib.buf(dst)
+        self._check(self._lib.ssb_sign_batch(self._h, n, sk.ctypes.data_as(_lib._u8p), ri.ctypes.data_as(_lib._u32p),
+                                             len(roots), rt.ctypes.data_as(_lib._u8p), dp, len(dst),
+                                             out.ctypes.data_as(_lib._u8p)), "ssb_sign_batch")
+        return [out[96 * i:96 * (i + 1)].tobytes() for i in range(n)]
+
+    def sk_to_pk_batch(self, sks: Sequence[int]) -> List[bytes]:
+        n = len(sks)
+        if n == 0:
+            return []
+        sk = np.frombuffer(b"".join(int(k).to_bytes(32, "little") for k in sks), dtype=np.uint8)
+        out = np.zeros(48 * n, dtype=np.uint8)
+        self._check(self._lib.ssb_sk_to_pk_batch(self._h, n, sk.ctypes.data_as(_lib._u8p),
+                                                 out.ctypes.data_as(_lib._u8p)), "ssb_sk_to_pk_batch")
+        return [out[48 * i:48 * (i + 1)].tobytes() for i in range(n)]
+
+    def lagrange_coeffs(self, ids: Sequence[int]) -> List[int]:
+        t = len(ids)
+        if t == 0:
+            return []
+        x = np.ascontiguousarray(np.asarray([int(i) for i in ids], dtype=np.uint64))
+        out = np.zeros(32 * t, dtype=np.uint8)
+        self._check(self._lib.ssb_lagrange_coeffs(self._h, t, x.ctypes.data_as(_lib._u64p),
+                                                  out.ctypes.data_as(_lib._u8p)), "ssb_lagrange_coeffs")
+        return [int.from_bytes(out[32 * i:32 * (i + 1)].tobytes(), "little") for i in range(t)]
+
+    def threshold_aggregate_batch_raw(self, t: Sequence[int], share_off: Sequence[int], sigs: bytes, pks: bytes,
+                                      ids: Sequence[int], job_root: Sequence[int], roots: Sequence[bytes],
+                                      seed: int = 0x5AFE57A4E, dst: bytes = DST):
+        """Packed form: returns (out_sig96[J,96], status[J], err[J,2], share_verdicts[N])."""
+        J = len(t)
+        off = np.ascontiguousarray(np.asarray(share_off, dtype=np.uint32))
+        N = int(off[-1]) if J else 0
+        tt = np.ascontiguousarray(np.asarray(t, dtype=np.uint32))
+        sg = np.frombuffer(sigs, dtype=np.uint8) if N else np.zeros(1, np.uint8)
+        pk = np.frombuffer(pks, dtype=np.uint8) if N else np.zeros(1, np.uint8)
+        idv = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64)) if N else np.zeros(1, np.uint64)
+        jr = np.ascontiguousarray(np.asarray(job_root, dtype=np.uint32))
+        rt = np.frombuffer(b"".join(roots), dtype=np.uint8)
+        out = np.zeros((max(J, 1), 96), dtype=np.uint8)
+        st = np.zeros(max(J, 1), dtype=np.int32)
+        err = np.zeros((max(J, 1), 2), dtype=np.uint64)
+        ver = np.zeros(max(N, 1), dtype=np.uint8)
+        d, dp = _lib.buf(dst)
+        self._check(self._lib.ssb_threshold_aggregate_batch(
+            self._h, J, off.ctypes.data_as(_lib._u32p), tt.ctypes.data_as(_lib._u32p), sg.ctypes.data_as(_lib._u8p),
+            pk.ctypes.data_as(_lib._u8p), idv.ctypes.data_as(_lib._u64p), jr.ctypes.data_as(_lib._u32p), len(roots),
+            rt.ctypes.data_as(_lib._u8p), dp, len(dst), seed & (2**64 - 1), out.ctypes.data_as(_lib._u8p),
+            st.ctypes.data_as(_lib._i32p), err.ctypes.data_as(_lib._u64p), ver.ctypes.data_as(_lib._u8p)),
+            "ssb_threshold_aggregate_batch")
+        return out[:J], st[:J], err[:J], ver[:N]
+
+    def unsafe_aggregate_batch_raw(self, share_off: Sequence[int], sigs: bytes, ids: Sequence[int]):
+        J = len(share_off) - 1
+        off = np.ascontiguousarray(np.asarray(share_off, dtype=np.uint32))
+        N = int(off[-1])
+        sg = np.frombuffer(sigs, dtype=np.uint8) if N else np.zeros(1, np.uint8)
+        idv = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64)) if N else np.zeros(1, np.uint64)
+        out = np.zeros((max(J, 1), 96), dtype=np.uint8)
+        st = np.zeros(max(J, 1), dtype=np.int32)
+        self._check(self._lib.ssb_unsafe_aggregate_batch(
+            self._h, J, off.ctypes.data_as(_lib._u32p), sg.ctypes.data_as(_lib._u8p), idv.ctypes.data_as(_lib._u64p),
+            out.ctypes.data_as(_lib._u8p), st.ctypes.data_as(_lib._i32p)), "ssb_unsafe_aggregate_batch")
+        return out[:J], st[:J]
+
+
+_DEFAULT_ENGINE: Optional[Engine] = None
+
+
+def default_engine() -> Engine:
+    global _DEFAULT_ENGINE
+    if _DEFAULT_ENGINE is None:
+        _DEFAULT_ENGINE = Engine(int(os.environ.get("SSB_DEVICE", "0")))
+    return _DEFAULT_ENGINE
+
+
+# ------------------------------------------------------------------------------------------
+# The reference API
+# ------------------------------------------------------------------------------------------
+@dataclass
+class ThresholdJob:
+    """One call's worth of threshold_aggregate arguments (SURVEY.md §8b batched entry point)."""
+    sigs: Sequence[bytes]
+    pks: Sequence[bytes]
+    ids: Sequence[int]
+    msg: bytes
+
+
+class ThresholdSignature:
+    """GenericThresholdSignature<HipThresholdSignature> (src/crypto/generic_threshold.rs:25-180)."""
+
+    def __init__(self, threshold: int, engine: Optional[Engine] = None):
+        self._t = int(threshold)
+        self._engine = engine
+
+    @classmethod
+    def new(cls, threshold: int, engine: Optional[Engine] = None) -> "ThresholdSignature":
+        return cls.infinity(threshold, engine)
+
+    @classmethod
+    def infinity(cls, threshold: int, engine: Optional[Engine] = None) -> "ThresholdSignature":
+        return cls(threshold, engine)
+
+    def threshold(self) -> int:
+        return self._t
+
+    @property
+    def engine(self) -> Engine:
+        return self._engine or default_engine()
+
+    def threshold_aggregate(self, sigs: Sequence[bytes], pks: Sequence[bytes], ids: Sequence[int],
+                            msg: bytes) -> bytes:
+        """Returns the 96-byte combined signature or raises the DvfError the reference returns."""
+        r = self.threshold_aggregate_batch([ThresholdJob(sigs, pks, ids, msg)])[0]
+        if isinstance(r, DvfError):
+            raise r
+        return r
+
+    def threshold_aggregate_batch(self, jobs: Sequence[ThresholdJob], seed: int = 0x5AFE57A4E
+                                  ) -> List[Union[bytes, DvfError]]:
+        results: List[Union[bytes, DvfError, None]] = [None] * len(jobs)
+        t = self._t
+        if t < 1 or t > MAX_T:
+            raise ValueError("threshold must be in [1, %d]" % MAX_T)
+        roots: dict = {}
+        dev_jobs = []
+        for j, job in enumerate(jobs):
+            # length checks, in the reference's order (generic_threshold.rs:133-141)
+            if len(job.sigs) != len(job.pks):
+                results[j] = DifferentLength(len(job.sigs), len(job.pks))
+                continue
+            if len(job.sigs) != len(job.ids):
+                results[j] = DifferentLength(len(job.sigs), len(job.ids))
+                continue
+            if len(job.msg) != 32:
+                raise ValueError("msg must be a 32-byte Hash256")
+            dev_jobs.append(j)
+            roots.setdefault(bytes(job.msg), len(roots))
+        if dev_jobs:
+            offs = [0]
+            sigs, pks, ids, jr = [], [], [], []
+            for j in dev_jobs:
+                job = jobs[j]
+                for s, p, i in zip(job.sigs, job.pks, job.ids):
+                    if len(s) != 96 or len(p) != 48:
+                        raise ValueError("signatures are 96 bytes, public keys 48 bytes")
+                    sigs.append(bytes(s)); pks.append(bytes(p)); ids.append(int(i))
+                offs.append(len(sigs))
+                jr.append(roots[bytes(job.msg)])
+            root_list = sorted(roots, key=roots.get)
+            out, st, err, _ = self.engine.threshold_aggregate_batch_raw(
+                [t] * len(dev_jobs), offs, b"".join(sigs), b"".join(pks), ids, jr, root_list, seed)
+            for k, j in enumerate(dev_jobs):
+                e = _error_from(int(st[k]), int(err[k, 0]), int(err[k, 1]))
+                results[j] = e if e is not None else out[k].tobytes()
+        return results  # type: ignore[return-value]
+
+    def unsafe_aggregate(self, sigs: Sequence[bytes], ids: Sequence[int]) -> bytes:
+        """src/crypto/impls/blst.rs:67-87: combine the first t shares with Lagrange coefficients of
+        `ids` (which must have exactly t entries: require(...) panics otherwise)."""
+        t = self._t
+        if len(ids) != t:
+            raise ValueError("Different length")   # require() panic, src/utils/error.rs:4-8
+        if len(sigs) < t:
+            raise IndexError("index out of bounds")  # sigs[i] for i < t
+        out, st = self.engine.unsafe_aggregate_batch_raw([0, t], b"".join(bytes(s) for s in sigs[:t]), list(ids))
+        e = _error_from(int(st[0]), 0, 0)
+        if e is not None:
+            raise e
+        return out[0].tobytes()
