@@ -1,0 +1,261 @@
+"""Benchmark: the threshold-BLS hot path on MI355X (BASELINE.json metric, config C2 per GPU).
+
+One step = one ssb_threshold_aggregate_batch_dev pass over one batch resident in HBM:
+  4,096 validators x 4 operator shares (3-of-4), 64 distinct signing roots  (BASELINE.json configs[1])
+  = hash_to_G2 per root + verify every partial signature (RLC multi-pairing, exact fallback)
+    + reference scan/selection + Lagrange combine + compress,
+  and for N > 1 the per-batch RCCL all-gather of verdict bitmaps, statuses and combined signatures.
+Scaling is weak: every rank runs its own C2 batch (distinct validators), no data-path collective.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--validators V] [--no-cpu-baseline]
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+METRIC = "verified partial sigs/sec + combined threshold sigs/sec, 1 and 8 MI355X"
+MAD_PEAK_MEASURED = 3.8235e13  # v_mad_u64_u32/s, profiles/r01_madpeak.json (16 chains, 4096 WGs)
+MAD_PEAK_ISSUE = 256 * 4 * 16 * 2.4e9  # 16 lanes/clk/SIMD (wave64 mad = 4 cycles) x 1024 SIMDs x 2.4 GHz
+
+
+def opcount_mads():
+    with open(os.path.join(ROOT, "bench_tools", "opcount.json")) as f:
+        oc = json.load(f)
+    return {k: 300.0 * (v["fp_mul"] + v["fp_sqr"]) + 136.0 * v["fr_mul"] for k, v in oc.items() if isinstance(v, dict)}
+
+
+def kernel_mads(mads, V, t, n, n_roots):
+    """Algorithmic MADs per launch of each kernel (per-unit counts x units per launch)."""
+    N = V * n
+    comb_sum = mads["combine_sum_t3"] if t <= 3 else mads["combine_sum_t10"]
+    lag = mads["lagrange_t3"] if t <= 3 else (mads["lagrange_t5"] if t <= 5 else mads["lagrange_t10"])
+    return {
+        "k_hash_to_g2": n_roots * mads["hash_to_g2"],
+        "k_decode": N * mads["decode"],
+        "k_rlc_mul": N * mads["rlc"],
+        "k_sum": N * (mads["sum_g1_add"] + mads["sum_g2_add"]) + n_roots * mads["to_affine_g1"] + mads["to_affine_g2"],
+        "k_miller": (n_roots + 1) * mads["miller_pair"],
+        "k_final": n_roots * mads["fp12_mul"] + mads["final_exp"],
+        "k_lagrange": V * lag,
+        "k_combine_terms": V * t * mads["combine_term"],
+        "k_combine_sum": V * comb_sum,
+    }
+
+
+def make_workload(engine, V, t, n, n_roots, rank):
+    """Synthetic committees: deterministic keys (seed 0x5AFE57A4E, rank), Shamir shares, partial
+    signatures from the engine's batched signer (H(m)*sk), public keys sk*g1."""
+    seed = b"ssbls-bench" + (0x5AFE57A4E).to_bytes(8, "little") + rank.to_bytes(4, "little")
+    roots = [hashlib.sha256(seed + b"root" + i.to_bytes(4, "little")).digest() for i in range(n_roots)]
+
+    def h(*parts):
+        return int.from_bytes(hashlib.sha256(seed + b"".join(parts)).digest(), "little") % R_ORDER
+
+    share_sk, ids, share_root, jr, master = [], [], [], [], []
+    for v in range(V):
+        vb = v.to_bytes(4, "little")
+        coeffs = [h(b"sk", vb)] + [h(b"c", vb, k.to_bytes(4, "little")) for k in range(1, t)]
+        master.append(coeffs[0])
+        for i in range(1, n + 1):
+            acc = 0
+            for c in reversed(coeffs):
+                acc = (acc * i + c) % R_ORDER
+            share_sk.append(acc)
+            ids.append(i)
+            share_root.append(v % n_roots)
+        jr.append(v % n_roots)
+    sigs = engine.sign_batch(share_sk, share_root, roots)
+    pks = engine.sk_to_pk_batch(share_sk)
+    return dict(roots=roots, sigs=b"".join(sigs), pks=b"".join(pks), ids=ids, job_root=jr, master=master,
+                share_sigs=sigs, share_pks=pks)
+
+
+def cpu_baseline(wl, t, n, n_val=4):
+    """The oracle (pure-Python CPU restatement, 1 core) on a bounded sample of the same workload:
+    n_val validators x n shares: verify every share, then Lagrange-combine the first t valid."""
+    from oracle import bls12_381 as B
+    roots = wl["roots"]
+    t0 = time.perf_counter()
+    ok = True
+    for v in range(n_val):
+        root = roots[wl["job_root"][v]]
+        h = B.hash_to_g2(root)  # once per root, like the engine
+        pts, ids = [], []
+        for k in range(n):
+            i = v * n + k
+            pk = B.g1_decompress(wl["share_pks"][i])
+            sig = B.g2_decompress(wl["share_sigs"][i])
+            good = B.verify_points(pk, sig, root, h=h)
+            ok &= good
+            if good and len(pts) < t:
+                pts.append(sig)
+                ids.append(wl["ids"][i])
+        B.g2_compress(B.unsafe_aggregate_points(pts, ids, t))
+    dt = time.perf_counter() - t0
+    return dict(value=round(n_val * n / dt, 3), unit="partial_sigs/s", cores=1, kind="port",
+                combined_per_s=round(n_val / dt, 3), seconds=round(dt, 2), all_valid=bool(ok),
+                sample="%d validators x %d shares of the rank-0 C2 batch (verify all + %d-of-%d combine), "
+                       "oracle/bls12_381.py, 1 thread" % (n_val, n, t, n))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--validators", type=int, default=4096)
+    ap.add_argument("--threshold", type=int, default=3)
+    ap.add_argument("--operators", type=int, default=4)
+    ap.add_argument("--roots", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from safestakeoperator_amd.build import build
+    if rank == 0 or world == 1:
+        build(verbose=False)
+    if dist is not None:
+        dist.barrier()
+    from safestakeoperator_amd import Engine, DST
+    from safestakeoperator_amd import _lib
+
+    V, t, n, n_roots = args.validators, args.threshold, args.operators, args.roots
+    N = V * n
+    eng = Engine(local)
+    wl = make_workload(eng, V, t, n, n_roots, rank)
+
+    # inputs resident in HBM before the timed region
+    def dt8(b):
+        return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_sig = dt8(wl["sigs"])
+    d_pk = dt8(wl["pks"])
+    d_ids = torch.tensor(wl["ids"], dtype=torch.int64, device=dev)
+    d_off = torch.arange(0, N + 1, n, dtype=torch.int32, device=dev)
+    d_t = torch.full((V,), t, dtype=torch.int32, device=dev)
+    d_jr = torch.tensor(wl["job_root"], dtype=torch.int32, device=dev)
+    d_roots = dt8(b"".join(wl["roots"]))
+    d_out = torch.empty((V, 96), dtype=torch.uint8, device=dev)
+    d_st = torch.empty((V,), dtype=torch.int32, device=dev)
+    d_err = torch.empty((V, 2), dtype=torch.int64, device=dev)
+    d_ver = torch.empty((N,), dtype=torch.uint8, device=dev)
+    from safestakeoperator_amd.shard import exchange
+    dst_arr = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
+    lib = eng._lib
+    seed_base = 0x5AFE57A4E ^ (rank << 40)
+
+    def step(i):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = lib.ssb_threshold_aggregate_batch_dev(
+            eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(), d_pk.data_ptr(), d_ids.data_ptr(),
+            d_jr.data_ptr(), n_roots, d_roots.data_ptr(), ctypes.cast(dst_arr, _lib._u8p), len(DST),
+            (seed_base + i) & (2 ** 64 - 1), d_out.data_ptr(), d_st.data_ptr(), d_err.data_ptr(), d_ver.data_ptr(),
+            ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
+        if dist is not None:
+            exchange(d_ver, d_out, d_st)  # RCCL all-gather over xGMI: the one exchange step
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    # correctness of the benchmarked batch: every share valid, every combine == master signature
+    ok_st = bool((d_st == 0).all().item()) and bool((d_ver == 1).all().item())
+    msig = eng.sign_batch(wl["master"][:64], wl["job_root"][:64], wl["roots"])
+    out_host = d_out.cpu().numpy()
+    ok_comb = all(out_host[v].tobytes() == msig[v] for v in range(min(64, V)))
+
+    eng.kernel_timing(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = {k: eng.kernel_time(k) for k in ["k_hash_to_g2", "k_decode", "k_rlc_mul", "k_sum", "k_miller", "k_final",
+                                         "k_fallback_verify", "k_select", "k_lagrange", "k_combine_terms",
+                                         "k_combine_sum"]}
+    eng.kernel_timing(False)
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        okt = torch.tensor([1 if (ok_st and ok_comb) else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok_all = bool(okt.item())
+    else:
+        ok_all = ok_st and ok_comb
+
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        total_shares = N * world * args.steps
+        value = total_shares / elapsed
+        combined = V * world * args.steps / elapsed
+        mads = opcount_mads()
+        km = kernel_mads(mads, V, t, n, n_roots)
+        avg = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in kt.items()}
+        dom = max((k for k in km), key=lambda k: avg.get(k, 0.0))
+        achieved = km[dom] / (avg[dom] * 1e-3) / 1e12 if avg[dom] > 0 else 0.0
+        peak = MAD_PEAK_MEASURED / 1e12
+        step_mads = sum(km.values())
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "partial_sigs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32-limb modular integer (BLS12-381 Fp/Fr)",
+            "data": "synthetic (deterministic keys, GPU-signed shares)",
+            "config": {"workload": "C2: %d validators x %d shares (%d-of-%d), %d roots per GPU; verify + combine"
+                                   % (V, n, t, n, n_roots),
+                       "validators_per_gpu": V, "threshold": t, "operators": n, "roots": n_roots,
+                       "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world},
+            "combined_sigs_per_s": round(combined, 1),
+            "results_ok": ok_all,
+            "roofline": {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),
+                         "peak": round(peak, 2), "unit": "TMAD/s", "frac": round(achieved / peak, 5),
+                         "traffic": None, "mads_per_launch": km[dom], "avg_launch_ms": round(avg[dom], 4)},
+            "step_roofline": {"mads_per_step_per_gpu": step_mads,
+                              "achieved_TMAD_s": round(step_mads * world * args.steps / elapsed / 1e12, 4),
+                              "frac": round(step_mads * world * args.steps / elapsed / MAD_PEAK_MEASURED / world, 5)},
+            "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(wl, t, n)
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -69,8 +69,12 @@ typedef struct ssb_ctx ssb_ctx;
 int ssb_create(ssb_ctx** out, int device_ordinal);
 void ssb_destroy(ssb_ctx* ctx);
 const char* ssb_last_error(const ssb_ctx* ctx);
-/* Device-side timing of the dominant kernel of the last call on this context (ms, hipEvent). */
+/* Device-side kernel timing with hipEvents recorded on the engine's stream around each launch.
+ * ssb_last_kernel_ms: the last launch of `kernel_name`.  ssb_kernel_timing(ctx, 1) clears and
+ * starts accumulating every launch; ssb_kernel_time returns the total and the launch count. */
 int ssb_last_kernel_ms(const ssb_ctx* ctx, const char* kernel_name, float* ms);
+int ssb_kernel_timing(ssb_ctx* ctx, int on);
+int ssb_kernel_time(ssb_ctx* ctx, const char* kernel_name, float* total_ms, int* launches);
 
 /* hash_to_G2 of n 32-byte messages; out: n x 192 bytes (blst_p2_serialize layout). */
 int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* dst, size_t dst_len,

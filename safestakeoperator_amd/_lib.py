@@ -20,6 +20,8 @@ SIGNATURES = {
     "ssb_destroy": (None, [_ctx]),
     "ssb_last_error": (ctypes.c_char_p, [_ctx]),
     "ssb_last_kernel_ms": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float)]),
+    "ssb_kernel_timing": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "ssb_kernel_time": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]),
     "ssb_hash_to_g2": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _sz, _u8p]),
     "ssb_verify_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _u32p, _sz, _u8p, _u8p, _sz, ctypes.c_uint64, _u8p]),
     "ssb_threshold_aggregate_batch": (ctypes.c_int, [_ctx, _sz, _u32p, _u32p, _u8p, _u8p, _u64p, _u32p, _sz, _u8p,

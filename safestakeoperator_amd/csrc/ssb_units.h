@@ -1,0 +1,112 @@
+// ssb_units.h -- the per-work-unit bodies of the engine's kernels.  The gfx950 kernels in
+// ssbls.hip call exactly these functions; the host op counter (tests/native/host_math.cpp,
+// SSB_OPCOUNT) calls the same functions to measure the algorithmic work per unit
+// (MADs/unit = 300*(Fp mul + Fp sqr) + 136*(Fr mul)).
+#pragma once
+#include "ssb_pairing.h"
+#include "ssb_h2c.h"
+
+namespace ssb {
+
+enum : uint32_t { FLAG_CANDIDATE = 1u << 16 };
+
+SSB_INL uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
+  // splitmix64(seed ^ golden*i), forced non-zero
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (i + 1));
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z ? z : 1ull;
+}
+
+SSB_INL g1_aff g1_neg_generator() {
+  g1_aff ng; ng.x = fp_from_c(G1_GEN_X); ng.y = fp_from_c(G1_GEN_NEG_Y); ng.inf = 0;
+  return ng;
+}
+
+// unit "decode": one share -> decompressed signature (+ subgroup check) and public key.
+// flags: bits 0..7 signature DEC_* bits, bits 8..15 public-key DEC_* bits, bit 16 candidate
+SSB_FN uint32_t unit_decode(g2_aff& sig, g1_aff& pk, const uint8_t* sig96, const uint8_t* pk48, int group_check) {
+  uint32_t st = g2_decompress(sig, sig96);
+  if ((st & DEC_OK) && group_check && g2_in_subgroup(sig)) st |= DEC_IN_GROUP;
+  uint32_t pst = 0;
+  if (pk48) pst = g1_decompress(pk, pk48);
+  const bool cand = (st & DEC_OK) && !(st & DEC_INF) && (st & DEC_IN_GROUP) && (pst & DEC_OK) && !(pst & DEC_INF);
+  return st | (pst << 8) | (cand ? FLAG_CANDIDATE : 0u);
+}
+
+// unit "rlc": r*sig and r*pk for the share's 64-bit RLC scalar
+SSB_FN void unit_rlc(g2_jac& rsig, g1_jac& rpk, const g2_aff& sig, const g1_aff& pk, uint64_t r) {
+  const uint32_t k[2] = {(uint32_t)r, (uint32_t)(r >> 32)};
+  jac_mul_aff(rsig, sig, k, 2);
+  jac_mul_aff(rpk, pk, k, 2);
+}
+
+// unit "verify_one": exact single-signature pairing check e(pk,H) == e(g1,sig)
+SSB_FN bool unit_verify_one(const g1_aff& pk, const g2_aff& sig, const g2_aff& H) {
+  fp12 f1, f2;
+  miller_loop(f1, pk, H);
+  g1_aff ng = g1_neg_generator();
+  miller_loop(f2, ng, sig);
+  fp12_mul(f1, f1, f2);
+  fp12 e;
+  final_exponentiation(e, f1);
+  return fp12_is_one(e);
+}
+
+// unit "combine_term": lambda_i * sig_i (blst_p2_mult with 255-bit scalar)
+SSB_FN void unit_combine_term(g2_jac& r, const g2_aff& sig, const uint32_t* lam8) {
+  jac_mul_w4(r, sig, lam8, 8);
+}
+
+// unit "combine_sum": sum of t terms, affine, compressed (src/crypto/impls/blst.rs:74-86)
+SSB_FN void unit_combine_sum(uint8_t* out96, const g2_jac* terms, uint32_t t) {
+  g2_jac acc; jac_set_inf(acc);
+  for (uint32_t k = 0; k < t; ++k) jac_add(acc, acc, terms[k]);
+  g2_aff a; jac_to_aff(a, acc);
+  g2_compress(out96, a);
+}
+
+// unit "lagrange": lambda_i = prod_{j!=i} x_j (x_j - x_i)^{-1} mod r (src/crypto/impls/blst.rs:19-39)
+// with blst's inverse(0) = 0; one Fr inversion per job (Montgomery's trick).  `lam` receives
+// canonical little-endian limbs (blst_scalar.b).
+SSB_FN void unit_lagrange(fr* lam, const uint64_t* x, uint32_t t) {
+  fr prefix = fr_one();
+  for (uint32_t i = 0; i < t; ++i) {
+    fr xi; fr_from_u64(xi, x[i]);
+    fr den = fr_one();
+    for (uint32_t k = 0; k < t; ++k) {
+      if (k == i) continue;
+      fr xk, d; fr_from_u64(xk, x[k]);
+      fr_sub(d, xk, xi);
+      fr_mul(den, den, d);
+    }
+    lam[i] = den;
+    if (!fr_is_zero(den)) fr_mul(prefix, prefix, den);
+  }
+  fr inv; fr_inv(inv, prefix);            // inv = 1 / prod_{k nz} den_k
+  for (int i = (int)t - 1; i >= 0; --i) {
+    fr den = lam[i];
+    fr out;
+    if (fr_is_zero(den)) {
+      out = fr_zero();
+    } else {
+      fr pre = fr_one();                  // prod_{k<i, nz} den_k (recomputed; t is small)
+      for (int k = 0; k < i; ++k) { fr dk = lam[k]; if (!fr_is_zero(dk)) fr_mul(pre, pre, dk); }
+      fr dinv; fr_mul(dinv, pre, inv);    // inv = 1/prod_{k<=i,nz} den_k  ->  pre*inv = 1/den_i
+      fr_mul(inv, inv, den);
+      fr xi; fr_from_u64(xi, x[i]);
+      fr num = fr_one();
+      for (uint32_t k = 0; k < t; ++k) {
+        if ((int)k == i) continue;
+        fr xk; fr_from_u64(xk, x[k]);
+        fr_mul(num, num, xk);
+      }
+      fr_mul(out, num, dinv);
+    }
+    fr c; fr_from_mont(c, out);
+    lam[i] = c;
+  }
+}
+
+}  // namespace ssb

@@ -22,8 +22,7 @@
 #include <map>
 #include <mutex>
 
-#include "ssb_pairing.h"
-#include "ssb_h2c.h"
+#include "ssb_units.h"
 #include "../../include/ssbls.h"
 
 using namespace ssb;
@@ -32,16 +31,6 @@ namespace {
 
 struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
 
-enum : uint32_t { FLAG_CANDIDATE = 1u << 16 };
-
-__device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
-  // splitmix64(seed ^ golden*i), forced non-zero
-  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (i + 1));
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return z ? z : 1ull;
-}
 
 // ------------------------------------------------------------------------------------------
 // kernels
@@ -75,21 +64,14 @@ __global__ void __launch_bounds__(64) k_decode(int n, const uint8_t* __restrict_
                                                uint32_t* __restrict__ flags) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
-  uint8_t b[96];
+  uint8_t b[96], c[48];
   for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
-  g2_aff sig;
-  uint32_t st = g2_decompress(sig, b);
-  if ((st & DEC_OK) && group_check && g2_in_subgroup(sig)) st |= DEC_IN_GROUP;
+  if (pk48) for (int k = 0; k < 48; ++k) c[k] = pk48[48 * (size_t)s + k];
+  g2_aff sig; g1_aff pk;
+  const uint32_t fl = unit_decode(sig, pk, b, pk48 ? c : nullptr, group_check);
   sig_aff[s] = sig;
-  uint32_t pst = 0;
-  if (pk48) {
-    for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
-    g1_aff pk;
-    pst = g1_decompress(pk, b);
-    pk_aff[s] = pk;
-  }
-  const bool cand = (st & DEC_OK) && !(st & DEC_INF) && (st & DEC_IN_GROUP) && (pst & DEC_OK) && !(pst & DEC_INF);
-  flags[s] = st | (pst << 8) | (cand ? FLAG_CANDIDATE : 0u);
+  if (pk48) pk_aff[s] = pk;
+  flags[s] = fl;
 }
 
 __global__ void __launch_bounds__(64) k_rlc_mul(int n, uint64_t seed, const uint32_t* __restrict__ flags,
@@ -99,10 +81,7 @@ __global__ void __launch_bounds__(64) k_rlc_mul(int n, uint64_t seed, const uint
   if (s >= n) return;
   g2_jac a; g1_jac b;
   if (flags[s] & FLAG_CANDIDATE) {
-    const uint64_t r = rlc_scalar(seed, (uint64_t)s);
-    const uint32_t k[2] = {(uint32_t)r, (uint32_t)(r >> 32)};
-    jac_mul_aff(a, sig_aff[s], k, 2);
-    jac_mul_aff(b, pk_aff[s], k, 2);
+    unit_rlc(a, b, sig_aff[s], pk_aff[s], rlc_scalar(seed, (uint64_t)s));
   } else {
     jac_set_inf(a); jac_set_inf(b);
   }
@@ -170,7 +149,7 @@ __global__ void __launch_bounds__(64) k_miller(int n_roots, const g1_aff* __rest
   if (p < n_roots) {
     miller_loop(r, root_sum[p], H[p]);
   } else {
-    g1_aff ng; ng.x = fp_from_c(G1_GEN_X); ng.y = fp_from_c(G1_GEN_NEG_Y); ng.inf = 0;
+    g1_aff ng = g1_neg_generator();
     miller_loop(r, ng, *sig_sum);
   }
   f[p] = r;
@@ -205,14 +184,7 @@ __global__ void __launch_bounds__(64) k_fallback_verify(int n, const uint32_t* _
   if (s >= n) return;
   const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
   if (*ok || !cand) { verdict[s] = cand ? 1 : 0; return; }
-  fp12 f1, f2;
-  miller_loop(f1, pk_aff[s], H[share_root[s]]);
-  g1_aff ng; ng.x = fp_from_c(G1_GEN_X); ng.y = fp_from_c(G1_GEN_NEG_Y); ng.inf = 0;
-  miller_loop(f2, ng, sig_aff[s]);
-  fp12_mul(f1, f1, f2);
-  fp12 e;
-  final_exponentiation(e, f1);
-  verdict[s] = fp12_is_one(e) ? 1 : 0;
+  verdict[s] = unit_verify_one(pk_aff[s], sig_aff[s], H[share_root[s]]) ? 1 : 0;
 }
 
 // Reference scan (src/crypto/generic_threshold.rs:133-172) on the batch verdicts.
@@ -265,45 +237,9 @@ __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const u
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs || status[j] != SSB_DVF_OK) return;
   const uint32_t b = off[j], t = tt[j];
-  // pass 1: den_i (into lam slots), running prefix product of the non-zero ones
-  fr prefix = fr_one();
-  for (uint32_t i = 0; i < t; ++i) {
-    fr xi; fr_from_u64(xi, ids[sel[b + i]]);
-    fr den = fr_one();
-    for (uint32_t k = 0; k < t; ++k) {
-      if (k == i) continue;
-      fr xk, d; fr_from_u64(xk, ids[sel[b + k]]);
-      fr_sub(d, xk, xi);
-      fr_mul(den, den, d);
-    }
-    lam[b + i] = den;
-    if (!fr_is_zero(den)) fr_mul(prefix, prefix, den);
-  }
-  fr inv; fr_inv(inv, prefix);
-  // pass 2 (backwards): den_i^{-1}, then times num_i
-  for (int i = (int)t - 1; i >= 0; --i) {
-    fr den = lam[b + i];
-    fr out;
-    if (fr_is_zero(den)) {
-      out = fr_zero();
-    } else {
-      // pre = prod_{k<i, nz} den_k (recomputed; t is small)
-      fr pre = fr_one();
-      for (int k = 0; k < i; ++k) { fr dk = lam[b + k]; if (!fr_is_zero(dk)) fr_mul(pre, pre, dk); }
-      fr dinv; fr_mul(dinv, pre, inv);   // inv = 1/prod_{k<=i,nz} den_k, so pre*inv = 1/den_i
-      fr_mul(inv, inv, den);             // drop den_i from the running inverse
-      fr xi; fr_from_u64(xi, ids[sel[b + i]]);
-      fr num = fr_one();
-      for (uint32_t k = 0; k < t; ++k) {
-        if ((int)k == i) continue;
-        fr xk; fr_from_u64(xk, ids[sel[b + k]]);
-        fr_mul(num, num, xk);
-      }
-      fr_mul(out, num, dinv);
-    }
-    fr c; fr_from_mont(c, out);
-    lam[b + i] = c;  // canonical (blst_scalar little-endian limbs)
-  }
+  uint64_t x[SSB_MAX_T];
+  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
+  unit_lagrange(lam + b, x, t);
 }
 
 __global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
@@ -318,7 +254,7 @@ __global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __r
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
   const fr l = lam[s];
   g2_jac r;
-  jac_mul_w4(r, sig_aff[sel[s]], l.l, 8);  // blst_p2_mult(.., 255 bits)
+  unit_combine_term(r, sig_aff[sel[s]], l.l);  // blst_p2_mult(.., 255 bits)
   term[s] = r;
 }
 
@@ -329,10 +265,7 @@ __global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* 
   if (j >= n_jobs) return;
   uint8_t o[96];
   if (status[j] == SSB_DVF_OK) {
-    g2_jac acc; jac_set_inf(acc);  // infinity(t) start (src/crypto/impls/blst.rs:74)
-    for (uint32_t k = 0; k < tt[j]; ++k) jac_add(acc, acc, term[off[j] + k]);
-    g2_aff a; jac_to_aff(a, acc);
-    g2_compress(o, a);
+    unit_combine_sum(o, term + off[j], tt[j]);  // infinity(t) start (src/crypto/impls/blst.rs:74)
   } else {
     for (int k = 0; k < 96; ++k) o[k] = 0;
   }
@@ -404,7 +337,10 @@ struct ssb_ctx {
   void* io = nullptr;
   size_t io_bytes = 0;
   struct evpair { hipEvent_t a = nullptr, b = nullptr; bool used = false; };
-  std::map<std::string, evpair> timers;
+  std::map<std::string, evpair> timers;               // last launch of each kernel
+  bool accumulate = false;                             // ssb_kernel_timing(ctx, 1)
+  std::map<std::string, std::vector<evpair>> history;  // every launch while accumulating
+  std::vector<evpair> pool;
 };
 
 namespace {
@@ -445,14 +381,22 @@ int ensure_io(ssb_ctx* ctx, size_t bytes) {
 
 inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
+// hipEvent pair around one kernel launch on the engine's stream (the stream the kernel runs on)
 struct timed {
-  ssb_ctx* ctx; ssb_ctx::evpair* ev;
-  timed(ssb_ctx* c, const char* name) : ctx(c) {
-    ev = &ctx->timers[name];
-    if (!ev->a) { hipEventCreate(&ev->a); hipEventCreate(&ev->b); }
-    hipEventRecord(ev->a, ctx->stream);
+  ssb_ctx* ctx; ssb_ctx::evpair p; std::string name;
+  timed(ssb_ctx* c, const char* nm) : ctx(c), name(nm) {
+    if (!ctx->pool.empty()) { p = ctx->pool.back(); ctx->pool.pop_back(); }
+    else { hipEventCreate(&p.a); hipEventCreate(&p.b); }
+    hipEventRecord(p.a, ctx->stream);
   }
-  ~timed() { hipEventRecord(ev->b, ctx->stream); ev->used = true; }
+  ~timed() {
+    hipEventRecord(p.b, ctx->stream);
+    p.used = true;
+    if (ctx->accumulate) { ctx->history[name].push_back(p); return; }
+    auto it = ctx->timers.find(name);
+    if (it != ctx->timers.end() && it->second.a) ctx->pool.push_back(it->second);
+    ctx->timers[name] = p;
+  }
 };
 
 int fill_dst(ssb_ctx* ctx, dst_arg& d, const uint8_t* dst, size_t dst_len) {
@@ -530,6 +474,8 @@ void ssb_destroy(ssb_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->timers) { if (kv.second.a) hipEventDestroy(kv.second.a); if (kv.second.b) hipEventDestroy(kv.second.b); }
+  for (auto& kv : ctx->history) for (auto& p : kv.second) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
+  for (auto& p : ctx->pool) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->io) hipFree(ctx->io);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -545,6 +491,29 @@ int ssb_last_kernel_ms(const ssb_ctx* ctx_c, const char* name, float* ms) {
   if (it == ctx->timers.end() || !it->second.used) { ctx->err = "no timing for kernel"; return SSB_EINVAL; }
   SSB_HIP(hipEventSynchronize(it->second.b));
   SSB_HIP(hipEventElapsedTime(ms, it->second.a, it->second.b));
+  return SSB_OK;
+}
+
+int ssb_kernel_timing(ssb_ctx* ctx, int on) {
+  if (!ctx) return SSB_EINVAL;
+  SSB_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto& kv : ctx->history) for (auto& p : kv.second) ctx->pool.push_back(p);
+  ctx->history.clear();
+  ctx->accumulate = on != 0;
+  return SSB_OK;
+}
+
+int ssb_kernel_time(ssb_ctx* ctx, const char* name, float* total_ms, int* launches) {
+  if (!ctx || !name || !total_ms || !launches) return SSB_EINVAL;
+  *total_ms = 0.f; *launches = 0;
+  auto it = ctx->history.find(name);
+  if (it == ctx->history.end()) return SSB_OK;
+  for (auto& p : it->second) {
+    float ms = 0.f;
+    SSB_HIP(hipEventSynchronize(p.b));
+    SSB_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    *total_ms += ms; *launches += 1;
+  }
   return SSB_OK;
 }
 

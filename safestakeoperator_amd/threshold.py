@@ -144,6 +144,16 @@ class Engine:
         self._check(self._lib.ssb_last_kernel_ms(self._h, name.encode(), ctypes.byref(ms)), "ssb_last_kernel_ms")
         return float(ms.value)
 
+    def kernel_timing(self, on: bool):
+        self._check(self._lib.ssb_kernel_timing(self._h, 1 if on else 0), "ssb_kernel_timing")
+
+    def kernel_time(self, name: str):
+        """(total ms, launches) accumulated since kernel_timing(True)."""
+        ms, n = ctypes.c_float(), ctypes.c_int()
+        self._check(self._lib.ssb_kernel_time(self._h, name.encode(), ctypes.byref(ms), ctypes.byref(n)),
+                    "ssb_kernel_time")
+        return float(ms.value), int(n.value)
+
     # --- primitives -------------------------------------------------------------------------
     def hash_to_g2(self, msgs: Sequence[bytes], dst: bytes = DST) -> List[bytes]:
         n = len(msgs)

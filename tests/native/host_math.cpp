@@ -7,8 +7,7 @@
 #include <vector>
 #include <iostream>
 #include <sstream>
-#include "../../safestakeoperator_amd/csrc/ssb_pairing.h"
-#include "../../safestakeoperator_amd/csrc/ssb_h2c.h"
+#include "../../safestakeoperator_amd/csrc/ssb_units.h"
 
 #ifdef SSB_OPCOUNT
 ssb_opcounts g_ssb_counts;
@@ -81,11 +80,58 @@ int main() {
       g2_aff a1, a2; jac_to_aff(a1, r1); jac_to_aff(a2, r2);
       uint8_t o1[96], o2[96]; g2_compress(o1, a1); g2_compress(o2, a2);
       printf("%s %s\n", hex(o1, 96).c_str(), hex(o2, 96).c_str());
-    } else if (cmd == "opcount") {  // opcount <what>
+    } else if (cmd == "opcount") {  // opcount pk48 sig96 msg32 -> JSON of per-unit op counts
 #ifdef SSB_OPCOUNT
-      std::string what; is >> what;
+      std::string a, b, c; is >> a >> b >> c;
+      auto pkb = unhex(a), sb = unhex(b), mb = unhex(c);
+      std::string js = "{";
+      auto rec = [&](const char* name, double reps) {
+        char tmp[256];
+        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"fp_mul\": %.1f, \"fp_sqr\": %.1f, \"fr_mul\": %.1f}",
+                 js.size() > 1 ? ", " : "", name, g_ssb_counts.fp_mul / reps, g_ssb_counts.fp_sqr / reps,
+                 g_ssb_counts.fr_mul / reps);
+        js += tmp;
+        g_ssb_counts = {};
+      };
+      g2_aff sig, H; g1_aff pk;
       g_ssb_counts = {};
-      printf("n/a\n");
+      const int NR = 4;
+      for (int i = 0; i < NR; ++i) { uint8_t m[32]; for (int k = 0; k < 32; ++k) m[k] = mb[k] ^ (uint8_t)i; hash_to_g2(H, m, (const uint8_t*)DST, (int)strlen(DST)); }
+      rec("hash_to_g2", NR);
+      hash_to_g2(H, mb.data(), (const uint8_t*)DST, (int)strlen(DST));
+      g_ssb_counts = {};
+      uint32_t fl = unit_decode(sig, pk, sb.data(), pkb.data(), 1);
+      rec("decode", 1);
+      if (!(fl & FLAG_CANDIDATE)) { printf("ERR not a candidate\n"); fflush(stdout); continue; }
+      const int NS = 16;
+      g2_jac rs; g1_jac rp;
+      for (int i = 0; i < NS; ++i) unit_rlc(rs, rp, sig, pk, rlc_scalar(0x5AFE57A4Eull, (uint64_t)i));
+      rec("rlc", NS);
+      g1_jac acc1; jac_set_inf(acc1); jac_add(acc1, acc1, rp); g_ssb_counts = {};
+      for (int i = 0; i < NS; ++i) jac_add(acc1, acc1, rp);
+      rec("sum_g1_add", NS);
+      g2_jac acc2; jac_set_inf(acc2); jac_add(acc2, acc2, rs); jac_dbl(acc2, acc2); g_ssb_counts = {};
+      for (int i = 0; i < NS; ++i) jac_add(acc2, acc2, rs);
+      rec("sum_g2_add", NS);
+      { g1_aff a1; jac_to_aff(a1, acc1); } rec("to_affine_g1", 1);
+      { g2_aff a2; jac_to_aff(a2, acc2); } rec("to_affine_g2", 1);
+      fp12 f; miller_loop(f, pk, H); rec("miller_pair", 1);
+      fp12 f2; fp12_mul(f2, f, f); rec("fp12_mul", 1);
+      fp12 e; final_exponentiation(e, f2); rec("final_exp", 1);
+      bool ok = unit_verify_one(pk, sig, H); rec("verify_one", 1);
+      const uint64_t ids3[3] = {1, 2, 3}, ids5[5] = {1, 2, 3, 4, 5}, ids10[10] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10};
+      fr lam[10];
+      unit_lagrange(lam, ids3, 3); rec("lagrange_t3", 1);
+      unit_lagrange(lam, ids5, 5); rec("lagrange_t5", 1);
+      unit_lagrange(lam, ids10, 10); rec("lagrange_t10", 1);
+      g2_jac terms[10];
+      for (int i = 0; i < NS; ++i) { uint32_t l8[8]; for (int k = 0; k < 8; ++k) l8[k] = (uint32_t)rlc_scalar(77, 8 * i + k); l8[7] &= 0x73eda752u; unit_combine_term(terms[i % 10], sig, l8); }
+      rec("combine_term", NS);
+      uint8_t o96[96];
+      unit_combine_sum(o96, terms, 3); rec("combine_sum_t3", 1);
+      unit_combine_sum(o96, terms, 10); rec("combine_sum_t10", 1);
+      js += ok ? ", \"verify_ok\": true}" : ", \"verify_ok\": false}";
+      printf("%s\n", js.c_str());
 #else
       printf("disabled\n");
 #endif

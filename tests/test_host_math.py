@@ -1,0 +1,77 @@
+"""CPU: the device math headers compiled for the host (test-only build, never shipped) against
+the oracle's golden fixtures; and the committed op counts match the current device code."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "native"))
+import make_opcount  # noqa: E402
+
+GOLD = os.path.join(HERE, "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def host_exe():
+    return make_opcount.build_host(False)
+
+
+def _run(exe, lines):
+    r = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True, check=True)
+    return r.stdout.strip().split("\n")
+
+
+def test_hash_to_g2(host_exe):
+    hc = _load("hash_to_g2.json")["cases"]
+    out = _run(host_exe, ["h2g2 " + c["msg"] for c in hc])
+    assert out == [c["out192"] for c in hc]
+    v = _load("known_answers.json")["rfc9380_g2"][0]
+    o = _run(host_exe, ["h2g2 " + bytes(32).hex() + " " + v["dst"].encode().hex()])  # sanity: runs with custom DST
+    assert len(o[0]) == 384
+
+
+def test_point_decoding(host_exe):
+    pts = _load("points.json")
+    out = _run(host_exe, ["g2dec " + p["compressed"] for p in pts["g2"]] + ["g1dec " + p["compressed"] for p in pts["g1"]])
+    for p, line in zip(pts["g2"], out):
+        st, sub, unc, cmp_ = line.split()
+        assert int(st) & 1 and sub == "1" and unc == p["uncompressed"] and cmp_ == p["compressed"]
+    for p, line in zip(pts["g1"], out[len(pts["g2"]):]):
+        st, cmp_, x, y = line.split()
+        assert int(st) & 1 and cmp_ == p["compressed"]
+        if p["x"] is not None:
+            assert x == p["x"] and y == p["y"]
+
+
+def test_share_decoding_and_verify(host_exe):
+    cases = _load("threshold_cases.json")["cases"]
+    lines = []
+    for c in cases[:6]:
+        for s, p in zip(c["sigs"], c["pks"]):
+            lines.append("verify %s %s %s" % (p, s, c["root"]))
+    out = _run(host_exe, lines)
+    want = [v for c in cases[:6] for v in c["share_verdicts"]]
+    assert [o == "1" for o in out] == want
+
+
+def test_bad_encodings_rejected(host_exe):
+    c = [x for x in _load("threshold_cases.json")["cases"] if x["name"] == "bad_encoding_shares"][0]
+    out = _run(host_exe, ["g2dec " + s for s in c["sigs"][:3]])
+    assert all(line.split()[0] == "0" for line in out)
+    c = [x for x in _load("threshold_cases.json")["cases"] if x["name"] == "non_subgroup_share"][0]
+    st, sub = _run(host_exe, ["g2dec " + c["sigs"][0]])[0].split()[:2]
+    assert st == "1" and sub == "0"
+
+
+def test_opcount_is_current():
+    with open(make_opcount.OUT) as f:
+        committed = json.load(f)
+    assert make_opcount.measure() == committed

@@ -1,0 +1,102 @@
+"""CPU: the oracle against published known answers and the reference's relational tests."""
+import hashlib
+import json
+import os
+
+import pytest
+
+from oracle import bls12_381 as B
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def test_curve_constants():
+    assert B.g1_on_curve(B.G1_GEN) and B.g2_on_curve(B.G2_GEN)
+    assert B.g1_mul(B.G1_GEN, B.R) is None and B.g2_mul(B.G2_GEN, B.R) is None
+    ka = _load("known_answers.json")
+    assert B.g1_compress(B.G1_GEN).hex() == ka["generators"]["g1"]
+    assert B.g2_compress(B.G2_GEN).hex() == ka["generators"]["g2"]
+    assert len(bytes.fromhex(ka["infinity_signature"])) == 96
+    assert B.g2_compress(None).hex() == ka["infinity_signature"]
+
+
+def test_rfc9380_hash_to_g2_vector():
+    v = _load("known_answers.json")["rfc9380_g2"][0]
+    dst = v["dst"].encode()
+    u = B.hash_to_field_fp2(v["msg"].encode(), dst)
+    assert ["%096x" % u[0][0], "%096x" % u[0][1]] == v["u0"]
+    P = B.hash_to_g2(v["msg"].encode(), dst)
+    assert ["%096x" % P[0][0], "%096x" % P[0][1]] == v["P_x"]
+    assert ["%096x" % P[1][0], "%096x" % P[1][1]] == v["P_y"]
+
+
+def test_isogeny_maps_onto_e2():
+    for i in range(3):
+        u = (hashlib.sha256(b"u%d" % i).digest(), hashlib.sha256(b"v%d" % i).digest())
+        u = (int.from_bytes(u[0], "big") % B.P, int.from_bytes(u[1], "big") % B.P)
+        assert B.g2_on_curve(B.iso3_map(B.map_to_curve_sswu_e2p(u)))
+
+
+def test_eth_sign_and_interop_vectors():
+    ka = _load("known_answers.json")
+    v = ka["eth_sign"][0]
+    sk = int(v["privkey"], 16)
+    assert B.g1_compress(B.sk_to_pk(sk)).hex() == v["pubkey"]
+    assert B.g2_compress(B.sign(sk, bytes.fromhex(v["message"]))).hex() == v["signature"]
+    iv = ka["eth_interop"][0]
+    sk0 = int.from_bytes(hashlib.sha256((0).to_bytes(32, "little")).digest(), "little") % B.R
+    assert "%064x" % sk0 == iv["privkey"]
+    assert B.g1_compress(B.sk_to_pk(sk0)).hex() == iv["pubkey"]
+
+
+def test_subgroup_check_and_cofactor():
+    x = (5, 7)
+    while True:
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(x), x), B.B2))
+        if y is not None:
+            break
+        x = (x[0] + 1, x[1])
+    pt = (x, y)
+    assert not B.g2_in_subgroup(pt) and not B.g2_in_subgroup_slow(pt)
+    c = B.clear_cofactor_g2(pt)
+    assert c == B.g2_mul(pt, B.H_EFF_G2)
+    assert B.g2_in_subgroup(c) and B.g2_in_subgroup_slow(c)
+
+
+def test_lagrange_fixtures():
+    for c in _load("lagrange.json"):
+        ids = [int(x) for x in c["ids"]]
+        assert [x.to_bytes(32, "little").hex() for x in B.lagrange_coeffs(ids)] == c["lambdas_le"]
+
+
+def test_threshold_fixture_semantics():
+    """The reference's selection/error semantics on the committed verdicts, and its relational
+    property (tests/test_generic_threshold.rs:30-35): combine == master signature."""
+    for c in _load("threshold_cases.json")["cases"]:
+        vm = c["share_verdicts"]
+        st, pl = B.threshold_aggregate(c["t"], [bytes.fromhex(s) for s in c["sigs"]],
+                                       [bytes.fromhex(p) for p in c["pks"]], c["ids"],
+                                       bytes.fromhex(c["root"]), verify_fn=lambda i, vm=vm: vm[i])
+        assert st == c["expected_status"], c["name"]
+        if st == 0:
+            assert pl.hex() == c["expected_sig"] == c["master_sig"]
+        else:
+            assert list(pl) == c["expected_payload"]
+
+
+def test_verify_one_fixture_share():
+    c = _load("threshold_cases.json")["cases"][4]  # first_share_wrong_root
+    root = bytes.fromhex(c["root"])
+    assert B.verify(bytes.fromhex(c["pks"][1]), bytes.fromhex(c["sigs"][1]), root) is True
+    assert B.verify(bytes.fromhex(c["pks"][0]), bytes.fromhex(c["sigs"][0]), root) is False
+
+
+def test_decode_rejections():
+    assert pytest.raises(B.DecodeError, B.g2_decompress, bytes(96))           # no compression flag
+    assert pytest.raises(B.DecodeError, B.g2_decompress, bytes([0xE0]) + bytes(95))  # infinity + sign
+    assert B.g2_decompress(bytes([0xC0]) + bytes(95)) is None
