@@ -76,8 +76,8 @@ SSB_INL void mp_sub_mod(uint32_t* r, const uint32_t* a, const uint32_t* b, const
 // The outer loop is kept rolled (b is rotated so every access is a static register index):
 // the unrolled 12x12 body inlined at every call site made kernels ~12x larger.
 template <int N>
-SSB_INL void mp_mont_mul(uint32_t* r, const uint32_t* a, const uint32_t* b_in, const uint32_t* m,
-                         uint32_t minv) {
+SSB_INL void mp_mont_mul_cios(uint32_t* r, const uint32_t* a, const uint32_t* b_in, const uint32_t* m,
+                              uint32_t minv) {
   uint32_t t[N], b[N];
   uint32_t tN = 0;
 #pragma unroll
@@ -116,6 +116,258 @@ SSB_INL void mp_mont_mul(uint32_t* r, const uint32_t* a, const uint32_t* b_in, c
   const bool keep = (br != 0) && (tN == 0);
 #pragma unroll
   for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// (acc, top) += x * y : one v_mad_u64_u32 with its carry-out captured by v_addc into `top`.
+#define SSB_MAC(acc, top, x, y)                                                        \
+  do {                                                                                 \
+    uint64_t c_;                                                                       \
+    asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32_e64 %2, %1, 0, %2, %1"      \
+        : "+v"(acc), "=&s"(c_), "+v"(top) : "v"(x), "v"(y));                           \
+  } while (0)
+#define SSB_MACS(acc, top, x, y)                                                       \
+  do {                                                                                 \
+    uint64_t c_;                                                                       \
+    asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32_e64 %2, %1, 0, %2, %1"      \
+        : "+v"(acc), "=&s"(c_), "+v"(top) : "v"(x), "s"(y));                           \
+  } while (0)
+// four MACs into the same accumulator in ONE asm statement (one hipcc boundary pad per 4)
+#define SSB_MAC_STEP(X, Y) "v_mad_u64_u32 %0, %1, " X ", " Y ", %0\n\tv_addc_co_u32_e64 %2, %1, 0, %2, %1\n\t"
+#define SSB_MAC4(CX, CY, acc, top, x0, y0, x1, y1, x2, y2, x3, y3)                     \
+  do {                                                                                 \
+    uint64_t c_;                                                                       \
+    asm(SSB_MAC_STEP("%3", "%4") SSB_MAC_STEP("%5", "%6") SSB_MAC_STEP("%7", "%8")      \
+        SSB_MAC_STEP("%9", "%10")                                                      \
+        : "+v"(acc), "=&s"(c_), "+v"(top)                                              \
+        : CX(x0), CY(y0), CX(x1), CY(y1), CX(x2), CY(y2), CX(x3), CY(y3));             \
+  } while (0)
+#define SSB_MAC2(CX, CY, acc, top, x0, y0, x1, y1)                                     \
+  do {                                                                                 \
+    uint64_t c_;                                                                       \
+    asm(SSB_MAC_STEP("%3", "%4") SSB_MAC_STEP("%5", "%6")                              \
+        : "+v"(acc), "=&s"(c_), "+v"(top) : CX(x0), CY(y0), CX(x1), CY(y1));           \
+  } while (0)
+// two independent accumulator chains interleaved instruction by instruction (ILP 2 in one wave)
+#define SSB_MAC2X2(CX, CY, a0, t0, a1, t1, x0, y0, x1, y1, x2, y2, x3, y3)               \
+  do {                                                                                 \
+    uint64_t c0_, c1_;                                                                 \
+    asm("v_mad_u64_u32 %0, %2, %6, %7, %0\n\tv_mad_u64_u32 %3, %5, %8, %9, %3\n\t"      \
+        "v_addc_co_u32_e64 %1, %2, 0, %1, %2\n\tv_addc_co_u32_e64 %4, %5, 0, %4, %5\n\t"  \
+        "v_mad_u64_u32 %0, %2, %10, %11, %0\n\tv_mad_u64_u32 %3, %5, %12, %13, %3\n\t"    \
+        "v_addc_co_u32_e64 %1, %2, 0, %1, %2\n\tv_addc_co_u32_e64 %4, %5, 0, %4, %5"       \
+        : "+v"(a0), "+v"(t0), "=&s"(c0_), "+v"(a1), "+v"(t1), "=&s"(c1_)                 \
+        : CX(x0), CY(y0), CX(x1), CY(y1), CX(x2), CY(y2), CX(x3), CY(y3));             \
+  } while (0)
+#define SSB_V(x) "v"(x)
+#define SSB_S(x) "s"(x)
+#else
+#define SSB_MAC(acc, top, x, y)                                                        \
+  do {                                                                                 \
+    unsigned __int128 s_ = (unsigned __int128)(uint64_t)(x) * (uint32_t)(y) + (acc);   \
+    acc = (uint64_t)s_; top += (uint32_t)(s_ >> 64);                                   \
+  } while (0)
+#define SSB_MACS SSB_MAC
+#define SSB_MAC4(CX, CY, acc, top, x0, y0, x1, y1, x2, y2, x3, y3)                     \
+  do { SSB_MAC(acc, top, x0, y0); SSB_MAC(acc, top, x1, y1);                           \
+       SSB_MAC(acc, top, x2, y2); SSB_MAC(acc, top, x3, y3); } while (0)
+#define SSB_MAC2(CX, CY, acc, top, x0, y0, x1, y1)                                     \
+  do { SSB_MAC(acc, top, x0, y0); SSB_MAC(acc, top, x1, y1); } while (0)
+#define SSB_MAC2X2(CX, CY, a0, t0, a1, t1, x0, y0, x1, y1, x2, y2, x3, y3)               \
+  do { SSB_MAC(a0, t0, x0, y0); SSB_MAC(a1, t1, x1, y1);                               \
+       SSB_MAC(a0, t0, x2, y2); SSB_MAC(a1, t1, x3, y3); } while (0)
+#endif
+
+// Montgomery product by product scanning (FIPS): column k accumulates every a_j*b_{k-j} and
+// m_j*p_{k-j} into a 96-bit (acc, top) accumulator -- one v_mad_u64_u32 + one v_addc per
+// limb product -- then either fixes m_k (k < N) or emits r_{k-N}.  Fully unrolled.
+// Inputs < m < 2^(32N-2); output fully reduced.
+template <int N>
+SSB_INL void mp_mont_mul_fips(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* mod,
+                              uint32_t minv) {
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+  uint32_t top = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; ++k) {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (k - j >= 0 && k - j < N) SSB_MAC(acc, top, a[j], b[k - j]);
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < k && k - j < N) SSB_MACS(acc, top, m[j], mod[k - j]);
+    if (k < N) {
+      m[k] = (uint32_t)acc * minv;
+      SSB_MACS(acc, top, m[k], mod[0]);  // low word becomes 0
+    } else {
+      t[k - N] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  t[N - 1] = (uint32_t)acc;  // acc < 2^32 here since the result < 2m < 2^(32N)
+  uint32_t s2[N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s2[i] = subb(t[i], mod[i], br, br);
+  const bool keep = br != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
+}
+
+// Same product, two interleaved accumulators per column (even / odd j): consecutive MACs touch
+// different registers, which removes hipcc's post-asm wait-state pad and doubles the ILP.
+template <int N>
+SSB_INL void mp_mont_mul_fips2(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* mod,
+                               uint32_t minv) {
+  uint32_t m[N], t[N];
+  uint64_t acc0 = 0, acc1 = 0;
+  uint32_t top0 = 0, top1 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; ++k) {
+    int q = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (k - j >= 0 && k - j < N) {
+        if (q++ & 1) SSB_MAC(acc1, top1, a[j], b[k - j]); else SSB_MAC(acc0, top0, a[j], b[k - j]);
+      }
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < k && k - j < N) {
+        if (q++ & 1) SSB_MACS(acc1, top1, m[j], mod[k - j]); else SSB_MACS(acc0, top0, m[j], mod[k - j]);
+      }
+    // merge: (acc0, top0) += (acc1, top1)
+    {
+      uint32_t lo = (uint32_t)acc0, hi = (uint32_t)(acc0 >> 32), c;
+      lo = addc(lo, (uint32_t)acc1, 0u, c);
+      hi = addc(hi, (uint32_t)(acc1 >> 32), c, c);
+      top0 = top0 + top1 + c;
+      acc0 = ((uint64_t)hi << 32) | lo;
+      acc1 = 0; top1 = 0;
+    }
+    if (k < N) {
+      m[k] = (uint32_t)acc0 * minv;
+      SSB_MACS(acc0, top0, m[k], mod[0]);  // low word becomes 0
+    } else {
+      t[k - N] = (uint32_t)acc0;
+    }
+    acc0 = (acc0 >> 32) | ((uint64_t)top0 << 32);
+    top0 = 0;
+  }
+  t[N - 1] = (uint32_t)acc0;
+  uint32_t s2[N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s2[i] = subb(t[i], mod[i], br, br);
+  const bool keep = br != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
+}
+
+// FIPS with the column MACs issued four per asm statement.
+template <int N>
+SSB_INL void mp_mont_mul_fips4(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* mod,
+                               uint32_t minv) {
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+  uint32_t top = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; ++k) {
+    const int jlo = k - (N - 1) > 0 ? k - (N - 1) : 0;
+    const int jhi = k < N - 1 ? k : N - 1;  // a_j b_{k-j}, j in [jlo, jhi]
+#pragma unroll
+    for (int j = jlo; j <= jhi; j += 4) {
+      const int left = jhi - j + 1;
+      if (left >= 4) SSB_MAC4(SSB_V, SSB_V, acc, top, a[j], b[k - j], a[j + 1], b[k - j - 1], a[j + 2], b[k - j - 2], a[j + 3], b[k - j - 3]);
+      else if (left >= 2) { SSB_MAC2(SSB_V, SSB_V, acc, top, a[j], b[k - j], a[j + 1], b[k - j - 1]); if (left == 3) SSB_MAC(acc, top, a[j + 2], b[k - j - 2]); }
+      else SSB_MAC(acc, top, a[j], b[k - j]);
+    }
+    const int mhi = k - 1 < N - 1 ? k - 1 : N - 1;  // m_j p_{k-j}, j in [jlo, min(k-1, N-1)]
+#pragma unroll
+    for (int j = jlo; j <= mhi; j += 4) {
+      const int left = mhi - j + 1;
+      if (left >= 4) SSB_MAC4(SSB_V, SSB_S, acc, top, m[j], mod[k - j], m[j + 1], mod[k - j - 1], m[j + 2], mod[k - j - 2], m[j + 3], mod[k - j - 3]);
+      else if (left >= 2) { SSB_MAC2(SSB_V, SSB_S, acc, top, m[j], mod[k - j], m[j + 1], mod[k - j - 1]); if (left == 3) SSB_MACS(acc, top, m[j + 2], mod[k - j - 2]); }
+      else SSB_MACS(acc, top, m[j], mod[k - j]);
+    }
+    if (k < N) {
+      m[k] = (uint32_t)acc * minv;
+      SSB_MACS(acc, top, m[k], mod[0]);  // low word becomes 0
+    } else {
+      t[k - N] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  t[N - 1] = (uint32_t)acc;
+  uint32_t s2[N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s2[i] = subb(t[i], mod[i], br, br);
+  const bool keep = br != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
+}
+
+// FIPS, two accumulators interleaved inside each asm chunk (halves the dependent chain).
+template <int N>
+SSB_INL void mp_mont_mul_fips4x2(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* mod,
+                                 uint32_t minv) {
+  uint32_t m[N], t[N];
+  uint64_t acc = 0, acc1 = 0;
+  uint32_t top = 0, top1 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; ++k) {
+    const int jlo = k - (N - 1) > 0 ? k - (N - 1) : 0;
+    const int jhi = k < N - 1 ? k : N - 1;
+#pragma unroll
+    for (int j = jlo; j <= jhi; j += 4) {
+      const int left = jhi - j + 1;
+      if (left >= 4) SSB_MAC2X2(SSB_V, SSB_V, acc, top, acc1, top1, a[j], b[k - j], a[j + 1], b[k - j - 1], a[j + 2], b[k - j - 2], a[j + 3], b[k - j - 3]);
+      else if (left >= 2) { SSB_MAC2(SSB_V, SSB_V, acc1, top1, a[j], b[k - j], a[j + 1], b[k - j - 1]); if (left == 3) SSB_MAC(acc, top, a[j + 2], b[k - j - 2]); }
+      else SSB_MAC(acc, top, a[j], b[k - j]);
+    }
+    const int mhi = k - 1 < N - 1 ? k - 1 : N - 1;
+#pragma unroll
+    for (int j = jlo; j <= mhi; j += 4) {
+      const int left = mhi - j + 1;
+      if (left >= 4) SSB_MAC2X2(SSB_V, SSB_S, acc, top, acc1, top1, m[j], mod[k - j], m[j + 1], mod[k - j - 1], m[j + 2], mod[k - j - 2], m[j + 3], mod[k - j - 3]);
+      else if (left >= 2) { SSB_MAC2(SSB_V, SSB_S, acc1, top1, m[j], mod[k - j], m[j + 1], mod[k - j - 1]); if (left == 3) SSB_MACS(acc, top, m[j + 2], mod[k - j - 2]); }
+      else SSB_MACS(acc, top, m[j], mod[k - j]);
+    }
+    {  // merge the second chain
+      uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32), c;
+      lo = addc(lo, (uint32_t)acc1, 0u, c);
+      hi = addc(hi, (uint32_t)(acc1 >> 32), c, c);
+      top = top + top1 + c;
+      acc = ((uint64_t)hi << 32) | lo;
+      acc1 = 0; top1 = 0;
+    }
+    if (k < N) {
+      m[k] = (uint32_t)acc * minv;
+      SSB_MACS(acc, top, m[k], mod[0]);
+    } else {
+      t[k - N] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  t[N - 1] = (uint32_t)acc;
+  uint32_t s2[N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s2[i] = subb(t[i], mod[i], br, br);
+  const bool keep = br != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
+}
+
+// The engine's Montgomery product: FIPS with 4-MAC asm chunks.  Measured on MI355X
+// (bench_tools/fpmul_bench.hip, profiles/r01_fpmul_variants.json): 1.66x the throughput and
+// 0.55x the single-wave latency of the CIOS form above, bit-identical results.
+template <int N>
+SSB_INL void mp_mont_mul(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* m, uint32_t minv) {
+  mp_mont_mul_fips4<N>(r, a, b, m, minv);
 }
 
 template <int N>

@@ -1,6 +1,9 @@
 // ssbls.hip -- gfx950 kernels and the C ABI (include/ssbls.h) of the threshold-BLS engine.
 //
-// Pipeline of ssb_threshold_aggregate_batch_dev (one HIP stream, no host round trip):
+// Pipeline of ssb_threshold_aggregate_batch_dev (three HIP streams, no host round trip):
+//   side[0]: k_hash_to_g2  ||  main: decode -> RLC -> sums -> (wait hash) Miller -> final exp
+//   side[1] (after decode): speculative select -> Lagrange -> combine, assuming every decodable
+//   in-group share is valid; main then runs the exact select/combine only if the batch failed.
 //   k_share_map       share -> job, share -> root                          (bookkeeping)
 //   k_hash_to_g2      H(root) once per distinct signing root               (a-3)
 //   k_decode          G2 decompress + subgroup check, G1 decompress        (a-2 steps 1/4)
@@ -188,11 +191,16 @@ __global__ void __launch_bounds__(64) k_fallback_verify(int n, const uint32_t* _
 }
 
 // Reference scan (src/crypto/generic_threshold.rs:133-172) on the batch verdicts.
+// verdict == nullptr: SPECULATIVE selection from the decode flags (every candidate assumed valid);
+// it equals the exact selection whenever the RLC batch check passes.  skip_if_ok != nullptr: the
+// exact re-selection after a failed batch, a no-op when the batch passed.
 __global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                          const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
+                         const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
                          uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
+  if (skip_if_ok && *skip_if_ok) return;
   const uint32_t b = off[j], e = off[j + 1], t = tt[j];
   const uint32_t n = e - b;
   if (n < t) { status[j] = SSB_DVF_INSUFFICIENT_SIGNATURES; err[2 * j] = n; err[2 * j + 1] = t; return; }
@@ -203,7 +211,7 @@ __global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uin
     bool dup = false;
     for (uint32_t k = 0; k < cnt; ++k) dup = dup || (ids[sel[b + k]] == id);
     if (dup) continue;
-    if (verdict[s]) {
+    if (verdict ? (verdict[s] != 0) : ((flags[s] & FLAG_CANDIDATE) != 0)) {
       sel[b + cnt] = s;
       ++cnt;
       if (cnt >= t) break;
@@ -233,9 +241,11 @@ __global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const
 // blst convention inverse(0) = 0; one Fr inversion per job (Montgomery's trick).
 __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                            const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
-                           const int32_t* __restrict__ status, fr* __restrict__ lam) {
+                           const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
+                           fr* __restrict__ lam) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs || status[j] != SSB_DVF_OK) return;
+  if (skip_if_ok && *skip_if_ok) return;
   const uint32_t b = off[j], t = tt[j];
   uint64_t x[SSB_MAX_T];
   for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
@@ -246,9 +256,10 @@ __global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __r
                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                                       const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                                       const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
-                                                      g2_jac* __restrict__ term) {
+                                                      const uint32_t* __restrict__ skip_if_ok, g2_jac* __restrict__ term) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
+  if (skip_if_ok && *skip_if_ok) return;
   const uint32_t j = share_job[s];
   const uint32_t k = (uint32_t)s - off[j];
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
@@ -260,9 +271,11 @@ __global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __r
 
 __global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
-                                                    const g2_jac* __restrict__ term, uint8_t* __restrict__ out96) {
+                                                    const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
+                                                    uint8_t* __restrict__ out96) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
+  if (skip_if_ok && *skip_if_ok) return;
   uint8_t o[96];
   if (status[j] == SSB_DVF_OK) {
     unit_combine_sum(o, term + off[j], tt[j]);  // infinity(t) start (src/crypto/impls/blst.rs:74)
@@ -328,7 +341,9 @@ __global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restr
 // ------------------------------------------------------------------------------------------
 struct ssb_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;     // main chain: decode -> RLC -> sums -> Miller -> final exp
+  hipStream_t side[2] = {nullptr, nullptr};  // [0] hash_to_G2, [1] speculative combine
+  hipEvent_t ev_in = nullptr, ev_hash = nullptr, ev_dec = nullptr, ev_comb = nullptr, ev_out = nullptr;
   std::string err;
   // workspace arena (grown on demand, never shrunk)
   void* ws = nullptr;
@@ -383,14 +398,14 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 
 // hipEvent pair around one kernel launch on the engine's stream (the stream the kernel runs on)
 struct timed {
-  ssb_ctx* ctx; ssb_ctx::evpair p; std::string name;
-  timed(ssb_ctx* c, const char* nm) : ctx(c), name(nm) {
+  ssb_ctx* ctx; ssb_ctx::evpair p; std::string name; hipStream_t st;
+  timed(ssb_ctx* c, const char* nm, hipStream_t s = nullptr) : ctx(c), name(nm), st(s ? s : c->stream) {
     if (!ctx->pool.empty()) { p = ctx->pool.back(); ctx->pool.pop_back(); }
     else { hipEventCreate(&p.a); hipEventCreate(&p.b); }
-    hipEventRecord(p.a, ctx->stream);
+    hipEventRecord(p.a, st);
   }
   ~timed() {
-    hipEventRecord(p.b, ctx->stream);
+    hipEventRecord(p.b, st);
     p.used = true;
     if (ctx->accumulate) { ctx->history[name].push_back(p); return; }
     auto it = ctx->timers.find(name);
@@ -430,19 +445,27 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   return w;
 }
 
+template <class F>
 int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
                const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t seed,
-               uint8_t* d_verdict) {
-  hipStream_t st = ctx->stream;
-  if (n_roots) { timed t(ctx, "k_hash_to_g2"); hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n_roots, 64)), dim3(64), 0, st, (int)n_roots, d_roots, dst, w.H); }
+               uint8_t* d_verdict, F on_decoded) {
+  hipStream_t st = ctx->stream, sh = ctx->side[0];
+  // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
+  SSB_HIP(hipEventRecord(ctx->ev_in, st));
+  SSB_HIP(hipStreamWaitEvent(sh, ctx->ev_in, 0));
+  if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n_roots, 64)), dim3(64), 0, sh, (int)n_roots, d_roots, dst, w.H); }
+  SSB_HIP(hipEventRecord(ctx->ev_hash, sh));
   if (n) {
     { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, 1, w.sig_aff, w.pk_aff, w.flags); }
+    SSB_HIP(hipEventRecord(ctx->ev_dec, st));
+    if (on_decoded) on_decoded();
     { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_rlc_mul, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, seed, w.flags, w.sig_aff, w.pk_aff, w.rsig, w.rpk); }
   }
   { timed t(ctx, "k_sum");
     if (n_roots) hipLaunchKernelGGL(k_sum_g1_by_root, dim3((unsigned)n_roots), dim3(SUM_THREADS), 0, st, (int)n, d_share_root, w.flags, w.rpk, w.root_sum);
     hipLaunchKernelGGL(k_sum_g2_partial, dim3(G2_PARTS), dim3(SUM_THREADS), 0, st, (int)n, w.flags, w.rsig, w.part);
     hipLaunchKernelGGL(k_sum_g2_final, dim3(1), dim3(64), 0, st, G2_PARTS, w.part, w.sig_sum); }
+  SSB_HIP(hipStreamWaitEvent(st, ctx->ev_hash, 0));
   { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller, dim3(nblk(n_roots + 1, 64)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.sig_sum, w.f); }
   { timed t(ctx, "k_final"); hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, st, (int)(n_roots + 1), w.f, w.ok); }
   if (n) { timed t(ctx, "k_fallback_verify"); hipLaunchKernelGGL(k_fallback_verify, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict); }
@@ -464,7 +487,11 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   ssb_ctx* ctx = new (std::nothrow) ssb_ctx();
   if (!ctx) return SSB_ENOMEM;
   ctx->device = device_ordinal;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return SSB_EHIP; }
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->side[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->side[1], hipStreamNonBlocking) != hipSuccess) { delete ctx; return SSB_EHIP; }
+  for (hipEvent_t* e : {&ctx->ev_in, &ctx->ev_hash, &ctx->ev_dec, &ctx->ev_comb, &ctx->ev_out})
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { delete ctx; return SSB_EHIP; }
   *out = ctx;
   return SSB_OK;
 }
@@ -478,6 +505,8 @@ void ssb_destroy(ssb_ctx* ctx) {
   for (auto& p : ctx->pool) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->io) hipFree(ctx->io);
+  for (hipStream_t sd : ctx->side) if (sd) { hipStreamSynchronize(sd); hipStreamDestroy(sd); }
+  for (hipEvent_t e : {ctx->ev_in, ctx->ev_hash, ctx->ev_dec, ctx->ev_comb, ctx->ev_out}) if (e) hipEventDestroy(e);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -558,7 +587,7 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
   SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
   carve c{(char*)ctx->ws};
   verify_ws w = carve_verify(c, n, n_roots);
-  if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, d_root, d_roots, d, rlc_seed, d_v))) return rc;
+  if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, d_root, d_roots, d, rlc_seed, d_v, [] {}))) return rc;
   SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipStreamSynchronize(st));
   return SSB_OK;
@@ -580,13 +609,12 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
                 align_up(n * sizeof(g2_jac));
   if ((rc = ensure_ws(ctx, need))) return rc;
   hipStream_t user = (hipStream_t)stream;
-  hipStream_t st = ctx->stream;
-  // order the engine's private stream after the caller's stream, and back
-  hipEvent_t e_in, e_out;
-  SSB_HIP(hipEventCreateWithFlags(&e_in, hipEventDisableTiming));
-  SSB_HIP(hipEventCreateWithFlags(&e_out, hipEventDisableTiming));
-  SSB_HIP(hipEventRecord(e_in, user));
-  SSB_HIP(hipStreamWaitEvent(st, e_in, 0));
+  hipStream_t st = ctx->stream, sc = ctx->side[1];
+  // order the engine's streams after the caller's stream, and the caller's stream after them
+  hipEvent_t e_user;
+  SSB_HIP(hipEventCreateWithFlags(&e_user, hipEventDisableTiming));
+  SSB_HIP(hipEventRecord(e_user, user));
+  SSB_HIP(hipStreamWaitEvent(st, e_user, 0));
   carve c{(char*)ctx->ws};
   verify_ws w = carve_verify(c, n, n_roots);
   uint32_t* share_job = c.take<uint32_t>(n);
@@ -596,16 +624,27 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(n);
   hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, job_root, share_job, share_root);
-  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict))) return rc;
-  { timed tm(ctx, "k_select"); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, verdict, sel, out_status, out_err); }
-  { timed tm(ctx, "k_lagrange"); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, lam); }
-  if (n) { timed tm(ctx, "k_combine_terms"); hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, term); }
-  { timed tm(ctx, "k_combine_sum"); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, out_sig96); }
+  // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
+  auto spec = [&] {
+    hipStreamWaitEvent(sc, ctx->ev_dec, 0);
+    { timed tm(ctx, "k_select", sc); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err); }
+    { timed tm(ctx, "k_lagrange", sc); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)nullptr, lam); }
+    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, term); }
+    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, out_sig96); }
+    hipEventRecord(ctx->ev_comb, sc);
+  };
+  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict, spec))) return rc;
+  if (!n) spec();
+  // exact path, only if the RLC batch failed (every kernel is a no-op when w.ok == 1)
+  SSB_HIP(hipStreamWaitEvent(st, ctx->ev_comb, 0));
+  hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
+  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, lam);
+  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, out_sig96);
   SSB_HIP(hipGetLastError());
-  SSB_HIP(hipEventRecord(e_out, st));
-  SSB_HIP(hipStreamWaitEvent(user, e_out, 0));
-  hipEventDestroy(e_in);
-  hipEventDestroy(e_out);
+  SSB_HIP(hipEventRecord(ctx->ev_out, st));
+  SSB_HIP(hipStreamWaitEvent(user, ctx->ev_out, 0));
+  hipEventDestroy(e_user);
   return SSB_OK;
 }
 
@@ -693,9 +732,9 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, (const uint32_t*)nullptr, share_job, (uint32_t*)nullptr);
   if (n) hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, (const uint8_t*)nullptr, 0, sig_aff, (g1_aff*)nullptr, flags);
   hipLaunchKernelGGL(k_select_all, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, flags, sel, tt, d_st, err);
-  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, lam);
-  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, d_off, tt, d_st, sel, lam, sig_aff, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, d_out);
+  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, (const uint32_t*)nullptr, lam);
+  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, d_out);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
@@ -766,7 +805,7 @@ int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* ou
   SSB_HIP(hipMemcpyAsync(d_sel, sel.data(), t * 4, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_t, &tt, 4, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_st, &st0, 4, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_lagrange, dim3(1), dim3(64), 0, st, 1, d_off, d_t, d_ids, d_sel, d_st, d_lam);
+  hipLaunchKernelGGL(k_lagrange, dim3(1), dim3(64), 0, st, 1, d_off, d_t, d_ids, d_sel, d_st, (const uint32_t*)nullptr, d_lam);
   SSB_HIP(hipGetLastError());
   std::vector<fr> lam(t);
   SSB_HIP(hipMemcpyAsync(lam.data(), d_lam, t * sizeof(fr), hipMemcpyDeviceToHost, st));
