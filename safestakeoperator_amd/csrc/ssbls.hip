@@ -458,7 +458,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   if (n) {
     { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, 1, w.sig_aff, w.pk_aff, w.flags); }
     SSB_HIP(hipEventRecord(ctx->ev_dec, st));
-    if (on_decoded) on_decoded();
+    on_decoded();
     { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_rlc_mul, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, seed, w.flags, w.sig_aff, w.pk_aff, w.rsig, w.rpk); }
   }
   { timed t(ctx, "k_sum");
