@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libssbls.so")
 SOURCES = ["ssbls.hip"]
-HEADERS = ["ssb_field.h", "ssb_curve.h", "ssb_pairing.h", "ssb_h2c.h", "ssb_consts.h"]
+HEADERS = ["ssb_field.h", "ssb_curve.h", "ssb_pairing.h", "ssb_h2c.h", "ssb_consts.h", "ssb_units.h", "ssb_wave.h", "ssb_wave_tables.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SSB_OFFLOAD_ARCH", "gfx950")
 

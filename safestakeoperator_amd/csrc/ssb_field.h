@@ -398,7 +398,7 @@ SSB_INL bool mp_gt(const uint32_t* a, const uint32_t* b) {
 // ------------------------------------------------------------------------------------------
 // Fp
 // ------------------------------------------------------------------------------------------
-struct fp { uint32_t l[12]; };
+struct alignas(16) fp { uint32_t l[12]; };  // 16-B aligned: ds_read_b128 / dwordx4 moves
 
 SSB_INL fp fp_from_c(const fp_c& c) { fp r; for (int i = 0; i < 12; ++i) r.l[i] = c.l[i]; return r; }
 SSB_INL fp fp_zero() { fp r; for (int i = 0; i < 12; ++i) r.l[i] = 0; return r; }

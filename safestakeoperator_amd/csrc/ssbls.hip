@@ -26,6 +26,7 @@
 #include <mutex>
 
 #include "ssb_units.h"
+#include "ssb_wave.h"
 #include "../../include/ssbls.h"
 
 using namespace ssb;
@@ -156,6 +157,49 @@ __global__ void __launch_bounds__(64) k_miller(int n_roots, const g1_aff* __rest
     miller_loop(r, ng, *sig_sum);
   }
   f[p] = r;
+}
+
+// Wave-cooperative versions: one 64-lane workgroup per Miller loop / per final exponentiation.
+constexpr int WAVE_MILLER_SLOTS = wave::S_USER + 30;
+__global__ void __launch_bounds__(64) k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
+                                                    const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
+                                                    fp12* __restrict__ f) {
+  __shared__ fp slots[WAVE_MILLER_SLOTS];
+  const int p = blockIdx.x, lane = threadIdx.x;
+  g1_aff P; g2_aff Q;
+  if (p < n_roots) { P = root_sum[p]; Q = H[p]; } else { P = g1_neg_generator(); Q = *sig_sum; }
+  if (P.inf || Q.inf) {  // e(O, Q) = e(P, O) = 1  (uniform per workgroup)
+    if (lane == 0) f[p] = fp12_one();
+    return;
+  }
+  wave::ws w{slots};
+  wave::init(w, lane, 64);
+  const int B = wave::S_USER;
+  if (lane == 0) {
+    slots[B + 24] = Q.x.c0; slots[B + 25] = Q.x.c1; slots[B + 26] = Q.y.c0; slots[B + 27] = Q.y.c1;
+    slots[B + 28] = P.x; slots[B + 29] = P.y;
+  }
+  __syncthreads();
+  wave::miller(w, B, lane, 64);
+  if (lane == 0) { fp12 r; wave::load12(r, w, B); f[p] = r; }
+}
+
+constexpr int WAVE_FINAL_SLOTS = wave::S_USER + 12 * 10;
+__global__ void __launch_bounds__(64) k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok) {
+  __shared__ fp slots[WAVE_FINAL_SLOTS];
+  const int lane = threadIdx.x;
+  wave::ws w{slots};
+  wave::init(w, lane, 64);
+  const int ACC = wave::S_USER, IN = ACC + 12, TMP = ACC + 24;
+  if (lane == 0) wave::store12(w, ACC, f[0]);
+  __syncthreads();
+  for (int i = 1; i < npairs; ++i) {
+    if (lane == 0) wave::store12(w, IN, f[i]);
+    __syncthreads();
+    wave::run(w, wave::FP12_MUL, ACC, IN, ACC, lane, 64);
+  }
+  wave::final_exp(w, ACC, TMP, lane, 64);
+  if (lane == 0) { fp12 e; wave::load12(e, w, ACC); *ok = fp12_is_one(e) ? 1u : 0u; }
 }
 
 __global__ void __launch_bounds__(64) k_final(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok) {
@@ -466,8 +510,8 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     hipLaunchKernelGGL(k_sum_g2_partial, dim3(G2_PARTS), dim3(SUM_THREADS), 0, st, (int)n, w.flags, w.rsig, w.part);
     hipLaunchKernelGGL(k_sum_g2_final, dim3(1), dim3(64), 0, st, G2_PARTS, w.part, w.sig_sum); }
   SSB_HIP(hipStreamWaitEvent(st, ctx->ev_hash, 0));
-  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller, dim3(nblk(n_roots + 1, 64)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.sig_sum, w.f); }
-  { timed t(ctx, "k_final"); hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, st, (int)(n_roots + 1), w.f, w.ok); }
+  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_wave, dim3((unsigned)(n_roots + 1)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.sig_sum, w.f); }
+  { timed t(ctx, "k_final"); hipLaunchKernelGGL(k_final_wave, dim3(1), dim3(64), 0, st, (int)(n_roots + 1), w.f, w.ok); }
   if (n) { timed t(ctx, "k_fallback_verify"); hipLaunchKernelGGL(k_fallback_verify, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict); }
   SSB_HIP(hipGetLastError());
   return SSB_OK;

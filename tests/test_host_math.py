@@ -75,3 +75,20 @@ def test_opcount_is_current():
     with open(make_opcount.OUT) as f:
         committed = json.load(f)
     assert make_opcount.measure() == committed
+
+
+def test_wave_programs_match_single_lane(host_exe):
+    """The generated lane-parallel programs (Fp12 mul/sqr/frobenius/conj/sparse line/cyclotomic
+    square, final exponentiation, Miller loop) reproduce the single-lane functions exactly."""
+    c = _load("threshold_cases.json")["cases"][0]
+    ok, n = _run(host_exe, ["wave %s %s %s" % (c["pks"][0], c["sigs"][0], c["root"])])[0].split()
+    assert ok == n == "12"
+
+
+def test_wave_tables_are_current():
+    import subprocess, sys
+    gen = os.path.join(HERE, "..", "safestakeoperator_amd", "csrc", "gen_wave_tables.py")
+    hdr = os.path.join(HERE, "..", "safestakeoperator_amd", "csrc", "ssb_wave_tables.h")
+    before = open(hdr).read()
+    subprocess.run([sys.executable, gen], check=True, capture_output=True)
+    assert open(hdr).read() == before
