@@ -39,8 +39,8 @@ def kernel_mads(mads, V, t, n, n_roots):
     lag = mads["lagrange_t3"] if t <= 3 else (mads["lagrange_t5"] if t <= 5 else mads["lagrange_t10"])
     return {
         "k_hash_to_g2": n_roots * mads["hash_to_g2"],
-        "k_decode": N * mads["decode"],
-        "k_rlc_mul": N * mads["rlc"],
+        "k_decode": N * (mads["decode_sig"] + mads["decode_pk"]),
+        "k_rlc_mul": N * (mads["subgroup"] + mads["rlc_sig"] + mads["rlc_pk"]),
         "k_sum": N * (mads["sum_g1_add"] + mads["sum_g2_add"]) + n_roots * mads["to_affine_g1"] + mads["to_affine_g2"],
         "k_miller": (n_roots + 1) * mads["miller_pair"],
         "k_final": n_roots * mads["fp12_mul"] + mads["final_exp"],

@@ -440,7 +440,53 @@ SSB_FN void fp_pow(fp& r, const fp& a, const uint32_t* e) {
   }
   r = acc;
 }
-SSB_INL void fp_inv(fp& r, const fp& a) { fp_pow(r, a, EXP_P_MINUS_2); }  // inv(0) = 0
+SSB_INL void fp_inv_fermat(fp& r, const fp& a) { fp_pow(r, a, EXP_P_MINUS_2); }  // inv(0) = 0
+
+// Binary extended Euclid (variable time: inputs on this path are public).  For the Montgomery
+// form aR it returns (aR)^{-1} * R^3 / R = a^{-1} R.  inv(0) = 0.  About 4x fewer dependent
+// instructions than the Fermat chain, which matters on the single-lane inversions of the
+// latency-bound stages (to-affine of the RLC sums, SSWU, isogeny, final exponentiation).
+template <int N>
+SSB_INL void mp_shr1(uint32_t* a) {
+#pragma unroll
+  for (int i = 0; i < N - 1; ++i) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
+  a[N - 1] >>= 1;
+}
+// x/2 mod p for x < p
+SSB_INL void fp_half_mod(uint32_t* x) {
+  if (x[0] & 1u) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) x[i] = addc(x[i], P_LIMBS[i], c, c);
+    mp_shr1<12>(x);
+    x[11] |= c << 31;
+  } else {
+    mp_shr1<12>(x);
+  }
+}
+SSB_FN void fp_inv(fp& r, const fp& a) {
+  uint32_t u[12], v[12], x1[12], x2[12];
+  for (int i = 0; i < 12; ++i) { u[i] = a.l[i]; v[i] = P_LIMBS[i]; x1[i] = 0; x2[i] = 0; }
+  x1[0] = 1;
+  if (mp_is_zero<12>(u)) { r = fp_zero(); return; }
+  uint32_t one[12] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  while (!mp_eq<12>(u, one) && !mp_eq<12>(v, one)) {
+    while (!(u[0] & 1u)) { mp_shr1<12>(u); fp_half_mod(x1); }
+    while (!(v[0] & 1u)) { mp_shr1<12>(v); fp_half_mod(x2); }
+    if (!mp_gt<12>(v, u)) {  // u >= v
+      uint32_t br = 0;
+      for (int i = 0; i < 12; ++i) u[i] = subb(u[i], v[i], br, br);
+      mp_sub_mod<12>(x1, x1, x2, P_LIMBS);
+    } else {
+      uint32_t br = 0;
+      for (int i = 0; i < 12; ++i) v[i] = subb(v[i], u[i], br, br);
+      mp_sub_mod<12>(x2, x2, x1, P_LIMBS);
+    }
+  }
+  fp t;
+  for (int i = 0; i < 12; ++i) t.l[i] = mp_eq<12>(u, one) ? x1[i] : x2[i];
+  mp_mont_mul<12>(r.l, t.l, P_R3, P_LIMBS, P_INV32);
+}
 // returns true iff a is a square; r = a^((p+1)/4) (a root when it is)
 SSB_FN bool fp_sqrt(fp& r, const fp& a) {
   fp s, s2;

@@ -35,6 +35,25 @@ SSB_FN uint32_t unit_decode(g2_aff& sig, g1_aff& pk, const uint8_t* sig96, const
   return st | (pst << 8) | (cand ? FLAG_CANDIDATE : 0u);
 }
 
+// Split form used by the verify pipeline (independent per-share tasks, one thread each):
+//   decode_sig | decode_pk   then   subgroup | rlc_sig | rlc_pk
+SSB_FN uint32_t unit_decode_sig(g2_aff& sig, const uint8_t* sig96) { return g2_decompress(sig, sig96); }
+SSB_FN uint32_t unit_decode_pk(g1_aff& pk, const uint8_t* pk48) { return g1_decompress(pk, pk48); }
+SSB_FN uint32_t unit_subgroup(const g2_aff& sig) { return g2_in_subgroup(sig) ? DEC_IN_GROUP : 0u; }
+SSB_FN void unit_rlc_sig(g2_jac& r, const g2_aff& sig, uint64_t k) {
+  const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+  jac_mul_w4(r, sig, kw, 2);
+}
+SSB_FN void unit_rlc_pk(g1_jac& r, const g1_aff& pk, uint64_t k) {
+  const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+  jac_mul_w4(r, pk, kw, 2);
+}
+SSB_INL uint32_t combine_flags(uint32_t sf, uint32_t pf, uint32_t gf) {
+  const uint32_t st = sf | gf;
+  const bool cand = (st & DEC_OK) && !(st & DEC_INF) && (st & DEC_IN_GROUP) && (pf & DEC_OK) && !(pf & DEC_INF);
+  return st | (pf << 8) | (cand ? FLAG_CANDIDATE : 0u);
+}
+
 // unit "rlc": r*sig and r*pk for the share's 64-bit RLC scalar
 SSB_FN void unit_rlc(g2_jac& rsig, g1_jac& rpk, const g2_aff& sig, const g1_aff& pk, uint64_t r) {
   const uint32_t k[2] = {(uint32_t)r, (uint32_t)(r >> 32)};

@@ -78,6 +78,57 @@ __global__ void __launch_bounds__(64) k_decode(int n, const uint8_t* __restrict_
   flags[s] = fl;
 }
 
+// threads [0, n): signature decompress; [n, 2n): public-key decompress
+__global__ void __launch_bounds__(64) k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
+                                                g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
+                                                uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) {
+    uint8_t b[96];
+    for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)g + k];
+    g2_aff sig;
+    sflags[g] = unit_decode_sig(sig, b);
+    sig_aff[g] = sig;
+  } else if (g < 2 * n) {
+    const int s = g - n;
+    uint8_t b[48];
+    for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
+    g1_aff pk;
+    pflags[s] = unit_decode_pk(pk, b);
+    pk_aff[s] = pk;
+  }
+}
+
+// threads [0, n): G2 subgroup check; [n, 2n): r_i * sig_i; [2n, 3n): r_i * pk_i
+__global__ void __launch_bounds__(64) k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+                                                  const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
+                                                  const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
+                                                  g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) {
+    const uint32_t sf = sflags[g];
+    gflags[g] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[g]) : 0u;
+  } else if (g < 2 * n) {
+    const int s = g - n;
+    const uint32_t sf = sflags[s];
+    g2_jac r;
+    if ((sf & DEC_OK) && !(sf & DEC_INF)) unit_rlc_sig(r, sig_aff[s], rlc_scalar(seed, (uint64_t)s)); else jac_set_inf(r);
+    rsig[s] = r;
+  } else if (g < 3 * n) {
+    const int s = g - 2 * n;
+    const uint32_t pf = pflags[s];
+    g1_jac r;
+    if ((pf & DEC_OK) && !(pf & DEC_INF)) unit_rlc_pk(r, pk_aff[s], rlc_scalar(seed, (uint64_t)s)); else jac_set_inf(r);
+    rpk[s] = r;
+  }
+}
+
+__global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
+                        const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) flags[s] = combine_flags(sflags[s], pflags[s], gflags[s]);
+}
+
 __global__ void __launch_bounds__(64) k_rlc_mul(int n, uint64_t seed, const uint32_t* __restrict__ flags,
                                                 const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
                                                 g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
@@ -468,14 +519,14 @@ int fill_dst(ssb_ctx* ctx, dst_arg& d, const uint8_t* dst, size_t dst_len) {
 
 // The verification stage shared by verify_batch and threshold_aggregate_batch.
 struct verify_ws {
-  g2_aff* H; g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags;
+  g2_aff* H; g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags;
   g2_jac* rsig; g1_jac* rpk; g1_aff* root_sum; g2_jac* part; g2_aff* sig_sum; fp12* f; uint32_t* ok;
 };
 constexpr int G2_PARTS = 64;
 
 size_t verify_ws_bytes(size_t n, size_t n_roots) {
   return align_up(n_roots * sizeof(g2_aff)) + align_up(n * sizeof(g2_aff)) + align_up(n * sizeof(g1_aff)) +
-         align_up(n * 4) + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
+         align_up(n * 4) * 4 + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
          align_up(n_roots * sizeof(g1_aff)) + align_up(G2_PARTS * sizeof(g2_jac)) + align_up(sizeof(g2_aff)) +
          align_up((n_roots + 1) * sizeof(fp12)) + align_up(4);
 }
@@ -483,7 +534,8 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   verify_ws w;
   w.H = c.take<g2_aff>(n_roots); w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
-  w.flags = c.take<uint32_t>(n); w.rsig = c.take<g2_jac>(n); w.rpk = c.take<g1_jac>(n);
+  w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
+  w.gflags = c.take<uint32_t>(n); w.rsig = c.take<g2_jac>(n); w.rpk = c.take<g1_jac>(n);
   w.root_sum = c.take<g1_aff>(n_roots); w.part = c.take<g2_jac>(G2_PARTS); w.sig_sum = c.take<g2_aff>(1);
   w.f = c.take<fp12>(n_roots + 1); w.ok = c.take<uint32_t>(1);
   return w;
@@ -500,10 +552,11 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n_roots, 64)), dim3(64), 0, sh, (int)n_roots, d_roots, dst, w.H); }
   SSB_HIP(hipEventRecord(ctx->ev_hash, sh));
   if (n) {
-    { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, 1, w.sig_aff, w.pk_aff, w.flags); }
+    { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags); }
+    { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_check_rlc, dim3(nblk(3 * n, 64)), dim3(64), 0, st, (int)n, seed, w.sflags, w.pflags, w.sig_aff, w.pk_aff, w.gflags, w.rsig, w.rpk); }
+    hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, w.flags);
     SSB_HIP(hipEventRecord(ctx->ev_dec, st));
     on_decoded();
-    { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_rlc_mul, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, seed, w.flags, w.sig_aff, w.pk_aff, w.rsig, w.rpk); }
   }
   { timed t(ctx, "k_sum");
     if (n_roots) hipLaunchKernelGGL(k_sum_g1_by_root, dim3((unsigned)n_roots), dim3(SUM_THREADS), 0, st, (int)n, d_share_root, w.flags, w.rpk, w.root_sum);

@@ -104,8 +104,15 @@ int main() {
       uint32_t fl = unit_decode(sig, pk, sb.data(), pkb.data(), 1);
       rec("decode", 1);
       if (!(fl & FLAG_CANDIDATE)) { printf("ERR not a candidate\n"); fflush(stdout); continue; }
+      unit_decode_sig(sig, sb.data()); rec("decode_sig", 1);
+      unit_decode_pk(pk, pkb.data()); rec("decode_pk", 1);
+      unit_subgroup(sig); rec("subgroup", 1);
       const int NS = 16;
       g2_jac rs; g1_jac rp;
+      for (int i = 0; i < NS; ++i) unit_rlc_sig(rs, sig, rlc_scalar(0x5AFE57A4Eull, (uint64_t)i));
+      rec("rlc_sig", NS);
+      for (int i = 0; i < NS; ++i) unit_rlc_pk(rp, pk, rlc_scalar(0x5AFE57A4Eull, (uint64_t)i));
+      rec("rlc_pk", NS);
       for (int i = 0; i < NS; ++i) unit_rlc(rs, rp, sig, pk, rlc_scalar(0x5AFE57A4Eull, (uint64_t)i));
       rec("rlc", NS);
       g1_jac acc1; jac_set_inf(acc1); jac_add(acc1, acc1, rp); g_ssb_counts = {};
