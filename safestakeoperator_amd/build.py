@@ -15,14 +15,24 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SSB_OFFLOAD_ARCH", "gfx950")
 
 
-def _newest_input():
-    paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    paths.append(os.path.join(HERE, "..", "include", "ssbls.h"))
-    return max(os.path.getmtime(p) for p in paths)
+STAMP = LIB + ".srchash"
+
+
+def _source_hash():
+    """Content hash of every input (mtimes do not survive the copy to a GPU box)."""
+    import hashlib
+    h = hashlib.sha256()
+    paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(HERE, "..", "include", "ssbls.h")]
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    h.update(" ".join([HIPCC, ARCH]).encode())
+    return h.hexdigest()
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input():
+    want = _source_hash()
+    if not force and os.path.exists(LIB) and os.path.exists(STAMP) and open(STAMP).read().strip() == want:
         return LIB
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-shared", "-fPIC",
            "-Wno-unused-result", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
@@ -30,6 +40,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
         print("[ssbls] building:", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    with open(STAMP, "w") as f:
+        f.write(want + "\n")
     return LIB
 
 

@@ -29,16 +29,9 @@ class Ctx:
     def mat(self, form):
         ph = max([self.phase_of(s) for s in form.c] + [0])
         assert ph >= 1, "materialise only forms that depend on products"
-        # a materialisation cannot read another one of the same phase: inline those
-        d = {}
-        for s, c in form.c.items():
-            if s[0] == "M" and self.mats[s[1]][0] == ph:
-                for s2, c2 in self.mats[s[1]][1].c.items():
-                    d[s2] = d.get(s2, 0) + c * c2
-            else:
-                d[s] = d.get(s, 0) + c
-        form = L(d)
-        self.mats.append((ph, form))
+        # level inside the phase's linear stage: after every same-phase materialisation it reads
+        lvl = 1 + max([self.mats[s[1]][2] for s in form.c if s[0] == "M" and self.mats[s[1]][0] == ph] + [-1])
+        self.mats.append((ph, form, lvl))
         return L({("M", len(self.mats) - 1): 1})
 
     def phase_of(self, sym):
@@ -261,7 +254,7 @@ def miller_dbl(T, P):
     A = f2_sqr(X)
     B = f2_sqr(Y)
     C = f2_sqr(B)
-    t = f2_sub(f2_sub(f2_sqr(f2_add(X, B)), A), C)
+    t = mat2(f2_sub(f2_sub(f2_sqr(f2_add(X, B)), A), C))
     D = mat2(f2_dbl(t))
     E = mat2(f2_add(f2_dbl(A), A))
     F = f2_sqr(E)
@@ -271,7 +264,9 @@ def miller_dbl(T, P):
     x3 = mat2(f2_sub(F, f2_dbl(D)))
     z3 = mat2(f2_dbl(f2_mul(Y, Z)))
     y3 = f2_mul(E, mat2(f2_sub(D, x3)))
-    C8 = mat2(f2_dbl(f2_dbl(f2_dbl(C))))
+    C2 = mat2(f2_dbl(C))
+    C4 = mat2(f2_dbl(C2))
+    C8 = mat2(f2_dbl(C4))
     y3 = f2_sub(y3, C8)
     l4 = f2_mul_fp(mat2(f2_mul(z3, ZZ)), yP)
     return (x3, y3, z3), (l0, l1, l4)
@@ -315,10 +310,49 @@ def sym_vec(tag, n):
     return [L({(tag, i): 1}) for i in range(n)]
 
 
+OUT_CHUNK = 8
+
+
+def _nterms(form):
+    return sum(abs(c) for c in form.c.values())
+
+
+def split_outputs(outs):
+    """Outputs longer than OUT_CHUNK terms become sums of partial materialisations computed by
+    other lanes at the end of the last phase (the output lanes then add <= OUT_CHUNK terms)."""
+    if not CTX.products:
+        return outs
+    last = max(p[0] for p in CTX.products)
+    res = []
+    for o in outs:
+        if _nterms(o) <= OUT_CHUNK:
+            res.append(o)
+            continue
+        chunks, cur, n = [], {}, 0
+        for sym, c in sorted(o.c.items()):
+            if n + abs(c) > OUT_CHUNK and cur:
+                chunks.append(cur)
+                cur, n = {}, 0
+            cur[sym] = c
+            n += abs(c)
+        if cur:
+            chunks.append(cur)
+        acc = L()
+        for ch in chunks:
+            f_ = L(ch)
+            ph = max([CTX.phase_of(s_) for s_ in f_.c] + [0])
+            if ph >= 1:
+                acc = acc + CTX.mat(f_)
+            else:
+                acc = acc + f_
+        res.append(acc)
+    return res
+
+
 def trace(fn):
     global CTX
     CTX = Ctx()
-    outs = fn()
+    outs = split_outputs(fn())
     TRACED_MATS[0] = CTX.mats
     return CTX.products, outs
 
@@ -345,7 +379,7 @@ def encode(name, products, outs, na, nb, consts, mats=()):
     # renumber products phase-major so each phase is a contiguous lane range
     order = sorted(range(len(products)), key=lambda i: products[i][0])
     remap = {old: new for new, old in enumerate(order)}
-    morder = sorted(range(len(mats)), key=lambda i: mats[i][0])
+    morder = sorted(range(len(mats)), key=lambda i: (mats[i][0], mats[i][2]))
     mremap = {old: new for new, old in enumerate(morder)}
 
     def fix(form):
@@ -356,16 +390,22 @@ def encode(name, products, outs, na, nb, consts, mats=()):
         return L(d)
 
     prods = [(products[i][0], fix(products[i][1]), fix(products[i][2])) for i in order]
-    mts = [(mats[i][0], fix(mats[i][1])) for i in morder]
+    mts = [(mats[i][0], fix(mats[i][1]), mats[i][2]) for i in morder]
     outs = [fix(o) for o in outs]
     phase_end = [sum(1 for p in prods if p[0] <= ph) for ph in range(1, nphase + 1)]
-    mat_end = [sum(1 for m in mts if m[0] <= ph) for ph in range(1, nphase + 1)]
+    # linear stages: per phase, per level -> (phase, end index into mats)
+    stages = []
+    for ph in range(1, nphase + 1):
+        lv = sorted(set(m[2] for m in mts if m[0] == ph))
+        for l_ in lv:
+            stages.append((ph, sum(1 for m in mts if (m[0], m[2]) <= (ph, l_))))
+    mat_end = stages
     rows = []
     for ph, x, y in prods:
         xp, xn = terms(x)
         yp, yn = terms(y)
         rows.append((xp, xn, yp, yn))
-    mrows = [terms(m) for _, m in mts]
+    mrows = [terms(m) for _, m, _ in mts]
     orows = [terms(o) for o in outs]
     return dict(name=name, na=na, nb=nb, nk=nk, consts=consts, nprod=len(prods), nphase=nphase, nmat=len(mts),
                 phase_start=phase_end, mat_end=mat_end, rows=rows, mrows=mrows, orows=orows, nout=len(outs))
@@ -375,18 +415,18 @@ def programs():
     progs = []
     # fp12 mul: A = a (12), B = b (12)
     pr, o = trace(lambda: flat_fp12(f12_mul(sym_fp12("A"), sym_fp12("B"))))
-    progs.append(encode("FP12_MUL", pr, o, 12, 12, []))
+    progs.append(encode("FP12_MUL", pr, o, 12, 12, [], TRACED_MATS[0]))
     pr, o = trace(lambda: flat_fp12(f12_sqr(sym_fp12("A"))))
-    progs.append(encode("FP12_SQR", pr, o, 12, 0, []))
+    progs.append(encode("FP12_SQR", pr, o, 12, 0, [], TRACED_MATS[0]))
     pr, o = trace(lambda: flat_fp12(f12_cyc_sqr(sym_fp12("A"))))
-    progs.append(encode("FP12_CYC_SQR", pr, o, 12, 0, []))
+    progs.append(encode("FP12_CYC_SQR", pr, o, 12, 0, [], TRACED_MATS[0]))
 
     # sparse line multiply: B = (l0.c0, l0.c1, l1.c0, l1.c1, l4.c0, l4.c1)
     def mul014():
         b = sym_vec("B", 6)
         return flat_fp12(f12_mul_014(sym_fp12("A"), (b[0], b[1]), (b[2], b[3]), (b[4], b[5])))
     pr, o = trace(mul014)
-    progs.append(encode("FP12_MUL_014", pr, o, 12, 6, []))
+    progs.append(encode("FP12_MUL_014", pr, o, 12, 6, [], TRACED_MATS[0]))
     # frobenius n = 1, 2, 3: constants gamma_{n,k}, k = 1..5 (10 Fp)
     for n in (1, 2, 3):
         def frob(n=n):
@@ -396,9 +436,9 @@ def programs():
                 consts[i] = (k[2 * (i - 1)], k[2 * (i - 1) + 1])
             return flat_fp12(f12_frob(sym_fp12("A"), consts))
         pr, o = trace(frob)
-        progs.append(encode("FP12_FROB%d" % n, pr, o, 12, 0, [(n, k, c) for k in range(1, 6) for c in range(2)]))
+        progs.append(encode("FP12_FROB%d" % n, pr, o, 12, 0, [(n, k, c) for k in range(1, 6) for c in range(2)], TRACED_MATS[0]))
     pr, o = trace(lambda: flat_fp12(f12_conj(sym_fp12("A"))))
-    progs.append(encode("FP12_CONJ", pr, o, 12, 0, []))
+    progs.append(encode("FP12_CONJ", pr, o, 12, 0, [], TRACED_MATS[0]))
 
     # Miller doubling step: A = T (6: X, Y, Z as Fp2), B = P (2: xP, yP); out T'(6) + line(6)
     def mdbl():
@@ -430,7 +470,8 @@ def emit(progs):
     out.append("constexpr int MAX_OUT = %d;" % max(p["nout"] for p in progs))
     out.append("constexpr int MAX_SLOTS_OP = %d;" % max(1 + p["na"] + p["nb"] + p["nk"] + p["nprod"] + p["nmat"] for p in progs))
     out.append("constexpr int MAX_MAT = %d;" % max(p["nmat"] for p in progs))
-    out.append("struct prog { int na, nb, nk, nprod, nmat, nphase, nout; const uint8_t* phase_end; const uint8_t* mat_end;")
+    out.append("struct prog { int na, nb, nk, nprod, nmat, nphase, nout, nlin; const uint8_t* phase_end;")
+    out.append("  const uint8_t* lin;   // linear stages: (after phase index, end of its materialisation range)")
     out.append("  const uint8_t* cnt;   // per product: |x+|, |x-|, |y+|, |y-|")
     out.append("  const uint16_t* off;  // per product: offset of its term list in terms[]")
     out.append("  const uint8_t* ocnt;  // per materialisation, then per output: |+|, |-|")
@@ -451,15 +492,19 @@ def emit(progs):
         for (n, k, c) in p["consts"]:
             kc += [n, k, c]  # K slot = component c of gamma_{n,k} (FROBn[k])
         out.append("constexpr uint8_t %s_PH[] = {%s};" % (nm, ", ".join(map(str, p["phase_start"])) or "0"))
-        out.append("constexpr uint8_t %s_ME[] = {%s};" % (nm, ", ".join(map(str, p["mat_end"])) or "0"))
+        me = []
+        for (ph, end) in p["mat_end"]:
+            me += [ph - 1, end]   # (phase index, end) pairs: linear stages in order
+        out.append("constexpr uint8_t %s_ME[] = {%s};" % (nm, ", ".join(map(str, me)) or "0"))
         out.append("constexpr uint8_t %s_CNT[] = {%s};" % (nm, ", ".join(map(str, cnt)) or "0"))
         out.append("constexpr uint16_t %s_OFF[] = {%s};" % (nm, ", ".join(map(str, off)) or "0"))
         out.append("constexpr uint8_t %s_OCNT[] = {%s};" % (nm, ", ".join(map(str, ocnt))))
         out.append("constexpr uint16_t %s_OOFF[] = {%s};" % (nm, ", ".join(map(str, ooff))))
         out.append("constexpr uint8_t %s_TERMS[] = {%s};" % (nm, ", ".join(map(str, terms))))
         out.append("constexpr uint8_t %s_K[] = {%s};" % (nm, ", ".join(map(str, kc)) or "0"))
-        out.append("constexpr prog %s = {%d, %d, %d, %d, %d, %d, %d, %s_PH, %s_ME, %s_CNT, %s_OFF, %s_OCNT, %s_OOFF, %s_TERMS, %s_K};"
-                   % (nm, p["na"], p["nb"], p["nk"], p["nprod"], p["nmat"], p["nphase"], p["nout"], nm, nm, nm, nm, nm, nm, nm, nm))
+        out.append("constexpr prog %s = {%d, %d, %d, %d, %d, %d, %d, %d, %s_PH, %s_ME, %s_CNT, %s_OFF, %s_OCNT, %s_OOFF, %s_TERMS, %s_K};"
+                   % (nm, p["na"], p["nb"], p["nk"], p["nprod"], p["nmat"], p["nphase"], p["nout"], len(p["mat_end"]),
+                      nm, nm, nm, nm, nm, nm, nm, nm))
         out.append("// %s: %d products in %d phases, %d materialised, %d outputs, max terms/form %d" %
                    (nm, p["nprod"], p["nphase"], p["nmat"], p["nout"],
                     max([max(len(r[0]) + len(r[1]), len(r[2]) + len(r[3])) for r in p["rows"]] + [0])))

@@ -65,7 +65,7 @@ SSB_INL void form(fp& r, const ws& w, const prog& pg, const uint8_t* t, int np, 
 // Run program `pg` with inputs at slots [a, a+na), [b, b+nb); outputs to [dst, dst+nout).
 // dst may alias the inputs.
 SSB_FN void run(const ws& w, const prog& pg, int a, int b, int dst, int lane, int nlanes) {
-  int p0 = 0, m0 = 0;
+  int p0 = 0, m0 = 0, li = 0;
   for (int ph = 0; ph < pg.nphase; ++ph) {
     const int p1 = pg.phase_end[ph];
     for (int L = p0 + lane; L < p1; L += nlanes) {
@@ -77,15 +77,17 @@ SSB_FN void run(const ws& w, const prog& pg, int a, int b, int dst, int lane, in
       fp_mul(w.s[S_PSCR + L], x, y);
     }
     SSB_WAVE_SYNC();
-    const int m1 = pg.mat_end[ph];
-    for (int M = m0 + lane; M < m1; M += nlanes) {
-      fp r;
-      form(r, w, pg, pg.terms + pg.ooff[M], pg.ocnt[2 * M], pg.ocnt[2 * M + 1], a, b);
-      w.s[S_MSCR + M] = r;
-    }
-    if (m1 > m0) SSB_WAVE_SYNC();
     p0 = p1;
-    m0 = m1;
+    for (; li < pg.nlin && pg.lin[2 * li] == ph; ++li) {  // linear stages (levels) after this phase
+      const int m1 = pg.lin[2 * li + 1];
+      for (int M = m0 + lane; M < m1; M += nlanes) {
+        fp r;
+        form(r, w, pg, pg.terms + pg.ooff[M], pg.ocnt[2 * M], pg.ocnt[2 * M + 1], a, b);
+        w.s[S_MSCR + M] = r;
+      }
+      SSB_WAVE_SYNC();
+      m0 = m1;
+    }
   }
   for (int j = lane; j < pg.nout; j += nlanes) {
     const int o = pg.nmat + j;
