@@ -15,7 +15,7 @@
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define SSB_INL __host__ __device__ __forceinline__
-#define SSB_FN __host__ __device__ __noinline__
+#define SSB_FN __host__ __device__ inline __attribute__((noinline))
 #else
 #define SSB_INL inline
 #define SSB_FN inline

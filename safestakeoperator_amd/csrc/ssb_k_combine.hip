@@ -1,0 +1,99 @@
+// ssb_k_combine.hip -- kernels (gfx950): reference scan/selection, Lagrange coefficients, combine.
+// Launched from ssbls.hip (declarations in ssb_kernels.h); one TU per kernel family so the
+// library compiles in parallel.
+#include "ssb_kernels.h"
+#include "ssb_wave.h"
+
+namespace ssb {
+namespace k {
+
+__global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
+                         const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
+                         uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  const uint32_t b = off[j], e = off[j + 1], t = tt[j];
+  const uint32_t n = e - b;
+  if (n < t) { status[j] = SSB_DVF_INSUFFICIENT_SIGNATURES; err[2 * j] = n; err[2 * j + 1] = t; return; }
+  uint32_t cnt = 0;
+  for (uint32_t s = b; s < e; ++s) {
+    const uint64_t id = ids[s];
+    if (id == 0) { status[j] = SSB_DVF_INVALID_OPERATOR_ID; err[2 * j] = 0; err[2 * j + 1] = 0; return; }
+    bool dup = false;
+    for (uint32_t k = 0; k < cnt; ++k) dup = dup || (ids[sel[b + k]] == id);
+    if (dup) continue;
+    if (verdict ? (verdict[s] != 0) : ((flags[s] & FLAG_CANDIDATE) != 0)) {
+      sel[b + cnt] = s;
+      ++cnt;
+      if (cnt >= t) break;
+    }
+  }
+  if (cnt < t) { status[j] = SSB_DVF_INSUFFICIENT_VALID_SIGNATURES; err[2 * j] = cnt; err[2 * j + 1] = t; return; }
+  status[j] = SSB_DVF_OK; err[2 * j] = 0; err[2 * j + 1] = 0;
+}
+__global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ flags,
+                             uint32_t* __restrict__ sel, uint32_t* __restrict__ tt, int32_t* __restrict__ status,
+                             uint64_t* __restrict__ err) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  const uint32_t b = off[j], e = off[j + 1];
+  tt[j] = e - b;
+  int32_t st = SSB_DVF_OK;
+  for (uint32_t s = b; s < e; ++s) {
+    sel[s] = s;
+    if (!(flags[s] & DEC_OK)) st = SSB_DVF_BAD_SIGNATURE_ENCODING;
+  }
+  status[j] = st; err[2 * j] = 0; err[2 * j + 1] = 0;
+}
+__global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                           const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
+                           const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
+                           fr* __restrict__ lam) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs || status[j] != SSB_DVF_OK) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  const uint32_t b = off[j], t = tt[j];
+  uint64_t x[SSB_MAX_T];
+  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
+  unit_lagrange(lam + b, x, t);
+}
+__global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
+                                                      const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                                                      const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                                                      const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
+                                                      const uint32_t* __restrict__ skip_if_ok, g2_jac* __restrict__ term) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  const uint32_t j = share_job[s];
+  const uint32_t k = (uint32_t)s - off[j];
+  if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
+  const fr l = lam[s];
+  g2_jac r;
+  unit_combine_term(r, sig_aff[sel[s]], l.l);  // blst_p2_mult(.., 255 bits)
+  term[s] = r;
+}
+__global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
+                                                    const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
+                                                    uint8_t* __restrict__ out96) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  uint8_t o[96];
+  if (status[j] == SSB_DVF_OK) {
+    unit_combine_sum(o, term + off[j], tt[j]);  // infinity(t) start (src/crypto/impls/blst.rs:74)
+  } else {
+    for (int k = 0; k < 96; ++k) o[k] = 0;
+  }
+  for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
+}
+__global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+
+}  // namespace k
+}  // namespace ssb

@@ -1,0 +1,119 @@
+// ssb_k_verify.hip -- kernels (gfx950): share map, decompression, flags, RLC sums, exact fallback verify.
+// Launched from ssbls.hip (declarations in ssb_kernels.h); one TU per kernel family so the
+// library compiles in parallel.
+#include "ssb_kernels.h"
+#include "ssb_wave.h"
+
+namespace ssb {
+namespace k {
+
+__global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
+                            uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  const uint32_t r = job_root ? job_root[j] : 0u;
+  for (uint32_t s = off[j]; s < off[j + 1]; ++s) {
+    share_job[s] = (uint32_t)j;
+    if (share_root) share_root[s] = r;
+  }
+}
+__global__ void __launch_bounds__(64) k_decode(int n, const uint8_t* __restrict__ sig96,
+                                               const uint8_t* __restrict__ pk48, int group_check,
+                                               g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
+                                               uint32_t* __restrict__ flags) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  uint8_t b[96], c[48];
+  for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
+  if (pk48) for (int k = 0; k < 48; ++k) c[k] = pk48[48 * (size_t)s + k];
+  g2_aff sig; g1_aff pk;
+  const uint32_t fl = unit_decode(sig, pk, b, pk48 ? c : nullptr, group_check);
+  sig_aff[s] = sig;
+  if (pk48) pk_aff[s] = pk;
+  flags[s] = fl;
+}
+__global__ void __launch_bounds__(64) k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
+                                                g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
+                                                uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) {
+    uint8_t b[96];
+    for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)g + k];
+    g2_aff sig;
+    sflags[g] = unit_decode_sig(sig, b);
+    sig_aff[g] = sig;
+  } else if (g < 2 * n) {
+    const int s = g - n;
+    uint8_t b[48];
+    for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
+    g1_aff pk;
+    pflags[s] = unit_decode_pk(pk, b);
+    pk_aff[s] = pk;
+  }
+}
+__global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
+                        const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) flags[s] = combine_flags(sflags[s], pflags[s], gflags[s]);
+}
+__global__ void __launch_bounds__(SUM_THREADS) k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
+                                                                const uint32_t* __restrict__ flags,
+                                                                const g1_jac* __restrict__ rpk,
+                                                                g1_aff* __restrict__ root_sum) {
+  __shared__ g1_jac sh[SUM_THREADS];
+  const uint32_t b = blockIdx.x;
+  g1_jac acc; jac_set_inf(acc);
+  for (int s = threadIdx.x; s < n; s += SUM_THREADS)
+    if ((flags[s] & FLAG_CANDIDATE) && share_root[s] == b) jac_add(acc, acc, rpk[s]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { g1_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { g1_aff a; jac_to_aff(a, acc); root_sum[b] = a; }
+}
+__global__ void __launch_bounds__(SUM_THREADS) k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
+                                                                const g2_jac* __restrict__ rsig,
+                                                                g2_jac* __restrict__ part) {
+  __shared__ g2_jac sh[SUM_THREADS];
+  g2_jac acc; jac_set_inf(acc);
+  for (int s = blockIdx.x * SUM_THREADS + threadIdx.x; s < n; s += gridDim.x * SUM_THREADS)
+    if (flags[s] & FLAG_CANDIDATE) jac_add(acc, acc, rsig[s]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+__global__ void __launch_bounds__(64) k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
+                                                     g2_aff* __restrict__ out) {
+  __shared__ g2_jac sh[64];
+  g2_jac acc; jac_set_inf(acc);
+  for (int i = threadIdx.x; i < nparts; i += 64) jac_add(acc, acc, part[i]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { g2_aff a; jac_to_aff(a, acc); *out = a; }
+}
+__global__ void __launch_bounds__(64) k_fallback_verify(int n, const uint32_t* __restrict__ ok,
+                                                        const uint32_t* __restrict__ flags,
+                                                        const uint32_t* __restrict__ share_root,
+                                                        const g2_aff* __restrict__ H,
+                                                        const g2_aff* __restrict__ sig_aff,
+                                                        const g1_aff* __restrict__ pk_aff,
+                                                        uint8_t* __restrict__ verdict) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
+  if (*ok || !cand) { verdict[s] = cand ? 1 : 0; return; }
+  verdict[s] = unit_verify_one(pk_aff[s], sig_aff[s], H[share_root[s]]) ? 1 : 0;
+}
+
+}  // namespace k
+}  // namespace ssb

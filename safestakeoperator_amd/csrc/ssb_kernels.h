@@ -1,0 +1,96 @@
+// ssb_kernels.h -- host-side launchers of the kernels that live in their own translation units
+// (compiled in parallel, linked into libssbls.so).  Internal to the library: not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "ssb_units.h"
+#include "../../include/ssbls.h"
+
+namespace ssb {
+
+// DST passed by value to the hashing kernels
+struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
+
+namespace k {
+constexpr int SUM_THREADS = 128;   // k_sum_* block size
+
+__global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
+                            uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root);
+__global__ void k_decode(int n, const uint8_t* __restrict__ sig96,
+                                               const uint8_t* __restrict__ pk48, int group_check,
+                                               g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
+                                               uint32_t* __restrict__ flags);
+__global__ void k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
+                                                g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
+                                                uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags);
+__global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
+                        const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags);
+__global__ void k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
+                                                                const uint32_t* __restrict__ flags,
+                                                                const g1_jac* __restrict__ rpk,
+                                                                g1_aff* __restrict__ root_sum);
+__global__ void k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
+                                                                const g2_jac* __restrict__ rsig,
+                                                                g2_jac* __restrict__ part);
+__global__ void k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
+                                                     g2_aff* __restrict__ out);
+__global__ void k_fallback_verify(int n, const uint32_t* __restrict__ ok,
+                                                        const uint32_t* __restrict__ flags,
+                                                        const uint32_t* __restrict__ share_root,
+                                                        const g2_aff* __restrict__ H,
+                                                        const g2_aff* __restrict__ sig_aff,
+                                                        const g1_aff* __restrict__ pk_aff,
+                                                        uint8_t* __restrict__ verdict);
+__global__ void k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
+                                                    const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
+                                                    fp12* __restrict__ f);
+__global__ void k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok);
+__global__ void k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
+                                                   g2_aff* __restrict__ out);
+__global__ void k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
+                                             const g2_aff* __restrict__ H, uint8_t* __restrict__ out96);
+__global__ void k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48);
+__global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* __restrict__ out192);
+__global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
+                         const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
+                         uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err);
+__global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ flags,
+                             uint32_t* __restrict__ sel, uint32_t* __restrict__ tt, int32_t* __restrict__ status,
+                             uint64_t* __restrict__ err);
+__global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                           const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
+                           const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
+                           fr* __restrict__ lam);
+__global__ void k_combine_terms(int n, const uint32_t* __restrict__ share_job,
+                                                      const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                                                      const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                                                      const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
+                                                      const uint32_t* __restrict__ skip_if_ok, g2_jac* __restrict__ term);
+__global__ void k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
+                                                    const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
+                                                    uint8_t* __restrict__ out96);
+__global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b);
+
+}  // namespace k
+
+namespace launch {
+
+// Lane-group kernels (ssb_k_lane.hip), one group of lanes per share.
+//   gflags[s] = DEC_IN_GROUP if sig[s] passes psi(P) == [x]P (only for decodable, non-infinity
+//   signatures: sflags[s] has DEC_OK and not DEC_INF);  exc[s] |= 1 when an addition was
+//   exceptional (the share is then recomputed by the exact single-lane fallback).
+void lane_subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
+//   rsig[s] = rlc_scalar_odd(seed, s) * sig[s]   (or infinity when the signature is not decodable)
+void lane_rlc_g2(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const g2_aff* sig, g2_jac* rsig,
+                 uint32_t* exc);
+//   rpk[s] = rlc_scalar_odd(seed, s) * pk[s]      (exc bit 1)
+void lane_rlc_g1(hipStream_t st, int n, uint64_t seed, const uint32_t* pflags, const g1_aff* pk, g1_jac* rpk,
+                 uint32_t* exc);
+// exact single-lane recomputation of the shares whose lane-group stage raised exc
+void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
+                const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,
+                g1_jac* rpk);
+
+}  // namespace launch
+}  // namespace ssb

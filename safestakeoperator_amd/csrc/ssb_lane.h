@@ -1,0 +1,138 @@
+// ssb_lane.h -- runtime of the lane-group programs generated into ssb_lane_progs.h.
+//
+// A program runs one point / tower operation on a GROUP of G lanes: in every product round each
+// lane ("role") computes one Fp Montgomery product whose operands are short +-sums of LDS slots;
+// in every linear stage some lanes materialise longer forms (reduced mod p) into slots.  The
+// 64/G groups of a wave run independent operations in lockstep.  Slot codes (8 bit) select:
+//   0..47    shared constants of the workgroup (0 = zero)          -> g.k[code]
+//   48..175  the group's scratch                                    -> g.s[code - 48]
+//   176..199 input A, 200..223 input B, 224..255 output D          -> g.s[g.a/b/d + ...]
+// (A, B, D are group-relative slot indices chosen by the caller, beyond the scratch area.)
+//
+// Values in slots are fully reduced (< p).  A product operand of up to 3 terms is formed WITHOUT
+// reduction (negative terms enter as p - v, so the value is <= 3p); 3p * 3p < p * 2^384 keeps the
+// Montgomery product's output < 2p before its final conditional subtraction, so fp_mul accepts
+// it.  Materialised forms have up to 8 terms (<= 8p < 2^384) and are reduced by conditional
+// subtraction of 4p, 2p, p, p.
+//
+// The same source runs on the host (tests): LP_FOR loops over the roles of one group, and the
+// stores of a pass happen after every role computed, like the lockstep lanes of a wave.
+#pragma once
+#include "ssb_curve.h"
+
+namespace ssb {
+namespace lane {
+
+constexpr int LP_NCODE_CONST = 48, LP_NSCRATCH = 128;
+
+struct grp {
+  fp* k;           // shared constants (LP_NCODE_CONST slots)
+  fp* s;           // this group's slots: [0, LP_NSCRATCH) scratch, then caller-owned
+  int a, b, d;     // group-relative slot index of input A, input B, output D
+  uint32_t* flag;  // this group's check word (bit per check component)
+  int role;        // lane index inside the group (device)
+};
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define SSB_LP_FN __host__ __device__ __noinline__
+#else
+#define SSB_LP_FN inline
+#endif
+#define SSB_LP_TABLE constexpr
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LP_DECL_T fp T_
+#define LP_FOR(G) for (int role = g.role, once_ = 1; once_; once_ = 0)
+#define LP_T T_
+#define LP_SYNC() __syncthreads()
+#define LP_FOR_ALL_CONSTS(i) for (int i = threadIdx.x; i < LP_NCODE_CONST; i += blockDim.x)
+#else
+#define LP_DECL_T fp T_[64]
+#define LP_FOR(G) for (int role = 0; role < (G); ++role)
+#define LP_T T_[role]
+#define LP_SYNC() ((void)0)
+#define LP_FOR_ALL_CONSTS(i) for (int i = 0; i < LP_NCODE_CONST; ++i)
+#endif
+
+#define LP_SEL8(imm) ((uint32_t)((imm) >> (8 * role)) & 0xffu)
+#define LP_SELT(tab) ((uint32_t)(tab)[role])
+#define LP_BIT(imm) ((uint32_t)((imm) >> role) & 1u)
+
+SSB_INL fp* lp_ptr(const grp& g, uint32_t c) {
+  const int base = c >= 224u ? g.d - 224 : (c >= 200u ? g.b - 200 : (c >= 176u ? g.a - 176 : -48));
+  return c < (uint32_t)LP_NCODE_CONST ? g.k + c : g.s + ((int)c + base);
+}
+
+// ---- 12-limb helpers without modular reduction ----
+SSB_INL void lp_add_raw(fp& x, const fp& v) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x.l[i] = addc(x.l[i], v.l[i], c, c);
+}
+SSB_INL void lp_pminus(fp& r, const fp& v) {  // p - v (v < p)
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = subb(P_LIMBS[i], v.l[i], br, br);
+}
+SSB_INL void lp_sel(fp& r, const fp& a, const fp& b, uint32_t s) {  // r = s ? a : b
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = s ? a.l[i] : b.l[i];
+}
+
+template <class GR> SSB_INL void lp_ld(fp& x, const GR& g, uint32_t c) { x = *lp_ptr(g, c); }
+template <class GR> SSB_INL void lp_ld_neg(fp& x, const GR& g, uint32_t c) { lp_pminus(x, *lp_ptr(g, c)); }
+template <class GR> SSB_INL void lp_ld_sgn(fp& x, const GR& g, uint32_t c, uint32_t s) {
+  const fp v = *lp_ptr(g, c);
+  fp n; lp_pminus(n, v);
+  lp_sel(x, n, v, s);
+}
+template <class GR> SSB_INL void lp_acc(fp& x, const GR& g, uint32_t c) { lp_add_raw(x, *lp_ptr(g, c)); }
+template <class GR> SSB_INL void lp_acc_neg(fp& x, const GR& g, uint32_t c) {
+  fp n; lp_pminus(n, *lp_ptr(g, c));
+  lp_add_raw(x, n);
+}
+template <class GR> SSB_INL void lp_acc_sgn(fp& x, const GR& g, uint32_t c, uint32_t s) {
+  const fp v = *lp_ptr(g, c);
+  fp n; lp_pminus(n, v);
+  fp t; lp_sel(t, n, v, s);
+  lp_add_raw(x, t);
+}
+template <class GR> SSB_INL void lp_st(const GR& g, uint32_t c, const fp& v) { *lp_ptr(g, c) = v; }
+
+// x >= m*p ? x - m*p : x   (m*p given as limbs)
+SSB_INL void lp_csub(fp& x, const uint32_t* mp) {
+  fp t;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) t.l[i] = subb(x.l[i], mp[i], br, br);
+  lp_sel(x, x, t, br);
+}
+constexpr uint32_t LP_P2[12] = {0xffff5556u, 0x73fdffffu, 0x62a7ffffu, 0x3d57fffdu, 0xed61ec48u, 0xce61a541u,
+                                0xe70a257eu, 0xc8ee9709u, 0x869759aeu, 0x96374f6cu, 0x72ffcd34u, 0x340223d4u};
+constexpr uint32_t LP_P4[12] = {0xfffeaaacu, 0xe7fbffffu, 0xc54ffffeu, 0x7aaffffau, 0xdac3d890u, 0x9cc34a83u,
+                                0xce144afdu, 0x91dd2e13u, 0x0d2eb35du, 0x2c6e9ed9u, 0xe5ff9a69u, 0x680447a8u};
+SSB_INL void lp_reduce1(fp& x) { lp_csub(x, P_LIMBS); }
+SSB_INL void lp_reduce2(fp& x) { lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
+SSB_INL void lp_reduce3(fp& x) { lp_csub(x, LP_P2); lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
+SSB_INL void lp_reduce4(fp& x) { lp_csub(x, LP_P4); lp_csub(x, LP_P2); lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
+
+template <class GR> SSB_INL void lp_chk(const GR& g, const fp& v, uint32_t bit) {
+  if (bit < 31u && fp_is_zero(v)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicOr(g.flag, 1u << bit);
+#else
+    *g.flag |= 1u << bit;
+#endif
+  }
+}
+
+// true iff one of the program's checks fired (all components of some check were zero)
+SSB_INL bool lp_fired(uint32_t flag, const uint32_t* masks, int n) {
+  bool f = false;
+  for (int i = 0; i < n; ++i) f = f || ((flag & masks[i]) == masks[i] && masks[i] != 0u);
+  return f;
+}
+
+}  // namespace lane
+}  // namespace ssb
+
+#include "ssb_lane_progs.h"

@@ -19,6 +19,10 @@ SSB_INL uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
   return z ? z : 1ull;
 }
 
+// the RLC scalars the lane-group stage uses: odd, so the regular signed-window recoding applies
+// (63 random bits per share; lighthouse draws 64: the batch soundness error stays 2^-63)
+SSB_INL uint64_t rlc_scalar_odd(uint64_t seed, uint64_t i) { return rlc_scalar(seed, i) | 1ull; }
+
 SSB_INL g1_aff g1_neg_generator() {
   g1_aff ng; ng.x = fp_from_c(G1_GEN_X); ng.y = fp_from_c(G1_GEN_NEG_Y); ng.inf = 0;
   return ng;

@@ -27,407 +27,13 @@
 
 #include "ssb_units.h"
 #include "ssb_wave.h"
+#include "ssb_kernels.h"
 #include "../../include/ssbls.h"
 
 using namespace ssb;
+using namespace ssb::k;
 
 namespace {
-
-struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
-
-
-// ------------------------------------------------------------------------------------------
-// kernels
-// ------------------------------------------------------------------------------------------
-__global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
-                            uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_jobs) return;
-  const uint32_t r = job_root ? job_root[j] : 0u;
-  for (uint32_t s = off[j]; s < off[j + 1]; ++s) {
-    share_job[s] = (uint32_t)j;
-    if (share_root) share_root[s] = r;
-  }
-}
-
-__global__ void __launch_bounds__(64) k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
-                                                   g2_aff* __restrict__ out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t m[32];
-  for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
-  g2_aff h;
-  hash_to_g2(h, m, dst.b, dst.len);
-  out[i] = h;
-}
-
-// flags: bits 0..7 signature DEC_* bits, bits 8..15 public-key DEC_* bits, bit 16 candidate
-__global__ void __launch_bounds__(64) k_decode(int n, const uint8_t* __restrict__ sig96,
-                                               const uint8_t* __restrict__ pk48, int group_check,
-                                               g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
-                                               uint32_t* __restrict__ flags) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  uint8_t b[96], c[48];
-  for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
-  if (pk48) for (int k = 0; k < 48; ++k) c[k] = pk48[48 * (size_t)s + k];
-  g2_aff sig; g1_aff pk;
-  const uint32_t fl = unit_decode(sig, pk, b, pk48 ? c : nullptr, group_check);
-  sig_aff[s] = sig;
-  if (pk48) pk_aff[s] = pk;
-  flags[s] = fl;
-}
-
-// threads [0, n): signature decompress; [n, 2n): public-key decompress
-__global__ void __launch_bounds__(64) k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
-                                                g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
-                                                uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) {
-    uint8_t b[96];
-    for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)g + k];
-    g2_aff sig;
-    sflags[g] = unit_decode_sig(sig, b);
-    sig_aff[g] = sig;
-  } else if (g < 2 * n) {
-    const int s = g - n;
-    uint8_t b[48];
-    for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
-    g1_aff pk;
-    pflags[s] = unit_decode_pk(pk, b);
-    pk_aff[s] = pk;
-  }
-}
-
-// threads [0, n): G2 subgroup check; [n, 2n): r_i * sig_i; [2n, 3n): r_i * pk_i
-__global__ void __launch_bounds__(64) k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
-                                                  const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
-                                                  const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
-                                                  g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) {
-    const uint32_t sf = sflags[g];
-    gflags[g] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[g]) : 0u;
-  } else if (g < 2 * n) {
-    const int s = g - n;
-    const uint32_t sf = sflags[s];
-    g2_jac r;
-    if ((sf & DEC_OK) && !(sf & DEC_INF)) unit_rlc_sig(r, sig_aff[s], rlc_scalar(seed, (uint64_t)s)); else jac_set_inf(r);
-    rsig[s] = r;
-  } else if (g < 3 * n) {
-    const int s = g - 2 * n;
-    const uint32_t pf = pflags[s];
-    g1_jac r;
-    if ((pf & DEC_OK) && !(pf & DEC_INF)) unit_rlc_pk(r, pk_aff[s], rlc_scalar(seed, (uint64_t)s)); else jac_set_inf(r);
-    rpk[s] = r;
-  }
-}
-
-__global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
-                        const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) flags[s] = combine_flags(sflags[s], pflags[s], gflags[s]);
-}
-
-__global__ void __launch_bounds__(64) k_rlc_mul(int n, uint64_t seed, const uint32_t* __restrict__ flags,
-                                                const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
-                                                g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  g2_jac a; g1_jac b;
-  if (flags[s] & FLAG_CANDIDATE) {
-    unit_rlc(a, b, sig_aff[s], pk_aff[s], rlc_scalar(seed, (uint64_t)s));
-  } else {
-    jac_set_inf(a); jac_set_inf(b);
-  }
-  rsig[s] = a;
-  rpk[s] = b;
-}
-
-// One block per root: sum r_i*pk_i over the candidate shares of that root.
-constexpr int SUM_THREADS = 128;
-__global__ void __launch_bounds__(SUM_THREADS) k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
-                                                                const uint32_t* __restrict__ flags,
-                                                                const g1_jac* __restrict__ rpk,
-                                                                g1_aff* __restrict__ root_sum) {
-  __shared__ g1_jac sh[SUM_THREADS];
-  const uint32_t b = blockIdx.x;
-  g1_jac acc; jac_set_inf(acc);
-  for (int s = threadIdx.x; s < n; s += SUM_THREADS)
-    if ((flags[s] & FLAG_CANDIDATE) && share_root[s] == b) jac_add(acc, acc, rpk[s]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) { g1_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) { g1_aff a; jac_to_aff(a, acc); root_sum[b] = a; }
-}
-
-__global__ void __launch_bounds__(SUM_THREADS) k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
-                                                                const g2_jac* __restrict__ rsig,
-                                                                g2_jac* __restrict__ part) {
-  __shared__ g2_jac sh[SUM_THREADS];
-  g2_jac acc; jac_set_inf(acc);
-  for (int s = blockIdx.x * SUM_THREADS + threadIdx.x; s < n; s += gridDim.x * SUM_THREADS)
-    if (flags[s] & FLAG_CANDIDATE) jac_add(acc, acc, rsig[s]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[blockIdx.x] = acc;
-}
-
-__global__ void __launch_bounds__(64) k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
-                                                     g2_aff* __restrict__ out) {
-  __shared__ g2_jac sh[64];
-  g2_jac acc; jac_set_inf(acc);
-  for (int i = threadIdx.x; i < nparts; i += 64) jac_add(acc, acc, part[i]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = 32; w > 0; w >>= 1) {
-    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) { g2_aff a; jac_to_aff(a, acc); *out = a; }
-}
-
-// pairs 0..n_roots-1: (sum_root r_i pk_i, H(root));  pair n_roots: (-g1, sum r_i sig_i)
-__global__ void __launch_bounds__(64) k_miller(int n_roots, const g1_aff* __restrict__ root_sum,
-                                               const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
-                                               fp12* __restrict__ f) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p > n_roots) return;
-  fp12 r;
-  if (p < n_roots) {
-    miller_loop(r, root_sum[p], H[p]);
-  } else {
-    g1_aff ng = g1_neg_generator();
-    miller_loop(r, ng, *sig_sum);
-  }
-  f[p] = r;
-}
-
-// Wave-cooperative versions: one 64-lane workgroup per Miller loop / per final exponentiation.
-constexpr int WAVE_MILLER_SLOTS = wave::S_USER + 30;
-__global__ void __launch_bounds__(64) k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
-                                                    const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
-                                                    fp12* __restrict__ f) {
-  __shared__ fp slots[WAVE_MILLER_SLOTS];
-  const int p = blockIdx.x, lane = threadIdx.x;
-  g1_aff P; g2_aff Q;
-  if (p < n_roots) { P = root_sum[p]; Q = H[p]; } else { P = g1_neg_generator(); Q = *sig_sum; }
-  if (P.inf || Q.inf) {  // e(O, Q) = e(P, O) = 1  (uniform per workgroup)
-    if (lane == 0) f[p] = fp12_one();
-    return;
-  }
-  wave::ws w{slots};
-  wave::init(w, lane, 64);
-  const int B = wave::S_USER;
-  if (lane == 0) {
-    slots[B + 24] = Q.x.c0; slots[B + 25] = Q.x.c1; slots[B + 26] = Q.y.c0; slots[B + 27] = Q.y.c1;
-    slots[B + 28] = P.x; slots[B + 29] = P.y;
-  }
-  __syncthreads();
-  wave::miller(w, B, lane, 64);
-  if (lane == 0) { fp12 r; wave::load12(r, w, B); f[p] = r; }
-}
-
-constexpr int WAVE_FINAL_SLOTS = wave::S_USER + 12 * 10;
-__global__ void __launch_bounds__(64) k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok) {
-  __shared__ fp slots[WAVE_FINAL_SLOTS];
-  const int lane = threadIdx.x;
-  wave::ws w{slots};
-  wave::init(w, lane, 64);
-  const int ACC = wave::S_USER, IN = ACC + 12, TMP = ACC + 24;
-  if (lane == 0) wave::store12(w, ACC, f[0]);
-  __syncthreads();
-  for (int i = 1; i < npairs; ++i) {
-    if (lane == 0) wave::store12(w, IN, f[i]);
-    __syncthreads();
-    wave::run(w, wave::FP12_MUL, ACC, IN, ACC, lane, 64);
-  }
-  wave::final_exp(w, ACC, TMP, lane, 64);
-  if (lane == 0) { fp12 e; wave::load12(e, w, ACC); *ok = fp12_is_one(e) ? 1u : 0u; }
-}
-
-__global__ void __launch_bounds__(64) k_final(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok) {
-  __shared__ fp12 sh[64];
-  fp12 acc = fp12_one();
-  for (int i = threadIdx.x; i < npairs; i += 64) fp12_mul(acc, acc, f[i]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = 32; w > 0; w >>= 1) {
-    if (threadIdx.x < w) { fp12 o = sh[threadIdx.x + w]; fp12_mul(acc, acc, o); sh[threadIdx.x] = acc; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    fp12 e;
-    final_exponentiation(e, acc);
-    *ok = fp12_is_one(e) ? 1u : 0u;
-  }
-}
-
-// Exact per-share verify, run only when the RLC batch check failed.
-__global__ void __launch_bounds__(64) k_fallback_verify(int n, const uint32_t* __restrict__ ok,
-                                                        const uint32_t* __restrict__ flags,
-                                                        const uint32_t* __restrict__ share_root,
-                                                        const g2_aff* __restrict__ H,
-                                                        const g2_aff* __restrict__ sig_aff,
-                                                        const g1_aff* __restrict__ pk_aff,
-                                                        uint8_t* __restrict__ verdict) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
-  if (*ok || !cand) { verdict[s] = cand ? 1 : 0; return; }
-  verdict[s] = unit_verify_one(pk_aff[s], sig_aff[s], H[share_root[s]]) ? 1 : 0;
-}
-
-// Reference scan (src/crypto/generic_threshold.rs:133-172) on the batch verdicts.
-// verdict == nullptr: SPECULATIVE selection from the decode flags (every candidate assumed valid);
-// it equals the exact selection whenever the RLC batch check passes.  skip_if_ok != nullptr: the
-// exact re-selection after a failed batch, a no-op when the batch passed.
-__global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
-                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
-                         const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
-                         uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_jobs) return;
-  if (skip_if_ok && *skip_if_ok) return;
-  const uint32_t b = off[j], e = off[j + 1], t = tt[j];
-  const uint32_t n = e - b;
-  if (n < t) { status[j] = SSB_DVF_INSUFFICIENT_SIGNATURES; err[2 * j] = n; err[2 * j + 1] = t; return; }
-  uint32_t cnt = 0;
-  for (uint32_t s = b; s < e; ++s) {
-    const uint64_t id = ids[s];
-    if (id == 0) { status[j] = SSB_DVF_INVALID_OPERATOR_ID; err[2 * j] = 0; err[2 * j + 1] = 0; return; }
-    bool dup = false;
-    for (uint32_t k = 0; k < cnt; ++k) dup = dup || (ids[sel[b + k]] == id);
-    if (dup) continue;
-    if (verdict ? (verdict[s] != 0) : ((flags[s] & FLAG_CANDIDATE) != 0)) {
-      sel[b + cnt] = s;
-      ++cnt;
-      if (cnt >= t) break;
-    }
-  }
-  if (cnt < t) { status[j] = SSB_DVF_INSUFFICIENT_VALID_SIGNATURES; err[2 * j] = cnt; err[2 * j + 1] = t; return; }
-  status[j] = SSB_DVF_OK; err[2 * j] = 0; err[2 * j + 1] = 0;
-}
-
-// unsafe_aggregate: every share of the job, in order; a share that does not decode -> error
-__global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ flags,
-                             uint32_t* __restrict__ sel, uint32_t* __restrict__ tt, int32_t* __restrict__ status,
-                             uint64_t* __restrict__ err) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_jobs) return;
-  const uint32_t b = off[j], e = off[j + 1];
-  tt[j] = e - b;
-  int32_t st = SSB_DVF_OK;
-  for (uint32_t s = b; s < e; ++s) {
-    sel[s] = s;
-    if (!(flags[s] & DEC_OK)) st = SSB_DVF_BAD_SIGNATURE_ENCODING;
-  }
-  status[j] = st; err[2 * j] = 0; err[2 * j + 1] = 0;
-}
-
-// lambda_i = prod_{j!=i} x_j (x_j - x_i)^{-1} mod r (src/crypto/impls/blst.rs:19-39), with the
-// blst convention inverse(0) = 0; one Fr inversion per job (Montgomery's trick).
-__global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
-                           const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
-                           const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
-                           fr* __restrict__ lam) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_jobs || status[j] != SSB_DVF_OK) return;
-  if (skip_if_ok && *skip_if_ok) return;
-  const uint32_t b = off[j], t = tt[j];
-  uint64_t x[SSB_MAX_T];
-  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
-  unit_lagrange(lam + b, x, t);
-}
-
-__global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
-                                                      const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
-                                                      const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
-                                                      const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
-                                                      const uint32_t* __restrict__ skip_if_ok, g2_jac* __restrict__ term) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  if (skip_if_ok && *skip_if_ok) return;
-  const uint32_t j = share_job[s];
-  const uint32_t k = (uint32_t)s - off[j];
-  if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
-  const fr l = lam[s];
-  g2_jac r;
-  unit_combine_term(r, sig_aff[sel[s]], l.l);  // blst_p2_mult(.., 255 bits)
-  term[s] = r;
-}
-
-__global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
-                                                    const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
-                                                    const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
-                                                    uint8_t* __restrict__ out96) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_jobs) return;
-  if (skip_if_ok && *skip_if_ok) return;
-  uint8_t o[96];
-  if (status[j] == SSB_DVF_OK) {
-    unit_combine_sum(o, term + off[j], tt[j]);  // infinity(t) start (src/crypto/impls/blst.rs:74)
-  } else {
-    for (int k = 0; k < 96; ++k) o[k] = 0;
-  }
-  for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
-}
-
-// Batched local partial signing H(root)*sk (SecretKey::sign, src/node/dvfcore.rs:241-243).
-__global__ void __launch_bounds__(64) k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
-                                             const g2_aff* __restrict__ H, uint8_t* __restrict__ out96) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t k[8];
-  for (int w = 0; w < 8; ++w) {
-    const uint8_t* q = sk32le + 32 * (size_t)i + 4 * w;
-    k[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-  }
-  g2_jac r;
-  jac_mul_w4(r, H[root_idx[i]], k, 8);
-  g2_aff a; jac_to_aff(a, r);
-  uint8_t o[96];
-  g2_compress(o, a);
-  for (int b = 0; b < 96; ++b) out96[96 * (size_t)i + b] = o[b];
-}
-
-// sk -> pk = sk*g1, compressed (SecretKey::public_key)
-__global__ void __launch_bounds__(64) k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t k[8];
-  for (int w = 0; w < 8; ++w) {
-    const uint8_t* q = sk32le + 32 * (size_t)i + 4 * w;
-    k[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-  }
-  g1_aff g; g.x = fp_from_c(G1_GEN_X); g.y = fp_from_c(G1_GEN_Y); g.inf = 0;
-  g1_jac r;
-  jac_mul_w4(r, g, k, 8);
-  g1_aff a; jac_to_aff(a, r);
-  uint8_t o[48];
-  g1_compress(o, a);
-  for (int b = 0; b < 48; ++b) out48[48 * (size_t)i + b] = o[b];
-}
-
-__global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* __restrict__ out192) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t o[192];
-  g2_serialize(o, pts[i]);
-  for (int k = 0; k < 192; ++k) out192[192 * (size_t)i + k] = o[k];
-}
-
-__global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) b[i] = a[i];
-}
 
 }  // namespace
 
@@ -437,8 +43,10 @@ __global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restr
 struct ssb_ctx {
   int device = 0;
   hipStream_t stream = nullptr;     // main chain: decode -> RLC -> sums -> Miller -> final exp
-  hipStream_t side[2] = {nullptr, nullptr};  // [0] hash_to_G2, [1] speculative combine
+  hipStream_t side[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] hash_to_G2, [1] speculative combine,
+                                                               // [2] RLC on G2, [3] RLC on G1
   hipEvent_t ev_in = nullptr, ev_hash = nullptr, ev_dec = nullptr, ev_comb = nullptr, ev_out = nullptr;
+  hipEvent_t ev_sdec = nullptr, ev_r2 = nullptr, ev_r1 = nullptr;
   std::string err;
   // workspace arena (grown on demand, never shrunk)
   void* ws = nullptr;
@@ -521,6 +129,7 @@ int fill_dst(ssb_ctx* ctx, dst_arg& d, const uint8_t* dst, size_t dst_len) {
 struct verify_ws {
   g2_aff* H; g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags;
   g2_jac* rsig; g1_jac* rpk; g1_aff* root_sum; g2_jac* part; g2_aff* sig_sum; fp12* f; uint32_t* ok;
+  uint32_t* exc;  // 3n: lane-group exceptions (subgroup, RLC G2, RLC G1)
 };
 constexpr int G2_PARTS = 64;
 
@@ -528,7 +137,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
   return align_up(n_roots * sizeof(g2_aff)) + align_up(n * sizeof(g2_aff)) + align_up(n * sizeof(g1_aff)) +
          align_up(n * 4) * 4 + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
          align_up(n_roots * sizeof(g1_aff)) + align_up(G2_PARTS * sizeof(g2_jac)) + align_up(sizeof(g2_aff)) +
-         align_up((n_roots + 1) * sizeof(fp12)) + align_up(4);
+         align_up((n_roots + 1) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
@@ -538,6 +147,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.gflags = c.take<uint32_t>(n); w.rsig = c.take<g2_jac>(n); w.rpk = c.take<g1_jac>(n);
   w.root_sum = c.take<g1_aff>(n_roots); w.part = c.take<g2_jac>(G2_PARTS); w.sig_sum = c.take<g2_aff>(1);
   w.f = c.take<fp12>(n_roots + 1); w.ok = c.take<uint32_t>(1);
+  w.exc = c.take<uint32_t>(3 * n);
   return w;
 }
 
@@ -553,7 +163,18 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   SSB_HIP(hipEventRecord(ctx->ev_hash, sh));
   if (n) {
     { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags); }
-    { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_check_rlc, dim3(nblk(3 * n, 64)), dim3(64), 0, st, (int)n, seed, w.sflags, w.pflags, w.sig_aff, w.pk_aff, w.gflags, w.rsig, w.rpk); }
+    // lane-group stage: subgroup check (main) || r*sig (side 2) || r*pk (side 3)
+    SSB_HIP(hipEventRecord(ctx->ev_sdec, st));
+    SSB_HIP(hipStreamWaitEvent(ctx->side[2], ctx->ev_sdec, 0));
+    SSB_HIP(hipStreamWaitEvent(ctx->side[3], ctx->ev_sdec, 0));
+    { timed t(ctx, "k_lane_rlc_g2", ctx->side[2]); launch::lane_rlc_g2(ctx->side[2], (int)n, seed, w.sflags, w.sig_aff, w.rsig, w.exc + n); }
+    { timed t(ctx, "k_lane_rlc_g1", ctx->side[3]); launch::lane_rlc_g1(ctx->side[3], (int)n, seed, w.pflags, w.pk_aff, w.rpk, w.exc + 2 * n); }
+    { timed t(ctx, "k_lane_subgroup"); launch::lane_subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags, w.exc); }
+    SSB_HIP(hipEventRecord(ctx->ev_r2, ctx->side[2]));
+    SSB_HIP(hipEventRecord(ctx->ev_r1, ctx->side[3]));
+    SSB_HIP(hipStreamWaitEvent(st, ctx->ev_r2, 0));
+    SSB_HIP(hipStreamWaitEvent(st, ctx->ev_r1, 0));
+    launch::lane_fixup(st, (int)n, seed, w.sflags, w.pflags, w.sig_aff, w.pk_aff, w.exc, w.gflags, w.rsig, w.rpk);
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, w.flags);
     SSB_HIP(hipEventRecord(ctx->ev_dec, st));
     on_decoded();
@@ -586,8 +207,11 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   ctx->device = device_ordinal;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->side[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->side[1], hipStreamNonBlocking) != hipSuccess) { delete ctx; return SSB_EHIP; }
-  for (hipEvent_t* e : {&ctx->ev_in, &ctx->ev_hash, &ctx->ev_dec, &ctx->ev_comb, &ctx->ev_out})
+      hipStreamCreateWithFlags(&ctx->side[1], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->side[2], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->side[3], hipStreamNonBlocking) != hipSuccess) { delete ctx; return SSB_EHIP; }
+  for (hipEvent_t* e : {&ctx->ev_in, &ctx->ev_hash, &ctx->ev_dec, &ctx->ev_comb, &ctx->ev_out, &ctx->ev_sdec,
+                        &ctx->ev_r2, &ctx->ev_r1})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { delete ctx; return SSB_EHIP; }
   *out = ctx;
   return SSB_OK;
@@ -603,7 +227,8 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->io) hipFree(ctx->io);
   for (hipStream_t sd : ctx->side) if (sd) { hipStreamSynchronize(sd); hipStreamDestroy(sd); }
-  for (hipEvent_t e : {ctx->ev_in, ctx->ev_hash, ctx->ev_dec, ctx->ev_comb, ctx->ev_out}) if (e) hipEventDestroy(e);
+  for (hipEvent_t e : {ctx->ev_in, ctx->ev_hash, ctx->ev_dec, ctx->ev_comb, ctx->ev_out, ctx->ev_sdec, ctx->ev_r2, ctx->ev_r1})
+    if (e) hipEventDestroy(e);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -9,6 +9,7 @@
 #include <sstream>
 #include "../../safestakeoperator_amd/csrc/ssb_units.h"
 #include "../../safestakeoperator_amd/csrc/ssb_wave.h"
+#include "../../safestakeoperator_amd/csrc/ssb_lane_ops.h"
 
 #ifdef SSB_OPCOUNT
 ssb_opcounts g_ssb_counts;
@@ -38,6 +39,95 @@ static bool verify_full(const g1_aff& pk, const g2_aff& sig, const g2_aff& h) {
   fp12_mul(f1, f1, f2);
   fp12 e; final_exponentiation(e, f1);
   return fp12_is_one(e);
+}
+
+
+// ---- lane-group programs (host emulation, role loop) against the single-lane code ----
+struct host_group {
+  std::vector<fp> K, S;
+  uint32_t flag = 0;
+  lane::grp g;
+  host_group() : K(lane::LP_NCODE_CONST), S(lane::LP_NSCRATCH + 256) {
+    g = lane::grp{K.data(), S.data(), 0, 0, 0, &flag, 0};
+    lane::lp_init_consts(g);
+  }
+  fp* u(int i) { return &S[lane::LP_NSCRATCH + i]; }
+  int U(int i) const { return lane::LP_NSCRATCH + i; }
+};
+template <class F> static void put_jac(host_group& h, int at, const jac<F>& p) {
+  const fp* q = (const fp*)&p; for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) *h.u(at + i) = q[i];
+}
+template <class F> static bool eq_jac(host_group& h, int at, const jac<F>& p) {
+  const fp* q = (const fp*)&p; bool ok = true;
+  for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) ok = ok && fp_eq(*h.u(at + i), q[i]);
+  return ok;
+}
+template <class F> static void put_aff(host_group& h, int at, const aff<F>& p) {
+  const fp* q = (const fp*)&p; for (int i = 0; i < (int)(2 * sizeof(F) / sizeof(fp)); ++i) *h.u(at + i) = q[i];
+}
+template <class F> static bool same_point(host_group& h, int at, const jac<F>& p) {
+  jac<F> r; fp* q = (fp*)&r; for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) q[i] = *h.u(at + i);
+  aff<F> a, b; jac_to_aff(a, r); jac_to_aff(b, p);
+  return a.inf == b.inf && (a.inf || (f_eq(a.x, b.x) && f_eq(a.y, b.y)));
+}
+
+static void lane_selftest(const uint8_t* seed32) {
+  int ok = 0, n = 0;
+  host_group h;
+  lane::grp& g = h.g;
+  g2_aff P, Q, Hraw;
+  uint8_t m[32];
+  for (int k = 0; k < 32; ++k) m[k] = seed32[k];
+  hash_to_g2(P, m, (const uint8_t*)DST, (int)strlen(DST));
+  m[0] ^= 1; hash_to_g2(Q, m, (const uint8_t*)DST, (int)strlen(DST));
+  { // a point on E2 that is NOT in G2: the isogeny image before cofactor clearing
+    uint8_t uni[256]; m[1] ^= 7; expand_message_xmd_256(uni, m, (const uint8_t*)DST, (int)strlen(DST));
+    fp2 u; fp_from_be64_mod(u.c0, uni); fp_from_be64_mod(u.c1, uni + 64);
+    fp2 x, y; map_to_curve_sswu(x, y, u); iso3_map(Hraw, x, y); }
+  g2_jac J1, J2, t;
+  jac_from_aff(J1, P); jac_dbl(J1, J1); jac_add_aff(J1, J1, Q);        // 2P + Q, Z != 1
+  jac_from_aff(J2, Q); jac_dbl(J2, J2); jac_add_aff(J2, J2, Q);        // 3Q
+  uint32_t exc = 0;
+  // G2 dbl / add / madd: bit-identical Jacobian coordinates
+  put_jac(h, 0, J1); lane::g2_dbl(g, h.U(0), h.U(6)); jac_dbl(t, J1); ok += eq_jac(h, 6, t); ++n;
+  put_jac(h, 0, J1); put_jac(h, 6, J2); lane::g2_add(g, h.U(0), h.U(6), h.U(12), exc); jac_add(t, J1, J2); ok += eq_jac(h, 12, t); ++n;
+  ok += exc == 0; ++n;
+  put_jac(h, 0, J1); put_aff(h, 6, Q); lane::g2_madd(g, h.U(0), h.U(6), h.U(12), exc); jac_add_aff(t, J1, Q); ok += eq_jac(h, 12, t); ++n;
+  ok += exc == 0; ++n;
+  // in-place (d == a)
+  put_jac(h, 0, J1); put_jac(h, 6, J2); lane::g2_add(g, h.U(0), h.U(6), h.U(0), exc); jac_add(t, J1, J2); ok += eq_jac(h, 0, t); ++n;
+  // exceptional: J1 + J1 and J1 + (-J1) raise exc
+  { uint32_t e2 = 0; put_jac(h, 0, J1); put_jac(h, 6, J1); lane::g2_add(g, h.U(0), h.U(6), h.U(12), e2); ok += e2 == 1; ++n; }
+  { uint32_t e2 = 0; g2_jac nj; jac_neg(nj, J1); put_jac(h, 0, J1); put_jac(h, 6, nj); lane::g2_add(g, h.U(0), h.U(6), h.U(12), e2); ok += e2 == 1; ++n; }
+  { uint32_t e2 = 0; g2_jac inf; jac_set_inf(inf); put_jac(h, 0, inf); put_jac(h, 6, J1); lane::g2_add(g, h.U(0), h.U(6), h.U(12), e2); ok += e2 == 1; ++n; }
+  // 64-bit windowed multiplication (odd scalars)
+  for (int r = 0; r < 4; ++r) {
+    uint64_t k = rlc_scalar(0x1234 + r, (uint64_t)r) | 1ull;
+    if (r == 3) k = 1ull;
+    uint32_t e = 0;
+    put_aff(h, 0, P);
+    lane::g2_mul_u64_odd(g, h.U(0), k, h.U(4), h.U(52), h.U(58), e);
+    const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+    jac_mul_aff(t, P, kw, 2);
+    ok += same_point(h, 52, t) && e == 0; ++n;
+  }
+  // G1: generator multiples
+  { g1_aff G1; G1.x = fp_from_c(G1_GEN_X); G1.y = fp_from_c(G1_GEN_Y); G1.inf = 0;
+    g1_jac A1, A2, t1; jac_from_aff(A1, G1); jac_dbl(A1, A1); jac_add_aff(A1, A1, G1); jac_from_aff(A2, G1); jac_dbl(A2, A2);
+    put_jac(h, 0, A1); lane::g1_dbl(g, h.U(0), h.U(3)); jac_dbl(t1, A1); ok += eq_jac(h, 3, t1); ++n;
+    put_jac(h, 0, A1); put_jac(h, 3, A2); lane::g1_add(g, h.U(0), h.U(3), h.U(6), exc); jac_add(t1, A1, A2); ok += eq_jac(h, 6, t1); ++n;
+    put_jac(h, 0, A1); put_aff(h, 3, G1); lane::g1_madd(g, h.U(0), h.U(3), h.U(6), exc); jac_add_aff(t1, A1, G1); ok += eq_jac(h, 6, t1); ++n;
+    uint64_t k = rlc_scalar(99, 5) | 1ull; uint32_t e = 0;
+    put_aff(h, 0, G1); lane::g1_mul_u64_odd(g, h.U(0), k, h.U(2), h.U(30), h.U(33), e);
+    const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+    jac_mul_aff(t1, G1, kw, 2); ok += same_point(h, 30, t1) && e == 0; ++n; }
+  // subgroup check: a G2 point passes, the raw isogeny image fails
+  { uint32_t e = 0; put_aff(h, 0, P); bool in = lane::g2_subgroup_check(g, h.U(0), h.U(4), h.U(10), e);
+    ok += in && e == 0 && g2_in_subgroup(P); ++n; }
+  { uint32_t e = 0; put_aff(h, 0, Hraw); bool in = lane::g2_subgroup_check(g, h.U(0), h.U(4), h.U(10), e);
+    ok += !in && (e == 0) && !g2_in_subgroup(Hraw); ++n; }
+  ok += exc == 0; ++n;
+  printf("%d %d\n", ok, n);
 }
 
 int main() {
@@ -194,6 +284,9 @@ int main() {
         wave::miller(w, B0, 0, 1);
         wave::load12(r2, w, B0); ok += fp12_eq(f1, r2); ++n; }
       printf("%d %d\n", ok, n);
+    } else if (cmd == "lane") {  // lane <seed32hex>: lane-group programs vs single-lane code
+      std::string s; is >> s; auto b = unhex(s);
+      lane_selftest(b.data());
     } else if (cmd.empty()) {
       continue;
     } else {

@@ -92,3 +92,20 @@ def test_wave_tables_are_current():
     before = open(hdr).read()
     subprocess.run([sys.executable, gen], check=True, capture_output=True)
     assert open(hdr).read() == before
+
+
+def test_lane_programs_match_single_lane(host_exe):
+    """The generated lane-group programs (G2/G1 dbl, add, mixed add with exception checks, the
+    windowed 64-bit multiplication, the subgroup check) reproduce the single-lane code."""
+    for seed in ("00" * 31 + "01", "5a" * 32):
+        ok, n = _run(host_exe, ["lane " + seed])[0].split()
+        assert ok == n, (ok, n)
+
+
+def test_lane_programs_are_current():
+    import subprocess, sys
+    gen = os.path.join(HERE, "..", "safestakeoperator_amd", "csrc", "gen_lane_progs.py")
+    hdr = os.path.join(HERE, "..", "safestakeoperator_amd", "csrc", "ssb_lane_progs.h")
+    before = open(hdr).read()
+    subprocess.run([sys.executable, gen], check=True, capture_output=True)
+    assert open(hdr).read() == before
