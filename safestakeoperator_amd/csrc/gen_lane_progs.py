@@ -275,67 +275,144 @@ def syms_of(f):
     return list(f.c.keys())
 
 
+def wt(f):
+    """Bound of a form's value in units of p: every term (|c| v mod p, or p minus it) is <= p."""
+    return len(f.c)
+
+
+def subst(f, sym, g):
+    c = f.c.get(sym, 0)
+    if not c:
+        return f
+    d = dict(f.c)
+    del d[sym]
+    return L(d) + g * c
+
+
 class Sched:
-    """Turns a traced program into stages.  A stage is ("lin", items) -- materialisations whose
-    inputs are ready, reduced mod p and stored --, ("prod", items) -- at most G products -- ,
-    ("chk", items) -- zero tests -- or ("out", items).  Items: ("P", i), ("M", j), ("O", k),
-    ("C", c, k)."""
+    """Turns a traced program into stages.  A stage is ("lin", items) -- materialisations,
+    reduced mod p and stored, and zero checks --, ("prod", items) -- at most G products -- or
+    ("out", items) -- outputs (and leftover checks).  Items: ("P", i), ("M", j), ("O", k),
+    ("C", c, k).  Materialisations written in the formulas are SOFT: one is inlined into its
+    consumers whenever the consumers stay within the bounds (product operands wx * wy <= 9,
+    other forms <= 8 terms), which removes linear stages from the dependency chain."""
 
     def __init__(self, prog, outs):
         self.p, self.G = prog, prog.G
-        # operand forms with > MAXT terms become materialisations
-        self.prods = [(self._limit(x), self._limit(y)) for x, y in prog.prods]
-        # every materialisation (including the ones created here) has <= MAXM terms
-        j = 0
-        while j < len(prog.mats):
-            prog.mats[j] = self._chunk(prog.mats[j])
-            j += 1
-        self.outs = [self._chunk(o) for o in outs]
-        self.checks = [[self._chunk(c) for c in chk] for chk in prog.checks]
-        j = 0
-        while j < len(prog.mats):
-            prog.mats[j] = self._chunk(prog.mats[j])
-            j += 1
-        self.mats = prog.mats
+        self.prods = [list(xy) for xy in prog.prods]
+        self.mats = list(prog.mats)
+        self.alive = [True] * len(self.mats)
+        self.outs = list(outs)
+        self.checks = [list(c) for c in prog.checks]
+        self._eliminate()
+        self._enforce()
+
+    # -- every form that may reference a symbol --
+    def _consumers(self):
+        for i, xy in enumerate(self.prods):
+            yield ("P", i)
+        for j in range(len(self.mats)):
+            if self.alive[j]:
+                yield ("M", j)
+        for k in range(len(self.outs)):
+            yield ("O", k)
+        for c, chk in enumerate(self.checks):
+            for k in range(len(chk)):
+                yield ("C", c, k)
+
+    def _ok(self, it, forms):
+        if it[0] == "P":
+            return wt(forms[0]) * wt(forms[1]) <= 9
+        return wt(forms[0]) <= MAXM
+
+    def _get(self, it):
+        if it[0] == "P":
+            return self.prods[it[1]]
+        if it[0] == "M":
+            return [self.mats[it[1]]]
+        if it[0] == "O":
+            return [self.outs[it[1]]]
+        return [self.checks[it[1]][it[2]]]
+
+    def _set(self, it, forms):
+        if it[0] == "P":
+            self.prods[it[1]] = forms
+        elif it[0] == "M":
+            self.mats[it[1]] = forms[0]
+        elif it[0] == "O":
+            self.outs[it[1]] = forms[0]
+        else:
+            self.checks[it[1]][it[2]] = forms[0]
+
+    def _eliminate(self):
+        changed = True
+        while changed:
+            changed = False
+            for j in range(len(self.mats)):
+                if not self.alive[j]:
+                    continue
+                sym = ("M", j)
+                g = self.mats[j]
+                trial = []
+                ok = True
+                for it in self._consumers():
+                    if it == ("M", j):
+                        continue
+                    fs = self._get(it)
+                    if not any(sym in f.c for f in fs):
+                        continue
+                    nf = [subst(f, sym, g) for f in fs]
+                    if not self._ok(it, nf):
+                        ok = False
+                        break
+                    trial.append((it, nf))
+                if ok:
+                    for it, nf in trial:
+                        self._set(it, nf)
+                    self.alive[j] = False
+                    changed = True
+
+    def _new_mat(self, f):
+        self.mats.append(f)
+        self.alive.append(True)
+        return L({("M", len(self.mats) - 1): 1})
 
     def _chunk(self, f):
-        """f with <= MAXM terms, splitting it into materialised parts when longer."""
-        if f.weight() <= MAXM:
+        """f with <= MAXM terms: longer forms become sums of materialised parts."""
+        if wt(f) <= MAXM:
             return f
-        parts, cur, w = [], {}, 0
-        for s, c in sorted(f.c.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
-            sg = 1 if c > 0 else -1
-            n = abs(c)
-            while n:
-                take = min(n, MAXM - w)
-                cur[s] = cur.get(s, 0) + sg * take
-                w += take
-                n -= take
-                if w == MAXM:
-                    parts.append(L(cur))
-                    cur, w = {}, 0
-        if cur:
-            parts.append(L(cur))
+        items = sorted(f.c.items(), key=lambda kv: (kv[0][0], str(kv[0][1])))
         acc = L()
-        for q in parts:
-            acc = acc + self.p.mat(q)
+        for i in range(0, len(items), MAXM):
+            part = L(dict(items[i:i + MAXM]))
+            acc = acc + self._new_mat(part)
         return self._chunk(acc)
 
-    def _limit(self, f):
-        if f.weight() <= MAXT:
-            return f
-        return self.p.mat(self._chunk(f))
+    def _enforce(self):
+        for i, (x, y) in enumerate(self.prods):
+            while wt(x) * wt(y) > 9:
+                if wt(x) >= wt(y):
+                    x = self._new_mat(self._chunk(x))
+                else:
+                    y = self._new_mat(self._chunk(y))
+            self.prods[i] = [x, y]
+        j = 0
+        while j < len(self.mats):
+            if self.alive[j]:
+                self.mats[j] = self._chunk(self.mats[j])
+            j += 1
+        self.outs = [self._chunk(o) for o in self.outs]
+        self.checks = [[self._chunk(c) for c in chk] for chk in self.checks]
 
     def schedule(self):
-        P, G = self.p, self.G
-        mats = self.mats
-        # dependency heights for priorities
+        G = self.G
+        mats = [j for j in range(len(self.mats)) if self.alive[j]]
         users = {}
         for i, (x, y) in enumerate(self.prods):
             for s in syms_of(x) + syms_of(y):
                 users.setdefault(s, []).append(("P", i))
-        for j, f in enumerate(mats):
-            for s in syms_of(f):
+        for j in mats:
+            for s in syms_of(self.mats[j]):
                 users.setdefault(s, []).append(("M", j))
         memo = {}
 
@@ -351,18 +428,25 @@ class Sched:
         avail = set()
         stages = []
         done_p, done_m = set(), set()
+        pend_chk = [("C", c, k) for c, chk in enumerate(self.checks) for k in range(len(chk))]
 
         def ready(f):
             return all(s[0] in "ABK" or s in avail for s in syms_of(f))
 
+        def take_checks(n):
+            got = [it for it in pend_chk if ready(self.checks[it[1]][it[2]])][:n]
+            for it in got:
+                pend_chk.remove(it)
+            return got
+
         n_rounds = 0
         while len(done_p) < len(self.prods) or len(done_m) < len(mats):
-            # linear stage: every ready materialisation, in dependency levels
             while True:
-                lvl = [("M", j) for j in range(len(mats)) if ("M", j) not in done_m and ready(mats[j])]
+                lvl = [("M", j) for j in mats if ("M", j) not in done_m and ready(self.mats[j])]
                 if not lvl:
                     break
-                stages.append(("lin", lvl))
+                pad = (-len(lvl)) % G
+                stages.append(("lin", lvl + take_checks(pad)))
                 for it in lvl:
                     done_m.add(it)
                     avail.add(it)
@@ -370,7 +454,7 @@ class Sched:
                   if ("P", i) not in done_p and ready(self.prods[i][0]) and ready(self.prods[i][1])]
             if not rp:
                 if len(done_p) < len(self.prods) or len(done_m) < len(mats):
-                    raise RuntimeError("%s: deadlock" % P.name)
+                    raise RuntimeError("%s: deadlock" % self.p.name)
                 break
             rp.sort(key=lambda it: -height(it))
             pick = rp[:G]
@@ -379,14 +463,12 @@ class Sched:
             for it in pick:
                 done_p.add(it)
                 avail.add(it)
-        # checks: as soon as ready -> put them in a final check stage (cheap, no store)
-        chk_items = [("C", c, k) for c, chk in enumerate(self.checks) for k in range(len(chk))]
-        if chk_items:
-            stages.append(("chk", chk_items))
         outs = [("O", k) for k in range(len(self.outs))]
-        stages.append(("out", outs))
+        stages.append(("out", outs + take_checks(len(pend_chk))))
+        assert not pend_chk
         self.stages = stages
         self.n_rounds = n_rounds
+        self.n_mats = len(mats)
         return stages
 
     def form_of(self, it):
@@ -398,21 +480,23 @@ class Sched:
             return self.checks[it[1]][it[2]]
         raise KeyError(it)
 
+    def forms_of(self, it):
+        return self.prods[it[1]] if it[0] == "P" else [self.form_of(it)]
+
     def allocate(self):
-        """Scratch slots by liveness at stage granularity."""
+        """Scratch slots by liveness at stage granularity (a value's slot is reusable from the
+        stage after its last read; never within a stage, whose passes may run in sequence)."""
         last_use = {}
         for si, (kind, items) in enumerate(self.stages):
             for it in items:
-                forms = self.prods[it[1]] if it[0] == "P" else (self.form_of(it),)
-                for f in forms:
+                for f in self.forms_of(it):
                     for s in syms_of(f):
                         if s[0] in "PM":
                             last_use[s] = si
         slot = {}
         free = list(range(N_SCR))
-        busy = {}  # slot -> symbol
+        busy = {}
         for si, (kind, items) in enumerate(self.stages):
-            # release values whose last use is before this stage
             for sl, s in list(busy.items()):
                 if last_use.get(s, -1) < si:
                     del busy[sl]
@@ -421,10 +505,8 @@ class Sched:
             for it in items:
                 if it[0] in "PM":
                     if it not in last_use:
-                        slot[it] = None  # dead value (never read): junk slot
+                        slot[it] = None
                         continue
-                    if not free:
-                        raise RuntimeError("%s: out of scratch slots" % self.p.name)
                     sl = free.pop(0)
                     busy[sl] = it
                     slot[it] = sl
@@ -452,21 +534,19 @@ class Sched:
 # emission
 # ------------------------------------------------------------------------------------------
 def terms_of(f):
-    """-> list of (sign, sym) with |coef| repetition, positives first."""
-    pos, neg = [], []
-    for s, c in sorted(f.c.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
-        (pos if c > 0 else neg).extend([s] * abs(c))
-    return [(0, s) for s in pos] + [(1, s) for s in neg]
+    """-> list of (sign, magnitude, sym): unit terms first (cheap), then scaled ones."""
+    items = sorted(f.c.items(), key=lambda kv: (abs(kv[1]) != 1, kv[1] < 0, kv[0][0], str(kv[0][1])))
+    return [(1 if c < 0 else 0, abs(c), s) for s, c in items]
 
 
 class Emitter:
     def __init__(self, sch):
         self.s, self.G = sch, sch.G
         self.lines = []
-        self.tables = []  # for G > 8: (name, bytes)
+        self.tables = []
 
-    def sel(self, codes, tag):
-        """per-role 8-bit codes -> a C expression of `role`."""
+    def sel(self, codes):
+        """per-role 8-bit values -> a C expression of `role`."""
         G = self.G
         codes = list(codes) + [0] * (G - len(codes))
         if G <= 8:
@@ -485,41 +565,63 @@ class Emitter:
         return "0x%xull" % v
 
     def emit_form(self, var, forms):
-        """forms: per role (L or None). Accumulates var = sum of +-terms (value < weight * p)."""
-        G = self.G
+        """var = sum over terms of (+-)(|c| v mod p): each term <= p, so var <= wt * p."""
+        G, out = self.G, self.lines
         tl = [terms_of(f) if f is not None else [] for f in forms]
         T = max([len(t) for t in tl] + [1])
         for k in range(T):
-            codes, sg = [], []
+            codes, sg, mg = [], [], []
             for r in range(G):
                 if r < len(tl) and k < len(tl[r]):
-                    sgn, sym = tl[r][k]
-                    codes.append(self.s.code(sym)); sg.append(sgn)
+                    sgn, m, sym = tl[r][k]
+                    codes.append(self.s.code(sym)); sg.append(sgn); mg.append(m)
                 else:
-                    codes.append(0); sg.append(0)
-            src = self.sel(codes, var)
-            uni = "pos" if all(b == 0 for b in sg) else ("neg" if all(b == 1 for b in sg) else "mix")
-            if k == 0:
-                if uni == "pos":
-                    self.lines.append("      lp_ld(%s, g, %s);" % (var, src))
-                elif uni == "neg":
-                    self.lines.append("      lp_ld_neg(%s, g, %s);" % (var, src))
-                else:
-                    self.lines.append("      lp_ld_sgn(%s, g, %s, LP_BIT(%s));" % (var, src, self.bits(sg)))
+                    codes.append(0); sg.append(0); mg.append(1)
+            src = self.sel(codes)
+            first = k == 0
+            if all(m == 1 for m in mg):
+                val = None
             else:
-                if uni == "pos":
-                    self.lines.append("      lp_acc(%s, g, %s);" % (var, src))
-                elif uni == "neg":
-                    self.lines.append("      lp_acc_neg(%s, g, %s);" % (var, src))
+                # u = m * v mod p, left to right over the bits of m (per-role m)
+                nb = max(m.bit_length() for m in mg)
+                out.append("      { fp v_, u_; lp_ld(v_, g, %s);" % src)
+                top = [(m >> (nb - 1)) & 1 for m in mg]
+                if all(top):
+                    out.append("        u_ = v_;")
                 else:
-                    self.lines.append("      lp_acc_sgn(%s, g, %s, LP_BIT(%s));" % (var, src, self.bits(sg)))
+                    out.append("        u_ = fp_zero(); lp_sel(u_, v_, u_, LP_BIT(%s));" % self.bits(top))
+                for bit in range(nb - 2, -1, -1):
+                    out.append("        lp_dbl_mod(u_);")
+                    bs = [(m >> bit) & 1 for m in mg]
+                    if all(bs):
+                        out.append("        lp_add_mod(u_, v_);")
+                    elif any(bs):
+                        out.append("        lp_add_mod_sel(u_, v_, LP_BIT(%s));" % self.bits(bs))
+                val = "u_"
+            uni = "pos" if all(b == 0 for b in sg) else ("neg" if all(b == 1 for b in sg) else "mix")
+            if val is None:
+                if first:
+                    fn = {"pos": "lp_ld(%s, g, %s);", "neg": "lp_ld_neg(%s, g, %s);",
+                          "mix": "lp_ld_sgn(%s, g, %s, LP_BIT(" + self.bits(sg) + "));"}[uni]
+                else:
+                    fn = {"pos": "lp_acc(%s, g, %s);", "neg": "lp_acc_neg(%s, g, %s);",
+                          "mix": "lp_acc_sgn(%s, g, %s, LP_BIT(" + self.bits(sg) + "));"}[uni]
+                out.append("      " + fn % (var, src))
+            else:
+                if first:
+                    fn = {"pos": "%s = u_;", "neg": "lp_pminus(%s, u_);",
+                          "mix": "{ fp n_; lp_pminus(n_, u_); lp_sel(%s, n_, u_, LP_BIT(" + self.bits(sg) + ")); }"}[uni]
+                else:
+                    fn = {"pos": "lp_add_raw(%s, u_);", "neg": "{ fp n_; lp_pminus(n_, u_); lp_add_raw(%s, n_); }",
+                          "mix": "{ fp n_; lp_pminus(n_, u_); lp_sel(n_, n_, u_, LP_BIT(" + self.bits(sg) + ")); lp_add_raw(%s, n_); }"}[uni]
+                out.append("        " + fn % var + " }")
         return T
 
     def reduce_line(self, forms):
-        """Forms evaluate to values <= w*p (negative terms enter as p - v); reduce to [0, p)."""
-        w = max(f.weight() for f in forms)
-        neg = any(c < 0 for f in forms for c in f.c.values())
-        if w <= 1 and not neg:
+        """Forms evaluate to values <= w*p (terms <= p each); reduce to [0, p)."""
+        w = max(wt(f) for f in forms)
+        exact = all(wt(f) <= 1 and all(c == 1 for c in f.c.values()) for f in forms)
+        if exact:
             return None
         steps = 1 if w <= 1 else (2 if w <= 2 else (3 if w <= 4 else 4))
         return "      lp_reduce%d(LP_T);" % steps
@@ -530,18 +632,17 @@ class Emitter:
         out = self.lines
         nout = len(s.outs)
         staged = nout > G
-        stage_base = s.n_scratch  # output staging after the scratch area
+        stage_base = s.n_scratch
         n_scr_total = s.n_scratch + (nout if staged else 0)
         assert n_scr_total <= N_SCR, (P.name, n_scr_total)
         junk = C_SCR + s.junk
-        # check bits: component k of check c -> bit (offset(c) + k); fires when all set
         cbit, masks, b = {}, [], 0
         for c, chk in enumerate(s.checks):
             for k in range(len(chk)):
-                cbit[(c, k)] = 1 << (b + k)
+                cbit[(c, k)] = b + k
             masks.append(((1 << len(chk)) - 1) << b)
             b += len(chk)
-        assert b <= 32
+        assert b <= 30
         self.masks = masks
         for (kind, items) in s.stages:
             for p0 in range(0, len(items), G):
@@ -557,7 +658,7 @@ class Emitter:
                     out.append("    }")
                     dst = [C_SCR + s.slot[it] if s.slot[it] is not None else junk for it in chunk]
                     dst += [junk] * (G - len(dst))
-                    out.append("    LP_FOR(%d) lp_st(g, %s, LP_T);" % (G, self.sel(dst, "d")))
+                    out.append("    LP_FOR(%d) lp_st(g, %s, LP_T);" % (G, self.sel(dst)))
                 else:
                     forms = [s.form_of(it) for it in chunk]
                     out.append("    LP_FOR(%d) {" % G)
@@ -566,27 +667,21 @@ class Emitter:
                     if red:
                         out.append(red)
                     out.append("    }")
-                    if kind == "chk":
-                        bits = [cbit[(it[1], it[2])] for it in chunk] + [0] * (G - len(chunk))
-                        v = 0
-                        for r, bb in enumerate(bits):  # per-role bit index (5 bits) packed, 0x1f = none
-                            idx = bb.bit_length() - 1 if bb else 31
-                            v |= idx << (5 * r) if G <= 12 else 0
-                        if G <= 12:
-                            out.append("    LP_FOR(%d) lp_chk(g, LP_T, (uint32_t)((0x%xull >> (5 * role)) & 31u));" % (G, v))
-                        else:
-                            self.tables.append(("%s_c%d" % (P.name, len(self.tables)),
-                                                [(bb.bit_length() - 1) if bb else 31 for bb in bits]))
-                            out.append("    LP_FOR(%d) lp_chk(g, LP_T, LP_SELT(%s));" % (G, self.tables[-1][0]))
-                    else:
-                        if kind == "lin":
-                            dst = [C_SCR + s.slot[it] if s.slot[it] is not None else junk for it in chunk]
+                    dst, cb = [], []
+                    for it in chunk:
+                        if it[0] == "C":
+                            dst.append(junk); cb.append(cbit[(it[1], it[2])])
+                        elif it[0] == "M":
+                            dst.append(C_SCR + s.slot[it] if s.slot[it] is not None else junk); cb.append(31)
                         elif staged:
-                            dst = [C_SCR + stage_base + it[1] for it in chunk]
+                            dst.append(C_SCR + stage_base + it[1]); cb.append(31)
                         else:
-                            dst = [C_D + it[1] for it in chunk]
-                        dst += [junk] * (G - len(dst))
-                        out.append("    LP_FOR(%d) lp_st(g, %s, LP_T);" % (G, self.sel(dst, "d")))
+                            dst.append(C_D + it[1]); cb.append(31)
+                    dst += [junk] * (G - len(dst))
+                    cb += [31] * (G - len(cb))
+                    out.append("    LP_FOR(%d) lp_st(g, %s, LP_T);" % (G, self.sel(dst)))
+                    if any(c != 31 for c in cb):
+                        out.append("    LP_FOR(%d) lp_chk(g, LP_T, %s);" % (G, self.sel(cb)))
                 out.append("    LP_SYNC();")
                 out.append("  }")
         if staged:
@@ -596,8 +691,8 @@ class Emitter:
                 dst = [C_D + p0 + r for r in range(n)] + [junk] * (G - n)
                 out.append("  {  // copy outputs %d..%d" % (p0, p0 + n - 1))
                 out.append("    LP_DECL_T;")
-                out.append("    LP_FOR(%d) lp_ld(LP_T, g, %s);" % (G, self.sel(src, "s")))
-                out.append("    LP_FOR(%d) lp_st(g, %s, LP_T);" % (G, self.sel(dst, "d")))
+                out.append("    LP_FOR(%d) lp_ld(LP_T, g, %s);" % (G, self.sel(src)))
+                out.append("    LP_FOR(%d) lp_st(g, %s, LP_T);" % (G, self.sel(dst)))
                 out.append("    LP_SYNC();")
                 out.append("  }")
         self.n_scr_total = n_scr_total
@@ -618,11 +713,12 @@ def emit_header(progs):
         em = Emitter(sch)
         body = em.emit()
         nprod = len(sch.prods)
+        nmat = sch.n_mats
         for name, codes in em.tables:
             hdr.append("SSB_LP_TABLE uint8_t %s[%d] = {%s};" % (name, len(codes), ", ".join(map(str, codes))))
         hdr.append("// %s: G=%d, %d products in %d rounds (%.0f%% lane use), %d materialisations, %d outputs, "
                    "%d scratch slots, %d stages"
-                   % (P.name, P.G, nprod, sch.n_rounds, 100.0 * nprod / max(1, sch.n_rounds * P.G), len(sch.mats),
+                   % (P.name, P.G, nprod, sch.n_rounds, 100.0 * nprod / max(1, sch.n_rounds * P.G), nmat,
                       len(sch.outs), em.n_scr_total, len(sch.stages)))
         summary.append((P.name, P.G, nprod, sch.n_rounds, len(sch.stages), em.n_scr_total))
         hdr.append("constexpr int %s_G = %d, %s_SCRATCH = %d, %s_NOUT = %d, %s_ROUNDS = %d;"
@@ -630,7 +726,7 @@ def emit_header(progs):
         hdr.append("constexpr uint32_t %s_CHECK_MASKS[%d] = {%s};"
                    % (P.name, max(1, len(em.masks)), ", ".join("0x%xu" % m for m in em.masks) or "0u"))
         hdr.append("constexpr int %s_NCHECK = %d;" % (P.name, len(em.masks)))
-        hdr.append("template <class GR> SSB_LP_FN void lp_%s(GR& g) {" % P.name.lower())
+        hdr.append("template <class GR> SSB_LP_FN void lp_%s(GR g) {" % P.name.lower())
         hdr += body
         hdr.append("}")
     hdr.append("}  // namespace lane")
@@ -658,7 +754,7 @@ def main():
     ps = programs()
     txt, summary = emit_header(ps)
     consts = const_init_table()
-    init = ["template <class GR> SSB_LP_FN void lp_init_consts(GR& g) {",
+    init = ["template <class GR> SSB_LP_FN void lp_init_consts(GR g) {",
             "  LP_FOR_ALL_CONSTS(i) {"]
     init.append("    fp v;")
     init.append("    switch (i) {")

@@ -11,6 +11,7 @@
 #pragma once
 #include <cstdint>
 #include "ssb_consts.h"
+#include "ssb_exp_chains.h"
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
@@ -442,6 +443,28 @@ SSB_FN void fp_pow(fp& r, const fp& a, const uint32_t* e) {
 }
 SSB_INL void fp_inv_fermat(fp& r, const fp& a) { fp_pow(r, a, EXP_P_MINUS_2); }  // inv(0) = 0
 
+// a^e for a fixed exponent given as a sliding-window schedule (gen_exp_chains.py): 8 odd powers,
+// then per step `sq` squarings and a multiplication by a^digit.  The schedule index is uniform,
+// so the table pick is a select chain, not an indexed (scratch) access.
+SSB_INL fp fp_pick8(const fp* t, int i) {
+  fp r = t[0];
+  for (int k = 1; k < 8; ++k) if (i == k) r = t[k];
+  return r;
+}
+SSB_FN void fp_pow_sw(fp& r, const fp& a, const uint8_t* sch, int n) {
+  fp t[8], a2;
+  t[0] = a;
+  fp_sqr(a2, a);
+  for (int i = 1; i < 8; ++i) fp_mul(t[i], t[i - 1], a2);
+  fp acc = fp_pick8(t, (sch[1] - 1) >> 1);
+  for (int s = 1; s < n; ++s) {
+    const int sq = sch[2 * s], d = sch[2 * s + 1];
+    for (int k = 0; k < sq; ++k) fp_sqr(acc, acc);
+    if (d) { const fp m = fp_pick8(t, (d - 1) >> 1); fp_mul(acc, acc, m); }
+  }
+  r = acc;
+}
+
 // Binary extended Euclid (variable time: inputs on this path are public).  For the Montgomery
 // form aR it returns (aR)^{-1} * R^3 / R = a^{-1} R.  inv(0) = 0.  About 4x fewer dependent
 // instructions than the Fermat chain, which matters on the single-lane inversions of the
@@ -490,7 +513,7 @@ SSB_FN void fp_inv(fp& r, const fp& a) {
 // returns true iff a is a square; r = a^((p+1)/4) (a root when it is)
 SSB_FN bool fp_sqrt(fp& r, const fp& a) {
   fp s, s2;
-  fp_pow(s, a, EXP_P_PLUS_1_DIV_4);
+  fp_pow_sw(s, a, EXPW_P_PLUS_1_DIV_4, EXPW_P_PLUS_1_DIV_4_N);
   fp_sqr(s2, s);
   r = s;
   return fp_eq(s2, a);
@@ -627,7 +650,7 @@ SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) {
   fp c, half = fp_from_c(FP_HALF);
   fp_add(c, a.c0, s);
   fp_mul(c, c, half);                       // c = (a0 + s)/2  (nonzero since a1 != 0)
-  fp_pow(t, c, EXP_P_MINUS_3_DIV_4);        // t = c^((p-3)/4)
+  fp_pow_sw(t, c, EXPW_P_MINUS_3_DIV_4, EXPW_P_MINUS_3_DIV_4_N);  // t = c^((p-3)/4)
   fp x, x2;
   fp_mul(x, c, t);                          // x^2 = c if c is a square, else -c
   fp_sqr(x2, x);

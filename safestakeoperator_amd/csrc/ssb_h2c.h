@@ -189,6 +189,46 @@ SSB_FN void clear_cofactor_g2(g2_jac& r, const g2_jac& P) {
   jac_add(r, t3, n);
 }
 
+// ---- the same hash split into the stages of the batched pipeline (ssb_k_hash.hip) ----
+// stage 1: u0, u1 from expand_message_xmd
+SSB_FN void h2c_field(fp2& u0, fp2& u1, const uint8_t* msg32, const uint8_t* dst, int dst_len) {
+  uint8_t uni[256];
+  expand_message_xmd_256(uni, msg32, dst, dst_len);
+  fp_from_be64_mod(u0.c0, uni);
+  fp_from_be64_mod(u0.c1, uni + 64);
+  fp_from_be64_mod(u1.c0, uni + 128);
+  fp_from_be64_mod(u1.c1, uni + 192);
+}
+// stage 2 (one lane per candidate): x1 (cand 0) or x2 = Z u^2 x1 (cand 1), and a square root of
+// g(x); returns whether g(x) is a square.  map_to_curve_sswu takes x1 when g(x1) is a square,
+// else x2 (then g(x2) is), exactly as the sequential code above.
+SSB_FN bool sswu_candidate(fp2& x, fp2& y, const fp2& u, int cand) {
+  fp2 Z = fp2_from_c(SSWU_Z);
+  fp2 zu2, den, x1, t, g;
+  fp2_sqr(zu2, u);
+  fp2_mul(zu2, zu2, Z);
+  fp2_sqr(den, zu2);
+  fp2_add(den, den, zu2);
+  if (fp2_is_zero(den)) {
+    x1 = fp2_from_c(SSWU_B_OVER_ZA);
+  } else {
+    fp2_inv(t, den);
+    fp2 one = fp2_one();
+    fp2_add(t, t, one);
+    fp2 nboa = fp2_from_c(SSWU_MINUS_B_OVER_A);
+    fp2_mul(x1, nboa, t);
+  }
+  if (cand) fp2_mul(x, zu2, x1); else x = x1;
+  sswu_g(g, x);
+  return fp2_sqrt(y, g);
+}
+// stage 2 tail: sign of y, then the 3-isogeny
+SSB_FN void sswu_finish(g2_aff& q, const fp2& u, const fp2& x, const fp2& y_in) {
+  fp2 y = y_in;
+  if (fp2_sgn0(u) != fp2_sgn0(y)) fp2_neg(y, y);
+  iso3_map(q, x, y);
+}
+
 SSB_FN void hash_to_g2(g2_aff& out, const uint8_t* msg32, const uint8_t* dst, int dst_len) {
   uint8_t uni[256];
   expand_message_xmd_256(uni, msg32, dst, dst_len);

@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(64) k_lane_subgroup(int n, const uint32_t* __r
   __shared__ uint32_t flg[G2NG];
   const int gi = threadIdx.x / G2G, role = threadIdx.x % G2G;
   const int s = blockIdx.x * G2NG + gi;
-  grp g{lds, lds + LP_NCODE_CONST + gi * SG_GS, 0, 0, 0, &flg[gi], role};
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + gi * SG_GS, 0, 0, 0, (lu32*)&flg[gi], role};
   lp_init_consts(g);
   const bool act = s < n && (sflags[s] & DEC_OK) && !(sflags[s] & DEC_INF);
   const int P = G2S0, ACC = P + 4, TMP = ACC + 6;
@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(64) k_lane_rlc_g2(int n, uint64_t seed, const 
   __shared__ uint32_t flg[G2NG];
   const int gi = threadIdx.x / G2G, role = threadIdx.x % G2G;
   const int s = blockIdx.x * G2NG + gi;
-  grp g{lds, lds + LP_NCODE_CONST + gi * R2_GS, 0, 0, 0, &flg[gi], role};
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + gi * R2_GS, 0, 0, 0, (lu32*)&flg[gi], role};
   lp_init_consts(g);
   const bool act = s < n && (sflags[s] & DEC_OK) && !(sflags[s] & DEC_INF);
   const int P = G2S0, TAB = P + 4, ACC = TAB + 48, TMP = ACC + 6;
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(64) k_lane_rlc_g1(int n, uint64_t seed, const 
   __shared__ uint32_t flg[G1NG];
   const int gi = threadIdx.x / G1G, role = threadIdx.x % G1G;
   const int s = blockIdx.x * G1NG + gi;
-  grp g{lds, lds + LP_NCODE_CONST + gi * R1_GS, 0, 0, 0, &flg[gi], role};
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + gi * R1_GS, 0, 0, 0, (lu32*)&flg[gi], role};
   lp_init_consts(g);
   const bool act = s < n && (pflags[s] & DEC_OK) && !(pflags[s] & DEC_INF);
   const int P = G1S0, TAB = P + 2, ACC = TAB + 24, TMP = ACC + 3;

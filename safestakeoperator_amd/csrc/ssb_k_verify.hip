@@ -51,6 +51,32 @@ __global__ void __launch_bounds__(64) k_decode2(int n, const uint8_t* __restrict
     pk_aff[s] = pk;
   }
 }
+// threads [0, n): G2 subgroup check; [n, 2n): r_i * sig_i; [2n, 3n): r_i * pk_i  (single lane each:
+// at C2 size the chip has spare waves, so the per-share chains run one per lane; the lane-group
+// versions in ssb_k_lane.hip cost ~6x the instructions for ~2x lower latency)
+__global__ void __launch_bounds__(64) k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+                                                  const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
+                                                  const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
+                                                  g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) {
+    const uint32_t sf = sflags[g];
+    gflags[g] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[g]) : 0u;
+  } else if (g < 2 * n) {
+    const int s = g - n;
+    const uint32_t sf = sflags[s];
+    g2_jac r;
+    if ((sf & DEC_OK) && !(sf & DEC_INF)) unit_rlc_sig(r, sig_aff[s], rlc_scalar_odd(seed, (uint64_t)s)); else jac_set_inf(r);
+    rsig[s] = r;
+  } else if (g < 3 * n) {
+    const int s = g - 2 * n;
+    const uint32_t pf = pflags[s];
+    g1_jac r;
+    if ((pf & DEC_OK) && !(pf & DEC_INF)) unit_rlc_pk(r, pk_aff[s], rlc_scalar_odd(seed, (uint64_t)s)); else jac_set_inf(r);
+    rpk[s] = r;
+  }
+}
+
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
                         const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;

@@ -22,6 +22,10 @@ __global__ void k_decode(int n, const uint8_t* __restrict__ sig96,
 __global__ void k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
                                                 g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
                                                 uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags);
+__global__ void k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+                            const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
+                            const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
+                            g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk);
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
                         const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags);
 __global__ void k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
@@ -87,6 +91,9 @@ void lane_rlc_g2(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, c
 //   rpk[s] = rlc_scalar_odd(seed, s) * pk[s]      (exc bit 1)
 void lane_rlc_g1(hipStream_t st, int n, uint64_t seed, const uint32_t* pflags, const g1_aff* pk, g1_jac* rpk,
                  uint32_t* exc);
+// staged hash_to_G2 of n roots into out (ssb_k_hash.hip); ws: hash_ws_bytes(n) device bytes
+size_t hash_ws_bytes(size_t n);
+void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws);
 // exact single-lane recomputation of the shares whose lane-group stage raised exc
 void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
                 const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,

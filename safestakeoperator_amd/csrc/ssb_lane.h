@@ -25,15 +25,27 @@ namespace lane {
 
 constexpr int LP_NCODE_CONST = 48, LP_NSCRATCH = 128;
 
-struct grp {
-  fp* k;           // shared constants (LP_NCODE_CONST slots)
-  fp* s;           // this group's slots: [0, LP_NSCRATCH) scratch, then caller-owned
+// LDS pointers carry address space 3 on the device, so slot traffic is ds_read/ds_write_b128
+// (generic pointers would compile to flat_* accesses).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SSB_LDS __attribute__((address_space(3)))
+#else
+#define SSB_LDS
+#endif
+typedef SSB_LDS fp lfp;
+typedef SSB_LDS uint32_t lu32;
+
+struct grp {       // passed BY VALUE to the programs (lives in registers)
+  lfp* k;          // shared constants (LP_NCODE_CONST slots)
+  lfp* s;          // this group's slots: [0, scratch) program scratch, then caller-owned
   int a, b, d;     // group-relative slot index of input A, input B, output D
-  uint32_t* flag;  // this group's check word (bit per check component)
+  lu32* flag;      // this group's check word (bit per check component)
   int role;        // lane index inside the group (device)
 };
 
-#if defined(__HIPCC__) || defined(__HIP__)
+#if (defined(__HIPCC__) || defined(__HIP__)) && defined(SSB_LP_INLINE)
+#define SSB_LP_FN __host__ __device__ __forceinline__
+#elif defined(__HIPCC__) || defined(__HIP__)
 #define SSB_LP_FN __host__ __device__ __noinline__
 #else
 #define SSB_LP_FN inline
@@ -57,7 +69,7 @@ struct grp {
 #define LP_SELT(tab) ((uint32_t)(tab)[role])
 #define LP_BIT(imm) ((uint32_t)((imm) >> role) & 1u)
 
-SSB_INL fp* lp_ptr(const grp& g, uint32_t c) {
+SSB_INL lfp* lp_ptr(const grp& g, uint32_t c) {
   const int base = c >= 224u ? g.d - 224 : (c >= 200u ? g.b - 200 : (c >= 176u ? g.a - 176 : -48));
   return c < (uint32_t)LP_NCODE_CONST ? g.k + c : g.s + ((int)c + base);
 }
@@ -98,6 +110,12 @@ template <class GR> SSB_INL void lp_acc_sgn(fp& x, const GR& g, uint32_t c, uint
 }
 template <class GR> SSB_INL void lp_st(const GR& g, uint32_t c, const fp& v) { *lp_ptr(g, c) = v; }
 
+// modular doubling / addition of reduced values (< p)
+SSB_INL void lp_csub(fp& x, const uint32_t* mp);
+SSB_INL void lp_dbl_mod(fp& u) { fp t = u; lp_add_raw(u, t); lp_csub(u, P_LIMBS); }
+SSB_INL void lp_add_mod(fp& u, const fp& v) { lp_add_raw(u, v); lp_csub(u, P_LIMBS); }
+SSB_INL void lp_add_mod_sel(fp& u, const fp& v, uint32_t s) { fp t = u; lp_add_mod(t, v); lp_sel(u, t, u, s); }
+
 // x >= m*p ? x - m*p : x   (m*p given as limbs)
 SSB_INL void lp_csub(fp& x, const uint32_t* mp) {
   fp t;
@@ -118,7 +136,7 @@ SSB_INL void lp_reduce4(fp& x) { lp_csub(x, LP_P4); lp_csub(x, LP_P2); lp_csub(x
 template <class GR> SSB_INL void lp_chk(const GR& g, const fp& v, uint32_t bit) {
   if (bit < 31u && fp_is_zero(v)) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    atomicOr(g.flag, 1u << bit);
+    atomicOr((uint32_t*)g.flag, 1u << bit);
 #else
     *g.flag |= 1u << bit;
 #endif

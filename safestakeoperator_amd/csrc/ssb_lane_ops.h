@@ -13,7 +13,7 @@ namespace ssb {
 namespace lane {
 
 // ---- program calls (inputs/outputs by group-relative slot) ----
-template <class GR> SSB_INL void lg_reset_flag(GR& g) {
+template <class GR> SSB_INL void lg_reset_flag(const GR& g) {
   LP_FOR(1) { if (role == 0) *g.flag = 0u; }
   LP_SYNC();
 }
@@ -146,6 +146,50 @@ template <class GR> SSB_INL bool g2_subgroup_check(GR& g, int p, int acc, int tm
   bool eq = true;
   for (int i = 0; i < 4; ++i) eq = eq && fp_is_zero(g.s[tmp + 4 + i]);
   return eq;
+}
+
+// dst = -src for a G2 Jacobian point (6 slots; negate Y)
+template <class GR> SSB_INL void g2_neg_copy(GR& g, int src, int dst) {
+  constexpr int G = G2_ADD_G;
+  LP_FOR(G) {
+    if (role < 6) {
+      fp v = g.s[src + role];
+      if (role == 2 || role == 3) fp_neg(v, v);
+      g.s[dst + role] = v;
+    }
+  }
+  LP_SYNC();
+}
+template <class GR> SSB_INL void g2_psi(GR& g, int a, int d) { g.a = a; g.d = d; lp_g2_psi(g); }
+
+// acc = [|x|]P for a G2 Jacobian P at slot `p` (6 slots)
+template <class GR> SSB_INL void g2_mul_x_abs(GR& g, int p, int acc, uint32_t& exc) {
+  lg_copy<G2_ADD_G>(g, p, acc, 6);
+  for (int i = 62; i >= 0; --i) {
+    g2_dbl(g, acc, acc);
+    if ((BLS_X_ABS >> i) & 1ull) g2_add(g, acc, p, acc, exc);
+  }
+}
+
+// h_eff * P (RFC 9380 G.3, the same chain as ssb::clear_cofactor_g2) for a Jacobian P at `p`;
+// result at `r`.  Work slots: 5 x 6 starting at `w`.
+template <class GR> SSB_INL void g2_clear_cofactor(GR& g, int p, int r, int w, uint32_t& exc) {
+  const int T1 = w, T2 = w + 6, T3 = w + 12, N = w + 18, X = w + 24;
+  g2_mul_x_abs(g, p, X, exc);        // [|x|]P
+  g2_neg_copy(g, X, T1);             // t1 = [x]P
+  g2_psi(g, p, T2);                  // t2 = psi(P)
+  g2_dbl(g, p, T3);                  // 2P
+  g2_psi(g, T3, T3);
+  g2_psi(g, T3, T3);                 // t3 = psi^2(2P)
+  g2_neg_copy(g, T2, N);
+  g2_add(g, T3, N, T3, exc);         // t3 = psi^2(2P) - psi(P)
+  g2_add(g, T1, T2, T2, exc);        // t2 = [x]P + psi(P)
+  g2_mul_x_abs(g, T2, N, exc);
+  g2_neg_copy(g, N, T2);             // t2 = [x^2]P + [x]psi(P)
+  g2_add(g, T3, T2, T3, exc);
+  g2_add(g, T3, X, T3, exc);         // - t1 = [|x|]P
+  g2_neg_copy(g, p, N);
+  g2_add(g, T3, N, r, exc);          // - P
 }
 
 }  // namespace lane

@@ -130,6 +130,7 @@ struct verify_ws {
   g2_aff* H; g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags;
   g2_jac* rsig; g1_jac* rpk; g1_aff* root_sum; g2_jac* part; g2_aff* sig_sum; fp12* f; uint32_t* ok;
   uint32_t* exc;  // 3n: lane-group exceptions (subgroup, RLC G2, RLC G1)
+  char* hws;      // staged hash_to_G2 workspace
 };
 constexpr int G2_PARTS = 64;
 
@@ -137,7 +138,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
   return align_up(n_roots * sizeof(g2_aff)) + align_up(n * sizeof(g2_aff)) + align_up(n * sizeof(g1_aff)) +
          align_up(n * 4) * 4 + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
          align_up(n_roots * sizeof(g1_aff)) + align_up(G2_PARTS * sizeof(g2_jac)) + align_up(sizeof(g2_aff)) +
-         align_up((n_roots + 1) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4);
+         align_up((n_roots + 1) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4) + align_up(launch::hash_ws_bytes(n_roots));
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
@@ -148,6 +149,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.root_sum = c.take<g1_aff>(n_roots); w.part = c.take<g2_jac>(G2_PARTS); w.sig_sum = c.take<g2_aff>(1);
   w.f = c.take<fp12>(n_roots + 1); w.ok = c.take<uint32_t>(1);
   w.exc = c.take<uint32_t>(3 * n);
+  w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   return w;
 }
 
@@ -159,22 +161,11 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
   SSB_HIP(hipEventRecord(ctx->ev_in, st));
   SSB_HIP(hipStreamWaitEvent(sh, ctx->ev_in, 0));
-  if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n_roots, 64)), dim3(64), 0, sh, (int)n_roots, d_roots, dst, w.H); }
+  if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
   SSB_HIP(hipEventRecord(ctx->ev_hash, sh));
   if (n) {
     { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags); }
-    // lane-group stage: subgroup check (main) || r*sig (side 2) || r*pk (side 3)
-    SSB_HIP(hipEventRecord(ctx->ev_sdec, st));
-    SSB_HIP(hipStreamWaitEvent(ctx->side[2], ctx->ev_sdec, 0));
-    SSB_HIP(hipStreamWaitEvent(ctx->side[3], ctx->ev_sdec, 0));
-    { timed t(ctx, "k_lane_rlc_g2", ctx->side[2]); launch::lane_rlc_g2(ctx->side[2], (int)n, seed, w.sflags, w.sig_aff, w.rsig, w.exc + n); }
-    { timed t(ctx, "k_lane_rlc_g1", ctx->side[3]); launch::lane_rlc_g1(ctx->side[3], (int)n, seed, w.pflags, w.pk_aff, w.rpk, w.exc + 2 * n); }
-    { timed t(ctx, "k_lane_subgroup"); launch::lane_subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags, w.exc); }
-    SSB_HIP(hipEventRecord(ctx->ev_r2, ctx->side[2]));
-    SSB_HIP(hipEventRecord(ctx->ev_r1, ctx->side[3]));
-    SSB_HIP(hipStreamWaitEvent(st, ctx->ev_r2, 0));
-    SSB_HIP(hipStreamWaitEvent(st, ctx->ev_r1, 0));
-    launch::lane_fixup(st, (int)n, seed, w.sflags, w.pflags, w.sig_aff, w.pk_aff, w.exc, w.gflags, w.rsig, w.rpk);
+    { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_check_rlc, dim3(nblk(3 * n, 64)), dim3(64), 0, st, (int)n, seed, w.sflags, w.pflags, w.sig_aff, w.pk_aff, w.gflags, w.rsig, w.rpk); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, w.flags);
     SSB_HIP(hipEventRecord(ctx->ev_dec, st));
     on_decoded();
@@ -274,12 +265,13 @@ int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t*
   if (!msgs32 || !out192) { ctx->err = "null pointer"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
-  size_t need = align_up(n * 32) + align_up(n * sizeof(g2_aff)) + align_up(n * 192);
+  size_t need = align_up(n * 32) + align_up(n * sizeof(g2_aff)) + align_up(n * 192) + align_up(launch::hash_ws_bytes(n));
   if ((rc = ensure_ws(ctx, need))) return rc;
   carve c{(char*)ctx->ws};
   uint8_t* d_msg = c.take<uint8_t>(n * 32); g2_aff* d_h = c.take<g2_aff>(n); uint8_t* d_out = c.take<uint8_t>(n * 192);
+  char* hws = c.take<char>(launch::hash_ws_bytes(n));
   SSB_HIP(hipMemcpyAsync(d_msg, msgs32, n * 32, hipMemcpyHostToDevice, ctx->stream));
-  { timed t(ctx, "k_hash_to_g2"); hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->stream, (int)n, d_msg, d, d_h); }
+  { timed t(ctx, "k_hash_to_g2"); launch::hash_to_g2(ctx->stream, (int)n, d_msg, d, d_h, hws); }
   hipLaunchKernelGGL(k_serialize_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->stream, (int)n, d_h, d_out);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out192, d_out, n * 192, hipMemcpyDeviceToHost, ctx->stream));
@@ -472,16 +464,18 @@ int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t
   for (size_t i = 0; i < n; ++i) if (root_idx[i] >= n_roots) { ctx->err = "root_idx out of range"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
-  size_t need = align_up(n * 32) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n_roots * sizeof(g2_aff)) + align_up(n * 96);
+  size_t need = align_up(n * 32) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n_roots * sizeof(g2_aff)) + align_up(n * 96) +
+                align_up(launch::hash_ws_bytes(n_roots));
   if ((rc = ensure_ws(ctx, need))) return rc;
   carve c{(char*)ctx->ws};
   uint8_t* d_sk = c.take<uint8_t>(n * 32); uint32_t* d_ri = c.take<uint32_t>(n); uint8_t* d_roots = c.take<uint8_t>(n_roots * 32);
   g2_aff* d_h = c.take<g2_aff>(n_roots); uint8_t* d_out = c.take<uint8_t>(n * 96);
+  char* hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   hipStream_t st = ctx->stream;
   SSB_HIP(hipMemcpyAsync(d_sk, sk32le, n * 32, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_ri, root_idx, n * 4, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_hash_to_g2, dim3(nblk(n_roots, 64)), dim3(64), 0, st, (int)n_roots, d_roots, d, d_h);
+  launch::hash_to_g2(st, (int)n_roots, d_roots, d, d_h, hws);
   { timed tm(ctx, "k_sign"); hipLaunchKernelGGL(k_sign, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sk, d_ri, d_h, d_out); }
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n * 96, hipMemcpyDeviceToHost, st));

@@ -126,6 +126,20 @@ static void lane_selftest(const uint8_t* seed32) {
     ok += in && e == 0 && g2_in_subgroup(P); ++n; }
   { uint32_t e = 0; put_aff(h, 0, Hraw); bool in = lane::g2_subgroup_check(g, h.U(0), h.U(4), h.U(10), e);
     ok += !in && (e == 0) && !g2_in_subgroup(Hraw); ++n; }
+  // cofactor clearing of q0 + q1 (the hash pipeline's lane-group stage) vs clear_cofactor_g2
+  { uint32_t e = 0; g2_jac S; jac_from_aff(S, Hraw); jac_add_aff(S, S, Q);
+    put_jac(h, 0, S); lane::g2_clear_cofactor(g, h.U(0), h.U(6), h.U(12), e);
+    g2_jac R; clear_cofactor_g2(R, S); ok += same_point(h, 6, R) && e == 0; ++n;
+    // staged hash == hash_to_g2
+    fp2 u0, u1; h2c_field(u0, u1, m, (const uint8_t*)DST, (int)strlen(DST));
+    g2_aff q[2]; const fp2* us[2] = {&u0, &u1};
+    for (int j = 0; j < 2; ++j) {
+      fp2 x0, y0, x1, y1; bool ok0 = sswu_candidate(x0, y0, *us[j], 0); bool ok1 = sswu_candidate(x1, y1, *us[j], 1);
+      sswu_finish(q[j], *us[j], ok0 ? x0 : x1, ok0 ? y0 : y1); (void)ok1; }
+    g2_jac T; jac_from_aff(T, q[0]); jac_add_aff(T, T, q[1]);
+    put_jac(h, 0, T); lane::g2_clear_cofactor(g, h.U(0), h.U(6), h.U(12), e);
+    g2_aff want; hash_to_g2(want, m, (const uint8_t*)DST, (int)strlen(DST));
+    g2_jac wj; jac_from_aff(wj, want); ok += same_point(h, 6, wj) && e == 0; ++n; }
   ok += exc == 0; ++n;
   printf("%d %d\n", ok, n);
 }
