@@ -20,8 +20,8 @@ reduced by conditional subtraction), and allocates LDS slots by liveness.  The e
 the device with one role per lane and on the host (tests) with a loop over roles, so the programs
 are checked against the single-lane code on the CPU.
 
-Slot codes (8 bit): 0..47 shared constants (0 = zero), 48..175 group scratch, 176..199 input A,
-200..223 input B, 224..255 output D.
+Slot codes (16 bit): 0..47 shared constants (0 = zero), 48..447 group scratch, 448..479 input A,
+480..511 input B, 512..543 output D.
 
 Run: python safestakeoperator_amd/csrc/gen_lane_progs.py
 """
@@ -31,7 +31,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 MAXT = 3     # max terms of an inlined product operand (value < 3p)
 MAXM = 8     # max terms of a materialised form (value < 8p < 2^384)
-C_SCR, C_A, C_B, C_D = 48, 176, 200, 224
+C_SCR, C_A, C_B, C_D = 48, 448, 480, 512
 N_SCR = C_A - C_SCR
 
 # shared constants (Fp components, Montgomery form, from ssb_consts.h): name -> code
@@ -218,6 +218,157 @@ def jac_add_aff(X1, Y1, Z1, x2, y2):  # madd-2007-bl (q affine, not infinity)
     return x3, y3, z3
 
 
+# ---------------- Fp6 / Fp12 tower, mirroring ssb_field.h ----------------
+def f6_add(a, b): return tuple(f2_add(x, y) for x, y in zip(a, b))
+def f6_sub(a, b): return tuple(f2_sub(x, y) for x, y in zip(a, b))
+def f6_neg(a): return tuple(f2_neg(x) for x in a)
+def f6_mul_v(a): return (f2_mul_xi(a[2]), a[0], a[1])
+
+
+def f6_mul(a, b):
+    t0 = f2_mul(a[0], b[0])
+    t1 = f2_mul(a[1], b[1])
+    t2 = f2_mul(a[2], b[2])
+    u = f2_sub(f2_sub(f2_mul(f2_add(a[1], a[2]), f2_add(b[1], b[2])), t1), t2)
+    c0 = f2_add(f2_mul_xi(u), t0)
+    u = f2_sub(f2_sub(f2_mul(f2_add(a[0], a[1]), f2_add(b[0], b[1])), t0), t1)
+    c1 = f2_add(u, f2_mul_xi(t2))
+    u = f2_sub(f2_sub(f2_mul(f2_add(a[0], a[2]), f2_add(b[0], b[2])), t0), t2)
+    c2 = f2_add(u, t1)
+    return (c0, c1, c2)
+
+
+def f6_mul_01(a, b0, b1):
+    aa = f2_mul(a[0], b0)
+    bb = f2_mul(a[1], b1)
+    t1 = f2_add(f2_mul_xi(f2_mul(a[2], b1)), aa)
+    t2 = f2_sub(f2_sub(f2_mul(f2_add(b0, b1), f2_add(a[0], a[1])), aa), bb)
+    t3 = f2_add(f2_mul(a[2], b0), bb)
+    return (t1, t2, t3)
+
+
+def f6_mul_1(a, b1):
+    return (f2_mul_xi(f2_mul(a[2], b1)), f2_mul(a[0], b1), f2_mul(a[1], b1))
+
+
+def f12_mul(a, b):
+    t0 = f6_mul(a[0], b[0])
+    t1 = f6_mul(a[1], b[1])
+    c1 = f6_sub(f6_sub(f6_mul(f6_add(a[0], a[1]), f6_add(b[0], b[1])), t0), t1)
+    return (f6_add(t0, f6_mul_v(t1)), c1)
+
+
+def f12_sqr(a):
+    ab = f6_mul(a[0], a[1])
+    s0 = f6_add(a[0], a[1])
+    s1 = f6_add(a[0], f6_mul_v(a[1]))
+    s0 = f6_sub(f6_mul(s0, s1), ab)
+    c0 = f6_sub(s0, f6_mul_v(ab))
+    return (c0, f6_add(ab, ab))
+
+
+def f12_mul_014(f, o0, o1, o4):
+    aa = f6_mul_01(f[0], o0, o1)
+    bb = f6_mul_1(f[1], o4)
+    o = f2_add(o1, o4)
+    s_ = f6_mul_01(f6_add(f[1], f[0]), o0, o)
+    c1 = f6_sub(f6_sub(s_, aa), bb)
+    c0 = f6_add(f6_mul_v(bb), aa)
+    return (c0, c1)
+
+
+def fp4_sqr(a, b):
+    t0 = f2_sqr(a)
+    t1 = f2_sqr(b)
+    c0 = f2_add(f2_mul_xi(t1), t0)
+    t2 = f2_sub(f2_sub(f2_sqr(f2_add(a, b)), t0), t1)
+    return c0, t2
+
+
+def f12_cyc_sqr(f):
+    z0, z4, z3 = f[0]
+    z2, z1, z5 = f[1]
+    t0, t1 = fp4_sqr(z0, z1)
+    z0 = f2_add(f2_dbl(f2_sub(t0, z0)), t0)
+    z1 = f2_add(f2_dbl(f2_add(t1, z1)), t1)
+    t0, t1 = fp4_sqr(z2, z3)
+    t2, t3 = fp4_sqr(z4, z5)
+    z4 = f2_add(f2_dbl(f2_sub(t0, z4)), t0)
+    z5 = f2_add(f2_dbl(f2_add(t1, z5)), t1)
+    t0 = f2_mul_xi(t3)
+    z2 = f2_add(f2_dbl(f2_add(t0, z2)), t0)
+    z3 = f2_add(f2_dbl(f2_sub(t2, z3)), t2)
+    return ((z0, z4, z3), (z2, z1, z5))
+
+
+def f12_frob(a, n):
+    c = [a[0][0], a[1][0], a[0][1], a[1][1], a[0][2], a[1][2]]
+    out = []
+    for k in range(6):
+        x = c[k]
+        if n & 1:
+            x = f2_conj(x)
+        if k:
+            x = f2_mul(x, K2("FROB%d[%d]" % (n, k)))
+        out.append(x)
+    return ((out[0], out[2], out[4]), (out[1], out[3], out[5]))
+
+
+def f12_conj(a): return (a[0], f6_neg(a[1]))
+
+
+def sym_fp12(T, off=0):
+    s_ = [T(off + i) for i in range(12)]
+    f2s = [(s_[2 * k], s_[2 * k + 1]) for k in range(6)]
+    return ((f2s[0], f2s[1], f2s[2]), (f2s[3], f2s[4], f2s[5]))
+
+
+def flat12(a):
+    return [c for f6 in a for f2_ in f6 for c in f2_]
+
+
+# ---------------- Miller loop steps, mirroring ssb_pairing.h ----------------
+def miller_dbl(T, P):
+    X, Y, Z = T
+    xP, yP = P
+    A_ = f2_sqr(X)
+    B_ = f2_sqr(Y)
+    C = f2_sqr(B_)
+    D = f2_dbl(f2_sub(f2_sub(f2_sqr(f2_add(X, B_)), A_), C))
+    E = mat2(f2_add(f2_dbl(A_), A_))
+    F = f2_sqr(E)
+    ZZ = mat2(f2_sqr(Z))
+    l0 = f2_sub(f2_mul(E, X), f2_dbl(B_))
+    l1 = f2_mul_fp(mat2(f2_neg(f2_mul(E, ZZ))), xP)
+    x3 = mat2(f2_sub(F, f2_dbl(D)))
+    z3 = mat2(f2_dbl(f2_mul(Y, Z)))
+    y3 = f2_sub(f2_mul(E, mat2(f2_sub(D, x3))), f2_dbl(f2_dbl(f2_dbl(C))))
+    l4 = f2_mul_fp(mat2(f2_mul(z3, ZZ)), yP)
+    return (x3, y3, z3), (l0, l1, l4)
+
+
+def miller_add(T, Q, P):
+    X, Y, Z = T
+    xQ, yQ = Q
+    xP, yP = P
+    ZZ = mat2(f2_sqr(Z))
+    U2 = f2_mul(xQ, ZZ)
+    S2 = f2_mul(mat2(f2_mul(yQ, Z)), ZZ)
+    H = mat2(f2_sub(U2, X))
+    rr = mat2(f2_dbl(f2_sub(S2, Y)))
+    HH = mat2(f2_sqr(H))
+    I = mat2(f2_dbl(f2_dbl(HH)))
+    J = mat2(f2_mul(H, I))
+    V = mat2(f2_mul(X, I))
+    x3 = mat2(f2_sub(f2_sub(f2_sqr(rr), J), f2_dbl(V)))
+    y3 = f2_sub(f2_mul(rr, f2_sub(V, x3)), f2_dbl(f2_mul(Y, J)))
+    z3 = mat2(f2_sub(f2_sub(f2_sqr(f2_add(Z, H)), ZZ), HH))
+    l0 = f2_sub(f2_mul(rr, xQ), f2_mul(yQ, z3))
+    l1 = f2_mul_fp(f2_neg(rr), xP)
+    l4 = f2_mul_fp(z3, yP)
+    return (x3, y3, z3), (l0, l1, l4)
+
+
 def sym_pt2(T, off=0):
     return ((T(off), T(off + 1)), (T(off + 2), T(off + 3)), (T(off + 4), T(off + 5)))
 
@@ -265,7 +416,32 @@ def programs():
     define("G1_DBL", 3, 0, 4, lambda: flat(*jac_dbl(A(0), A(1), A(2))))
     define("G1_ADD", 3, 3, 4, lambda: flat(*jac_add(A(0), A(1), A(2), B(0), B(1), B(2))))
     define("G1_MADD", 3, 2, 4, lambda: flat(*jac_add_aff(A(0), A(1), A(2), B(0), B(1))))
+    # ---- Fp12 (G = 64, one program per wave): A = a (12), B = b (12) ----
+    define("FP12_MUL", 12, 12, 64, lambda: flat12(f12_mul(sym_fp12(A), sym_fp12(B))))
+    define("FP12_SQR", 12, 0, 64, lambda: flat12(f12_sqr(sym_fp12(A))))
+    define("FP12_CYC_SQR", 12, 0, 64, lambda: flat12(f12_cyc_sqr(sym_fp12(A))))
+    define("FP12_CONJ", 12, 0, 64, lambda: flat12(f12_conj(sym_fp12(A))))
+    for n in (1, 2, 3):
+        define("FP12_FROB%d" % n, 12, 0, 64, lambda n=n: flat12(f12_frob(sym_fp12(A), n)))
+
+    # Miller iteration, fused: f <- f^2 * l_{T,T}(P), T <- 2T.  A = f (12) | T (6), B = (xP, yP)
+    def miller_iter(first=False):
+        f = sym_fp12(A)
+        T = ((A(12), A(13)), (A(14), A(15)), (A(16), A(17)))
+        T2, (l0, l1, l4) = miller_dbl(T, (B(0), B(1)))
+        f2 = f if first else f12_sqr(f)
+        return flat12(f12_mul_014(f2, l0, l1, l4)) + flat(*T2)
+    define("MILLER_ITER", 18, 2, 64, miller_iter)
+
+    # Miller addition step: f <- f * l_{T,Q}(P), T <- T + Q.  A = f | T, B = (xQ, yQ, xP, yP)
+    def miller_addstep():
+        f = sym_fp12(A)
+        T = ((A(12), A(13)), (A(14), A(15)), (A(16), A(17)))
+        T2, (l0, l1, l4) = miller_add(T, ((B(0), B(1)), (B(2), B(3))), (B(4), B(5)))
+        return flat12(f12_mul_014(f, l0, l1, l4)) + flat(*T2)
+    define("MILLER_ADDSTEP", 18, 6, 64, miller_addstep)
     return ps
+
 
 
 # ------------------------------------------------------------------------------------------
@@ -546,14 +722,31 @@ class Emitter:
         self.tables = []
 
     def sel(self, codes):
-        """per-role 8-bit values -> a C expression of `role`."""
+        """per-role values (< 2^16) -> a C expression of `role`: packed immediates for small
+        groups, a table otherwise."""
         G = self.G
         codes = list(codes) + [0] * (G - len(codes))
-        if G <= 8:
+        assert all(0 <= c < 65536 for c in codes)
+        if G <= 8 and max(codes) < 256:
             v = 0
             for r, c in enumerate(codes):
-                v |= (c & 0xFF) << (8 * r)
+                v |= c << (8 * r)
             return "LP_SEL8(0x%016xull)" % v
+        if G <= 4:
+            v = 0
+            for r, c in enumerate(codes):
+                v |= c << (16 * r)
+            return "LP_SEL16(0x%016xull)" % v
+        if G <= 8:
+            lo = hi = 0
+            for r, c in enumerate(codes):
+                if r < 4:
+                    lo |= c << (16 * r)
+                else:
+                    hi |= c << (16 * (r - 4))
+            return "LP_SEL16X2(0x%016xull, 0x%016xull)" % (lo, hi)
+        if len(set(codes)) == 1:
+            return "%du" % codes[0]
         name = "%s_t%d" % (self.s.p.name, len(self.tables))
         self.tables.append((name, codes))
         return "LP_SELT(%s)" % name
@@ -715,7 +908,7 @@ def emit_header(progs):
         nprod = len(sch.prods)
         nmat = sch.n_mats
         for name, codes in em.tables:
-            hdr.append("SSB_LP_TABLE uint8_t %s[%d] = {%s};" % (name, len(codes), ", ".join(map(str, codes))))
+            hdr.append("SSB_LP_TABLE uint16_t %s[%d] = {%s};" % (name, len(codes), ", ".join(map(str, codes))))
         hdr.append("// %s: G=%d, %d products in %d rounds (%.0f%% lane use), %d materialisations, %d outputs, "
                    "%d scratch slots, %d stages"
                    % (P.name, P.G, nprod, sch.n_rounds, 100.0 * nprod / max(1, sch.n_rounds * P.G), nmat,

@@ -3,6 +3,7 @@
 // library compiles in parallel.
 #include "ssb_kernels.h"
 #include "ssb_wave.h"
+#include "ssb_lane_ops.h"
 
 namespace ssb {
 namespace k {
@@ -46,6 +47,78 @@ __global__ void __launch_bounds__(64) k_final_wave(int npairs, const fp12* __res
   }
   wave::final_exp(w, ACC, TMP, lane, 64);
   if (lane == 0) { fp12 e; wave::load12(e, w, ACC); *ok = fp12_is_one(e) ? 1u : 0u; }
+}
+
+// ---- lane-program versions (straight-line programs of gen_lane_progs.py, G = 64) ----
+constexpr int ML_S0 = lane::MILLER_ITER_SCRATCH > lane::MILLER_ADDSTEP_SCRATCH ? lane::MILLER_ITER_SCRATCH
+                                                                               : lane::MILLER_ADDSTEP_SCRATCH;
+constexpr int ML_SLOTS = ML_S0 + 18 + 6;
+// pairs 0..n_roots-1: (sum_root r_i pk_i, H(root));  pair n_roots: (-g1, sum r_i sig_i)
+__global__ void __launch_bounds__(64) k_miller_lane(int n_roots, const g1_aff* __restrict__ root_sum,
+                                                    const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
+                                                    fp12* __restrict__ f) {
+  using namespace ssb::lane;
+  __shared__ fp lds[LP_NCODE_CONST + ML_SLOTS];
+  __shared__ uint32_t flg;
+  const int p = blockIdx.x, lane_ = threadIdx.x;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  g1_aff P; g2_aff Q;
+  if (p < n_roots) { P = root_sum[p]; Q = H[p]; } else { P = g1_neg_generator(); Q = *sig_sum; }
+  if (P.inf || Q.inf) {  // e(O, Q) = e(P, O) = 1  (uniform per workgroup)
+    if (lane_ == 0) f[p] = fp12_one();
+    return;
+  }
+  lp_init_consts(g);
+  const int F = ML_S0, B = F + 18;
+  if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
+  if (lane_ == 4) g.s[B + 4] = P.x;
+  if (lane_ == 5) g.s[B + 5] = P.y;
+  __syncthreads();
+  f12_miller(g, F, B);
+  if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
+}
+
+// out[w] = prod of in[8w .. 8w+7]
+__global__ void __launch_bounds__(64) k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out) {
+  using namespace ssb::lane;
+  __shared__ fp lds[LP_NCODE_CONST + FP12_MUL_SCRATCH + 24];
+  __shared__ uint32_t flg;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, (int)threadIdx.x};
+  lp_init_consts(g);
+  const int ACC = FP12_MUL_SCRATCH, IN = ACC + 12;
+  const int b = blockIdx.x * 8, e = min(n, b + 8);
+  if (threadIdx.x < 12) g.s[ACC + threadIdx.x] = ((const fp*)&in[b])[threadIdx.x];
+  __syncthreads();
+  for (int i = b + 1; i < e; ++i) {
+    if (threadIdx.x < 12) g.s[IN + threadIdx.x] = ((const fp*)&in[i])[threadIdx.x];
+    __syncthreads();
+    f12_mul(g, ACC, IN, ACC);
+  }
+  if (threadIdx.x < 12) ((fp*)&out[blockIdx.x])[threadIdx.x] = g.s[ACC + threadIdx.x];
+}
+
+// product of the n values, then ONE final exponentiation -> batch verdict
+constexpr int FE_S0 = lane::FP12_MUL_SCRATCH;
+__global__ void __launch_bounds__(64) k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok) {
+  using namespace ssb::lane;
+  __shared__ fp lds[LP_NCODE_CONST + FE_S0 + 12 + 12 + 84];
+  __shared__ uint32_t flg;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, (int)threadIdx.x};
+  lp_init_consts(g);
+  const int ACC = FE_S0, IN = ACC + 12, TMP = IN + 12;
+  if (threadIdx.x < 12) g.s[ACC + threadIdx.x] = ((const fp*)&in[0])[threadIdx.x];
+  __syncthreads();
+  for (int i = 1; i < n; ++i) {
+    if (threadIdx.x < 12) g.s[IN + threadIdx.x] = ((const fp*)&in[i])[threadIdx.x];
+    __syncthreads();
+    f12_mul(g, ACC, IN, ACC);
+  }
+  f12_final_exp(g, ACC, TMP);
+  if (threadIdx.x == 0) {
+    fp12 e;
+    ld12(e, g.s + ACC);
+    *ok = fp12_is_one(e) ? 1u : 0u;
+  }
 }
 
 }  // namespace k

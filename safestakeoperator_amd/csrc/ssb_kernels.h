@@ -48,6 +48,10 @@ __global__ void k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
                                                     const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
                                                     fp12* __restrict__ f);
 __global__ void k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok);
+__global__ void k_miller_lane(int n_roots, const g1_aff* __restrict__ root_sum, const g2_aff* __restrict__ H,
+                              const g2_aff* __restrict__ sig_sum, fp12* __restrict__ f);
+__global__ void k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out);
+__global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok);
 __global__ void k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
                                                    g2_aff* __restrict__ out);
 __global__ void k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,

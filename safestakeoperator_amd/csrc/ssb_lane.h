@@ -5,8 +5,8 @@
 // in every linear stage some lanes materialise longer forms (reduced mod p) into slots.  The
 // 64/G groups of a wave run independent operations in lockstep.  Slot codes (8 bit) select:
 //   0..47    shared constants of the workgroup (0 = zero)          -> g.k[code]
-//   48..175  the group's scratch                                    -> g.s[code - 48]
-//   176..199 input A, 200..223 input B, 224..255 output D          -> g.s[g.a/b/d + ...]
+//   48..447  the group's scratch                                    -> g.s[code - 48]
+//   448..479 input A, 480..511 input B, 512..543 output D          -> g.s[g.a/b/d + ...]
 // (A, B, D are group-relative slot indices chosen by the caller, beyond the scratch area.)
 //
 // Values in slots are fully reduced (< p).  A product operand of up to 3 terms is formed WITHOUT
@@ -23,7 +23,7 @@
 namespace ssb {
 namespace lane {
 
-constexpr int LP_NCODE_CONST = 48, LP_NSCRATCH = 128;
+constexpr int LP_NCODE_CONST = 48, LP_NSCRATCH = 400;
 
 // LDS pointers carry address space 3 on the device, so slot traffic is ds_read/ds_write_b128
 // (generic pointers would compile to flat_* accesses).
@@ -66,11 +66,13 @@ struct grp {       // passed BY VALUE to the programs (lives in registers)
 #endif
 
 #define LP_SEL8(imm) ((uint32_t)((imm) >> (8 * role)) & 0xffu)
+#define LP_SEL16(imm) ((uint32_t)((imm) >> (16 * role)) & 0xffffu)
+#define LP_SEL16X2(lo, hi) ((uint32_t)((role < 4 ? (lo) : (hi)) >> (16 * (role & 3))) & 0xffffu)
 #define LP_SELT(tab) ((uint32_t)(tab)[role])
 #define LP_BIT(imm) ((uint32_t)((imm) >> role) & 1u)
 
 SSB_INL lfp* lp_ptr(const grp& g, uint32_t c) {
-  const int base = c >= 224u ? g.d - 224 : (c >= 200u ? g.b - 200 : (c >= 176u ? g.a - 176 : -48));
+  const int base = c >= 512u ? g.d - 512 : (c >= 480u ? g.b - 480 : (c >= 448u ? g.a - 448 : -48));
   return c < (uint32_t)LP_NCODE_CONST ? g.k + c : g.s + ((int)c + base);
 }
 

@@ -192,5 +192,96 @@ template <class GR> SSB_INL void g2_clear_cofactor(GR& g, int p, int r, int w, u
   g2_add(g, T3, N, r, exc);          // - P
 }
 
+// ---- Fp12 programs (G = 64, one group per wave) ----
+SSB_INL void ld12(fp12& f, const lfp* s) {
+  fp2* v[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int k = 0; k < 6; ++k) { v[k]->c0 = s[2 * k]; v[k]->c1 = s[2 * k + 1]; }
+}
+SSB_INL void st12(lfp* s, const fp12& f) {
+  const fp2 v[6] = {f.c0.c0, f.c0.c1, f.c0.c2, f.c1.c0, f.c1.c1, f.c1.c2};
+  for (int k = 0; k < 6; ++k) { s[2 * k] = v[k].c0; s[2 * k + 1] = v[k].c1; }
+}
+template <class GR> SSB_INL void f12_mul(GR& g, int a, int b, int d) { g.a = a; g.b = b; g.d = d; lp_fp12_mul(g); }
+template <class GR> SSB_INL void f12_cyc_sqr(GR& g, int a, int d) { g.a = a; g.d = d; lp_fp12_cyc_sqr(g); }
+template <class GR> SSB_INL void f12_conj(GR& g, int a, int d) { g.a = a; g.d = d; lp_fp12_conj(g); }
+template <class GR> SSB_INL void f12_frob(GR& g, int n, int a, int d) {
+  g.a = a; g.d = d;
+  if (n == 1) lp_fp12_frob1(g); else if (n == 2) lp_fp12_frob2(g); else lp_fp12_frob3(g);
+}
+
+// r = f^x (x = -0xd201000000010000), f cyclotomic; r != f
+template <class GR> SSB_INL void f12_cyc_exp_x(GR& g, int r, int f) {
+  lg_copy<64>(g, f, r, 12);
+  for (int i = 62; i >= 0; --i) {
+    f12_cyc_sqr(g, r, r);
+    if ((BLS_X_ABS >> i) & 1ull) f12_mul(g, r, f, r);
+  }
+  f12_conj(g, r, r);
+}
+
+// final exponentiation of the Fp12 value at `f` (in place); 7 x 12 work slots at `tmp`.
+// Same chain as ssb::final_exponentiation.
+template <class GR> SSB_INL void f12_final_exp(GR& g, int f, int tmp) {
+  const int t0 = tmp, t1 = tmp + 12, t2 = tmp + 24, t3 = tmp + 36, t4 = tmp + 48, t5 = tmp + 60, t6 = tmp + 72;
+  f12_conj(g, f, t0);
+  LP_FOR(1) {
+    if (role == 0) {  // one Fp12 inversion, on one lane
+      fp12 x, xi;
+      ld12(x, g.s + f);
+      fp12_inv(xi, x);
+      st12(g.s + t1, xi);
+    }
+  }
+  LP_SYNC();
+  f12_mul(g, t0, t1, t2);
+  lg_copy<64>(g, t2, t1, 12);
+  f12_frob(g, 2, t2, t2);
+  f12_mul(g, t2, t1, t2);
+  f12_cyc_sqr(g, t2, t1);
+  f12_conj(g, t1, t1);
+  f12_cyc_exp_x(g, t3, t2);
+  f12_cyc_sqr(g, t3, t4);
+  f12_mul(g, t1, t3, t5);
+  f12_cyc_exp_x(g, t1, t5);
+  f12_cyc_exp_x(g, t0, t1);
+  f12_cyc_exp_x(g, t6, t0);
+  f12_mul(g, t6, t4, t6);
+  f12_cyc_exp_x(g, t4, t6);
+  f12_conj(g, t5, t5);
+  f12_mul(g, t5, t2, t5);
+  f12_mul(g, t4, t5, t4);
+  f12_conj(g, t2, t5);
+  f12_mul(g, t1, t2, t1);
+  f12_frob(g, 3, t1, t1);
+  f12_mul(g, t6, t5, t6);
+  f12_frob(g, 1, t6, t6);
+  f12_mul(g, t3, t0, t3);
+  f12_frob(g, 2, t3, t3);
+  f12_mul(g, t3, t1, t3);
+  f12_mul(g, t3, t6, t3);
+  f12_mul(g, t3, t4, f);
+}
+
+// Miller loop f_{|x|,Q}(P) (conjugated).  Slots: F = f (12) | T (6) at `F`; B = (xQ0, xQ1, yQ0,
+// yQ1, xP, yP) at `b`.  Same schedule as ssb::miller_loop (the first squaring of f = 1 is a
+// harmless no-op here).
+template <class GR> SSB_INL void f12_miller(GR& g, int F, int b) {
+  LP_FOR(64) {
+    if (role < 18) {
+      fp v;
+      if (role < 12) v = (role == 0) ? fp_one() : fp_zero();
+      else if (role < 16) v = g.s[b + role - 12];
+      else v = (role == 16) ? fp_one() : fp_zero();
+      g.s[F + role] = v;
+    }
+  }
+  LP_SYNC();
+  for (int i = 62; i >= 0; --i) {
+    g.a = F; g.b = b + 4; g.d = F; lp_miller_iter(g);
+    if ((BLS_X_ABS >> i) & 1ull) { g.a = F; g.b = b; g.d = F; lp_miller_addstep(g); }
+  }
+  f12_conj(g, F, F);
+}
+
 }  // namespace lane
 }  // namespace ssb

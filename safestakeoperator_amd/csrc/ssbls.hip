@@ -138,7 +138,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
   return align_up(n_roots * sizeof(g2_aff)) + align_up(n * sizeof(g2_aff)) + align_up(n * sizeof(g1_aff)) +
          align_up(n * 4) * 4 + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
          align_up(n_roots * sizeof(g1_aff)) + align_up(G2_PARTS * sizeof(g2_jac)) + align_up(sizeof(g2_aff)) +
-         align_up((n_roots + 1) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4) + align_up(launch::hash_ws_bytes(n_roots));
+         align_up((n_roots + 1 + (n_roots + 8) / 8 + 1) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4) + align_up(launch::hash_ws_bytes(n_roots));
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
@@ -147,7 +147,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
   w.gflags = c.take<uint32_t>(n); w.rsig = c.take<g2_jac>(n); w.rpk = c.take<g1_jac>(n);
   w.root_sum = c.take<g1_aff>(n_roots); w.part = c.take<g2_jac>(G2_PARTS); w.sig_sum = c.take<g2_aff>(1);
-  w.f = c.take<fp12>(n_roots + 1); w.ok = c.take<uint32_t>(1);
+  w.f = c.take<fp12>(n_roots + 1 + (n_roots + 8) / 8 + 1); w.ok = c.take<uint32_t>(1);
   w.exc = c.take<uint32_t>(3 * n);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   return w;
@@ -175,8 +175,13 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     hipLaunchKernelGGL(k_sum_g2_partial, dim3(G2_PARTS), dim3(SUM_THREADS), 0, st, (int)n, w.flags, w.rsig, w.part);
     hipLaunchKernelGGL(k_sum_g2_final, dim3(1), dim3(64), 0, st, G2_PARTS, w.part, w.sig_sum); }
   SSB_HIP(hipStreamWaitEvent(st, ctx->ev_hash, 0));
-  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_wave, dim3((unsigned)(n_roots + 1)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.sig_sum, w.f); }
-  { timed t(ctx, "k_final"); hipLaunchKernelGGL(k_final_wave, dim3(1), dim3(64), 0, st, (int)(n_roots + 1), w.f, w.ok); }
+  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_lane, dim3((unsigned)(n_roots + 1)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.sig_sum, w.f); }
+  {
+    timed t(ctx, "k_final");
+    const int np = (int)(n_roots + 1), nparts = (np + 7) / 8;
+    hipLaunchKernelGGL(k_fp12_prod8, dim3((unsigned)nparts), dim3(64), 0, st, np, w.f, w.f + np);
+    hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, nparts, w.f + np, w.ok);
+  }
   if (n) { timed t(ctx, "k_fallback_verify"); hipLaunchKernelGGL(k_fallback_verify, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict); }
   SSB_HIP(hipGetLastError());
   return SSB_OK;

@@ -141,6 +141,21 @@ static void lane_selftest(const uint8_t* seed32) {
     g2_aff want; hash_to_g2(want, m, (const uint8_t*)DST, (int)strlen(DST));
     g2_jac wj; jac_from_aff(wj, want); ok += same_point(h, 6, wj) && e == 0; ++n; }
   ok += exc == 0; ++n;
+  // Fp12 programs, the lane final exponentiation and Miller loop
+  { g1_aff pk; pk.x = fp_from_c(G1_GEN_X); pk.y = fp_from_c(G1_GEN_Y); pk.inf = 0;
+    fp12 f1, f2, r1, r2; miller_loop(f1, pk, P); g1_aff ng = g1_neg_generator(); miller_loop(f2, ng, Q);
+    lane::st12(g.s + h.U(0), f1); lane::st12(g.s + h.U(12), f2);
+    lane::f12_mul(g, h.U(0), h.U(12), h.U(24)); fp12_mul(r1, f1, f2); lane::ld12(r2, g.s + h.U(24)); ok += fp12_eq(r1, r2); ++n;
+    g.a = h.U(0); g.d = h.U(24); lane::lp_fp12_sqr(g); fp12_sqr(r1, f1); lane::ld12(r2, g.s + h.U(24)); ok += fp12_eq(r1, r2); ++n;
+    for (int k = 1; k <= 3; ++k) { lane::f12_frob(g, k, h.U(0), h.U(24)); fp12_frob(r1, f1, k); lane::ld12(r2, g.s + h.U(24)); ok += fp12_eq(r1, r2); ++n; }
+    { fp12 t0, t1, cy; fp12_conj(t0, f1); fp12_inv(t1, f1); fp12_mul(cy, t0, t1); fp12_frob(t0, cy, 2); fp12_mul(cy, t0, cy);
+      lane::st12(g.s + h.U(0), cy); lane::f12_cyc_sqr(g, h.U(0), h.U(24)); fp12_cyc_sqr(r1, cy); lane::ld12(r2, g.s + h.U(24)); ok += fp12_eq(r1, r2); ++n; }
+    { fp12 m; fp12_mul(m, f1, f2); final_exponentiation(r1, m);
+      lane::st12(g.s + h.U(0), m); lane::f12_final_exp(g, h.U(0), h.U(12)); lane::ld12(r2, g.s + h.U(0)); ok += fp12_eq(r1, r2); ++n; }
+    { // Miller loop of (pk, P)
+      const int F = h.U(100), Bq = h.U(130);
+      g.s[Bq] = P.x.c0; g.s[Bq + 1] = P.x.c1; g.s[Bq + 2] = P.y.c0; g.s[Bq + 3] = P.y.c1; g.s[Bq + 4] = pk.x; g.s[Bq + 5] = pk.y;
+      lane::f12_miller(g, F, Bq); lane::ld12(r2, g.s + F); ok += fp12_eq(f1, r2); ++n; } }
   printf("%d %d\n", ok, n);
 }
 
