@@ -50,10 +50,11 @@ __global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const
 __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                            const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
                            const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
-                           fr* __restrict__ lam) {
+                           const uint32_t* __restrict__ fast, fr* __restrict__ lam) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs || status[j] != SSB_DVF_OK) return;
   if (skip_if_ok && *skip_if_ok) return;
+  if (fast && fast[j]) return;
   const uint32_t b = off[j], t = tt[j];
   uint64_t x[SSB_MAX_T];
   for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
@@ -63,11 +64,13 @@ __global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __r
                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                                       const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                                       const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
-                                                      const uint32_t* __restrict__ skip_if_ok, g2_jac* __restrict__ term) {
+                                                      const uint32_t* __restrict__ skip_if_ok, const uint32_t* __restrict__ fast,
+                                                      g2_jac* __restrict__ term) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   if (skip_if_ok && *skip_if_ok) return;
   const uint32_t j = share_job[s];
+  if (fast && fast[j]) return;
   const uint32_t k = (uint32_t)s - off[j];
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
   const fr l = lam[s];
@@ -78,10 +81,11 @@ __global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __r
 __global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
-                                                    uint8_t* __restrict__ out96) {
+                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
+  if (fast && fast[j]) return;
   uint8_t o[96];
   if (status[j] == SSB_DVF_OK) {
     unit_combine_sum(o, term + off[j], tt[j]);  // infinity(t) start (src/crypto/impls/blst.rs:74)
@@ -90,6 +94,35 @@ __global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* 
   }
   for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
 }
+// Small-integer Lagrange fast path (unit_lagrange_small): every selected share is a verified
+// (hence order-r) point, so sum c_i sig_i with the integer c_i == lambda_i mod r is the reference's
+// combination.  fast[j] = 1 when the job was finished here; the 255-bit path skips those jobs.
+__global__ void __launch_bounds__(64) k_combine_fast(int n_jobs, const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
+                                                     const uint32_t* __restrict__ sel, const uint64_t* __restrict__ ids,
+                                                     const g2_aff* __restrict__ sig_aff,
+                                                     const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ fast,
+                                                     uint8_t* __restrict__ out96) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  uint32_t done = 0;
+  if (status[j] == SSB_DVF_OK) {
+    const uint32_t t = tt[j], b = off[j];
+    uint64_t x[SSB_MAX_T];
+    int64_t c[SSB_MAX_T];
+    const g2_aff* pts[SSB_MAX_T];
+    for (uint32_t i = 0; i < t; ++i) { x[i] = ids[sel[b + i]]; pts[i] = &sig_aff[sel[b + i]]; }
+    if (unit_lagrange_small(c, x, t)) {
+      uint8_t o[96];
+      unit_combine_small(o, pts, c, t);
+      for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
+      done = 1;
+    }
+  }
+  fast[j] = done;
+}
+
 __global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) b[i] = a[i];

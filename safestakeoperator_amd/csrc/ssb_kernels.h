@@ -68,16 +68,22 @@ __global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const
 __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                            const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
                            const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
-                           fr* __restrict__ lam);
+                           const uint32_t* __restrict__ fast, fr* __restrict__ lam);
 __global__ void k_combine_terms(int n, const uint32_t* __restrict__ share_job,
                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                                       const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                                       const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
-                                                      const uint32_t* __restrict__ skip_if_ok, g2_jac* __restrict__ term);
+                                                      const uint32_t* __restrict__ skip_if_ok, const uint32_t* __restrict__ fast,
+                                                      g2_jac* __restrict__ term);
 __global__ void k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
-                                                    uint8_t* __restrict__ out96);
+                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96);
+__global__ void k_combine_fast(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                               const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                               const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
+                               const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ fast,
+                               uint8_t* __restrict__ out96);
 __global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b);
 
 }  // namespace k

@@ -132,4 +132,61 @@ SSB_FN void unit_lagrange(fr* lam, const uint64_t* x, uint32_t t) {
   }
 }
 
+// ---- small-integer Lagrange fast path -------------------------------------------------------
+// lambda_i = prod_{j!=i} x_j / (x_j - x_i) as a reduced rational, fraction by fraction (int64
+// with overflow checks).  Returns true iff every lambda_i is an integer c_i (|c_i| < 2^62): then
+// sum c_i sig_i == sum (lambda_i mod r) sig_i for points of order r, i.e. the reference's
+// combination (src/crypto/impls/blst.rs:19-39,67-87) with t tiny scalars instead of t 255-bit
+// ones.  Ids 1..t (SafeStake's usual committees) give c_i = (-1)^(i-1) binomial(t, i).
+// Duplicate ids (a zero denominator) are never eligible.
+SSB_INL int64_t i64_gcd(int64_t a, int64_t b) {
+  if (a < 0) a = -a;
+  if (b < 0) b = -b;
+  while (b) { const int64_t t = a % b; a = b; b = t; }
+  return a;
+}
+SSB_FN bool unit_lagrange_small(int64_t* c, const uint64_t* x, uint32_t t) {
+  for (uint32_t i = 0; i < t; ++i) {
+    int64_t num = 1, den = 1;
+    for (uint32_t k = 0; k < t; ++k) {
+      if (k == i) continue;
+      if (x[k] >= (1ull << 62) || x[i] >= (1ull << 62)) return false;
+      int64_t a = (int64_t)x[k], b = (int64_t)x[k] - (int64_t)x[i];
+      if (b == 0) return false;
+      int64_t g = i64_gcd(a, b); a /= g; b /= g;   // num/den and a/b both reduced: cross-reduce
+      g = i64_gcd(a, den); a /= g; den /= g;
+      g = i64_gcd(num, b); num /= g; b /= g;
+      if (__builtin_mul_overflow(num, a, &num) || __builtin_mul_overflow(den, b, &den)) return false;
+    }
+    if (den == -1) { num = -num; den = 1; }
+    if (den != 1 || num >= (1ll << 62) || num <= -(1ll << 62)) return false;
+    c[i] = num;
+  }
+  return true;
+}
+// sum c_i P_i by interleaved signed binary (shared doublings), start at infinity; exact for every
+// input (jac_add_aff handles infinity, doubling and opposite points).
+SSB_FN void unit_combine_small(uint8_t* out96, const g2_aff* const* pts, const int64_t* c, uint32_t t) {
+  int nb = 0;
+  for (uint32_t i = 0; i < t; ++i) {
+    const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
+    const int b = m ? 64 - __builtin_clzll(m) : 0;
+    nb = b > nb ? b : nb;
+  }
+  g2_jac acc; jac_set_inf(acc);
+  for (int b = nb - 1; b >= 0; --b) {
+    jac_dbl(acc, acc);
+    for (uint32_t i = 0; i < t; ++i) {
+      const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
+      if ((m >> b) & 1ull) {
+        g2_aff q = *pts[i];
+        if (c[i] < 0) fp2_neg(q.y, q.y);
+        jac_add_aff(acc, acc, q);
+      }
+    }
+  }
+  g2_aff a; jac_to_aff(a, acc);
+  g2_compress(out96, a);
+}
+
 }  // namespace ssb

@@ -325,7 +325,7 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   const size_t n = n_shares;
   size_t need = verify_ws_bytes(n, n_roots) + align_up(n * 4) * 3 + align_up(n) + align_up(n * sizeof(fr)) +
-                align_up(n * sizeof(g2_jac));
+                align_up(n * sizeof(g2_jac)) + align_up(n_jobs * 4);
   if ((rc = ensure_ws(ctx, need))) return rc;
   hipStream_t user = (hipStream_t)stream;
   hipStream_t st = ctx->stream, sc = ctx->side[1];
@@ -342,14 +342,16 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   uint8_t* verdict = share_verdicts ? share_verdicts : c.take<uint8_t>(n);
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(n);
+  uint32_t* fast = c.take<uint32_t>(n_jobs);
   hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, job_root, share_job, share_root);
   // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
   auto spec = [&] {
     hipStreamWaitEvent(sc, ctx->ev_dec, 0);
     { timed tm(ctx, "k_select", sc); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err); }
-    { timed tm(ctx, "k_lagrange", sc); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)nullptr, lam); }
-    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, term); }
-    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, out_sig96); }
+    { timed tm(ctx, "k_combine_fast", sc); hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)nullptr, fast, out_sig96); }
+    { timed tm(ctx, "k_lagrange", sc); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)nullptr, (const uint32_t*)fast, lam); }
+    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
+    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96); }
     hipEventRecord(ctx->ev_comb, sc);
   };
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict, spec))) return rc;
@@ -357,9 +359,10 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   // exact path, only if the RLC batch failed (every kernel is a no-op when w.ok == 1)
   SSB_HIP(hipStreamWaitEvent(st, ctx->ev_comb, 0));
   hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
-  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, lam);
-  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, out_sig96);
+  hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)w.ok, fast, out_sig96);
+  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, (const uint32_t*)fast, lam);
+  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, (const uint32_t*)fast, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, (const uint32_t*)fast, out_sig96);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->ev_out, st));
   SSB_HIP(hipStreamWaitEvent(user, ctx->ev_out, 0));
@@ -451,9 +454,10 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, (const uint32_t*)nullptr, share_job, (uint32_t*)nullptr);
   if (n) hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, (const uint8_t*)nullptr, 0, sig_aff, (g1_aff*)nullptr, flags);
   hipLaunchKernelGGL(k_select_all, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, flags, sel, tt, d_st, err);
-  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, (const uint32_t*)nullptr, lam);
-  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, d_out);
+  // unsafe_aggregate does not subgroup-check its inputs (blst.rs:77-84): always the exact 255-bit path
+  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, (const uint32_t*)nullptr, (const uint32_t*)nullptr, lam);
+  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, (const uint32_t*)nullptr, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
@@ -526,7 +530,7 @@ int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* ou
   SSB_HIP(hipMemcpyAsync(d_sel, sel.data(), t * 4, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_t, &tt, 4, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_st, &st0, 4, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_lagrange, dim3(1), dim3(64), 0, st, 1, d_off, d_t, d_ids, d_sel, d_st, (const uint32_t*)nullptr, d_lam);
+  hipLaunchKernelGGL(k_lagrange, dim3(1), dim3(64), 0, st, 1, d_off, d_t, d_ids, d_sel, d_st, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_lam);
   SSB_HIP(hipGetLastError());
   std::vector<fr> lam(t);
   SSB_HIP(hipMemcpyAsync(lam.data(), d_lam, t * sizeof(fr), hipMemcpyDeviceToHost, st));

@@ -313,6 +313,19 @@ int main() {
         wave::miller(w, B0, 0, 1);
         wave::load12(r2, w, B0); ok += fp12_eq(f1, r2); ++n; }
       printf("%d %d\n", ok, n);
+    } else if (cmd == "lagsmall") {  // lagsmall t id1 .. idt : fast integer path vs 255-bit path
+      int t; is >> t; std::vector<uint64_t> ids(t); for (int i = 0; i < t; ++i) is >> ids[i];
+      std::vector<g2_aff> P(t); std::vector<const g2_aff*> pp(t);
+      for (int i = 0; i < t; ++i) { uint8_t m[32] = {0}; m[0] = (uint8_t)i; m[1] = 0x77; hash_to_g2(P[i], m, (const uint8_t*)DST, (int)strlen(DST)); pp[i] = &P[i]; }
+      std::vector<int64_t> c(t); std::vector<fr> lam(t);
+      const bool elig = unit_lagrange_small(c.data(), ids.data(), (uint32_t)t);
+      unit_lagrange(lam.data(), ids.data(), (uint32_t)t);
+      std::vector<g2_jac> terms(t);
+      for (int i = 0; i < t; ++i) unit_combine_term(terms[i], P[i], lam[i].l);
+      uint8_t a[96], b[96]; unit_combine_sum(a, terms.data(), (uint32_t)t);
+      int same = -1;
+      if (elig) { unit_combine_small(b, pp.data(), c.data(), (uint32_t)t); same = memcmp(a, b, 96) == 0; }
+      printf("%d %d\n", elig ? 1 : 0, same);
     } else if (cmd == "lane") {  // lane <seed32hex>: lane-group programs vs single-lane code
       std::string s; is >> s; auto b = unhex(s);
       lane_selftest(b.data());

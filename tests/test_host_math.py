@@ -109,3 +109,17 @@ def test_lane_programs_are_current():
     before = open(hdr).read()
     subprocess.run([sys.executable, gen], check=True, capture_output=True)
     assert open(hdr).read() == before
+
+
+def test_small_lagrange_fast_path(host_exe):
+    """Integer Lagrange coefficients (ids 1..t and other id sets whose lambda_i are integers) give
+    the same combined signature as the 255-bit lambda_i mod r path; other sets are not eligible."""
+    cases = {(1, 2, 3): 1, (3, 1, 2): 1, (2, 3, 4): 1, (1, 2, 3, 4, 5): 1, tuple(range(1, 11)): 1,
+             (4, 2, 7, 1, 5, 6, 3): 1, (1, 2, 4): 0, (5, 9, 100): 0, (1, 1, 2): 0}
+    lines = ["lagsmall %d %s" % (len(k), " ".join(map(str, k))) for k in cases]
+    out = _run(host_exe, lines)
+    for (ids, elig), line in zip(cases.items(), out):
+        e, same = map(int, line.split())
+        assert e == elig, (ids, line)
+        if elig:
+            assert same == 1, ids
