@@ -78,6 +78,31 @@ __global__ void __launch_bounds__(64) k_miller_lane(int n_roots, const g1_aff* _
   if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
 }
 
+// pairs [0, n_roots): (S_r, H(root r));  [n_roots, 2 n_roots): (-g1, T_r)
+__global__ void __launch_bounds__(64) k_miller_roots(int n_roots, const g1_aff* __restrict__ s1,
+                                                     const g2_aff* __restrict__ H, const g2_aff* __restrict__ s2,
+                                                     fp12* __restrict__ f) {
+  using namespace ssb::lane;
+  __shared__ fp lds[LP_NCODE_CONST + ML_SLOTS];
+  __shared__ uint32_t flg;
+  const int p = blockIdx.x, lane_ = threadIdx.x;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  g1_aff P; g2_aff Q;
+  if (p < n_roots) { P = s1[p]; Q = H[p]; } else { P = g1_neg_generator(); Q = s2[p - n_roots]; }
+  if (P.inf || Q.inf) {  // e(O, Q) = e(P, O) = 1  (uniform per workgroup)
+    if (lane_ == 0) f[p] = fp12_one();
+    return;
+  }
+  lp_init_consts(g);
+  const int F = ML_S0, B = F + 18;
+  if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
+  if (lane_ == 4) g.s[B + 4] = P.x;
+  if (lane_ == 5) g.s[B + 5] = P.y;
+  __syncthreads();
+  f12_miller(g, F, B);
+  if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
+}
+
 // out[w] = prod of in[8w .. 8w+7]
 __global__ void __launch_bounds__(64) k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out) {
   using namespace ssb::lane;

@@ -141,5 +141,64 @@ __global__ void __launch_bounds__(64) k_fallback_verify(int n, const uint32_t* _
   verdict[s] = unit_verify_one(pk_aff[s], sig_aff[s], H[share_root[s]]) ? 1 : 0;
 }
 
+// ---- per-root RLC sums: counting sort of the shares by root, then one block per (root, group) ----
+__global__ void k_root_hist(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) atomicAdd(&cnt[share_root[s]], 1u);
+}
+__global__ void k_root_scan(int n_roots, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
+                            uint32_t* __restrict__ cursor) {
+  if (threadIdx.x != 0) return;
+  uint32_t acc = 0;
+  for (int r = 0; r < n_roots; ++r) { start[r] = acc; cursor[r] = acc; acc += cnt[r]; }
+}
+__global__ void k_root_scatter(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cursor,
+                               uint32_t* __restrict__ perm) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
+}
+// blocks [0, n_roots): S_r = sum r_i pk_i over the candidate shares of root r (G1);
+// blocks [n_roots, 2 n_roots): T_r = sum r_i sig_i (G2).  Affine outputs (infinity if none).
+// The summation order inside a segment is whatever the scatter produced: the affine sum is the
+// same group element either way, and jac_add is exact for every input.
+__global__ void __launch_bounds__(SEG_THREADS) k_sum_seg(int n_roots, const uint32_t* __restrict__ start,
+                                                         const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
+                                                         const uint32_t* __restrict__ flags, const g1_jac* __restrict__ rpk,
+                                                         const g2_jac* __restrict__ rsig, g1_aff* __restrict__ s1,
+                                                         g2_aff* __restrict__ s2) {
+  __shared__ g2_jac sh2[SEG_THREADS];
+  g1_jac* sh1 = (g1_jac*)sh2;
+  const bool g1 = (int)blockIdx.x < n_roots;
+  const int r = g1 ? blockIdx.x : blockIdx.x - n_roots;
+  const uint32_t b = start[r], e = b + cnt[r];
+  if (g1) {
+    g1_jac acc; jac_set_inf(acc);
+    for (uint32_t k = b + threadIdx.x; k < e; k += SEG_THREADS) {
+      const uint32_t s = perm[k];
+      if (flags[s] & FLAG_CANDIDATE) jac_add(acc, acc, rpk[s]);
+    }
+    sh1[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = SEG_THREADS / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) { g1_jac o = sh1[threadIdx.x + w]; jac_add(acc, acc, o); sh1[threadIdx.x] = acc; }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) { g1_aff a; jac_to_aff(a, acc); s1[r] = a; }
+  } else {
+    g2_jac acc; jac_set_inf(acc);
+    for (uint32_t k = b + threadIdx.x; k < e; k += SEG_THREADS) {
+      const uint32_t s = perm[k];
+      if (flags[s] & FLAG_CANDIDATE) jac_add(acc, acc, rsig[s]);
+    }
+    sh2[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = SEG_THREADS / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) { g2_jac o = sh2[threadIdx.x + w]; jac_add(acc, acc, o); sh2[threadIdx.x] = acc; }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) { g2_aff a; jac_to_aff(a, acc); s2[r] = a; }
+  }
+}
+
 }  // namespace k
 }  // namespace ssb

@@ -12,6 +12,16 @@ struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
 
 namespace k {
 constexpr int SUM_THREADS = 128;   // k_sum_* block size
+constexpr int SEG_THREADS = 64;    // k_sum_seg block size
+__global__ void k_root_hist(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt);
+__global__ void k_root_scan(int n_roots, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
+                            uint32_t* __restrict__ cursor);
+__global__ void k_root_scatter(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cursor,
+                               uint32_t* __restrict__ perm);
+__global__ void k_sum_seg(int n_roots, const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                          const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
+                          const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ rsig, g1_aff* __restrict__ s1,
+                          g2_aff* __restrict__ s2);
 
 __global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
                             uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root);
@@ -50,6 +60,8 @@ __global__ void k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
 __global__ void k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok);
 __global__ void k_miller_lane(int n_roots, const g1_aff* __restrict__ root_sum, const g2_aff* __restrict__ H,
                               const g2_aff* __restrict__ sig_sum, fp12* __restrict__ f);
+__global__ void k_miller_roots(int n_roots, const g1_aff* __restrict__ s1, const g2_aff* __restrict__ H,
+                               const g2_aff* __restrict__ s2, fp12* __restrict__ f);
 __global__ void k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out);
 __global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok);
 __global__ void k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,

@@ -73,6 +73,7 @@ namespace {
   } while (0)
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+const fp12 FP12_ONE_HOST = fp12_one();
 
 struct carve {
   char* base; size_t off = 0;
@@ -129,16 +130,25 @@ int fill_dst(ssb_ctx* ctx, dst_arg& d, const uint8_t* dst, size_t dst_len) {
 struct verify_ws {
   g2_aff* H; g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags;
   g2_jac* rsig; g1_jac* rpk; g1_aff* root_sum; g2_jac* part; g2_aff* sig_sum; fp12* f; uint32_t* ok;
+  g2_aff* root_sig;   // per-root sum of r_i sig_i
+  uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;  // shares sorted by root
   uint32_t* exc;  // 3n: lane-group exceptions (subgroup, RLC G2, RLC G1)
   char* hws;      // staged hash_to_G2 workspace
 };
 constexpr int G2_PARTS = 64;
+// Miller values of 2 n_roots pairs plus the levels of the 8-ary product tree
+inline size_t fp12_slots(size_t n_roots) {
+  size_t np = 2 * n_roots + 1, tot = np;
+  while (np > 8) { np = (np + 7) / 8; tot += np; }
+  return tot + 1;
+}
 
 size_t verify_ws_bytes(size_t n, size_t n_roots) {
   return align_up(n_roots * sizeof(g2_aff)) + align_up(n * sizeof(g2_aff)) + align_up(n * sizeof(g1_aff)) +
          align_up(n * 4) * 4 + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
          align_up(n_roots * sizeof(g1_aff)) + align_up(G2_PARTS * sizeof(g2_jac)) + align_up(sizeof(g2_aff)) +
-         align_up((n_roots + 1 + (n_roots + 8) / 8 + 1) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4) + align_up(launch::hash_ws_bytes(n_roots));
+         align_up(fp12_slots(n_roots) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4) + align_up(launch::hash_ws_bytes(n_roots)) +
+         align_up(n_roots * sizeof(g2_aff)) + 3 * align_up(n_roots * 4) + align_up(n * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
@@ -147,9 +157,12 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
   w.gflags = c.take<uint32_t>(n); w.rsig = c.take<g2_jac>(n); w.rpk = c.take<g1_jac>(n);
   w.root_sum = c.take<g1_aff>(n_roots); w.part = c.take<g2_jac>(G2_PARTS); w.sig_sum = c.take<g2_aff>(1);
-  w.f = c.take<fp12>(n_roots + 1 + (n_roots + 8) / 8 + 1); w.ok = c.take<uint32_t>(1);
+  w.f = c.take<fp12>(fp12_slots(n_roots)); w.ok = c.take<uint32_t>(1);
   w.exc = c.take<uint32_t>(3 * n);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
+  w.root_sig = c.take<g2_aff>(n_roots);
+  w.rcnt = c.take<uint32_t>(n_roots); w.rstart = c.take<uint32_t>(n_roots); w.rcur = c.take<uint32_t>(n_roots);
+  w.perm = c.take<uint32_t>(n);
   return w;
 }
 
@@ -171,16 +184,28 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     on_decoded();
   }
   { timed t(ctx, "k_sum");
-    if (n_roots) hipLaunchKernelGGL(k_sum_g1_by_root, dim3((unsigned)n_roots), dim3(SUM_THREADS), 0, st, (int)n, d_share_root, w.flags, w.rpk, w.root_sum);
-    hipLaunchKernelGGL(k_sum_g2_partial, dim3(G2_PARTS), dim3(SUM_THREADS), 0, st, (int)n, w.flags, w.rsig, w.part);
-    hipLaunchKernelGGL(k_sum_g2_final, dim3(1), dim3(64), 0, st, G2_PARTS, w.part, w.sig_sum); }
+    if (n_roots) {
+      SSB_HIP(hipMemsetAsync(w.rcnt, 0, n_roots * 4, st));
+      if (n) hipLaunchKernelGGL(k_root_hist, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, d_share_root, w.rcnt);
+      hipLaunchKernelGGL(k_root_scan, dim3(1), dim3(64), 0, st, (int)n_roots, w.rcnt, w.rstart, w.rcur);
+      if (n) hipLaunchKernelGGL(k_root_scatter, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, d_share_root, w.rcur, w.perm);
+      hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)(2 * n_roots)), dim3(SEG_THREADS), 0, st, (int)n_roots, w.rstart, w.rcnt,
+                         w.perm, w.flags, w.rpk, w.rsig, w.root_sum, w.root_sig);
+    }
+  }
   SSB_HIP(hipStreamWaitEvent(st, ctx->ev_hash, 0));
-  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_lane, dim3((unsigned)(n_roots + 1)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.sig_sum, w.f); }
+  { timed t(ctx, "k_miller"); if (n_roots) hipLaunchKernelGGL(k_miller_roots, dim3((unsigned)(2 * n_roots)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.root_sig, w.f); }
   {
     timed t(ctx, "k_final");
-    const int np = (int)(n_roots + 1), nparts = (np + 7) / 8;
-    hipLaunchKernelGGL(k_fp12_prod8, dim3((unsigned)nparts), dim3(64), 0, st, np, w.f, w.f + np);
-    hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, nparts, w.f + np, w.ok);
+    int np = (int)(2 * n_roots);
+    fp12* cur = w.f;
+    if (np == 0) { np = 1; SSB_HIP(hipMemcpyAsync(cur, &FP12_ONE_HOST, sizeof(fp12), hipMemcpyHostToDevice, st)); }
+    while (np > 8) {
+      const int nparts = (np + 7) / 8;
+      hipLaunchKernelGGL(k_fp12_prod8, dim3((unsigned)nparts), dim3(64), 0, st, np, cur, cur + np);
+      cur += np; np = nparts;
+    }
+    hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok);
   }
   if (n) { timed t(ctx, "k_fallback_verify"); hipLaunchKernelGGL(k_fallback_verify, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict); }
   SSB_HIP(hipGetLastError());
