@@ -29,8 +29,9 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-MAXT = 3     # max terms of an inlined product operand (value < 3p)
-MAXM = 8     # max terms of a materialised form (value < 8p < 2^384)
+MAXT = 3     # max unit terms of a plain-summed product operand (value <= 3p)
+MAXM = 8     # max unit terms of a plain-summed materialised form (value <= 8p < 2^384)
+TMAX = 16    # max terms of any form (longer ones, and scaled ones, use the accumulator engine)
 C_SCR, C_A, C_B, C_D = 48, 448, 480, 512
 N_SCR = C_A - C_SCR
 
@@ -497,9 +498,9 @@ class Sched:
                 yield ("C", c, k)
 
     def _ok(self, it, forms):
-        if it[0] == "P":
-            return wt(forms[0]) * wt(forms[1]) <= 9
-        return wt(forms[0]) <= MAXM
+        # the accumulator engine (ssb_lane.h la_*) reduces any form to < 2p: only the cost,
+        # i.e. the number of distinct terms, is bounded
+        return all(len(f.c) <= TMAX for f in forms)
 
     def _get(self, it):
         if it[0] == "P":
@@ -554,24 +555,17 @@ class Sched:
         return L({("M", len(self.mats) - 1): 1})
 
     def _chunk(self, f):
-        """f with <= MAXM terms: longer forms become sums of materialised parts."""
-        if wt(f) <= MAXM:
+        """f with <= TMAX terms: longer forms become sums of materialised parts."""
+        if len(f.c) <= TMAX:
             return f
         items = sorted(f.c.items(), key=lambda kv: (kv[0][0], str(kv[0][1])))
         acc = L()
-        for i in range(0, len(items), MAXM):
-            part = L(dict(items[i:i + MAXM]))
-            acc = acc + self._new_mat(part)
+        for i in range(0, len(items), TMAX):
+            acc = acc + self._new_mat(L(dict(items[i:i + TMAX])))
         return self._chunk(acc)
 
     def _enforce(self):
-        for i, (x, y) in enumerate(self.prods):
-            while wt(x) * wt(y) > 9:
-                if wt(x) >= wt(y):
-                    x = self._new_mat(self._chunk(x))
-                else:
-                    y = self._new_mat(self._chunk(y))
-            self.prods[i] = [x, y]
+        self.prods = [[self._chunk(x), self._chunk(y)] for x, y in self.prods]
         j = 0
         while j < len(self.mats):
             if self.alive[j]:
@@ -810,6 +804,36 @@ class Emitter:
                 out.append("        " + fn % var + " }")
         return T
 
+    @staticmethod
+    def simple(f, maxw):
+        return f is None or (len(f.c) <= maxw and all(abs(c) == 1 for c in f.c.values()))
+
+    def emit_acc(self, var, forms, exact):
+        """var = the forms' values via the accumulator engine: < 2p, or < p when exact."""
+        G, out = self.G, self.lines
+        tl = [terms_of(f) if f is not None else [] for f in forms]
+        T = max([len(t) for t in tl] + [1])
+        out.append("      { lacc A_; la_zero(A_);")
+        Ks = []
+        for r in range(G):
+            Ks.append(sum(m for (sg, m, sym) in (tl[r] if r < len(tl) else []) if sg))
+        for k in range(T):
+            codes, cp, cn = [], [], []
+            for r in range(G):
+                if r < len(tl) and k < len(tl[r]):
+                    sg, m, sym = tl[r][k]
+                    codes.append(self.s.code(sym)); cp.append(0 if sg else m); cn.append(m if sg else 0)
+                else:
+                    codes.append(0); cp.append(0); cn.append(0)
+            src = self.sel(codes)
+            if all(c == 0 for c in cn):
+                out.append("        la_ld_pos(A_, g, %s, %s);" % (src, self.sel(cp)))
+            elif all(c == 0 for c in cp):
+                out.append("        la_ld_neg(A_, g, %s, %s);" % (src, self.sel(cn)))
+            else:
+                out.append("        la_ld_mix(A_, g, %s, %s, %s);" % (src, self.sel(cp), self.sel(cn)))
+        out.append("        la_fin(%s, A_, %s, %s); }" % (var, self.sel(Ks), "true" if exact else "false"))
+
     def reduce_line(self, forms):
         """Forms evaluate to values <= w*p (terms <= p each); reduce to [0, p)."""
         w = max(wt(f) for f in forms)
@@ -845,8 +869,27 @@ class Emitter:
                 if kind == "prod":
                     out.append("    LP_FOR(%d) {" % G)
                     out.append("      fp x, y;")
-                    self.emit_form("x", [s.prods[it[1]][0] for it in chunk])
-                    self.emit_form("y", [s.prods[it[1]][1] for it in chunk])
+                    xs = [s.prods[it[1]][0] for it in chunk]
+                    ys = [s.prods[it[1]][1] for it in chunk]
+                    xp = all(self.simple(f, MAXT) for f in xs)
+                    yp = all(self.simple(f, MAXT) for f in ys)
+                    bx = max(len(f.c) for f in xs) if xp else 2
+                    by = max(len(f.c) for f in ys) if yp else 2
+                    if bx * by > 9:  # plain sums too wide for the Montgomery bound: reduce one side
+                        if xp and (bx >= by or not yp):
+                            xp, bx = False, 2
+                        else:
+                            yp, by = False, 2
+                    if bx * by > 9:
+                        xp = yp = False
+                    if xp:
+                        self.emit_form("x", xs)
+                    else:
+                        self.emit_acc("x", xs, False)
+                    if yp:
+                        self.emit_form("y", ys)
+                    else:
+                        self.emit_acc("y", ys, False)
                     out.append("      fp_mul(LP_T, x, y);")
                     out.append("    }")
                     dst = [C_SCR + s.slot[it] if s.slot[it] is not None else junk for it in chunk]
@@ -855,10 +898,13 @@ class Emitter:
                 else:
                     forms = [s.form_of(it) for it in chunk]
                     out.append("    LP_FOR(%d) {" % G)
-                    self.emit_form("LP_T", forms)
-                    red = self.reduce_line(forms)
-                    if red:
-                        out.append(red)
+                    if all(self.simple(f, MAXM) for f in forms):
+                        self.emit_form("LP_T", forms)
+                        red = self.reduce_line(forms)
+                        if red:
+                            out.append(red)
+                    else:
+                        self.emit_acc("LP_T", forms, True)
                     out.append("    }")
                     dst, cb = [], []
                     for it in chunk:

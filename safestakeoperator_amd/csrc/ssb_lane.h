@@ -135,6 +135,53 @@ SSB_INL void lp_reduce2(fp& x) { lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
 SSB_INL void lp_reduce3(fp& x) { lp_csub(x, LP_P2); lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
 SSB_INL void lp_reduce4(fp& x) { lp_csub(x, LP_P4); lp_csub(x, LP_P2); lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
 
+// ---- the accumulator engine for long / scaled forms ----------------------------------------
+// value = sum_pos c v + sum_neg |c| (p - v), per 32-bit limb in 64-bit accumulators (ONE
+// v_mad_u64_u32 per limb and term, no carry chain), then a signed carry propagation and one
+// Barrett-style step: q = floor(top / (p_hi + 1)) underestimates value / p, so value - q p lies in
+// [0, 2p) (an operand for fp_mul) and one conditional subtraction makes it < p (a stored value).
+struct lacc { uint64_t a[12], b[12]; };
+SSB_INL void la_zero(lacc& x) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) { x.a[i] = 0; x.b[i] = 0; }
+}
+SSB_INL void la_pos(lacc& x, const fp& v, uint32_t c) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x.a[i] = (uint64_t)v.l[i] * c + x.a[i];
+}
+SSB_INL void la_neg(lacc& x, const fp& v, uint32_t c) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x.b[i] = (uint64_t)v.l[i] * c + x.b[i];
+}
+SSB_INL void la_mix(lacc& x, const fp& v, uint32_t cp, uint32_t cn) { la_pos(x, v, cp); la_neg(x, v, cn); }
+template <class GR> SSB_INL void la_ld_pos(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_pos(x, *lp_ptr(g, code), c); }
+template <class GR> SSB_INL void la_ld_neg(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_neg(x, *lp_ptr(g, code), c); }
+template <class GR> SSB_INL void la_ld_mix(lacc& x, const GR& g, uint32_t code, uint32_t cp, uint32_t cn) {
+  la_mix(x, *lp_ptr(g, code), cp, cn);
+}
+constexpr double LA_INV_PHI = 1.0 / (436277738.0 + 1.0) * (1.0 - 1e-12);  // 1 / ((p >> 352) + 1), rounded down
+SSB_INL void la_fin(fp& r, const lacc& x, uint32_t K, bool exact) {
+  int64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint64_t t = (uint64_t)P_LIMBS[i] * K + x.a[i];
+    const int64_t d = (int64_t)(t - x.b[i]) + carry;
+    r.l[i] = (uint32_t)d;
+    carry = d >> 32;
+  }
+  const uint64_t hi = ((uint64_t)carry << 32) | r.l[11];  // value >> 352 (carry >= 0: value >= 0)
+  const uint32_t q = (uint32_t)((double)hi * LA_INV_PHI);
+  uint64_t pc = 0;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint64_t pr = (uint64_t)P_LIMBS[i] * q + pc;
+    pc = pr >> 32;
+    r.l[i] = subb(r.l[i], (uint32_t)pr, br, br);
+  }
+  if (exact) { lp_csub(r, P_LIMBS); lp_csub(r, P_LIMBS); }
+}
+
 template <class GR> SSB_INL void lp_chk(const GR& g, const fp& v, uint32_t bit) {
   if (bit < 31u && fp_is_zero(v)) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -326,6 +326,32 @@ int main() {
       int same = -1;
       if (elig) { unit_combine_small(b, pp.data(), c.data(), (uint32_t)t); same = memcmp(a, b, 96) == 0; }
       printf("%d %d\n", elig ? 1 : 0, same);
+    } else if (cmd == "lafin") {  // lafin <trials>: accumulator engine vs repeated modular add/sub
+      int trials; is >> trials;
+      uint64_t st = 0x9E3779B97F4A7C15ull;
+      auto rnd = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
+      int bad = 0;
+      for (int tr = 0; tr < trials; ++tr) {
+        const int t = 1 + (int)(rnd() % 16);
+        lane::lacc A; lane::la_zero(A);
+        uint32_t K = 0;
+        fp want = fp_zero();
+        for (int k = 0; k < t; ++k) {
+          fp v;
+          const int kind = (int)(rnd() % 4);
+          for (int i = 0; i < 12; ++i) v.l[i] = kind == 0 ? 0u : (kind == 1 ? P_LIMBS[i] : (uint32_t)rnd());
+          if (kind == 1) v.l[0] -= 1;                       // p - 1
+          if (kind >= 2) { v.l[11] &= 0x0fffffffu; }         // < p
+          const int m = (tr & 1) ? 1 + (int)(rnd() % 300) : 1 + (int)(rnd() % 3);
+          const bool neg = rnd() & 1;
+          if (neg) { lane::la_neg(A, v, (uint32_t)m); K += (uint32_t)m; } else lane::la_pos(A, v, (uint32_t)m);
+          for (int j = 0; j < m; ++j) { if (neg) fp_sub(want, want, v); else fp_add(want, want, v); }
+        }
+        fp r, r2; lane::la_fin(r, A, K, true); lane::la_fin(r2, A, K, false);
+        fp r2m; lane::lp_csub(r2, P_LIMBS); r2m = r2; lane::lp_csub(r2m, P_LIMBS);
+        if (!fp_eq(r, want) || !fp_eq(r2m, want)) ++bad;
+      }
+      printf("%d\n", bad);
     } else if (cmd == "lane") {  // lane <seed32hex>: lane-group programs vs single-lane code
       std::string s; is >> s; auto b = unhex(s);
       lane_selftest(b.data());

@@ -123,3 +123,9 @@ def test_small_lagrange_fast_path(host_exe):
         assert e == elig, (ids, line)
         if elig:
             assert same == 1, ids
+
+
+def test_accumulator_engine_reduction(host_exe):
+    """la_fin (sum of scaled +-terms, one Barrett-style step) equals the modular sum, including the
+    edge values 0 and p-1 and coefficients up to 300 per term."""
+    assert _run(host_exe, ["lafin 20000"]) == ["0"]
