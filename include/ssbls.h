@@ -69,6 +69,11 @@ typedef struct ssb_ctx ssb_ctx;
 int ssb_create(ssb_ctx** out, int device_ordinal);
 void ssb_destroy(ssb_ctx* ctx);
 const char* ssb_last_error(const ssb_ctx* ctx);
+/* Number of pipeline slots (1..8, default 1).  Each slot owns its streams and workspace; calls of
+ * ssb_threshold_aggregate_batch_dev go to the slots round robin, so up to `depth` independent
+ * batches are in flight and overlap on the device (e.g. the duties of consecutive slots).  Each
+ * call's outputs are ready when the caller's `stream` reaches them. */
+int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth);
 /* Device-side kernel timing with hipEvents recorded on the engine's stream around each launch.
  * ssb_last_kernel_ms: the last launch of `kernel_name`.  ssb_kernel_timing(ctx, 1) clears and
  * starts accumulating every launch; ssb_kernel_time returns the total and the launch count. */

@@ -19,6 +19,7 @@ SIGNATURES = {
     "ssb_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
     "ssb_destroy": (None, [_ctx]),
     "ssb_last_error": (ctypes.c_char_p, [_ctx]),
+    "ssb_set_pipeline_depth": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_last_kernel_ms": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float)]),
     "ssb_kernel_timing": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_kernel_time": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]),

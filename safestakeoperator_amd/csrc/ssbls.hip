@@ -40,17 +40,26 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-struct ssb_ctx {
-  int device = 0;
+// One pipeline slot: its own streams, events and workspace, so batches submitted to different
+// slots (ssb_set_pipeline_depth) are independent and overlap on the device.
+struct ssb_slot {
   hipStream_t stream = nullptr;     // main chain: decode -> RLC -> sums -> Miller -> final exp
   hipStream_t side[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] hash_to_G2, [1] speculative combine,
-                                                               // [2] RLC on G2, [3] RLC on G1
+                                                               // [2], [3] spare
   hipEvent_t ev_in = nullptr, ev_hash = nullptr, ev_dec = nullptr, ev_comb = nullptr, ev_out = nullptr;
-  hipEvent_t ev_sdec = nullptr, ev_r2 = nullptr, ev_r1 = nullptr;
-  std::string err;
+  hipEvent_t ev_sdec = nullptr, ev_r2 = nullptr, ev_r1 = nullptr, ev_user = nullptr;
   // workspace arena (grown on demand, never shrunk)
   void* ws = nullptr;
   size_t ws_bytes = 0;
+};
+constexpr int SSB_MAX_SLOTS = 8;
+
+struct ssb_ctx {
+  int device = 0;
+  ssb_slot sl[SSB_MAX_SLOTS];
+  int nslots = 1, next = 0;
+  ssb_slot* cur = &sl[0];           // the slot the current call runs on
+  std::string err;
   // host staging arena
   void* io = nullptr;
   size_t io_bytes = 0;
@@ -81,11 +90,11 @@ struct carve {
 };
 
 int ensure_ws(ssb_ctx* ctx, size_t bytes) {
-  if (bytes <= ctx->ws_bytes) return SSB_OK;
-  if (ctx->ws) { hipStreamSynchronize(ctx->stream); hipFree(ctx->ws); ctx->ws = nullptr; ctx->ws_bytes = 0; }
+  if (bytes <= ctx->cur->ws_bytes) return SSB_OK;
+  if (ctx->cur->ws) { hipStreamSynchronize(ctx->cur->stream); hipFree(ctx->cur->ws); ctx->cur->ws = nullptr; ctx->cur->ws_bytes = 0; }
   size_t want = bytes + bytes / 4;
-  if (hipMalloc(&ctx->ws, want) != hipSuccess) { ctx->err = "hipMalloc workspace failed"; ctx->ws = nullptr; return SSB_ENOMEM; }
-  ctx->ws_bytes = want;
+  if (hipMalloc(&ctx->cur->ws, want) != hipSuccess) { ctx->err = "hipMalloc workspace failed"; ctx->cur->ws = nullptr; return SSB_ENOMEM; }
+  ctx->cur->ws_bytes = want;
   return SSB_OK;
 }
 
@@ -100,10 +109,30 @@ int ensure_io(ssb_ctx* ctx, size_t bytes) {
 
 inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
+int init_slot(ssb_slot& S) {
+  if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
+  for (hipStream_t& sd : S.side)
+    if (hipStreamCreateWithFlags(&sd, hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
+  for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user})
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
+  return SSB_OK;
+}
+void sync_slot(ssb_slot& S) {
+  if (S.stream) hipStreamSynchronize(S.stream);
+  for (hipStream_t sd : S.side) if (sd) hipStreamSynchronize(sd);
+}
+void free_slot(ssb_slot& S) {
+  if (S.ws) hipFree(S.ws);
+  for (hipStream_t sd : S.side) if (sd) hipStreamDestroy(sd);
+  for (hipEvent_t e : {S.ev_in, S.ev_hash, S.ev_dec, S.ev_comb, S.ev_out, S.ev_sdec, S.ev_r2, S.ev_r1, S.ev_user})
+    if (e) hipEventDestroy(e);
+  if (S.stream) hipStreamDestroy(S.stream);
+}
+
 // hipEvent pair around one kernel launch on the engine's stream (the stream the kernel runs on)
 struct timed {
   ssb_ctx* ctx; ssb_ctx::evpair p; std::string name; hipStream_t st;
-  timed(ssb_ctx* c, const char* nm, hipStream_t s = nullptr) : ctx(c), name(nm), st(s ? s : c->stream) {
+  timed(ssb_ctx* c, const char* nm, hipStream_t s = nullptr) : ctx(c), name(nm), st(s ? s : c->cur->stream) {
     if (!ctx->pool.empty()) { p = ctx->pool.back(); ctx->pool.pop_back(); }
     else { hipEventCreate(&p.a); hipEventCreate(&p.b); }
     hipEventRecord(p.a, st);
@@ -170,17 +199,17 @@ template <class F>
 int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
                const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t seed,
                uint8_t* d_verdict, F on_decoded) {
-  hipStream_t st = ctx->stream, sh = ctx->side[0];
+  hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
-  SSB_HIP(hipEventRecord(ctx->ev_in, st));
-  SSB_HIP(hipStreamWaitEvent(sh, ctx->ev_in, 0));
+  SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
+  SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
   if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
-  SSB_HIP(hipEventRecord(ctx->ev_hash, sh));
+  SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
   if (n) {
     { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags); }
     { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_check_rlc, dim3(nblk(3 * n, 64)), dim3(64), 0, st, (int)n, seed, w.sflags, w.pflags, w.sig_aff, w.pk_aff, w.gflags, w.rsig, w.rpk); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, w.flags);
-    SSB_HIP(hipEventRecord(ctx->ev_dec, st));
+    SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));
     on_decoded();
   }
   { timed t(ctx, "k_sum");
@@ -193,7 +222,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
                          w.perm, w.flags, w.rpk, w.rsig, w.root_sum, w.root_sig);
     }
   }
-  SSB_HIP(hipStreamWaitEvent(st, ctx->ev_hash, 0));
+  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
   { timed t(ctx, "k_miller"); if (n_roots) hipLaunchKernelGGL(k_miller_roots, dim3((unsigned)(2 * n_roots)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.root_sig, w.f); }
   {
     timed t(ctx, "k_final");
@@ -226,14 +255,7 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   ssb_ctx* ctx = new (std::nothrow) ssb_ctx();
   if (!ctx) return SSB_ENOMEM;
   ctx->device = device_ordinal;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->side[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->side[1], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->side[2], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->side[3], hipStreamNonBlocking) != hipSuccess) { delete ctx; return SSB_EHIP; }
-  for (hipEvent_t* e : {&ctx->ev_in, &ctx->ev_hash, &ctx->ev_dec, &ctx->ev_comb, &ctx->ev_out, &ctx->ev_sdec,
-                        &ctx->ev_r2, &ctx->ev_r1})
-    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) { delete ctx; return SSB_EHIP; }
+  if (init_slot(ctx->sl[0]) != SSB_OK) { delete ctx; return SSB_EHIP; }
   *out = ctx;
   return SSB_OK;
 }
@@ -241,17 +263,26 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
 void ssb_destroy(ssb_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
-  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
   for (auto& kv : ctx->timers) { if (kv.second.a) hipEventDestroy(kv.second.a); if (kv.second.b) hipEventDestroy(kv.second.b); }
   for (auto& kv : ctx->history) for (auto& p : kv.second) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   for (auto& p : ctx->pool) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
-  if (ctx->ws) hipFree(ctx->ws);
   if (ctx->io) hipFree(ctx->io);
-  for (hipStream_t sd : ctx->side) if (sd) { hipStreamSynchronize(sd); hipStreamDestroy(sd); }
-  for (hipEvent_t e : {ctx->ev_in, ctx->ev_hash, ctx->ev_dec, ctx->ev_comb, ctx->ev_out, ctx->ev_sdec, ctx->ev_r2, ctx->ev_r1})
-    if (e) hipEventDestroy(e);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
+}
+
+int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
+  if (!ctx || depth < 1 || depth > SSB_MAX_SLOTS) return SSB_EINVAL;
+  SSB_HIP(hipSetDevice(ctx->device));
+  for (int i = ctx->nslots; i < depth; ++i) {
+    if (init_slot(ctx->sl[i]) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
+    ctx->nslots = i + 1;
+  }
+  for (int i = depth; i < ctx->nslots; ++i) { sync_slot(ctx->sl[i]); free_slot(ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
+  ctx->nslots = depth;
+  ctx->next = 0;
+  return SSB_OK;
 }
 
 const char* ssb_last_error(const ssb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -268,7 +299,7 @@ int ssb_last_kernel_ms(const ssb_ctx* ctx_c, const char* name, float* ms) {
 
 int ssb_kernel_timing(ssb_ctx* ctx, int on) {
   if (!ctx) return SSB_EINVAL;
-  SSB_HIP(hipStreamSynchronize(ctx->stream));
+  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
   for (auto& kv : ctx->history) for (auto& p : kv.second) ctx->pool.push_back(p);
   ctx->history.clear();
   ctx->accumulate = on != 0;
@@ -297,15 +328,15 @@ int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t*
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   size_t need = align_up(n * 32) + align_up(n * sizeof(g2_aff)) + align_up(n * 192) + align_up(launch::hash_ws_bytes(n));
   if ((rc = ensure_ws(ctx, need))) return rc;
-  carve c{(char*)ctx->ws};
+  carve c{(char*)ctx->cur->ws};
   uint8_t* d_msg = c.take<uint8_t>(n * 32); g2_aff* d_h = c.take<g2_aff>(n); uint8_t* d_out = c.take<uint8_t>(n * 192);
   char* hws = c.take<char>(launch::hash_ws_bytes(n));
-  SSB_HIP(hipMemcpyAsync(d_msg, msgs32, n * 32, hipMemcpyHostToDevice, ctx->stream));
-  { timed t(ctx, "k_hash_to_g2"); launch::hash_to_g2(ctx->stream, (int)n, d_msg, d, d_h, hws); }
-  hipLaunchKernelGGL(k_serialize_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->stream, (int)n, d_h, d_out);
+  SSB_HIP(hipMemcpyAsync(d_msg, msgs32, n * 32, hipMemcpyHostToDevice, ctx->cur->stream));
+  { timed t(ctx, "k_hash_to_g2"); launch::hash_to_g2(ctx->cur->stream, (int)n, d_msg, d, d_h, hws); }
+  hipLaunchKernelGGL(k_serialize_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->cur->stream, (int)n, d_h, d_out);
   SSB_HIP(hipGetLastError());
-  SSB_HIP(hipMemcpyAsync(out192, d_out, n * 192, hipMemcpyDeviceToHost, ctx->stream));
-  SSB_HIP(hipStreamSynchronize(ctx->stream));
+  SSB_HIP(hipMemcpyAsync(out192, d_out, n * 192, hipMemcpyDeviceToHost, ctx->cur->stream));
+  SSB_HIP(hipStreamSynchronize(ctx->cur->stream));
   return SSB_OK;
 }
 
@@ -324,12 +355,12 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
   carve ci{(char*)ctx->io};
   uint8_t* d_pk = ci.take<uint8_t>(n * 48); uint8_t* d_sig = ci.take<uint8_t>(n * 96);
   uint32_t* d_root = ci.take<uint32_t>(n); uint8_t* d_roots = ci.take<uint8_t>(n_roots * 32); uint8_t* d_v = ci.take<uint8_t>(n);
-  hipStream_t st = ctx->stream;
+  hipStream_t st = ctx->cur->stream;
   SSB_HIP(hipMemcpyAsync(d_pk, pk48, n * 48, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_sig, sig96, n * 96, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_root, root_idx, n * 4, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
-  carve c{(char*)ctx->ws};
+  carve c{(char*)ctx->cur->ws};
   verify_ws w = carve_verify(c, n, n_roots);
   if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, d_root, d_roots, d, rlc_seed, d_v, [] {}))) return rc;
   SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
@@ -347,19 +378,21 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0 ||
       (n_shares && (!sig96 || !pk48 || !ids))) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  ctx->cur = &ctx->sl[ctx->next];   // pipeline slot: batches on different slots overlap
+  ctx->next = (ctx->next + 1) % ctx->nslots;
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   const size_t n = n_shares;
   size_t need = verify_ws_bytes(n, n_roots) + align_up(n * 4) * 3 + align_up(n) + align_up(n * sizeof(fr)) +
                 align_up(n * sizeof(g2_jac)) + align_up(n_jobs * 4);
   if ((rc = ensure_ws(ctx, need))) return rc;
   hipStream_t user = (hipStream_t)stream;
-  hipStream_t st = ctx->stream, sc = ctx->side[1];
+  hipStream_t st = ctx->cur->stream, sc = ctx->cur->side[1];
   // order the engine's streams after the caller's stream, and the caller's stream after them
   hipEvent_t e_user;
   SSB_HIP(hipEventCreateWithFlags(&e_user, hipEventDisableTiming));
   SSB_HIP(hipEventRecord(e_user, user));
   SSB_HIP(hipStreamWaitEvent(st, e_user, 0));
-  carve c{(char*)ctx->ws};
+  carve c{(char*)ctx->cur->ws};
   verify_ws w = carve_verify(c, n, n_roots);
   uint32_t* share_job = c.take<uint32_t>(n);
   uint32_t* share_root = c.take<uint32_t>(n);
@@ -371,26 +404,26 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, job_root, share_job, share_root);
   // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
   auto spec = [&] {
-    hipStreamWaitEvent(sc, ctx->ev_dec, 0);
+    hipStreamWaitEvent(sc, ctx->cur->ev_dec, 0);
     { timed tm(ctx, "k_select", sc); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err); }
     { timed tm(ctx, "k_combine_fast", sc); hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)nullptr, fast, out_sig96); }
     { timed tm(ctx, "k_lagrange", sc); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)nullptr, (const uint32_t*)fast, lam); }
     if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96); }
-    hipEventRecord(ctx->ev_comb, sc);
+    hipEventRecord(ctx->cur->ev_comb, sc);
   };
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict, spec))) return rc;
   if (!n) spec();
   // exact path, only if the RLC batch failed (every kernel is a no-op when w.ok == 1)
-  SSB_HIP(hipStreamWaitEvent(st, ctx->ev_comb, 0));
+  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_comb, 0));
   hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
   hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)w.ok, fast, out_sig96);
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, (const uint32_t*)fast, lam);
   if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, (const uint32_t*)fast, term);
   hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, (const uint32_t*)fast, out_sig96);
   SSB_HIP(hipGetLastError());
-  SSB_HIP(hipEventRecord(ctx->ev_out, st));
-  SSB_HIP(hipStreamWaitEvent(user, ctx->ev_out, 0));
+  SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
+  SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
   hipEventDestroy(e_user);
   return SSB_OK;
 }
@@ -423,7 +456,7 @@ int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* s
   uint32_t* d_off = ci.take<uint32_t>(n_jobs + 1); uint32_t* d_t = ci.take<uint32_t>(n_jobs); uint32_t* d_jr = ci.take<uint32_t>(n_jobs);
   uint8_t* d_roots = ci.take<uint8_t>(n_roots * 32); uint8_t* d_out = ci.take<uint8_t>(n_jobs * 96);
   int32_t* d_st = ci.take<int32_t>(n_jobs); uint64_t* d_err = ci.take<uint64_t>(n_jobs * 2); uint8_t* d_v = ci.take<uint8_t>(n);
-  hipStream_t st = ctx->stream;
+  hipStream_t st = ctx->cur->stream;
   if (n) {
     SSB_HIP(hipMemcpyAsync(d_sig, sig96, n * 96, hipMemcpyHostToDevice, st));
     SSB_HIP(hipMemcpyAsync(d_pk, pk48, n * 48, hipMemcpyHostToDevice, st));
@@ -466,11 +499,11 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   carve ci{(char*)ctx->io};
   uint8_t* d_sig = ci.take<uint8_t>(n * 96); uint64_t* d_ids = ci.take<uint64_t>(n); uint32_t* d_off = ci.take<uint32_t>(n_jobs + 1);
   uint8_t* d_out = ci.take<uint8_t>(n_jobs * 96); int32_t* d_st = ci.take<int32_t>(n_jobs);
-  carve c{(char*)ctx->ws};
+  carve c{(char*)ctx->cur->ws};
   g2_aff* sig_aff = c.take<g2_aff>(n); uint32_t* flags = c.take<uint32_t>(n); uint32_t* share_job = c.take<uint32_t>(n);
   uint32_t* sel = c.take<uint32_t>(n); uint32_t* tt = c.take<uint32_t>(n_jobs); uint64_t* err = c.take<uint64_t>(n_jobs * 2);
   fr* lam = c.take<fr>(n); g2_jac* term = c.take<g2_jac>(n);
-  hipStream_t st = ctx->stream;
+  hipStream_t st = ctx->cur->stream;
   if (n) {
     SSB_HIP(hipMemcpyAsync(d_sig, sig96, n * 96, hipMemcpyHostToDevice, st));
     SSB_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, st));
@@ -501,11 +534,11 @@ int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t
   size_t need = align_up(n * 32) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n_roots * sizeof(g2_aff)) + align_up(n * 96) +
                 align_up(launch::hash_ws_bytes(n_roots));
   if ((rc = ensure_ws(ctx, need))) return rc;
-  carve c{(char*)ctx->ws};
+  carve c{(char*)ctx->cur->ws};
   uint8_t* d_sk = c.take<uint8_t>(n * 32); uint32_t* d_ri = c.take<uint32_t>(n); uint8_t* d_roots = c.take<uint8_t>(n_roots * 32);
   g2_aff* d_h = c.take<g2_aff>(n_roots); uint8_t* d_out = c.take<uint8_t>(n * 96);
   char* hws = c.take<char>(launch::hash_ws_bytes(n_roots));
-  hipStream_t st = ctx->stream;
+  hipStream_t st = ctx->cur->stream;
   SSB_HIP(hipMemcpyAsync(d_sk, sk32le, n * 32, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_ri, root_idx, n * 4, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
@@ -525,9 +558,9 @@ int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* o
   int rc;
   size_t need = align_up(n * 32) + align_up(n * 48);
   if ((rc = ensure_ws(ctx, need))) return rc;
-  carve c{(char*)ctx->ws};
+  carve c{(char*)ctx->cur->ws};
   uint8_t* d_sk = c.take<uint8_t>(n * 32); uint8_t* d_out = c.take<uint8_t>(n * 48);
-  hipStream_t st = ctx->stream;
+  hipStream_t st = ctx->cur->stream;
   SSB_HIP(hipMemcpyAsync(d_sk, sk32le, n * 32, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_sk_to_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sk, d_out);
   SSB_HIP(hipGetLastError());
@@ -544,12 +577,12 @@ int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* ou
   int rc;
   size_t need = align_up(8 * 4) + align_up(t * 8) + align_up(t * 4) + align_up(4) + align_up(t * sizeof(fr));
   if ((rc = ensure_ws(ctx, need))) return rc;
-  carve c{(char*)ctx->ws};
+  carve c{(char*)ctx->cur->ws};
   uint32_t* d_off = c.take<uint32_t>(2); uint64_t* d_ids = c.take<uint64_t>(t); uint32_t* d_sel = c.take<uint32_t>(t);
   uint32_t* d_t = c.take<uint32_t>(1); int32_t* d_st = c.take<int32_t>(1); fr* d_lam = c.take<fr>(t);
   std::vector<uint32_t> sel(t); for (size_t i = 0; i < t; ++i) sel[i] = (uint32_t)i;
   uint32_t off[2] = {0, (uint32_t)t}; uint32_t tt = (uint32_t)t; int32_t st0 = 0;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = ctx->cur->stream;
   SSB_HIP(hipMemcpyAsync(d_off, off, 8, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_ids, ids, t * 8, hipMemcpyHostToDevice, st));
   SSB_HIP(hipMemcpyAsync(d_sel, sel.data(), t * 4, hipMemcpyHostToDevice, st));

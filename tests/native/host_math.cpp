@@ -257,6 +257,12 @@ int main() {
       uint8_t o96[96];
       unit_combine_sum(o96, terms, 3); rec("combine_sum_t3", 1);
       unit_combine_sum(o96, terms, 10); rec("combine_sum_t10", 1);
+      { // small-integer Lagrange path (ids 1..t): coefficients + the shared-doubling combination
+        const g2_aff* pp[10] = {&sig, &H, &sig, &H, &sig, &H, &sig, &H, &sig, &H};
+        int64_t c[10];
+        unit_lagrange_small(c, ids3, 3); unit_combine_small(o96, pp, c, 3); rec("combine_small_t3", 1);
+        unit_lagrange_small(c, ids5, 5); unit_combine_small(o96, pp, c, 5); rec("combine_small_t5", 1);
+        unit_lagrange_small(c, ids10, 10); unit_combine_small(o96, pp, c, 10); rec("combine_small_t10", 1); }
       js += ok ? ", \"verify_ok\": true}" : ", \"verify_ok\": false}";
       printf("%s\n", js.c_str());
 #else
