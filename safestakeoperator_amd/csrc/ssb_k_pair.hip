@@ -103,6 +103,52 @@ __global__ void __launch_bounds__(64) k_miller_roots(int n_roots, const g1_aff* 
   if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
 }
 
+// Exact per-share verification e(pk, H(m)) * e(-g1, sig) == 1, run when the RLC batch check
+// failed (a no-op otherwise).  A bounded grid of 64-lane workgroups strides over the shares; each
+// candidate runs two lane-program Miller loops, one Fp12 product and one final exponentiation out of
+// LDS (the single-lane form needs ~9 KB of scratch per lane, which a full-size grid cannot reserve
+// on every hardware queue).
+constexpr int FB_S0 = ML_S0 > lane::FP12_MUL_SCRATCH ? ML_S0 : lane::FP12_MUL_SCRATCH;
+constexpr int FB_SLOTS = FB_S0 + 18 + 6 + 18 + 84;
+__global__ void __launch_bounds__(64) k_fallback_lane(int n, const uint32_t* __restrict__ ok,
+                                                      const uint32_t* __restrict__ flags,
+                                                      const uint32_t* __restrict__ share_root,
+                                                      const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_aff,
+                                                      const g1_aff* __restrict__ pk_aff, uint8_t* __restrict__ verdict) {
+  using namespace ssb::lane;
+  if (*ok) return;  // uniform: the batch passed
+  __shared__ fp lds[LP_NCODE_CONST + FB_SLOTS];
+  __shared__ uint32_t flg;
+  const int lane_ = threadIdx.x;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  lp_init_consts(g);
+  const int F1 = FB_S0, B = F1 + 18, F2 = B + 6, TMP = F2 + 18;
+  for (int s = blockIdx.x; s < n; s += gridDim.x) {
+    if (!(flags[s] & FLAG_CANDIDATE)) continue;  // uniform per workgroup; verdict written by k_verdict_fast
+    const g1_aff pk = pk_aff[s];
+    const g2_aff h = H[share_root[s]], sg = sig_aff[s];
+    const g1_aff ng = g1_neg_generator();
+    if (lane_ < 4) g.s[B + lane_] = ((const fp*)&h)[lane_];
+    if (lane_ == 4) g.s[B + 4] = pk.x;
+    if (lane_ == 5) g.s[B + 5] = pk.y;
+    __syncthreads();
+    f12_miller(g, F1, B);                     // e(pk, H(m)) before the final exponentiation
+    if (lane_ < 4) g.s[B + lane_] = ((const fp*)&sg)[lane_];
+    if (lane_ == 4) g.s[B + 4] = ng.x;
+    if (lane_ == 5) g.s[B + 5] = ng.y;
+    __syncthreads();
+    f12_miller(g, F2, B);                     // e(-g1, sig)
+    f12_mul(g, F1, F2, F1);
+    f12_final_exp(g, F1, TMP);
+    if (lane_ == 0) {
+      fp12 e;
+      ld12(e, g.s + F1);
+      verdict[s] = fp12_is_one(e) ? 1 : 0;
+    }
+    __syncthreads();
+  }
+}
+
 // out[w] = prod of in[8w .. 8w+7]
 __global__ void __launch_bounds__(64) k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out) {
   using namespace ssb::lane;

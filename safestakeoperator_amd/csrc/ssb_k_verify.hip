@@ -127,18 +127,14 @@ __global__ void __launch_bounds__(64) k_sum_g2_final(int nparts, const g2_jac* _
   }
   if (threadIdx.x == 0) { g2_aff a; jac_to_aff(a, acc); *out = a; }
 }
-__global__ void __launch_bounds__(64) k_fallback_verify(int n, const uint32_t* __restrict__ ok,
-                                                        const uint32_t* __restrict__ flags,
-                                                        const uint32_t* __restrict__ share_root,
-                                                        const g2_aff* __restrict__ H,
-                                                        const g2_aff* __restrict__ sig_aff,
-                                                        const g1_aff* __restrict__ pk_aff,
-                                                        uint8_t* __restrict__ verdict) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
+// Verdicts when the RLC batch check passed (every candidate is valid) and for non-candidates; the
+// candidates of a failed batch are left to k_fallback_lane (ssb_k_pair.hip).
+__global__ void k_verdict_fast(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
+                               uint8_t* __restrict__ verdict) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
-  if (*ok || !cand) { verdict[s] = cand ? 1 : 0; return; }
-  verdict[s] = unit_verify_one(pk_aff[s], sig_aff[s], H[share_root[s]]) ? 1 : 0;
+  if (*ok || !cand) verdict[s] = cand ? 1 : 0;
 }
 
 // ---- per-root RLC sums: counting sort of the shares by root, then one block per (root, group) ----

@@ -47,13 +47,12 @@ __global__ void k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
                                                                 g2_jac* __restrict__ part);
 __global__ void k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
                                                      g2_aff* __restrict__ out);
-__global__ void k_fallback_verify(int n, const uint32_t* __restrict__ ok,
-                                                        const uint32_t* __restrict__ flags,
-                                                        const uint32_t* __restrict__ share_root,
-                                                        const g2_aff* __restrict__ H,
-                                                        const g2_aff* __restrict__ sig_aff,
-                                                        const g1_aff* __restrict__ pk_aff,
-                                                        uint8_t* __restrict__ verdict);
+__global__ void k_verdict_fast(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
+                               uint8_t* __restrict__ verdict);
+__global__ void k_fallback_lane(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
+                                const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ H,
+                                const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
+                                uint8_t* __restrict__ verdict);
 __global__ void k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
                                                     const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
                                                     fp12* __restrict__ f);

@@ -24,6 +24,7 @@
 #include <vector>
 #include <map>
 #include <mutex>
+#include <algorithm>
 
 #include "ssb_units.h"
 #include "ssb_wave.h"
@@ -111,8 +112,8 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 
 int init_slot(ssb_slot& S) {
   if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
-  for (hipStream_t& sd : S.side)
-    if (hipStreamCreateWithFlags(&sd, hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
+  for (int i = 0; i < 2; ++i)  // side[0] hash_to_G2, side[1] speculative combine (side[2..3] unused)
+    if (hipStreamCreateWithFlags(&S.side[i], hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
   for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
   return SSB_OK;
@@ -236,7 +237,12 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     }
     hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok);
   }
-  if (n) { timed t(ctx, "k_fallback_verify"); hipLaunchKernelGGL(k_fallback_verify, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict); }
+  if (n) {
+    timed t(ctx, "k_fallback_verify");
+    hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.ok, w.flags, d_verdict);
+    hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, st, (int)n, w.ok, w.flags,
+                       d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
+  }
   SSB_HIP(hipGetLastError());
   return SSB_OK;
 }
