@@ -174,6 +174,46 @@ template <class F> SSB_FN void jac_mul_w4(jac<F>& r, const aff<F>& p, const uint
   r = acc;
 }
 
+// [k]P for an affine P and an ODD scalar of `nwords` 32-bit LE words: regular signed window, w = 4
+// (Joye-Tunstall recoding: 8*nwords odd digits in [-15, 15], every window adds a table entry).
+// The table holds the 8 odd multiples P, 3P, .., 15P (half the 16-entry table of jac_mul_w4, so
+// half the private memory per lane).  Exact for every input: jac_add handles all special cases.
+template <class F> SSB_FN void jac_mul_sw4_odd(jac<F>& r, const aff<F>& p, const uint32_t* k_in, int nwords) {
+  int8_t dig[64];
+  uint32_t k[8];
+  for (int i = 0; i < 8; ++i) k[i] = i < nwords ? k_in[i] : 0u;
+  const int W = 8 * nwords;
+  for (int j = 0; j < W - 1; ++j) {  // d = (k mod 32) - 16;  k = (k - d) / 16
+    const int d = (int)(k[0] & 31u) - 16;
+    dig[j] = (int8_t)d;
+    uint32_t br = 0;                   // k -= d (d < 0: k += |d|), then k >>= 4
+    if (d >= 0) {
+      uint32_t s = (uint32_t)d;
+      for (int i = 0; i < nwords; ++i) { k[i] = subb(k[i], s, br, br); s = 0; }
+    } else {
+      uint32_t s = (uint32_t)(-d), c = 0;
+      for (int i = 0; i < nwords; ++i) { k[i] = addc(k[i], s, c, c); s = 0; }
+    }
+    for (int i = 0; i < nwords - 1; ++i) k[i] = (k[i] >> 4) | (k[i + 1] << 28);
+    k[nwords - 1] >>= 4;
+  }
+  dig[W - 1] = (int8_t)k[0];
+  jac<F> tab[8], p2;
+  jac_from_aff(tab[0], p);
+  jac_dbl(p2, tab[0]);
+  jac_add_aff(tab[1], p2, p);
+  for (int i = 2; i < 8; ++i) jac_add(tab[i], tab[i - 1], p2);
+  jac<F> acc = tab[(dig[W - 1] - 1) >> 1];
+  for (int j = W - 2; j >= 0; --j) {
+    jac_dbl(acc, acc); jac_dbl(acc, acc); jac_dbl(acc, acc); jac_dbl(acc, acc);
+    const int d = dig[j];
+    jac<F> t = tab[((d < 0 ? -d : d) - 1) >> 1];
+    if (d < 0) jac_neg(t, t);
+    jac_add(acc, acc, t);
+  }
+  r = acc;
+}
+
 // [|x|]P, x = -0xd201000000010000 (wave-uniform scalar: branch-free across lanes)
 template <class F> SSB_FN void jac_mul_x_abs(jac<F>& r, const jac<F>& p) {
   jac<F> acc = p;

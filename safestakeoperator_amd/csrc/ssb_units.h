@@ -44,13 +44,14 @@ SSB_FN uint32_t unit_decode(g2_aff& sig, g1_aff& pk, const uint8_t* sig96, const
 SSB_FN uint32_t unit_decode_sig(g2_aff& sig, const uint8_t* sig96) { return g2_decompress(sig, sig96); }
 SSB_FN uint32_t unit_decode_pk(g1_aff& pk, const uint8_t* pk48) { return g1_decompress(pk, pk48); }
 SSB_FN uint32_t unit_subgroup(const g2_aff& sig) { return g2_in_subgroup(sig) ? DEC_IN_GROUP : 0u; }
+// (k odd: the RLC scalars are rlc_scalar_odd)
 SSB_FN void unit_rlc_sig(g2_jac& r, const g2_aff& sig, uint64_t k) {
   const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
-  jac_mul_w4(r, sig, kw, 2);
+  jac_mul_sw4_odd(r, sig, kw, 2);
 }
 SSB_FN void unit_rlc_pk(g1_jac& r, const g1_aff& pk, uint64_t k) {
   const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
-  jac_mul_w4(r, pk, kw, 2);
+  jac_mul_sw4_odd(r, pk, kw, 2);
 }
 SSB_INL uint32_t combine_flags(uint32_t sf, uint32_t pf, uint32_t gf) {
   const uint32_t st = sf | gf;
@@ -77,9 +78,17 @@ SSB_FN bool unit_verify_one(const g1_aff& pk, const g2_aff& sig, const g2_aff& H
   return fp12_is_one(e);
 }
 
-// unit "combine_term": lambda_i * sig_i (blst_p2_mult with 255-bit scalar)
+// unit "combine_term": lambda_i * sig_i (blst_p2_mult with 255-bit scalar).  Odd lambda: signed
+// window directly; even lambda: (lambda + 1) sig - sig, exact for every point (unsafe_aggregate
+// does not subgroup-check, so lambda + r would not do).  lambda < r: lambda + 1 fits 255 bits.
 SSB_FN void unit_combine_term(g2_jac& r, const g2_aff& sig, const uint32_t* lam8) {
-  jac_mul_w4(r, sig, lam8, 8);
+  if (sig.inf) { jac_set_inf(r); return; }
+  uint32_t k[8];
+  uint32_t c = (lam8[0] & 1u) ? 0u : 1u;
+  const bool even = c != 0;
+  for (int i = 0; i < 8; ++i) k[i] = addc(lam8[i], 0u, c, c);
+  jac_mul_sw4_odd(r, sig, k, 8);
+  if (even) { g2_aff n = sig; fp2_neg(n.y, n.y); jac_add_aff(r, r, n); }
 }
 
 // unit "combine_sum": sum of t terms, affine, compressed (src/crypto/impls/blst.rs:74-86)
