@@ -18,6 +18,7 @@ import argparse
 import ctypes
 import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -25,10 +26,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # Hardware queues per process for the HIP runtime (read at HIP init, so before torch): every
-# pipeline slot drives 3 streams (main chain, hash_to_G2, speculative combine) plus the caller's
-# stream; with HIP's default of 4 queues the independent batches' kernels serialise on shared
-# queues (measured: 1.61M -> 2.52M partial sigs/s at 4 slots going from 4 to 16 queues).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# pipeline slot drives 3 streams (main chain, hash_to_G2, G1 sums + speculative combine) plus the
+# caller's stream; with HIP's default of 4 queues (the GPU box exports GPU_MAX_HW_QUEUES=4) the
+# independent batches' kernels serialise on shared queues (measured at 4 slots: 1.6M -> 2.4M
+# partial sigs/s going from 4 to 16 queues).  Raised here, never lowered, never above 32.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 METRIC = "verified partial sigs/sec + combined threshold sigs/sec, 1 and 8 MI355X"
@@ -42,19 +45,64 @@ def opcount_mads():
     return {k: 300.0 * (v["fp_mul"] + v["fp_sqr"]) + 136.0 * v["fr_mul"] for k, v in oc.items() if isinstance(v, dict)}
 
 
+def msm_plan(N, n_roots):
+    """The window widths / bucket teams of the RLC bucket MSMs (plan_msm in csrc/ssbls.hip)."""
+    def pick_c(n, g, cmin, cmax):
+        best = None
+        for c in range(cmin, cmax + 1):
+            W, B = (64 + c - 1) // c, 2 ** c
+            L = min(B, 64)
+            cost = n * W * (1 - 1 / B) + 1.5 * g * W * (2 * B + L * (math.log2(L) + 1))
+            if best is None or cost < best[0]:
+                best = (cost, c)
+        return best[1]
+
+    def pick_lj(n, g, c):
+        pb, lj = n / (g * 2 ** c), 0
+        while lj < 6 and pb / 2 ** (lj + 1) >= 8:
+            lj += 1
+        return lj
+    g1n = max(n_roots, 1)
+    c2, c1 = pick_c(N, 1, 3, 8), pick_c(N, g1n, 2, 8)
+    keys = lambda c, g: ((64 + c - 1) // c) * g * 2 ** c
+    while c1 > 2 and keys(c2, 1) + keys(c1, g1n) > 1024 * 1024:
+        c1 -= 1
+    return {"c2": c2, "W2": (64 + c2 - 1) // c2, "lj2": pick_lj(N, 1, c2),
+            "c1": c1, "W1": (64 + c1 - 1) // c1, "lj1": pick_lj(N, g1n, c1), "groups1": g1n,
+            "g1_msm": N >= 4096 * g1n}
+
+
+def msm_mads(mads, N, c, W, lj, groups, g):
+    """MADs of one bucket MSM launch sequence (curve g = "g1"/"g2"): entry madds, bucket-team
+    trees, window reduce (running sums, suffix scan, lane doublings, tree), to-affine/Horner."""
+    B, L = 2 ** c, min(2 ** c, 64)
+    m = B // L
+    madd, add, dbl = mads["madd_" + g], mads["sum_%s_add" % g], mads["dbl_" + g]
+    entries = N * W * (1 - 1 / B)
+    trees = groups * W * B * ((1 << lj) - 1) * add
+    scan = sum(L - off for off in (2 ** i for i in range(int(math.log2(L))))) if L > 1 else 0
+    window = groups * W * ((L * (2 * (m - 1) + 1) + scan + (L - 1)) * add + (L - 1) * math.log2(m) * dbl + (L - 1) * add)
+    return entries * madd + trees + window
+
+
 def kernel_mads(mads, V, t, n, n_roots):
     """Algorithmic MADs per launch of each kernel (per-unit counts x units per launch)."""
     N = V * n
-    comb_sum = mads["combine_sum_t3"] if t <= 3 else mads["combine_sum_t10"]
-    lag = mads["lagrange_t3"] if t <= 3 else (mads["lagrange_t5"] if t <= 5 else mads["lagrange_t10"])
+    p = msm_plan(N, n_roots)
     small = mads["combine_small_t3"] if t <= 3 else (mads["combine_small_t5"] if t <= 5 else mads["combine_small_t10"])
+    npairs = n_roots + p["W2"]
     return {
         "k_hash_to_g2": n_roots * mads["hash_to_g2"],
         "k_decode": N * (mads["decode_sig"] + mads["decode_pk"]),
-        "k_rlc_mul": N * (mads["subgroup"] + mads["rlc_sig"] + mads["rlc_pk"]),
-        "k_sum": N * (mads["sum_g1_add"] + mads["sum_g2_add"]) + n_roots * (mads["to_affine_g1"] + mads["to_affine_g2"]),
-        "k_miller": 2 * n_roots * mads["miller_pair"],
-        "k_final": (2 * n_roots - 1) * mads["fp12_mul"] + mads["final_exp"],
+        "k_subgroup": N * mads["subgroup"],
+        "k_msm_g2": msm_mads(mads, N, p["c2"], p["W2"], p["lj2"], 1, "g2") + p["W2"] * mads["to_affine_g2"],
+        "k_msm_g1": (msm_mads(mads, N, p["c1"], p["W1"], p["lj1"], p["groups1"], "g1")
+                     + p["groups1"] * ((p["W1"] - 1) * (p["c1"] * mads["dbl_g1"] + mads["sum_g1_add"])
+                                       + mads["to_affine_g1"])) if p["g1_msm"] else 0.0,
+        "k_rlc_pk": 0.0 if p["g1_msm"] else N * mads["rlc_pk"],
+        "k_sum_g1": 0.0 if p["g1_msm"] else N * mads["sum_g1_add"] + n_roots * mads["to_affine_g1"],
+        "k_miller": npairs * mads["miller_pair"],
+        "k_final": (npairs - 1) * mads["fp12_mul"] + mads["final_exp"],
         "k_combine_fast": V * small,   # ids 1..n: integer Lagrange coefficients (ssb_units.h)
     }
 
@@ -212,7 +260,8 @@ def main():
         step(1 + i, 0)
         torch.cuda.synchronize(dev)
         lat.append(time.perf_counter() - t0)
-    kt = {k: eng.kernel_time(k) for k in ["k_hash_to_g2", "k_decode", "k_rlc_mul", "k_sum", "k_miller", "k_final",
+    kt = {k: eng.kernel_time(k) for k in ["k_hash_to_g2", "k_decode", "k_subgroup", "k_msm_sort", "k_msm_g2",
+                                         "k_msm_g1", "k_rlc_pk", "k_sum_g1", "k_miller", "k_final",
                                          "k_fallback_verify", "k_select", "k_combine_fast", "k_lagrange",
                                          "k_combine_terms", "k_combine_sum"]}
     eng.kernel_timing(False)
@@ -236,9 +285,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    host_ms = []
     for i in range(args.steps):
+        th = time.perf_counter()
         step(args.warmup + i, i % S)
+        host_ms.append((time.perf_counter() - th) * 1e3)
     torch.cuda.synchronize(dev)
+    if os.environ.get("SSB_DEBUG_HOST"):
+        print("host ms per submit:", " ".join("%.2f" % x for x in host_ms), file=sys.stderr)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0

@@ -1,0 +1,258 @@
+// ssb_k_msm.hip -- the random-linear-combination sums of the batch verify as bucket MSMs
+// (the reference verifies share by share, src/crypto/generic_threshold.rs:156).
+//
+// The batch check  prod_r e(sum_{i in r} k_i pk_i, H_r) == e(g1, sum_i k_i sig_i)  needs, over the
+// candidate shares, one G1 sum per signing root and one G2 sum, with the 64-bit RLC scalars
+// k_i = rlc_scalar_odd(seed, i).  Both are computed as Pippenger bucket MSMs:
+//   - W = ceil(64 / c) windows of c bits; entry (i, w) lands in bucket (group, w, digit), digit 0
+//     dropped.  k_msm_sort<false> (count) / k_scan_* / k_msm_sort<true> (scatter) counting-sort the entries by bucket key
+//     (order inside a bucket is irrelevant: the group law is exact).
+//   - k_msm_bucket: a team of J lanes per bucket adds its points (mixed additions, strided), then
+//     tree-reduces the team through LDS.  Entries of shares that are not candidates (failed the
+//     subgroup check) are skipped here, so the sort can run before the check finishes.
+//   - k_msm_window: one workgroup per (group, window) forms sum_d d*B_d: each lane runs the
+//     running-sum trick over its m consecutive buckets, a Kogge-Stone suffix scan over the lanes
+//     supplies the lane offsets (sum_t t*S_t = sum_{t>=1} suffix_t), and a tree adds the lanes.
+//   - G1 (per root): k_msm_horner combines the windows, sum_w 2^(c w) W_w, one lane per root.
+//   - G2 (one group): no doubling chain -- window w becomes its own multi-pairing pair
+//     e([2^(c w)](-g1), W_w) with the constant [2^(c w)](-g1) precomputed on the host.
+// Every addition is the complete Jacobian formula of ssb_curve.h (infinity, doubling and opposite
+// inputs handled), so the sums are exact for any inputs.
+#include "ssb_kernels.h"
+
+namespace ssb {
+namespace k {
+
+SSB_INL bool share_decodable(uint32_t sf, uint32_t pf) {
+  return (sf & DEC_OK) && !(sf & DEC_INF) && (pf & DEC_OK) && !(pf & DEC_INF);
+}
+
+template <bool SCATTER>
+SSB_INL void msm_entries(int i, uint64_t k, uint32_t g, const msm_cfg& c, uint32_t* __restrict__ cnt,
+                         uint32_t* __restrict__ ent) {
+  const uint64_t mask = (1ull << c.c) - 1ull;
+  for (uint32_t w = 0; w < c.W; ++w) {
+    const uint32_t d = (uint32_t)((k >> (c.c * w)) & mask);
+    if (!d) continue;
+    const uint32_t key = c.base + ((g * c.W + w) << c.c) + d;
+    if (SCATTER) ent[atomicAdd(&cnt[key], 1u)] = (uint32_t)i;
+    else atomicAdd(&cnt[key], 1u);
+  }
+}
+
+// cnt[key] += 1 per (share, window) entry (SCATTER: ent[cursor[key]++] = share)
+template <bool SCATTER>
+__global__ void __launch_bounds__(256) k_msm_sort(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+                                                  const uint32_t* __restrict__ pflags,
+                                                  const uint32_t* __restrict__ share_root, msm_cfg c2, msm_cfg c1,
+                                                  uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !share_decodable(sflags[i], pflags[i])) return;
+  const uint32_t g = share_root[i];
+  if (g >= c1.ngroups) return;  // out-of-range root index: the share cannot enter the batch
+  const uint64_t k = rlc_scalar_odd(seed, (uint64_t)i);
+  msm_entries<SCATTER>(i, k, 0u, c2, cnt, ent);
+  msm_entries<SCATTER>(i, k, g, c1, cnt, ent);
+}
+// ---- exclusive scan of the bucket counts: 1024 per block, block totals, offsets ----
+constexpr int SCAN_T = 256, SCAN_PER = 4, SCAN_BLOCK = SCAN_T * SCAN_PER;
+SSB_INL uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    const uint32_t o = t >= off ? sh[t - off] : 0u;
+    __syncthreads();
+    sh[t] += o;
+    __syncthreads();
+  }
+  total = sh[SCAN_T - 1];
+  const uint32_t incl = sh[t];
+  __syncthreads();
+  return incl - v;
+}
+__global__ void __launch_bounds__(SCAN_T) k_scan_blocks(uint32_t K, const uint32_t* __restrict__ cnt,
+                                                        uint32_t* __restrict__ start, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t sh[SCAN_T];
+  const uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_PER;
+  uint32_t v[SCAN_PER], s = 0;
+  for (int q = 0; q < SCAN_PER; ++q) { v[q] = base + q < K ? cnt[base + q] : 0u; s += v[q]; }
+  uint32_t total;
+  uint32_t run = block_excl_scan(s, sh, total);
+  for (int q = 0; q < SCAN_PER; ++q) { if (base + q < K) start[base + q] = run; run += v[q]; }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+__global__ void __launch_bounds__(SCAN_T) k_scan_top(uint32_t nb, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t sh[SCAN_T];
+  const uint32_t base = threadIdx.x * SCAN_PER;
+  uint32_t v[SCAN_PER], s = 0;
+  for (int q = 0; q < SCAN_PER; ++q) { v[q] = base + q < nb ? bsum[base + q] : 0u; s += v[q]; }
+  uint32_t total;
+  uint32_t run = block_excl_scan(s, sh, total);
+  for (int q = 0; q < SCAN_PER; ++q) { if (base + q < nb) bsum[base + q] = run; run += v[q]; }
+}
+__global__ void __launch_bounds__(256) k_scan_add(uint32_t K, uint32_t* __restrict__ start,
+                                                  const uint32_t* __restrict__ bsum, uint32_t* __restrict__ cur) {
+  const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= K) return;
+  const uint32_t s = start[x] + bsum[x / SCAN_BLOCK];
+  start[x] = s;
+  cur[x] = s;
+}
+
+// ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup ----
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ start,
+                                                   const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ ent,
+                                                   const uint32_t* __restrict__ flags, const aff<F>* __restrict__ pts,
+                                                   jac<F>* __restrict__ bsum) {
+  __shared__ jac<F> sh[64];
+  const int lane = threadIdx.x, J = 1 << lj, j = lane & (J - 1);
+  const uint32_t b = blockIdx.x * (64u >> lj) + (uint32_t)(lane >> lj);
+  jac<F> acc;
+  jac_set_inf(acc);
+  if (b < nb) {
+    const uint32_t s = start[base + b], e = s + cnt[base + b];
+    for (uint32_t x = s + j; x < e; x += J) {
+      const uint32_t i = ent[x];
+      if (flags[i] & FLAG_CANDIDATE) jac_add_aff(acc, acc, pts[i]);
+    }
+  }
+  for (int h = J >> 1; h >= 1; h >>= 1) {
+    sh[lane] = acc;
+    __syncthreads();
+    if (j < h) { jac<F> o = sh[lane + h]; jac_add(acc, acc, o); }
+    __syncthreads();
+  }
+  if (j == 0 && b < nb) bsum[b] = acc;
+}
+
+// ---- window sums  sum_d d * B_d  (one workgroup per (group, window)) ----
+// G1: out_jac[gw] (Jacobian, for the Horner combine).  G2: the window is affine pair gw of the
+// multi-pairing: out_q[gw] = W_gw, out_p[gw] = [2^(c gw)](-g1) from negg1_pow.
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
+                                                   aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
+                                                   const g1_aff* __restrict__ negg1_pow) {
+  __shared__ jac<F> sh[64];
+  const int t = threadIdx.x, B = 1 << c, L = B < 64 ? B : 64, m = B / L;
+  const jac<F>* bk = bsum + (size_t)blockIdx.x * B;
+  jac<F> S, U;
+  jac_set_inf(S);
+  jac_set_inf(U);
+  if (t < L) {
+    for (int e = m - 1; e >= 1; --e) { jac<F> o = bk[t * m + e]; jac_add(S, S, o); jac_add(U, U, S); }
+    jac<F> o = bk[t * m]; jac_add(S, S, o);
+  }
+  // suffix scan over the lanes: S_t <- sum_{t' >= t} S_t'
+  for (int off = 1; off < L; off <<= 1) {
+    sh[t] = S;
+    __syncthreads();
+    if (t + off < L) { jac<F> o = sh[t + off]; jac_add(S, S, o); }
+    __syncthreads();
+  }
+  if (t >= 1 && t < L) {
+    for (int q = m; q > 1; q >>= 1) jac_dbl(S, S);
+    jac_add(U, U, S);
+  }
+  for (int h = L >> 1; h >= 1; h >>= 1) {
+    sh[t] = U;
+    __syncthreads();
+    if (t < h) { jac<F> o = sh[t + h]; jac_add(U, U, o); }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (out_jac) out_jac[blockIdx.x] = U;
+    if (out_q) {
+      aff<F> a;
+      jac_to_aff(a, U);
+      out_q[blockIdx.x] = a;
+      out_p[blockIdx.x] = negg1_pow[c * blockIdx.x];
+    }
+  }
+}
+
+// ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
+__global__ void __launch_bounds__(64) k_msm_horner(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
+                                                   g1_aff* __restrict__ out) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  const g1_jac* ws = wsum + (size_t)g * W;
+  g1_jac acc = ws[W - 1];
+  for (int w = W - 2; w >= 0; --w) {
+    for (int q = 0; q < c; ++q) jac_dbl(acc, acc);
+    g1_jac o = ws[w];
+    jac_add(acc, acc, o);
+  }
+  g1_aff a;
+  jac_to_aff(a, acc);
+  out[g] = a;
+}
+
+// per-share G1 RLC product (the G1 side when the roots' groups are small: 64 doublings per share
+// beat a per-root bucket MSM whose window reduce / Horner overheads dominate at ~256 shares/root)
+__global__ void __launch_bounds__(64) k_rlc_pk(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+                                               const uint32_t* __restrict__ pflags, const g1_aff* __restrict__ pk_aff,
+                                               g1_jac* __restrict__ rpk) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  g1_jac r;
+  if (share_decodable(sflags[s], pflags[s])) unit_rlc_pk(r, pk_aff[s], rlc_scalar_odd(seed, (uint64_t)s));
+  else jac_set_inf(r);
+  rpk[s] = r;
+}
+
+// subgroup check of every decodable signature (psi(P) == [x]P, sig_groupcheck)
+__global__ void __launch_bounds__(64) k_subgroup(int n, const uint32_t* __restrict__ sflags,
+                                                 const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint32_t sf = sflags[s];
+  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+}
+
+}  // namespace k
+
+namespace launch {
+
+using namespace ssb::k;
+
+void msm_sort(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
+              const uint32_t* share_root, const msm_cfg& c2, const msm_cfg& c1, uint32_t K, uint32_t* cnt,
+              uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent) {
+  hipMemsetAsync(cnt, 0, (size_t)K * 4, st);
+  const unsigned g = (unsigned)((n + 255) / 256), nb = (K + SCAN_BLOCK - 1) / SCAN_BLOCK;
+  if (n) hipLaunchKernelGGL(k_msm_sort<false>, dim3(g), dim3(256), 0, st, n, seed, sflags, pflags, share_root, c2, c1, cnt, ent);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(SCAN_T), 0, st, K, cnt, start, bsum);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, nb, bsum);
+  hipLaunchKernelGGL(k_scan_add, dim3((K + 255) / 256), dim3(256), 0, st, K, start, bsum, cur);
+  if (n) hipLaunchKernelGGL(k_msm_sort<true>, dim3(g), dim3(256), 0, st, n, seed, sflags, pflags, share_root, c2, c1, cur, ent);
+}
+
+void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+            const uint32_t* flags, const g2_aff* sig, g2_jac* bsum, g2_aff* pair_q, g1_aff* pair_p,
+            const g1_aff* negg1_pow) {
+  const uint32_t nb = c.ngroups * c.W << c.c;
+  hipLaunchKernelGGL(k_msm_bucket<fp2>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, start,
+                     cnt, ent, flags, sig, bsum);
+  hipLaunchKernelGGL(k_msm_window<fp2>, dim3(c.ngroups * c.W), dim3(64), 0, st, (int)c.c, (const g2_jac*)bsum,
+                     (g2_jac*)nullptr, pair_q, pair_p, negg1_pow);
+}
+
+void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+            const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum) {
+  const uint32_t nb = c.ngroups * c.W << c.c;
+  hipLaunchKernelGGL(k_msm_bucket<fp>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, start,
+                     cnt, ent, flags, pk, bsum);
+  hipLaunchKernelGGL(k_msm_window<fp>, dim3(c.ngroups * c.W), dim3(64), 0, st, (int)c.c, (const g1_jac*)bsum, wsum,
+                     (g1_aff*)nullptr, (g1_aff*)nullptr, (const g1_aff*)nullptr);
+  hipLaunchKernelGGL(k_msm_horner, dim3((c.ngroups + 63) / 64), dim3(64), 0, st, (int)c.ngroups, (int)c.c, (int)c.W,
+                     (const g1_jac*)wsum, root_sum);
+}
+
+void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags) {
+  if (n) hipLaunchKernelGGL(k_subgroup, dim3((n + 63) / 64), dim3(64), 0, st, n, sflags, sig, gflags);
+}
+
+}  // namespace launch
+}  // namespace ssb

@@ -78,17 +78,18 @@ __global__ void __launch_bounds__(64) k_miller_lane(int n_roots, const g1_aff* _
   if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
 }
 
-// pairs [0, n_roots): (S_r, H(root r));  [n_roots, 2 n_roots): (-g1, T_r)
-__global__ void __launch_bounds__(64) k_miller_roots(int n_roots, const g1_aff* __restrict__ s1,
-                                                     const g2_aff* __restrict__ H, const g2_aff* __restrict__ s2,
-                                                     fp12* __restrict__ f) {
+// one Miller loop per pair (P[p], Q[p]), one workgroup each: the roots' (S_r, H(root r)) and the
+// G2 MSM windows' ([2^(c w)](-g1), W_w)
+__global__ void __launch_bounds__(64) k_miller_pairs(int npairs, const g1_aff* __restrict__ Pa,
+                                                     const g2_aff* __restrict__ Qa, fp12* __restrict__ f) {
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + ML_SLOTS];
   __shared__ uint32_t flg;
   const int p = blockIdx.x, lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
-  g1_aff P; g2_aff Q;
-  if (p < n_roots) { P = s1[p]; Q = H[p]; } else { P = g1_neg_generator(); Q = s2[p - n_roots]; }
+  if (p >= npairs) return;
+  const g1_aff P = Pa[p];
+  const g2_aff Q = Qa[p];
   if (P.inf || Q.inf) {  // e(O, Q) = e(P, O) = 1  (uniform per workgroup)
     if (lane_ == 0) f[p] = fp12_one();
     return;

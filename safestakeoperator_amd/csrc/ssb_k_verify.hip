@@ -138,9 +138,9 @@ __global__ void k_verdict_fast(int n, const uint32_t* __restrict__ ok, const uin
 }
 
 // ---- per-root RLC sums: counting sort of the shares by root, then one block per (root, group) ----
-__global__ void k_root_hist(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt) {
+__global__ void k_root_hist(int n, int n_roots, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) atomicAdd(&cnt[share_root[s]], 1u);
+  if (s < n && share_root[s] < (uint32_t)n_roots) atomicAdd(&cnt[share_root[s]], 1u);
 }
 __global__ void k_root_scan(int n_roots, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
                             uint32_t* __restrict__ cursor) {
@@ -148,10 +148,10 @@ __global__ void k_root_scan(int n_roots, const uint32_t* __restrict__ cnt, uint3
   uint32_t acc = 0;
   for (int r = 0; r < n_roots; ++r) { start[r] = acc; cursor[r] = acc; acc += cnt[r]; }
 }
-__global__ void k_root_scatter(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cursor,
+__global__ void k_root_scatter(int n, int n_roots, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cursor,
                                uint32_t* __restrict__ perm) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
+  if (s < n && share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
 }
 // blocks [0, n_roots): S_r = sum r_i pk_i over the candidate shares of root r (G1);
 // blocks [n_roots, 2 n_roots): T_r = sum r_i sig_i (G2).  Affine outputs (infinity if none).

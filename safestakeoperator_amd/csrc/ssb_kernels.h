@@ -10,14 +10,21 @@ namespace ssb {
 // DST passed by value to the hashing kernels
 struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
 
+// One bucket MSM of the RLC sums (ssb_k_msm.hip): c-bit windows, W = ceil(64 / c) of them,
+// `ngroups` independent sums; bucket key = base + ((group * W + window) << c) + digit.
+struct msm_cfg { uint32_t c, W, base, ngroups; };
+
 namespace k {
 constexpr int SUM_THREADS = 128;   // k_sum_* block size
 constexpr int SEG_THREADS = 64;    // k_sum_seg block size
-__global__ void k_root_hist(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt);
+__global__ void k_root_hist(int n, int n_roots, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt);
 __global__ void k_root_scan(int n_roots, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
                             uint32_t* __restrict__ cursor);
-__global__ void k_root_scatter(int n, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cursor,
+__global__ void k_root_scatter(int n, int n_roots, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cursor,
                                uint32_t* __restrict__ perm);
+// rpk[s] = rlc_scalar_odd(seed, s) * pk[s] for every decodable share (infinity otherwise)
+__global__ void k_rlc_pk(int n, uint64_t seed, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
+                         const g1_aff* __restrict__ pk_aff, g1_jac* __restrict__ rpk);
 __global__ void k_sum_seg(int n_roots, const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
                           const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
                           const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ rsig, g1_aff* __restrict__ s1,
@@ -59,8 +66,8 @@ __global__ void k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
 __global__ void k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok);
 __global__ void k_miller_lane(int n_roots, const g1_aff* __restrict__ root_sum, const g2_aff* __restrict__ H,
                               const g2_aff* __restrict__ sig_sum, fp12* __restrict__ f);
-__global__ void k_miller_roots(int n_roots, const g1_aff* __restrict__ s1, const g2_aff* __restrict__ H,
-                               const g2_aff* __restrict__ s2, fp12* __restrict__ f);
+__global__ void k_miller_pairs(int npairs, const g1_aff* __restrict__ P, const g2_aff* __restrict__ Q,
+                               fp12* __restrict__ f);
 __global__ void k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out);
 __global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok);
 __global__ void k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
@@ -115,6 +122,20 @@ void lane_rlc_g1(hipStream_t st, int n, uint64_t seed, const uint32_t* pflags, c
 // staged hash_to_G2 of n roots into out (ssb_k_hash.hip); ws: hash_ws_bytes(n) device bytes
 size_t hash_ws_bytes(size_t n);
 void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws);
+// RLC sums as bucket MSMs (ssb_k_msm.hip).  msm_sort: counting sort of the (share, window)
+// entries of both MSMs by bucket key (K keys; cnt/start/cur: K words, bsum: 1024 words, ent: one
+// word per entry).  msm_g2: window sums of sum_i k_i sig_i as multi-pairing pairs
+// (pair_q[w] = W_w affine, pair_p[w] = [2^(c w)](-g1)).  msm_g1: root_sum[r] = sum_{i in r} k_i pk_i.
+void msm_sort(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
+              const uint32_t* share_root, const msm_cfg& c2, const msm_cfg& c1, uint32_t K, uint32_t* cnt,
+              uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent);
+void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+            const uint32_t* flags, const g2_aff* sig, g2_jac* bsum, g2_aff* pair_q, g1_aff* pair_p,
+            const g1_aff* negg1_pow);
+void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+            const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum);
+// gflags[s] = DEC_IN_GROUP when signature s (decodable, not infinity) passes psi(P) == [x]P
+void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags);
 // exact single-lane recomputation of the shares whose lane-group stage raised exc
 void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
                 const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,

@@ -25,6 +25,7 @@
 #include <map>
 #include <mutex>
 #include <algorithm>
+#include <cmath>
 
 #include "ssb_units.h"
 #include "ssb_wave.h"
@@ -45,8 +46,7 @@ namespace {
 // slots (ssb_set_pipeline_depth) are independent and overlap on the device.
 struct ssb_slot {
   hipStream_t stream = nullptr;     // main chain: decode -> RLC -> sums -> Miller -> final exp
-  hipStream_t side[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] hash_to_G2, [1] speculative combine,
-                                                               // [2], [3] spare
+  hipStream_t side[2] = {nullptr, nullptr};  // [0] hash_to_G2, [1] G1 MSM then the speculative combine
   hipEvent_t ev_in = nullptr, ev_hash = nullptr, ev_dec = nullptr, ev_comb = nullptr, ev_out = nullptr;
   hipEvent_t ev_sdec = nullptr, ev_r2 = nullptr, ev_r1 = nullptr, ev_user = nullptr;
   // workspace arena (grown on demand, never shrunk)
@@ -69,6 +69,7 @@ struct ssb_ctx {
   bool accumulate = false;                             // ssb_kernel_timing(ctx, 1)
   std::map<std::string, std::vector<evpair>> history;  // every launch while accumulating
   std::vector<evpair> pool;
+  g1_aff* negg1_pow = nullptr;                         // device: [2^s](-g1), s = 0..63 (G2 MSM pairs)
 };
 
 namespace {
@@ -112,7 +113,7 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 
 int init_slot(ssb_slot& S) {
   if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
-  for (int i = 0; i < 2; ++i)  // side[0] hash_to_G2, side[1] speculative combine (side[2..3] unused)
+  for (int i = 0; i < 2; ++i)
     if (hipStreamCreateWithFlags(&S.side[i], hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
   for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
@@ -157,42 +158,103 @@ int fill_dst(ssb_ctx* ctx, dst_arg& d, const uint8_t* dst, size_t dst_len) {
 }
 
 // The verification stage shared by verify_batch and threshold_aggregate_batch.
+//
+// RLC sums as bucket MSMs (ssb_k_msm.hip).  The window width of each MSM minimises
+//   madds (n W (1 - 2^-c))  +  1.5 x window-reduce additions (groups W (2^(c+1) + L (log2 L + 1)))
+// and the bucket teams get ~8 entries per lane.
+struct msm_plan { msm_cfg g2, g1; uint32_t K; int lj2, lj1; size_t n_ent; bool g1_msm; };
+constexpr uint32_t MSM_WMAX = 32;          // windows of the G2 MSM (c >= 2)
+constexpr uint32_t MSM_KMAX = 1024u * 1024u;  // bucket keys (two-level scan)
+
+inline int msm_pick_c(size_t n, size_t groups, int cmin, int cmax) {
+  double best = 1e300; int bc = cmin;
+  for (int c = cmin; c <= cmax; ++c) {
+    const double W = (64 + c - 1) / c, B = double(1u << c), L = B < 64 ? B : 64;
+    const double cost = double(n) * W * (1.0 - 1.0 / B) + 1.5 * double(groups) * W * (2.0 * B + L * (std::log2(L) + 1.0));
+    if (cost < best) { best = cost; bc = c; }
+  }
+  return bc;
+}
+inline int msm_pick_lj(size_t n, size_t groups, int c) {
+  const double per_bucket = double(n) / (double(groups) * double(1u << c));
+  int lj = 0;
+  while (lj < 6 && per_bucket / double(1 << (lj + 1)) >= 8.0) ++lj;
+  return lj;
+}
+// G1 side: a per-root bucket MSM only when the roots' groups are large; otherwise per-share
+// products (k_rlc_pk) + per-root segmented sums.  SSB_G1_PATH=msm|share forces one (tests).
+bool g1_use_msm(size_t n, size_t n_roots) {
+  const char* e = getenv("SSB_G1_PATH");
+  if (e && !strcmp(e, "msm")) return true;
+  if (e && !strcmp(e, "share")) return false;
+  return n >= 4096 * (n_roots ? n_roots : 1);
+}
+msm_plan plan_msm(size_t n, size_t n_roots) {
+  msm_plan p;
+  const size_t g1n = n_roots ? n_roots : 1;
+  p.g1_msm = g1_use_msm(n, n_roots);
+  int c2 = msm_pick_c(n, 1, 3, 8), c1 = msm_pick_c(n, g1n, 2, 8);  // c <= 8: <= 4 buckets per window lane
+  auto keys = [&](int c, size_t g) { return (size_t)((64 + c - 1) / c) * g << c; };
+  while (c1 > 2 && keys(c2, 1) + keys(c1, g1n) > MSM_KMAX) --c1;
+  p.g2 = msm_cfg{(uint32_t)c2, (uint32_t)((64 + c2 - 1) / c2), 0u, 1u};
+  p.g1 = msm_cfg{(uint32_t)c1, p.g1_msm ? (uint32_t)((64 + c1 - 1) / c1) : 0u, (uint32_t)keys(c2, 1), (uint32_t)g1n};
+  p.K = (uint32_t)(keys(c2, 1) + (p.g1_msm ? keys(c1, g1n) : 0));
+  p.lj2 = msm_pick_lj(n, 1, c2);
+  p.lj1 = msm_pick_lj(n, g1n, c1);
+  p.n_ent = n * (p.g2.W + p.g1.W);
+  return p;
+}
+
 struct verify_ws {
-  g2_aff* H; g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags;
-  g2_jac* rsig; g1_jac* rpk; g1_aff* root_sum; g2_jac* part; g2_aff* sig_sum; fp12* f; uint32_t* ok;
-  g2_aff* root_sig;   // per-root sum of r_i sig_i
-  uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;  // shares sorted by root
-  uint32_t* exc;  // 3n: lane-group exceptions (subgroup, RLC G2, RLC G1)
-  char* hws;      // staged hash_to_G2 workspace
+  msm_plan plan;
+  g2_aff* H;          // pair Q points: H(root r) for r < n_roots, then the G2 MSM windows
+  g1_aff* pair_p;     // pair P points: root sums, then [2^(c w)](-g1)
+  g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags;
+  fp12* f; uint32_t* ok;
+  char* hws;          // staged hash_to_G2 workspace
+  uint32_t* cnt; uint32_t* start; uint32_t* cur; uint32_t* sbsum; uint32_t* ent;   // MSM counting sort
+  g2_jac* b2; g1_jac* b1; g1_jac* w1;                                              // MSM buckets / windows
+  g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
+  size_t npairs;
 };
-constexpr int G2_PARTS = 64;
-// Miller values of 2 n_roots pairs plus the levels of the 8-ary product tree
-inline size_t fp12_slots(size_t n_roots) {
-  size_t np = 2 * n_roots + 1, tot = np;
+// Miller values of the pairs plus the levels of the 8-ary product tree
+inline size_t fp12_slots(size_t np) {
+  size_t tot = np;
   while (np > 8) { np = (np + 7) / 8; tot += np; }
   return tot + 1;
 }
 
 size_t verify_ws_bytes(size_t n, size_t n_roots) {
-  return align_up(n_roots * sizeof(g2_aff)) + align_up(n * sizeof(g2_aff)) + align_up(n * sizeof(g1_aff)) +
-         align_up(n * 4) * 4 + align_up(n * sizeof(g2_jac)) + align_up(n * sizeof(g1_jac)) +
-         align_up(n_roots * sizeof(g1_aff)) + align_up(G2_PARTS * sizeof(g2_jac)) + align_up(sizeof(g2_aff)) +
-         align_up(fp12_slots(n_roots) * sizeof(fp12)) + align_up(4) + align_up(3 * n * 4) + align_up(launch::hash_ws_bytes(n_roots)) +
-         align_up(n_roots * sizeof(g2_aff)) + 3 * align_up(n_roots * 4) + align_up(n * 4);
+  const msm_plan p = plan_msm(n, n_roots);
+  const size_t np = n_roots + MSM_WMAX;
+  return align_up(np * sizeof(g2_aff)) + align_up(np * sizeof(g1_aff)) + align_up(n * sizeof(g2_aff)) +
+         align_up(n * sizeof(g1_aff)) + align_up(n * 4) * 4 + align_up(fp12_slots(np) * sizeof(fp12)) + align_up(4) +
+         align_up(launch::hash_ws_bytes(n_roots)) + 3 * align_up((size_t)p.K * 4) + align_up(1024 * 4) +
+         align_up(p.n_ent * 4) + align_up(((size_t)p.g2.W << p.g2.c) * sizeof(g2_jac)) +
+         align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
+         align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
+         3 * align_up(n_roots * 4) + align_up(n * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   verify_ws w;
-  w.H = c.take<g2_aff>(n_roots); w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
+  w.plan = plan_msm(n, n_roots);
+  const size_t np = n_roots + MSM_WMAX;
+  w.H = c.take<g2_aff>(np); w.pair_p = c.take<g1_aff>(np);
+  w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
   w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
-  w.gflags = c.take<uint32_t>(n); w.rsig = c.take<g2_jac>(n); w.rpk = c.take<g1_jac>(n);
-  w.root_sum = c.take<g1_aff>(n_roots); w.part = c.take<g2_jac>(G2_PARTS); w.sig_sum = c.take<g2_aff>(1);
-  w.f = c.take<fp12>(fp12_slots(n_roots)); w.ok = c.take<uint32_t>(1);
-  w.exc = c.take<uint32_t>(3 * n);
+  w.gflags = c.take<uint32_t>(n);
+  w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
-  w.root_sig = c.take<g2_aff>(n_roots);
+  w.cnt = c.take<uint32_t>(w.plan.K); w.start = c.take<uint32_t>(w.plan.K); w.cur = c.take<uint32_t>(w.plan.K);
+  w.sbsum = c.take<uint32_t>(1024); w.ent = c.take<uint32_t>(w.plan.n_ent);
+  w.b2 = c.take<g2_jac>((size_t)w.plan.g2.W << w.plan.g2.c);
+  w.b1 = c.take<g1_jac>((size_t)w.plan.g1.ngroups * w.plan.g1.W << w.plan.g1.c);
+  w.w1 = c.take<g1_jac>((size_t)w.plan.g1.ngroups * w.plan.g1.W);
+  w.rpk = c.take<g1_jac>(n);
   w.rcnt = c.take<uint32_t>(n_roots); w.rstart = c.take<uint32_t>(n_roots); w.rcur = c.take<uint32_t>(n_roots);
   w.perm = c.take<uint32_t>(n);
+  w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
 
@@ -206,30 +268,47 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
   if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
   SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
+  hipStream_t s1 = ctx->cur->side[1];
+  const msm_plan& P = w.plan;
+  if (n) { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags); }
+  SSB_HIP(hipEventRecord(ctx->cur->ev_sdec, st));
+  // side[1]: per-share G1 products and the root segments, beside the subgroup checks
+  SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_sdec, 0));
+  if (!P.g1_msm) {
+    timed t(ctx, "k_rlc_pk", s1);
+    if (n) hipLaunchKernelGGL(k_rlc_pk, dim3(nblk(n, 64)), dim3(64), 0, s1, (int)n, seed, w.sflags, w.pflags, w.pk_aff, w.rpk);
+    SSB_HIP(hipMemsetAsync(w.rcnt, 0, n_roots * 4, s1));
+    if (n) hipLaunchKernelGGL(k_root_hist, dim3(nblk(n, 256)), dim3(256), 0, s1, (int)n, (int)n_roots, d_share_root, w.rcnt);
+    hipLaunchKernelGGL(k_root_scan, dim3(1), dim3(64), 0, s1, (int)n_roots, w.rcnt, w.rstart, w.rcur);
+    if (n) hipLaunchKernelGGL(k_root_scatter, dim3(nblk(n, 256)), dim3(256), 0, s1, (int)n, (int)n_roots, d_share_root, w.rcur, w.perm);
+  }
+  { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, seed, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent); }
   if (n) {
-    { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags); }
-    { timed t(ctx, "k_rlc_mul"); hipLaunchKernelGGL(k_check_rlc, dim3(nblk(3 * n, 64)), dim3(64), 0, st, (int)n, seed, w.sflags, w.pflags, w.sig_aff, w.pk_aff, w.gflags, w.rsig, w.rpk); }
+    { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, w.flags);
-    SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));
-    on_decoded();
   }
-  { timed t(ctx, "k_sum");
-    if (n_roots) {
-      SSB_HIP(hipMemsetAsync(w.rcnt, 0, n_roots * 4, st));
-      if (n) hipLaunchKernelGGL(k_root_hist, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, d_share_root, w.rcnt);
-      hipLaunchKernelGGL(k_root_scan, dim3(1), dim3(64), 0, st, (int)n_roots, w.rcnt, w.rstart, w.rcur);
-      if (n) hipLaunchKernelGGL(k_root_scatter, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, d_share_root, w.rcur, w.perm);
-      hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)(2 * n_roots)), dim3(SEG_THREADS), 0, st, (int)n_roots, w.rstart, w.rcnt,
-                         w.perm, w.flags, w.rpk, w.rsig, w.root_sum, w.root_sig);
-    }
+  SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));
+  // G1 sums (per root) on side[1] -- then the caller's speculative combine, off the critical path --
+  // G2 MSM on the main stream
+  SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
+  if (P.g1_msm) {
+    timed t(ctx, "k_msm_g1", s1);
+    launch::msm_g1(s1, P.g1, P.lj1, w.start, w.cnt, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p);
+  } else {
+    timed t(ctx, "k_sum_g1", s1);
+    hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)n_roots), dim3(SEG_THREADS), 0, s1, (int)n_roots, w.rstart, w.rcnt, w.perm,
+                       w.flags, w.rpk, (const g2_jac*)nullptr, w.pair_p, (g2_aff*)nullptr);
   }
+  SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
+  if (n) on_decoded();
+  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow); }
+  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
-  { timed t(ctx, "k_miller"); if (n_roots) hipLaunchKernelGGL(k_miller_roots, dim3((unsigned)(2 * n_roots)), dim3(64), 0, st, (int)n_roots, w.root_sum, w.H, w.root_sig, w.f); }
+  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f); }
   {
     timed t(ctx, "k_final");
-    int np = (int)(2 * n_roots);
+    int np = (int)w.npairs;
     fp12* cur = w.f;
-    if (np == 0) { np = 1; SSB_HIP(hipMemcpyAsync(cur, &FP12_ONE_HOST, sizeof(fp12), hipMemcpyHostToDevice, st)); }
     while (np > 8) {
       const int nparts = (np + 7) / 8;
       hipLaunchKernelGGL(k_fp12_prod8, dim3((unsigned)nparts), dim3(64), 0, st, np, cur, cur + np);
@@ -262,6 +341,15 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   if (!ctx) return SSB_ENOMEM;
   ctx->device = device_ordinal;
   if (init_slot(ctx->sl[0]) != SSB_OK) { delete ctx; return SSB_EHIP; }
+  {  // [2^s](-g1) for the window pairs of the G2 MSM
+    g1_aff h[64];
+    g1_jac p; jac_from_aff(p, g1_neg_generator());
+    for (int i = 0; i < 64; ++i) { jac_to_aff(h[i], p); jac_dbl(p, p); }
+    if (hipMalloc(&ctx->negg1_pow, sizeof(h)) != hipSuccess ||
+        hipMemcpy(ctx->negg1_pow, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
+      free_slot(ctx->sl[0]); delete ctx; return SSB_EHIP;
+    }
+  }
   *out = ctx;
   return SSB_OK;
 }
@@ -274,6 +362,7 @@ void ssb_destroy(ssb_ctx* ctx) {
   for (auto& kv : ctx->history) for (auto& p : kv.second) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   for (auto& p : ctx->pool) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   if (ctx->io) hipFree(ctx->io);
+  if (ctx->negg1_pow) hipFree(ctx->negg1_pow);
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
 }

@@ -240,6 +240,14 @@ int main() {
       g2_jac acc2; jac_set_inf(acc2); jac_add(acc2, acc2, rs); jac_dbl(acc2, acc2); g_ssb_counts = {};
       for (int i = 0; i < NS; ++i) jac_add(acc2, acc2, rs);
       rec("sum_g2_add", NS);
+      for (int i = 0; i < NS; ++i) jac_add_aff(acc1, acc1, pk);
+      rec("madd_g1", NS);
+      for (int i = 0; i < NS; ++i) jac_add_aff(acc2, acc2, sig);
+      rec("madd_g2", NS);
+      for (int i = 0; i < NS; ++i) jac_dbl(acc1, acc1);
+      rec("dbl_g1", NS);
+      for (int i = 0; i < NS; ++i) jac_dbl(acc2, acc2);
+      rec("dbl_g2", NS);
       { g1_aff a1; jac_to_aff(a1, acc1); } rec("to_affine_g1", 1);
       { g2_aff a2; jac_to_aff(a2, acc2); } rec("to_affine_g2", 1);
       fp12 f; miller_loop(f, pk, H); rec("miller_pair", 1);

@@ -142,9 +142,13 @@ def _gen_committees(engine, V, t, n, n_roots, seed=7):
     return roots, master, sigs, pks, ids, jr, msig
 
 
-def test_c2_full_size_properties(engine):
+@pytest.mark.parametrize("g1_path", ["auto", "msm"])
+def test_c2_full_size_properties(engine, g1_path, monkeypatch):
     """C2 size (4,096 validators x 4 shares, 3-of-4, 64 roots): every share verifies, every
-    combined signature equals the master signature, and a sample agrees with the oracle."""
+    combined signature equals the master signature, and a sample agrees with the oracle.  Both
+    G1 sides of the RLC check: per-share products + root sums (auto at this size) and the
+    per-root bucket MSM (SSB_G1_PATH=msm)."""
+    monkeypatch.setenv("SSB_G1_PATH", g1_path)
     V, t, n = 4096, 3, 4
     roots, master, sigs, pks, ids, jr, msig = _gen_committees(engine, V, t, n, 64)
     offs = list(range(0, V * n + 1, n))
@@ -159,9 +163,11 @@ def test_c2_full_size_properties(engine):
         assert B.verify(pks[v * n], sigs[v * n], roots[jr[v]])
 
 
-def test_c2_invalid_injection_exact_verdicts(engine):
+@pytest.mark.parametrize("g1_path", ["share", "msm"])
+def test_c2_invalid_injection_exact_verdicts(engine, g1_path, monkeypatch):
     """1% invalid shares (signature over another root): the RLC batch fails, the fallback gives
     exact per-share verdicts, and jobs still combine from the first t valid shares."""
+    monkeypatch.setenv("SSB_G1_PATH", g1_path)
     V, t, n = 512, 3, 4
     roots, master, sigs, pks, ids, jr, msig = _gen_committees(engine, V, t, n, 8, seed=11)
     rng = np.random.default_rng(5)
