@@ -25,13 +25,15 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# Hardware queues per process for the HIP runtime (read at HIP init, so before torch): every
-# pipeline slot drives 3 streams (main chain, hash_to_G2, G1 sums + speculative combine) plus the
-# caller's stream; with HIP's default of 4 queues (the GPU box exports GPU_MAX_HW_QUEUES=4) the
-# independent batches' kernels serialise on shared queues (measured at 4 slots: 1.6M -> 2.4M
-# partial sigs/s going from 4 to 16 queues).  Raised here, never lowered, never above 32.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
+def set_hw_queues(n):
+    """Hardware queues per process for the HIP runtime (read at HIP init, so before torch).  Each
+    pipeline slot drives `slot_streams` streams and the engine two context streams; with HIP's
+    default of 4 queues (the GPU box exports GPU_MAX_HW_QUEUES=4) independent batches serialise on
+    shared queues.  Raised here, never lowered, never above 32."""
+    n = max(16, min(32, n))
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < n:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(n)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 METRIC = "verified partial sigs/sec + combined threshold sigs/sec, 1 and 8 MI355X"
@@ -184,9 +186,12 @@ def main():
     ap.add_argument("--threshold", type=int, default=3)
     ap.add_argument("--operators", type=int, default=4)
     ap.add_argument("--roots", type=int, default=64)
-    ap.add_argument("--pipeline", type=int, default=4, help="independent batches in flight (engine pipeline slots)")
+    ap.add_argument("--pipeline", type=int, default=12, help="independent batches in flight (engine pipeline slots)")
+    ap.add_argument("--slot-streams", type=int, default=1, choices=(1, 3),
+                    help="streams per slot (1: batch in order on one queue; 3: hash / G1 side overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    set_hw_queues(args.pipeline * args.slot_streams + 4)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,7 +230,6 @@ def main():
     d_jr = torch.tensor(wl["job_root"], dtype=torch.int32, device=dev)
     d_roots = dt8(b"".join(wl["roots"]))
     S = max(1, args.pipeline)
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
     outs = [dict(out=torch.empty((V, 96), dtype=torch.uint8, device=dev), st=torch.empty((V,), dtype=torch.int32, device=dev),
                  err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev))
             for _ in range(S)]
@@ -234,9 +238,15 @@ def main():
     lib = eng._lib
     seed_base = 0x5AFE57A4E ^ (rank << 40)
 
+    streams = {}
+
     def step(i, k):
-        """batch i on pipeline slot k (engine slot k, caller stream k, output buffers k)"""
-        o, s = outs[k], streams[k]
+        """batch i on pipeline slot k (engine slot k, output buffers k); the caller's stream is the
+        slot's own main stream (ssb_slot_stream), so the bench adds no hardware queue"""
+        o = outs[k]
+        if k not in streams:
+            streams[k] = torch.cuda.ExternalStream(lib.ssb_slot_stream(eng.handle, k), device=dev)
+        s = streams[k]
         with torch.cuda.stream(s):
             rc = lib.ssb_threshold_aggregate_batch_dev(
                 eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(), d_pk.data_ptr(), d_ids.data_ptr(),
@@ -249,8 +259,9 @@ def main():
                 exchange(o["ver"], o["out"], o["st"])  # RCCL all-gather over xGMI: the one exchange step
 
     # phase 1: single-batch latency and per-kernel times (depth 1, no overlap between batches)
-    if lib.ssb_set_pipeline_depth(eng.handle, 1) != 0:
-        raise RuntimeError("ssb_set_pipeline_depth")
+    # (latency configuration: 3 streams per slot, hash_to_G2 and the G1 side beside the main chain)
+    if lib.ssb_set_pipeline_depth(eng.handle, 1) != 0 or lib.ssb_set_slot_streams(eng.handle, 3) != 0:
+        raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
     step(0, 0)
     torch.cuda.synchronize(dev)
     eng.kernel_timing(True)
@@ -268,8 +279,10 @@ def main():
     latency_ms = sorted(lat)[1] * 1e3
 
     # phase 2: the timed run, S batches in flight
-    if lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
-        raise RuntimeError("ssb_set_pipeline_depth")
+    # (throughput configuration: S slots of args.slot_streams streams)
+    if lib.ssb_set_slot_streams(eng.handle, args.slot_streams) != 0 or lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
+        raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
+    streams.clear()
     for i in range(max(args.warmup, S)):
         step(i, i % S)
     torch.cuda.synchronize(dev)
@@ -336,7 +349,7 @@ def main():
                                    % (V, n, t, n, n_roots),
                        "validators_per_gpu": V, "threshold": t, "operators": n, "roots": n_roots,
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
-                       "batches_in_flight": S},
+                       "batches_in_flight": S, "streams_per_slot": args.slot_streams},
             "batch_latency_ms": round(latency_ms, 3),
             "combined_sigs_per_s": round(combined, 1),
             "results_ok": ok_all,

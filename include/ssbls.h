@@ -69,11 +69,19 @@ typedef struct ssb_ctx ssb_ctx;
 int ssb_create(ssb_ctx** out, int device_ordinal);
 void ssb_destroy(ssb_ctx* ctx);
 const char* ssb_last_error(const ssb_ctx* ctx);
-/* Number of pipeline slots (1..8, default 1).  Each slot owns its streams and workspace; calls of
+/* Number of pipeline slots (1..16, default 1).  Each slot owns its streams and workspace; calls of
  * ssb_threshold_aggregate_batch_dev go to the slots round robin, so up to `depth` independent
  * batches are in flight and overlap on the device (e.g. the duties of consecutive slots).  Each
  * call's outputs are ready when the caller's `stream` reaches them. */
 int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth);
+/* Streams per slot: 3 (default) overlaps hash_to_G2 and the G1 side with the main chain inside a
+ * batch (lowest single-batch latency); 1 runs each batch in order on one stream, so one hardware
+ * queue per slot and more slots within the HIP runtime's per-queue scratch reservations (highest
+ * throughput with many batches in flight).  Re-creates the slots' streams. */
+int ssb_set_slot_streams(ssb_ctx* ctx, int streams);
+/* The main stream of pipeline slot `slot` (hipStream_t as void*), e.g. to pass it back as the
+ * `stream` of ssb_threshold_aggregate_batch_dev so a caller adds no hardware queue of its own. */
+void* ssb_slot_stream(ssb_ctx* ctx, int slot);
 /* Device-side kernel timing with hipEvents recorded on the engine's stream around each launch.
  * ssb_last_kernel_ms: the last launch of `kernel_name`.  ssb_kernel_timing(ctx, 1) clears and
  * starts accumulating every launch; ssb_kernel_time returns the total and the launch count. */

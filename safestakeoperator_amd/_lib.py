@@ -20,6 +20,8 @@ SIGNATURES = {
     "ssb_destroy": (None, [_ctx]),
     "ssb_last_error": (ctypes.c_char_p, [_ctx]),
     "ssb_set_pipeline_depth": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "ssb_set_slot_streams": (ctypes.c_int, [_ctx, ctypes.c_int]),
+    "ssb_slot_stream": (ctypes.c_void_p, [_ctx, ctypes.c_int]),
     "ssb_last_kernel_ms": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float)]),
     "ssb_kernel_timing": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_kernel_time": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]),
@@ -42,7 +44,7 @@ SIGNATURES = {
 def header_symbols():
     """Every function declared in include/ssbls.h."""
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ssb_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void\*?|const char\*)\s+(ssb_\w+)\s*\(", txt, re.M)))
 
 
 _LIB = None

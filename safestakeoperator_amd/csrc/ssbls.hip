@@ -46,19 +46,21 @@ namespace {
 // slots (ssb_set_pipeline_depth) are independent and overlap on the device.
 struct ssb_slot {
   hipStream_t stream = nullptr;     // main chain: decode -> RLC -> sums -> Miller -> final exp
-  hipStream_t side[2] = {nullptr, nullptr};  // [0] hash_to_G2, [1] G1 MSM then the speculative combine
+  hipStream_t side[2] = {nullptr, nullptr};  // [0] hash_to_G2, [1] G1 products / sums
   hipEvent_t ev_in = nullptr, ev_hash = nullptr, ev_dec = nullptr, ev_comb = nullptr, ev_out = nullptr;
-  hipEvent_t ev_sdec = nullptr, ev_r2 = nullptr, ev_r1 = nullptr, ev_user = nullptr;
+  hipEvent_t ev_sdec = nullptr, ev_r2 = nullptr, ev_r1 = nullptr, ev_user = nullptr, ev_fin = nullptr;
+  bool out_pending = false;         // ev_out marks the end of the last _dev batch on this slot
+  bool shared = false;              // side[] alias `stream` (one stream per slot)
   // workspace arena (grown on demand, never shrunk)
   void* ws = nullptr;
   size_t ws_bytes = 0;
 };
-constexpr int SSB_MAX_SLOTS = 8;
+constexpr int SSB_MAX_SLOTS = 16;
 
 struct ssb_ctx {
   int device = 0;
   ssb_slot sl[SSB_MAX_SLOTS];
-  int nslots = 1, next = 0;
+  int nslots = 1, next = 0, slot_streams = 3;
   ssb_slot* cur = &sl[0];           // the slot the current call runs on
   std::string err;
   // host staging arena
@@ -70,6 +72,11 @@ struct ssb_ctx {
   std::map<std::string, std::vector<evpair>> history;  // every launch while accumulating
   std::vector<evpair> pool;
   g1_aff* negg1_pow = nullptr;                         // device: [2^s](-g1), s = 0..63 (G2 MSM pairs)
+  // Context-wide streams for the kernels with the largest private segments (combine: up to 4.4 KB
+  // per lane, exact fallback: 2.6 KB), shared by all slots: the runtime reserves scratch per
+  // hardware queue for the largest kernel it has run, so these stay on two queues instead of
+  // every slot's.  spec: the speculative combines; tail: verdicts, exact fallback, exact combine.
+  hipStream_t spec = nullptr, tail = nullptr;
 };
 
 namespace {
@@ -91,8 +98,15 @@ struct carve {
   template <class T> T* take(size_t n) { T* p = (T*)(base + off); off += align_up(n * sizeof(T)); return p; }
 };
 
+// Every entry point takes the slot's workspace through here: the slot's main stream is ordered
+// after the end of the slot's previous batch (whose last kernels run on the context streams).
 int ensure_ws(ssb_ctx* ctx, size_t bytes) {
+  ssb_slot* S = ctx->cur;
+  if (S->out_pending) {
+    if (hipStreamWaitEvent(S->stream, S->ev_out, 0) != hipSuccess) { ctx->err = "hipStreamWaitEvent failed"; return SSB_EHIP; }
+  }
   if (bytes <= ctx->cur->ws_bytes) return SSB_OK;
+  if (S->out_pending) hipEventSynchronize(S->ev_out);
   if (ctx->cur->ws) { hipStreamSynchronize(ctx->cur->stream); hipFree(ctx->cur->ws); ctx->cur->ws = nullptr; ctx->cur->ws_bytes = 0; }
   size_t want = bytes + bytes / 4;
   if (hipMalloc(&ctx->cur->ws, want) != hipSuccess) { ctx->err = "hipMalloc workspace failed"; ctx->cur->ws = nullptr; return SSB_ENOMEM; }
@@ -111,22 +125,29 @@ int ensure_io(ssb_ctx* ctx, size_t bytes) {
 
 inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-int init_slot(ssb_slot& S) {
+// streams = 3: main chain + hash_to_G2 + G1 side, overlapping inside the batch (lowest latency);
+// streams = 1: the whole batch in order on one stream (side[] alias it) -- one hardware queue per
+// slot, so many more slots fit the runtime's per-queue scratch reservations (highest throughput).
+int init_slot(ssb_slot& S, int streams) {
   if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
-  for (int i = 0; i < 2; ++i)
-    if (hipStreamCreateWithFlags(&S.side[i], hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
-  for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user})
+  S.shared = streams == 1;
+  for (int i = 0; i < 2; ++i) {
+    if (S.shared) S.side[i] = S.stream;
+    else if (hipStreamCreateWithFlags(&S.side[i], hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
+  }
+  for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user, &S.ev_fin})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
   return SSB_OK;
 }
 void sync_slot(ssb_slot& S) {
   if (S.stream) hipStreamSynchronize(S.stream);
-  for (hipStream_t sd : S.side) if (sd) hipStreamSynchronize(sd);
+  if (!S.shared) for (hipStream_t sd : S.side) if (sd) hipStreamSynchronize(sd);
+  if (S.out_pending) hipEventSynchronize(S.ev_out);
 }
 void free_slot(ssb_slot& S) {
   if (S.ws) hipFree(S.ws);
-  for (hipStream_t sd : S.side) if (sd) hipStreamDestroy(sd);
-  for (hipEvent_t e : {S.ev_in, S.ev_hash, S.ev_dec, S.ev_comb, S.ev_out, S.ev_sdec, S.ev_r2, S.ev_r1, S.ev_user})
+  if (!S.shared) for (hipStream_t sd : S.side) if (sd) hipStreamDestroy(sd);
+  for (hipEvent_t e : {S.ev_in, S.ev_hash, S.ev_dec, S.ev_comb, S.ev_out, S.ev_sdec, S.ev_r2, S.ev_r1, S.ev_user, S.ev_fin})
     if (e) hipEventDestroy(e);
   if (S.stream) hipStreamDestroy(S.stream);
 }
@@ -261,7 +282,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
 template <class F>
 int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
                const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t seed,
-               uint8_t* d_verdict, F on_decoded) {
+               uint8_t* d_verdict, F on_decoded, hipStream_t tail) {
   hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
   SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
@@ -316,10 +337,15 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     }
     hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok);
   }
+  // verdicts (+ the exact per-share fallback when the batch failed) on the tail stream
+  if (tail != st) {
+    SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
+    SSB_HIP(hipStreamWaitEvent(tail, ctx->cur->ev_fin, 0));
+  }
   if (n) {
-    timed t(ctx, "k_fallback_verify");
-    hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.ok, w.flags, d_verdict);
-    hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, st, (int)n, w.ok, w.flags,
+    timed t(ctx, "k_fallback_verify", tail);
+    hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, tail, (int)n, w.ok, w.flags, d_verdict);
+    hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, tail, (int)n, w.ok, w.flags,
                        d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
   }
   SSB_HIP(hipGetLastError());
@@ -340,7 +366,9 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   ssb_ctx* ctx = new (std::nothrow) ssb_ctx();
   if (!ctx) return SSB_ENOMEM;
   ctx->device = device_ordinal;
-  if (init_slot(ctx->sl[0]) != SSB_OK) { delete ctx; return SSB_EHIP; }
+  if (init_slot(ctx->sl[0], ctx->slot_streams) != SSB_OK) { delete ctx; return SSB_EHIP; }
+  if (hipStreamCreateWithFlags(&ctx->spec, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx->sl[0]); delete ctx; return SSB_EHIP; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
@@ -363,6 +391,7 @@ void ssb_destroy(ssb_ctx* ctx) {
   for (auto& p : ctx->pool) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   if (ctx->io) hipFree(ctx->io);
   if (ctx->negg1_pow) hipFree(ctx->negg1_pow);
+  for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
 }
@@ -371,13 +400,31 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
   if (!ctx || depth < 1 || depth > SSB_MAX_SLOTS) return SSB_EINVAL;
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = ctx->nslots; i < depth; ++i) {
-    if (init_slot(ctx->sl[i]) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
+    if (init_slot(ctx->sl[i], ctx->slot_streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
     ctx->nslots = i + 1;
   }
   for (int i = depth; i < ctx->nslots; ++i) { sync_slot(ctx->sl[i]); free_slot(ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
   ctx->nslots = depth;
   ctx->next = 0;
   return SSB_OK;
+}
+
+int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
+  if (!ctx || (streams != 1 && streams != 3)) return SSB_EINVAL;
+  if (streams == ctx->slot_streams) return SSB_OK;
+  SSB_HIP(hipSetDevice(ctx->device));
+  for (int i = 0; i < ctx->nslots; ++i) { sync_slot(ctx->sl[i]); free_slot(ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
+  ctx->slot_streams = streams;
+  for (int i = 0; i < ctx->nslots; ++i)
+    if (init_slot(ctx->sl[i], streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
+  ctx->next = 0;
+  ctx->cur = &ctx->sl[0];
+  return SSB_OK;
+}
+
+void* ssb_slot_stream(ssb_ctx* ctx, int slot) {
+  if (!ctx || slot < 0 || slot >= ctx->nslots) return nullptr;
+  return (void*)ctx->sl[slot].stream;
 }
 
 const char* ssb_last_error(const ssb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -457,7 +504,7 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
   SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
   carve c{(char*)ctx->cur->ws};
   verify_ws w = carve_verify(c, n, n_roots);
-  if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, d_root, d_roots, d, rlc_seed, d_v, [] {}))) return rc;
+  if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, d_root, d_roots, d, rlc_seed, d_v, [] {}, st))) return rc;
   SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipStreamSynchronize(st));
   return SSB_OK;
@@ -481,7 +528,7 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
                 align_up(n * sizeof(g2_jac)) + align_up(n_jobs * 4);
   if ((rc = ensure_ws(ctx, need))) return rc;
   hipStream_t user = (hipStream_t)stream;
-  hipStream_t st = ctx->cur->stream, sc = ctx->cur->side[1];
+  hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = ctx->tail;
   // order the engine's streams after the caller's stream, and the caller's stream after them
   hipEvent_t e_user;
   SSB_HIP(hipEventCreateWithFlags(&e_user, hipEventDisableTiming));
@@ -507,10 +554,11 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
-  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict, spec))) return rc;
+  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict, spec, tl))) return rc;
   if (!n) spec();
   // exact path, only if the RLC batch failed (every kernel is a no-op when w.ok == 1)
-  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_comb, 0));
+  SSB_HIP(hipStreamWaitEvent(tl, ctx->cur->ev_comb, 0));
+  st = tl;
   hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
   hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)w.ok, fast, out_sig96);
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, (const uint32_t*)fast, lam);
@@ -518,6 +566,7 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, (const uint32_t*)fast, out_sig96);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
+  ctx->cur->out_pending = true;
   SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
   hipEventDestroy(e_user);
   return SSB_OK;
