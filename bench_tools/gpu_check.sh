@@ -14,6 +14,6 @@ echo "[gpu_check] bench"
 timeout -k 10 300 python -u bench.py --steps $STEPS --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 echo "[gpu_check] rocprof"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
+GPU_MAX_HW_QUEUES=20 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
 DB=$(find $OUT/prof -name '*.db' | head -1)
 python bench_tools/rocpd_stats.py "$DB" > $OUT/kernel_stats.csv && cut -c1-110 $OUT/kernel_stats.csv | head -24

@@ -16,7 +16,11 @@
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define SSB_INL __host__ __device__ __forceinline__
+#ifdef SSB_FN_INLINE  // experiment: every routine inlined (code size explodes; microbenchmarks only)
+#define SSB_FN __host__ __device__ __forceinline__
+#else
 #define SSB_FN __host__ __device__ inline __attribute__((noinline))
+#endif
 #else
 #define SSB_INL inline
 #define SSB_FN inline
@@ -410,6 +414,16 @@ SSB_INL void fp_add(fp& r, const fp& a, const fp& b) { mp_add_mod<12>(r.l, a.l, 
 SSB_INL void fp_sub(fp& r, const fp& a, const fp& b) { mp_sub_mod<12>(r.l, a.l, b.l, P_LIMBS); }
 SSB_INL void fp_dbl(fp& r, const fp& a) { mp_add_mod<12>(r.l, a.l, a.l, P_LIMBS); }
 SSB_INL void fp_neg(fp& r, const fp& a) { fp z = fp_zero(); fp_sub(r, z, a); }
+#if defined(SSB_FPMUL_CALL) && SSB_FPMUL_CALL == 2
+// experiment: one out-of-line Montgomery product, operands and result in VGPRs (by value)
+SSB_FN fp fp_mul_v(fp a, fp b) { fp r; mp_mont_mul<12>(r.l, a.l, b.l, P_LIMBS, P_INV32); return r; }
+SSB_INL void fp_mul(fp& r, const fp& a, const fp& b) { SSB_CNT(fp_mul); r = fp_mul_v(a, b); }
+SSB_INL void fp_sqr(fp& r, const fp& a) { SSB_CNT(fp_sqr); r = fp_mul_v(a, a); }
+#elif defined(SSB_FPMUL_CALL)
+SSB_FN void fp_mul_r(fp& r, const fp& a, const fp& b) { mp_mont_mul<12>(r.l, a.l, b.l, P_LIMBS, P_INV32); }
+SSB_INL void fp_mul(fp& r, const fp& a, const fp& b) { SSB_CNT(fp_mul); fp_mul_r(r, a, b); }
+SSB_INL void fp_sqr(fp& r, const fp& a) { SSB_CNT(fp_sqr); fp_mul_r(r, a, a); }
+#else
 SSB_INL void fp_mul(fp& r, const fp& a, const fp& b) {
   SSB_CNT(fp_mul);
   mp_mont_mul<12>(r.l, a.l, b.l, P_LIMBS, P_INV32);
@@ -418,6 +432,7 @@ SSB_INL void fp_sqr(fp& r, const fp& a) {
   SSB_CNT(fp_sqr);
   mp_mont_mul<12>(r.l, a.l, a.l, P_LIMBS, P_INV32);
 }
+#endif
 SSB_INL void fp_cmov(fp& r, const fp& a, bool c) {
   for (int i = 0; i < 12; ++i) r.l[i] = c ? a.l[i] : r.l[i];
 }

@@ -180,7 +180,8 @@ __global__ void __launch_bounds__(64) k_msm_horner(int ngroups, int c, int W, co
   const g1_jac* ws = wsum + (size_t)g * W;
   g1_jac acc = ws[W - 1];
   for (int w = W - 2; w >= 0; --w) {
-    for (int q = 0; q < c; ++q) jac_dbl(acc, acc);
+#pragma unroll 1
+    for (int q = 0; q < c; ++q) jac_dbl_inl(acc, acc);
     g1_jac o = ws[w];
     jac_add(acc, acc, o);
   }
