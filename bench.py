@@ -54,7 +54,8 @@ def msm_plan(N, n_roots):
         for c in range(cmin, cmax + 1):
             W, B = (64 + c - 1) // c, 2 ** c
             L = min(B, 64)
-            cost = n * W * (1 - 1 / B) + 1.5 * g * W * (2 * B + L * (math.log2(L) + 1))
+            reduce = 2 * (B - 1) if c <= 4 else 2 * B + L * (math.log2(L) + 1)
+            cost = n * W * (1 - 1 / B) + 1.5 * g * W * reduce
             if best is None or cost < best[0]:
                 best = (cost, c)
         return best[1]
@@ -71,7 +72,7 @@ def msm_plan(N, n_roots):
         c1 -= 1
     return {"c2": c2, "W2": (64 + c2 - 1) // c2, "lj2": pick_lj(N, 1, c2),
             "c1": c1, "W1": (64 + c1 - 1) // c1, "lj1": pick_lj(N, g1n, c1), "groups1": g1n,
-            "g1_msm": N >= 4096 * g1n}
+            "g1_msm": N >= 128 * g1n}
 
 
 def msm_mads(mads, N, c, W, lj, groups, g):
@@ -83,7 +84,11 @@ def msm_mads(mads, N, c, W, lj, groups, g):
     entries = N * W * (1 - 1 / B)
     trees = groups * W * B * ((1 << lj) - 1) * add
     scan = sum(L - off for off in (2 ** i for i in range(int(math.log2(L))))) if L > 1 else 0
-    window = groups * W * ((L * (2 * (m - 1) + 1) + scan + (L - 1)) * add + (L - 1) * math.log2(m) * dbl + (L - 1) * add)
+    if g == "g1" and c <= 4:
+        window = groups * W * 2 * (B - 1) * add
+    else:
+        window = groups * W * ((L * (2 * (m - 1) + 1) + scan + (L - 1)) * add + (L - 1) * math.log2(m) * dbl
+                               + (L - 1) * add)
     return entries * madd + trees + window
 
 

@@ -74,7 +74,8 @@ template <class F> SSB_INL void jac_dbl_inl(jac<F>& r, const jac<F>& p) {
 template <class F> SSB_FN void jac_dbl(jac<F>& r, const jac<F>& p) { jac_dbl_inl(r, p); }
 
 // madd-2007-bl: r = p + q, q affine.  Handles infinity and the doubling/opposite cases.
-template <class F> SSB_FN void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+// (_inl: inlined into the MSM bucket loops; jac_add_aff: out-of-line copy)
+template <class F> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   if (q.inf) { r = p; return; }
   if (jac_is_inf(p)) { jac_from_aff(r, q); return; }
   F Z1Z1, U2, S2, H, HH, I, J, rr, V, t;
@@ -99,6 +100,7 @@ template <class F> SSB_FN void jac_add_aff(jac<F>& r, const jac<F>& p, const aff
   f_add(z3, p.z, H); f_sqr(z3, z3); f_sub(z3, z3, Z1Z1); f_sub(z3, z3, HH);
   r.x = x3; r.y = y3; r.z = z3;
 }
+template <class F> SSB_FN void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) { jac_add_aff_inl(r, p, q); }
 
 // add-2007-bl: general Jacobian addition with the special cases.
 template <class F> SSB_FN void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {

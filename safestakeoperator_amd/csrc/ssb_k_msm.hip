@@ -100,22 +100,44 @@ __global__ void __launch_bounds__(256) k_scan_add(uint32_t K, uint32_t* __restri
   cur[x] = s;
 }
 
-// ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup ----
+// ---- bucket order: within each MSM's key range, buckets by entry count, largest first, so the
+// 64/J buckets that share a wave have (nearly) the same count and the lanes' loops stay converged
+// (Poisson-sized buckets in key order cost ~2x in divergence).  512 bins = 2 MSMs x counts 0..255
+// (larger counts share bin 255; only the convergence depends on the order, never the result).
+constexpr int ORDER_BINS = 512;
+__global__ void __launch_bounds__(256) k_order_hist(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ bins) {
+  const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+  if (key >= K) return;
+  const uint32_t c = cnt[key] < 255u ? cnt[key] : 255u;
+  atomicAdd(&bins[(key >= K2 ? 256u : 0u) + 255u - c], 1u);
+}
+__global__ void __launch_bounds__(256) k_order_scatter(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
+                                                       uint32_t* __restrict__ bins, uint32_t* __restrict__ order) {
+  const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+  if (key >= K) return;
+  const uint32_t c = cnt[key] < 255u ? cnt[key] : 255u;
+  order[atomicAdd(&bins[(key >= K2 ? 256u : 0u) + 255u - c], 1u)] = key;
+}
+
+// ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ start,
+__global__ void __launch_bounds__(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
+                                                   const uint32_t* __restrict__ start,
                                                    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ flags, const aff<F>* __restrict__ pts,
                                                    jac<F>* __restrict__ bsum) {
   __shared__ jac<F> sh[64];
   const int lane = threadIdx.x, J = 1 << lj, j = lane & (J - 1);
-  const uint32_t b = blockIdx.x * (64u >> lj) + (uint32_t)(lane >> lj);
+  const uint32_t ob = blockIdx.x * (64u >> lj) + (uint32_t)(lane >> lj);
+  const uint32_t key = ob < nb ? order[base + ob] : 0u, b = key - base;
   jac<F> acc;
   jac_set_inf(acc);
-  if (b < nb) {
-    const uint32_t s = start[base + b], e = s + cnt[base + b];
+  if (ob < nb) {
+    const uint32_t s = start[key], e = s + cnt[key];
     for (uint32_t x = s + j; x < e; x += J) {
       const uint32_t i = ent[x];
-      if (flags[i] & FLAG_CANDIDATE) jac_add_aff(acc, acc, pts[i]);
+      if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pts[i]; jac_add_aff_inl(acc, acc, q); }
     }
   }
   for (int h = J >> 1; h >= 1; h >>= 1) {
@@ -124,7 +146,7 @@ __global__ void __launch_bounds__(64) k_msm_bucket(uint32_t nb, uint32_t base, i
     if (j < h) { jac<F> o = sh[lane + h]; jac_add(acc, acc, o); }
     __syncthreads();
   }
-  if (j == 0 && b < nb) bsum[b] = acc;
+  if (j == 0 && ob < nb) bsum[b] = acc;
 }
 
 // ---- window sums  sum_d d * B_d  (one workgroup per (group, window)) ----
@@ -170,6 +192,26 @@ __global__ void __launch_bounds__(64) k_msm_window(int c, const jac<F>* __restri
       out_p[blockIdx.x] = negg1_pow[c * blockIdx.x];
     }
   }
+}
+
+// ---- window sums for narrow windows (2^c <= 16 buckets): one lane per (group, window), the
+// sequential running sum  R += B_d, U += R  for d = 2^c - 1 .. 1  (2 (2^c - 1) additions) ----
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
+                                                       jac<F>* __restrict__ out_jac) {
+  const uint32_t gw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gw >= ngw) return;
+  const int B = 1 << c;
+  const jac<F>* bk = bsum + (size_t)gw * B;
+  jac<F> R, U;
+  jac_set_inf(R);
+  jac_set_inf(U);
+  for (int d = B - 1; d >= 1; --d) {
+    jac<F> o = bk[d];
+    jac_add(R, R, o);
+    jac_add(U, U, R);
+  }
+  out_jac[gw] = U;
 }
 
 // ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
@@ -220,7 +262,7 @@ using namespace ssb::k;
 
 void msm_sort(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
               const uint32_t* share_root, const msm_cfg& c2, const msm_cfg& c1, uint32_t K, uint32_t* cnt,
-              uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent) {
+              uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent, uint32_t* order) {
   hipMemsetAsync(cnt, 0, (size_t)K * 4, st);
   const unsigned g = (unsigned)((n + 255) / 256), nb = (K + SCAN_BLOCK - 1) / SCAN_BLOCK;
   if (n) hipLaunchKernelGGL(k_msm_sort<false>, dim3(g), dim3(256), 0, st, n, seed, sflags, pflags, share_root, c2, c1, cnt, ent);
@@ -228,25 +270,34 @@ void msm_sort(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, cons
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, nb, bsum);
   hipLaunchKernelGGL(k_scan_add, dim3((K + 255) / 256), dim3(256), 0, st, K, start, bsum, cur);
   if (n) hipLaunchKernelGGL(k_msm_sort<true>, dim3(g), dim3(256), 0, st, n, seed, sflags, pflags, share_root, c2, c1, cur, ent);
+  // bucket order by count (bsum reused for the 512 bins)
+  hipMemsetAsync(bsum, 0, ORDER_BINS * 4, st);
+  hipLaunchKernelGGL(k_order_hist, dim3((K + 255) / 256), dim3(256), 0, st, K, c1.base, cnt, bsum);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, (uint32_t)ORDER_BINS, bsum);
+  hipLaunchKernelGGL(k_order_scatter, dim3((K + 255) / 256), dim3(256), 0, st, K, c1.base, cnt, bsum, order);
 }
 
-void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
             const uint32_t* flags, const g2_aff* sig, g2_jac* bsum, g2_aff* pair_q, g1_aff* pair_p,
             const g1_aff* negg1_pow) {
   const uint32_t nb = c.ngroups * c.W << c.c;
-  hipLaunchKernelGGL(k_msm_bucket<fp2>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, start,
+  hipLaunchKernelGGL(k_msm_bucket<fp2>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, order, start,
                      cnt, ent, flags, sig, bsum);
   hipLaunchKernelGGL(k_msm_window<fp2>, dim3(c.ngroups * c.W), dim3(64), 0, st, (int)c.c, (const g2_jac*)bsum,
                      (g2_jac*)nullptr, pair_q, pair_p, negg1_pow);
 }
 
-void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
             const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum) {
   const uint32_t nb = c.ngroups * c.W << c.c;
-  hipLaunchKernelGGL(k_msm_bucket<fp>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, start,
+  hipLaunchKernelGGL(k_msm_bucket<fp>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, order, start,
                      cnt, ent, flags, pk, bsum);
-  hipLaunchKernelGGL(k_msm_window<fp>, dim3(c.ngroups * c.W), dim3(64), 0, st, (int)c.c, (const g1_jac*)bsum, wsum,
-                     (g1_aff*)nullptr, (g1_aff*)nullptr, (const g1_aff*)nullptr);
+  if (c.c <= 4)
+    hipLaunchKernelGGL(k_msm_window_seq<fp>, dim3((c.ngroups * c.W + 63) / 64), dim3(64), 0, st, c.ngroups * c.W, (int)c.c,
+                       (const g1_jac*)bsum, wsum);
+  else
+    hipLaunchKernelGGL(k_msm_window<fp>, dim3(c.ngroups * c.W), dim3(64), 0, st, (int)c.c, (const g1_jac*)bsum, wsum,
+                       (g1_aff*)nullptr, (g1_aff*)nullptr, (const g1_aff*)nullptr);
   hipLaunchKernelGGL(k_msm_horner, dim3((c.ngroups + 63) / 64), dim3(64), 0, st, (int)c.ngroups, (int)c.c, (int)c.W,
                      (const g1_jac*)wsum, root_sum);
 }

@@ -128,11 +128,11 @@ void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst,
 // (pair_q[w] = W_w affine, pair_p[w] = [2^(c w)](-g1)).  msm_g1: root_sum[r] = sum_{i in r} k_i pk_i.
 void msm_sort(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
               const uint32_t* share_root, const msm_cfg& c2, const msm_cfg& c1, uint32_t K, uint32_t* cnt,
-              uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent);
-void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+              uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent, uint32_t* order);
+void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
             const uint32_t* flags, const g2_aff* sig, g2_jac* bsum, g2_aff* pair_q, g1_aff* pair_p,
             const g1_aff* negg1_pow);
-void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
+void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
             const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum);
 // gflags[s] = DEC_IN_GROUP when signature s (decodable, not infinity) passes psi(P) == [x]P
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags);

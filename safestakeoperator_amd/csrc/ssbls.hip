@@ -191,7 +191,9 @@ inline int msm_pick_c(size_t n, size_t groups, int cmin, int cmax) {
   double best = 1e300; int bc = cmin;
   for (int c = cmin; c <= cmax; ++c) {
     const double W = (64 + c - 1) / c, B = double(1u << c), L = B < 64 ? B : 64;
-    const double cost = double(n) * W * (1.0 - 1.0 / B) + 1.5 * double(groups) * W * (2.0 * B + L * (std::log2(L) + 1.0));
+    // windows of <= 16 buckets reduce sequentially in one lane (k_msm_window_seq)
+    const double reduce = c <= 4 ? 2.0 * (B - 1.0) : 2.0 * B + L * (std::log2(L) + 1.0);
+    const double cost = double(n) * W * (1.0 - 1.0 / B) + 1.5 * double(groups) * W * reduce;
     if (cost < best) { best = cost; bc = c; }
   }
   return bc;
@@ -208,7 +210,7 @@ bool g1_use_msm(size_t n, size_t n_roots) {
   const char* e = getenv("SSB_G1_PATH");
   if (e && !strcmp(e, "msm")) return true;
   if (e && !strcmp(e, "share")) return false;
-  return n >= 4096 * (n_roots ? n_roots : 1);
+  return n >= 128 * (n_roots ? n_roots : 1);
 }
 msm_plan plan_msm(size_t n, size_t n_roots) {
   msm_plan p;
@@ -234,6 +236,7 @@ struct verify_ws {
   fp12* f; uint32_t* ok;
   char* hws;          // staged hash_to_G2 workspace
   uint32_t* cnt; uint32_t* start; uint32_t* cur; uint32_t* sbsum; uint32_t* ent;   // MSM counting sort
+  uint32_t* order;                                                                 // buckets by count
   g2_jac* b2; g1_jac* b1; g1_jac* w1;                                              // MSM buckets / windows
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
   size_t npairs;
@@ -250,7 +253,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
   const size_t np = n_roots + MSM_WMAX;
   return align_up(np * sizeof(g2_aff)) + align_up(np * sizeof(g1_aff)) + align_up(n * sizeof(g2_aff)) +
          align_up(n * sizeof(g1_aff)) + align_up(n * 4) * 4 + align_up(fp12_slots(np) * sizeof(fp12)) + align_up(4) +
-         align_up(launch::hash_ws_bytes(n_roots)) + 3 * align_up((size_t)p.K * 4) + align_up(1024 * 4) +
+         align_up(launch::hash_ws_bytes(n_roots)) + 4 * align_up((size_t)p.K * 4) + align_up(1024 * 4) +
          align_up(p.n_ent * 4) + align_up(((size_t)p.g2.W << p.g2.c) * sizeof(g2_jac)) +
          align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
          align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
@@ -268,7 +271,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   w.cnt = c.take<uint32_t>(w.plan.K); w.start = c.take<uint32_t>(w.plan.K); w.cur = c.take<uint32_t>(w.plan.K);
-  w.sbsum = c.take<uint32_t>(1024); w.ent = c.take<uint32_t>(w.plan.n_ent);
+  w.sbsum = c.take<uint32_t>(1024); w.ent = c.take<uint32_t>(w.plan.n_ent); w.order = c.take<uint32_t>(w.plan.K);
   w.b2 = c.take<g2_jac>((size_t)w.plan.g2.W << w.plan.g2.c);
   w.b1 = c.take<g1_jac>((size_t)w.plan.g1.ngroups * w.plan.g1.W << w.plan.g1.c);
   w.w1 = c.take<g1_jac>((size_t)w.plan.g1.ngroups * w.plan.g1.W);
@@ -303,7 +306,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     hipLaunchKernelGGL(k_root_scan, dim3(1), dim3(64), 0, s1, (int)n_roots, w.rcnt, w.rstart, w.rcur);
     if (n) hipLaunchKernelGGL(k_root_scatter, dim3(nblk(n, 256)), dim3(256), 0, s1, (int)n, (int)n_roots, d_share_root, w.rcur, w.perm);
   }
-  { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, seed, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent); }
+  { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, seed, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent, w.order); }
   if (n) {
     { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, w.flags);
@@ -314,7 +317,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
     timed t(ctx, "k_msm_g1", s1);
-    launch::msm_g1(s1, P.g1, P.lj1, w.start, w.cnt, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p);
+    launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p);
   } else {
     timed t(ctx, "k_sum_g1", s1);
     hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)n_roots), dim3(SEG_THREADS), 0, s1, (int)n_roots, w.rstart, w.rcnt, w.perm,
@@ -322,7 +325,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
   if (n) on_decoded();
-  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow); }
+  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow); }
   SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
   { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f); }

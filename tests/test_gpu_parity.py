@@ -142,7 +142,7 @@ def _gen_committees(engine, V, t, n, n_roots, seed=7):
     return roots, master, sigs, pks, ids, jr, msig
 
 
-@pytest.mark.parametrize("g1_path", ["auto", "msm"])
+@pytest.mark.parametrize("g1_path", ["auto", "share"])
 def test_c2_full_size_properties(engine, g1_path, monkeypatch):
     """C2 size (4,096 validators x 4 shares, 3-of-4, 64 roots): every share verifies, every
     combined signature equals the master signature, and a sample agrees with the oracle.  Both
