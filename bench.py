@@ -92,15 +92,16 @@ def msm_mads(mads, N, c, W, lj, groups, g):
     return entries * madd + trees + window
 
 
-def kernel_mads(mads, V, t, n, n_roots):
-    """Algorithmic MADs per launch of each kernel (per-unit counts x units per launch)."""
+def kernel_mads(mads, V, t, n, n_roots, pk_cached=True):
+    """Algorithmic MADs per launch of each kernel (per-unit counts x units per launch).  With the
+    public-key cache the per-batch decode is the signatures only."""
     N = V * n
     p = msm_plan(N, n_roots)
     small = mads["combine_small_t3"] if t <= 3 else (mads["combine_small_t5"] if t <= 5 else mads["combine_small_t10"])
     npairs = n_roots + p["W2"]
     return {
         "k_hash_to_g2": n_roots * mads["hash_to_g2"],
-        "k_decode": N * (mads["decode_sig"] + mads["decode_pk"]),
+        "k_decode": N * (mads["decode_sig"] + (0.0 if pk_cached else mads["decode_pk"])),
         "k_subgroup": N * mads["subgroup"],
         "k_msm_g2": msm_mads(mads, N, p["c2"], p["W2"], p["lj2"], 1, "g2") + p["W2"] * mads["to_affine_g2"],
         "k_msm_g1": (msm_mads(mads, N, p["c1"], p["W1"], p["lj1"], p["groups1"], "g1")
@@ -195,9 +196,13 @@ def main():
     ap.add_argument("--slot-streams", type=int, default=1, choices=(1, 3),
                     help="streams per slot (1: batch in order on one queue; 3: hash / G1 side overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--compressed-pk", action="store_true",
+                    help="headline on the compressed-public-key entry point (default: keys decompressed once, "
+                         "ssb_pk_cache_set, as lighthouse's PublicKey holds them; the other variant is reported beside)")
     args = ap.parse_args()
     set_hw_queues(args.pipeline * args.slot_streams + 4)
 
+    import numpy as np
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -245,6 +250,13 @@ def main():
 
     streams = {}
 
+    # validator registration (outside the timed region): every operator key decompressed once
+    pk_host = np.frombuffer(wl["pks"], dtype=np.uint8)
+    if lib.ssb_pk_cache_set(eng.handle, N, pk_host.ctypes.data_as(_lib._u8p)) != 0:
+        raise RuntimeError("ssb_pk_cache_set: %s" % lib.ssb_last_error(eng.handle))
+    d_pkidx = torch.arange(0, N, dtype=torch.int32, device=dev)
+    use_cache = [not args.compressed_pk]
+
     def step(i, k):
         """batch i on pipeline slot k (engine slot k, output buffers k); the caller's stream is the
         slot's own main stream (ssb_slot_stream), so the bench adds no hardware queue"""
@@ -252,9 +264,11 @@ def main():
         if k not in streams:
             streams[k] = torch.cuda.ExternalStream(lib.ssb_slot_stream(eng.handle, k), device=dev)
         s = streams[k]
+        fn = lib.ssb_threshold_aggregate_batch_cached_dev if use_cache[0] else lib.ssb_threshold_aggregate_batch_dev
+        pk_arg = d_pkidx if use_cache[0] else d_pk
         with torch.cuda.stream(s):
-            rc = lib.ssb_threshold_aggregate_batch_dev(
-                eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(), d_pk.data_ptr(), d_ids.data_ptr(),
+            rc = fn(
+                eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(), pk_arg.data_ptr(), d_ids.data_ptr(),
                 d_jr.data_ptr(), n_roots, d_roots.data_ptr(), ctypes.cast(dst_arr, _lib._u8p), len(DST),
                 (seed_base + i) & (2 ** 64 - 1), o["out"].data_ptr(), o["st"].data_ptr(), o["err"].data_ptr(),
                 o["ver"].data_ptr(), ctypes.c_void_p(s.cuda_stream))
@@ -288,36 +302,50 @@ def main():
     if lib.ssb_set_slot_streams(eng.handle, args.slot_streams) != 0 or lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
         raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
     streams.clear()
-    for i in range(max(args.warmup, S)):
-        step(i, i % S)
-    torch.cuda.synchronize(dev)
-    # correctness of every slot's last batch: every share valid, every combine == master signature
     msig = eng.sign_batch(wl["master"][:64], wl["job_root"][:64], wl["roots"])
-    ok_st = ok_comb = True
-    for o in outs:
-        ok_st = ok_st and bool((o["st"] == 0).all().item()) and bool((o["ver"] == 1).all().item())
-        out_host = o["out"].cpu().numpy()
-        ok_comb = ok_comb and all(out_host[v].tobytes() == msig[v] for v in range(min(64, V)))
 
+    def warm_and_check():
+        """warmup, then correctness of every slot's last batch: every share valid, every combine ==
+        the master signature"""
+        for i in range(max(args.warmup, S)):
+            step(i, i % S)
+        torch.cuda.synchronize(dev)
+        ok_st = ok_comb = True
+        for o in outs:
+            ok_st = ok_st and bool((o["st"] == 0).all().item()) and bool((o["ver"] == 1).all().item())
+            out_host = o["out"].cpu().numpy()
+            ok_comb = ok_comb and all(out_host[v].tobytes() == msig[v] for v in range(min(64, V)))
+        return ok_st and ok_comb
+
+    def timed_run():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        host_ms = []
+        for i in range(args.steps):
+            th = time.perf_counter()
+            step(args.warmup + i, i % S)
+            host_ms.append((time.perf_counter() - th) * 1e3)
+        torch.cuda.synchronize(dev)
+        if os.environ.get("SSB_DEBUG_HOST"):
+            print("host ms per submit:", " ".join("%.2f" % x for x in host_ms), file=sys.stderr)
+        if dist is not None:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    # the other public-key variant first (reported beside the headline), then the headline
+    use_cache[0] = args.compressed_pk
+    ok_other = warm_and_check()
+    elapsed_other = timed_run()
+    use_cache[0] = not args.compressed_pk
+    ok_head = warm_and_check()
+    elapsed = timed_run()
+    ok_st = ok_comb = ok_head and ok_other
     if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    host_ms = []
-    for i in range(args.steps):
-        th = time.perf_counter()
-        step(args.warmup + i, i % S)
-        host_ms.append((time.perf_counter() - th) * 1e3)
-    torch.cuda.synchronize(dev)
-    if os.environ.get("SSB_DEBUG_HOST"):
-        print("host ms per submit:", " ".join("%.2f" % x for x in host_ms), file=sys.stderr)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, elapsed_other], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed, elapsed_other = float(tt[0].item()), float(tt[1].item())
         okt = torch.tensor([1 if (ok_st and ok_comb) else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_all = bool(okt.item())
@@ -330,7 +358,7 @@ def main():
         value = total_shares / elapsed
         combined = V * world * args.steps / elapsed
         mads = opcount_mads()
-        km = kernel_mads(mads, V, t, n, n_roots)
+        km = kernel_mads(mads, V, t, n, n_roots, pk_cached=not args.compressed_pk)
         avg = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in kt.items()}
         # the dominant kernel = the one doing most of the step's algorithmic work
         dom = max(km, key=lambda k: km[k] if avg.get(k, 0.0) > 0 else -1.0)
@@ -356,6 +384,11 @@ def main():
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
                        "batches_in_flight": S, "streams_per_slot": args.slot_streams},
             "batch_latency_ms": round(latency_ms, 3),
+            "public_keys": ("compressed per batch (ssb_threshold_aggregate_batch_dev)" if args.compressed_pk else
+                            "decompressed once at registration (ssb_pk_cache_set + _cached_dev), as lighthouse's "
+                            "PublicKey holds the point"),
+            ("value_pk_cached" if args.compressed_pk else "value_compressed_pk"):
+                round(N * world * args.steps / elapsed_other, 1),
             "combined_sigs_per_s": round(combined, 1),
             "results_ok": ok_all,
             "roofline": {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),

@@ -120,6 +120,20 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
                                       uint8_t* out_sig96, int32_t* out_status, uint64_t* out_err,
                                       uint8_t* share_verdicts, void* stream);
 
+/* Decoded public keys.  ssb_pk_cache_set decompresses n public keys once (synchronous) into the
+ * context's table (replacing any previous table), the way lighthouse's PublicKey holds the
+ * decompressed point; ssb_threshold_aggregate_batch_cached_dev then takes, per share, an index
+ * into that table instead of 48 compressed bytes.  A key that does not decode, decodes to
+ * infinity, or an index >= n makes the share invalid (verdict 0), as in the compressed path. */
+int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48);
+int ssb_threshold_aggregate_batch_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares,
+                                             const uint32_t* share_off, const uint32_t* t,
+                                             const uint8_t* sig96, const uint32_t* pk_index,
+                                             const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                                             const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                             uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
+                                             uint64_t* out_err, uint8_t* share_verdicts, void* stream);
+
 /* Batched unsafe_aggregate: job j combines ALL its shares [share_off[j], share_off[j+1]) with
  * Lagrange coefficients of its ids (t = share count), starting from infinity. */
 int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off,

@@ -34,6 +34,12 @@ SIGNATURES = {
                                                          ctypes.c_void_p, _sz, ctypes.c_void_p, _u8p, _sz,
                                                          ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_pk_cache_set": (ctypes.c_int, [_ctx, _sz, _u8p]),
+    "ssb_threshold_aggregate_batch_cached_dev": (ctypes.c_int, [_ctx, _sz, _sz, ctypes.c_void_p, ctypes.c_void_p,
+                                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                                ctypes.c_void_p, _sz, ctypes.c_void_p, _u8p, _sz,
+                                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "ssb_unsafe_aggregate_batch": (ctypes.c_int, [_ctx, _sz, _u32p, _u8p, _u64p, _u8p, _i32p]),
     "ssb_sign_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u32p, _sz, _u8p, _u8p, _sz, _u8p]),
     "ssb_sk_to_pk_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p]),

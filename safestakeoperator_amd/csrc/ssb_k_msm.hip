@@ -135,9 +135,17 @@ __global__ void __launch_bounds__(64) k_msm_bucket(uint32_t nb, uint32_t base, i
   jac_set_inf(acc);
   if (ob < nb) {
     const uint32_t s = start[key], e = s + cnt[key];
-    for (uint32_t x = s + j; x < e; x += J) {
-      const uint32_t i = ent[x];
-      if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pts[i]; jac_add_aff_inl(acc, acc, q); }
+    // software pipelined: the next entry's point is in flight while this one is added
+    uint32_t x = s + j, fl = 0;
+    aff<F> q;
+    if (x < e) { const uint32_t i = ent[x]; fl = flags[i]; q = pts[i]; }
+    while (x < e) {
+      const uint32_t xn = x + J;
+      uint32_t fn = 0;
+      aff<F> qn;
+      if (xn < e) { const uint32_t i = ent[xn]; fn = flags[i]; qn = pts[i]; }
+      if (fl & FLAG_CANDIDATE) jac_add_aff_inl(acc, acc, q);
+      q = qn; fl = fn; x = xn;
     }
   }
   for (int h = J >> 1; h >= 1; h >>= 1) {

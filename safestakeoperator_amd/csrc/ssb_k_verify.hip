@@ -51,6 +51,38 @@ __global__ void __launch_bounds__(64) k_decode2(int n, const uint8_t* __restrict
     pk_aff[s] = pk;
   }
 }
+// decoded-public-key path (ssb_pk_cache_set): n lanes decode the signatures, the public keys are
+// gathered from the context's table of points decompressed once (lighthouse's PublicKey holds the
+// decompressed point too: the reference never decompresses a key per verification)
+__global__ void __launch_bounds__(64) k_decode_sig(int n, const uint8_t* __restrict__ sig96, g2_aff* __restrict__ sig_aff,
+                                                   uint32_t* __restrict__ sflags) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  uint8_t b[96];
+  for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)g + k];
+  g2_aff sig;
+  sflags[g] = unit_decode_sig(sig, b);
+  sig_aff[g] = sig;
+}
+__global__ void __launch_bounds__(256) k_pk_gather(int n, const uint32_t* __restrict__ pk_index, uint32_t n_cache,
+                                                   const g1_aff* __restrict__ cache_aff, const uint32_t* __restrict__ cache_flags,
+                                                   g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ pflags) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint32_t i = pk_index[s];
+  if (i < n_cache) { pk_aff[s] = cache_aff[i]; pflags[s] = cache_flags[i]; }
+  else pflags[s] = 0u;  // out-of-range index: the share cannot verify
+}
+__global__ void __launch_bounds__(64) k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
+                                                  uint32_t* __restrict__ pflags) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  uint8_t b[48];
+  for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
+  g1_aff pk;
+  pflags[s] = unit_decode_pk(pk, b);
+  pk_aff[s] = pk;
+}
 // threads [0, n): G2 subgroup check; [n, 2n): r_i * sig_i; [2n, 3n): r_i * pk_i  (single lane each:
 // at C2 size the chip has spare waves, so the per-share chains run one per lane; the lane-group
 // versions in ssb_k_lane.hip cost ~6x the instructions for ~2x lower latency)

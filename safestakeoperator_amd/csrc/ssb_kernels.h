@@ -39,6 +39,13 @@ __global__ void k_decode(int n, const uint8_t* __restrict__ sig96,
 __global__ void k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
                                                 g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
                                                 uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags);
+__global__ void k_decode_sig(int n, const uint8_t* __restrict__ sig96, g2_aff* __restrict__ sig_aff,
+                             uint32_t* __restrict__ sflags);
+__global__ void k_pk_gather(int n, const uint32_t* __restrict__ pk_index, uint32_t n_cache,
+                            const g1_aff* __restrict__ cache_aff, const uint32_t* __restrict__ cache_flags,
+                            g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ pflags);
+__global__ void k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
+                            uint32_t* __restrict__ pflags);
 __global__ void k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
                             const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
                             const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,

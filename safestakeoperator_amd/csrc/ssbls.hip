@@ -77,6 +77,8 @@ struct ssb_ctx {
   // hardware queue for the largest kernel it has run, so these stay on two queues instead of
   // every slot's.  spec: the speculative combines; tail: verdicts, exact fallback, exact combine.
   hipStream_t spec = nullptr, tail = nullptr;
+  // decoded public keys (ssb_pk_cache_set): affine points + DEC_* flags, indexed by the caller
+  g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0;
 };
 
 namespace {
@@ -284,7 +286,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
 
 template <class F>
 int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
-               const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t seed,
+               const uint32_t* d_pk_index, const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t seed,
                uint8_t* d_verdict, F on_decoded, hipStream_t tail) {
   hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
@@ -294,7 +296,16 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
   hipStream_t s1 = ctx->cur->side[1];
   const msm_plan& P = w.plan;
-  if (n) { timed t(ctx, "k_decode"); hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags); }
+  if (n) {
+    timed t(ctx, "k_decode");
+    if (d_pk_index) {
+      hipLaunchKernelGGL(k_decode_sig, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, w.sig_aff, w.sflags);
+      hipLaunchKernelGGL(k_pk_gather, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, d_pk_index, (uint32_t)ctx->pkc_n,
+                         (const g1_aff*)ctx->pkc_aff, (const uint32_t*)ctx->pkc_flags, w.pk_aff, w.pflags);
+    } else {
+      hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags);
+    }
+  }
   SSB_HIP(hipEventRecord(ctx->cur->ev_sdec, st));
   // side[1]: per-share G1 products and the root segments, beside the subgroup checks
   SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_sdec, 0));
@@ -394,6 +405,8 @@ void ssb_destroy(ssb_ctx* ctx) {
   for (auto& p : ctx->pool) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   if (ctx->io) hipFree(ctx->io);
   if (ctx->negg1_pow) hipFree(ctx->negg1_pow);
+  if (ctx->pkc_aff) hipFree(ctx->pkc_aff);
+  if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
@@ -507,21 +520,26 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
   SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
   carve c{(char*)ctx->cur->ws};
   verify_ws w = carve_verify(c, n, n_roots);
-  if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, d_root, d_roots, d, rlc_seed, d_v, [] {}, st))) return rc;
+  if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, nullptr, d_root, d_roots, d, rlc_seed, d_v, [] {}, st))) return rc;
   SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipStreamSynchronize(st));
   return SSB_OK;
 }
 
-int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* share_off,
-                                      const uint32_t* t, const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids,
-                                      const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
-                                      const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
-                                      int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, void* stream) {
+}  // extern "C"
+
+namespace {
+// the body of the _dev entry points: public keys compressed (pk48) or from the cache (pk_index)
+int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* share_off,
+                  const uint32_t* t, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
+                  const uint64_t* ids, const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
+                  const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
+                  int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, void* stream) {
   if (!ctx) return SSB_EINVAL;
   if (n_jobs == 0) return SSB_OK;
   if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0 ||
-      (n_shares && (!sig96 || !pk48 || !ids))) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
+      (n_shares && (!sig96 || !(pk48 || pk_index) || !ids))) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
+  if (pk_index && !ctx->pkc_aff) { ctx->err = "no public-key cache (ssb_pk_cache_set)"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
   ctx->cur = &ctx->sl[ctx->next];   // pipeline slot: batches on different slots overlap
   ctx->next = (ctx->next + 1) % ctx->nslots;
@@ -557,7 +575,7 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
-  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, share_root, roots32, d, rlc_seed, verdict, spec, tl))) return rc;
+  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict, spec, tl))) return rc;
   if (!n) spec();
   // exact path, only if the RLC batch failed (every kernel is a no-op when w.ok == 1)
   SSB_HIP(hipStreamWaitEvent(tl, ctx->cur->ev_comb, 0));
@@ -572,6 +590,58 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
   ctx->cur->out_pending = true;
   SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
   hipEventDestroy(e_user);
+  return SSB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* share_off,
+                                      const uint32_t* t, const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids,
+                                      const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
+                                      const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
+                                      int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, void* stream) {
+  if (ctx && n_shares && !pk48) { ctx->err = "null pk48"; return SSB_EINVAL; }
+  return aggregate_dev(ctx, n_jobs, n_shares, share_off, t, sig96, pk48, nullptr, ids, job_root, n_roots, roots32, dst,
+                       dst_len, rlc_seed, out_sig96, out_status, out_err, share_verdicts, stream);
+}
+
+int ssb_threshold_aggregate_batch_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* share_off,
+                                             const uint32_t* t, const uint8_t* sig96, const uint32_t* pk_index,
+                                             const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                                             const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
+                                             uint8_t* out_sig96, int32_t* out_status, uint64_t* out_err,
+                                             uint8_t* share_verdicts, void* stream) {
+  if (ctx && n_shares && !pk_index) { ctx->err = "null pk_index"; return SSB_EINVAL; }
+  return aggregate_dev(ctx, n_jobs, n_shares, share_off, t, sig96, nullptr, pk_index, ids, job_root, n_roots, roots32, dst,
+                       dst_len, rlc_seed, out_sig96, out_status, out_err, share_verdicts, stream);
+}
+
+int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
+  if (!ctx) return SSB_EINVAL;
+  if (n && !pk48) { ctx->err = "null pk48"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
+  for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) SSB_HIP(hipStreamSynchronize(x));
+  if (ctx->pkc_aff) { hipFree(ctx->pkc_aff); ctx->pkc_aff = nullptr; }
+  if (ctx->pkc_flags) { hipFree(ctx->pkc_flags); ctx->pkc_flags = nullptr; }
+  ctx->pkc_n = 0;
+  if (!n) return SSB_OK;
+  uint8_t* d_in = nullptr;
+  if (hipMalloc(&ctx->pkc_aff, n * sizeof(g1_aff)) != hipSuccess || hipMalloc(&ctx->pkc_flags, n * 4) != hipSuccess ||
+      hipMalloc(&d_in, n * 48) != hipSuccess) {
+    ctx->err = "hipMalloc public-key cache failed";
+    if (d_in) hipFree(d_in);
+    return SSB_ENOMEM;
+  }
+  hipStream_t st = ctx->sl[0].stream;
+  SSB_HIP(hipMemcpyAsync(d_in, pk48, n * 48, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_decode_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_in, ctx->pkc_aff, ctx->pkc_flags);
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipStreamSynchronize(st));
+  hipFree(d_in);
+  ctx->pkc_n = n;
   return SSB_OK;
 }
 

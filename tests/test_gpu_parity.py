@@ -187,3 +187,62 @@ def test_c2_invalid_injection_exact_verdicts(engine, g1_path, monkeypatch):
             assert st[v] == 0 and out[v].tobytes() == msig[v]
         else:
             assert st[v] == 4 and list(err[v]) == [valid, t]
+
+
+def test_pk_cache_path_matches_compressed(engine):
+    """ssb_pk_cache_set + ssb_threshold_aggregate_batch_cached_dev (public keys decompressed once,
+    per-share indices) gives exactly the outputs of the compressed-key path, including invalid
+    shares, a key that does not decode and an out-of-range index."""
+    import ctypes
+    import torch
+    from safestakeoperator_amd import _lib
+    V, t, n = 256, 3, 4
+    roots, master, sigs, pks, ids, jr, msig = _gen_committees(engine, V, t, n, 4, seed=17)
+    sigs, pks = list(sigs), list(pks)
+    rng = np.random.default_rng(9)
+    bad = sorted(rng.choice(V * n, size=12, replace=False).tolist())
+    wrong = engine.sign_batch([7 + i for i in range(len(bad))], [0] * len(bad), [hashlib.sha256(b"y").digest()])
+    for k, i in enumerate(bad):
+        sigs[i] = wrong[k]
+    pks[5] = bytes([0xA0]) + b"\x11" * 47          # compressed flag, x >= p: does not decode
+    # the cache holds each distinct key once; shares refer to it by index
+    uniq = sorted(set(pks))
+    index = [uniq.index(k) for k in pks]
+    index[9] = len(uniq) + 3                          # out of range: share 9 must fail
+    pks_eff = list(pks)
+    pks_eff[9] = bytes([0xA0]) + b"\x11" * 47
+    offs = list(range(0, V * n + 1, n))
+    ref = engine.threshold_aggregate_batch_raw([t] * V, offs, b"".join(sigs), b"".join(pks_eff), ids, jr, roots)
+
+    lib = engine._lib
+    dev = torch.device("cuda", 0)
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_sig, d_pk = u8(b"".join(sigs)), u8(b"".join(pks_eff))
+    d_idx = torch.tensor(index, dtype=torch.int32, device=dev)
+    d_ids = torch.tensor(ids, dtype=torch.int64, device=dev)
+    d_off = torch.tensor(offs, dtype=torch.int32, device=dev)
+    d_t = torch.full((V,), t, dtype=torch.int32, device=dev)
+    d_jr = torch.tensor(jr, dtype=torch.int32, device=dev)
+    d_roots = u8(b"".join(roots))
+    cache = np.frombuffer(b"".join(uniq), dtype=np.uint8)
+    assert lib.ssb_pk_cache_set(engine.handle, len(uniq), cache.ctypes.data_as(_lib._u8p)) == 0
+    dst = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
+    for cached in (False, True):
+        out = torch.zeros((V, 96), dtype=torch.uint8, device=dev)
+        st = torch.zeros((V,), dtype=torch.int32, device=dev)
+        err = torch.zeros((V, 2), dtype=torch.int64, device=dev)
+        ver = torch.zeros((V * n,), dtype=torch.uint8, device=dev)
+        fn = lib.ssb_threshold_aggregate_batch_cached_dev if cached else lib.ssb_threshold_aggregate_batch_dev
+        rc = fn(engine.handle, V, V * n, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(),
+                (d_idx if cached else d_pk).data_ptr(), d_ids.data_ptr(), d_jr.data_ptr(), len(roots), d_roots.data_ptr(),
+                ctypes.cast(dst, _lib._u8p), len(DST), 0x5AFE57A4E, out.data_ptr(), st.data_ptr(), err.data_ptr(),
+                ver.data_ptr(), None)
+        assert rc == 0, lib.ssb_last_error(engine.handle)
+        torch.cuda.synchronize()
+        assert (ver.cpu().numpy() == ref[3]).all(), cached
+        assert (st.cpu().numpy() == ref[1]).all(), cached
+        assert (err.cpu().numpy().astype(np.uint64) == ref[2]).all(), cached
+        assert (out.cpu().numpy() == ref[0]).all(), cached
+    expect = np.ones(V * n, dtype=np.uint8)
+    expect[bad + [5, 9]] = 0
+    assert (ref[3] == expect).all()
