@@ -1,0 +1,1137 @@
+/* bls_c.c -- plain-C CPU restatement of SafeStake's threshold-BLS path on BLS12-381.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load this library (oracle/_build/libblsoracle.so, built by oracle/Makefile); the product
+ * path (safestakeoperator_amd, libssbls.so) never does.
+ *
+ * It restates, independently of the device code (64-bit limbs, CIOS Montgomery, affine Miller
+ * loop on the untwisted lines, textbook exponent for the final exponentiation), the same
+ * algorithm as oracle/bls12_381.py:
+ *   - Signature::verify(pk, msg) = blst verify(sig_groupcheck=true, pk_validate=false)
+ *     (reference call site src/crypto/generic_threshold.rs:156; same convention as
+ *     src/network/io_committee.rs:536-539): decompress, subgroup check psi(P) == [x]P,
+ *     e(pk, H(m)) * e(-g1, sig) == 1;
+ *   - hash_to_G2: RFC 9380 BLS12381G2_XMD:SHA-256_SSWU_RO_ with the DST of
+ *     src/crypto/impls/blst.rs:11;
+ *   - threshold_aggregate: src/crypto/generic_threshold.rs:132-175 (scan order, error order),
+ *     lagrange_coeffs src/crypto/impls/blst.rs:19-39 (blst_sk_inverse(0) = 0),
+ *     unsafe_aggregate src/crypto/impls/blst.rs:67-87.
+ * Pinned by the same known answers as the Python oracle (tests/golden/known_answers.json) and by
+ * agreement with it on the golden threshold cases (tests/test_oracle_c.py).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+typedef unsigned __int128 u128;
+typedef struct { uint64_t l[6]; } fp;
+typedef struct { fp c0, c1; } fp2;
+typedef struct { fp2 c0, c1, c2; } fp6;
+typedef struct { fp6 c0, c1; } fp12;
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fp: p = 0x1a0111ea...aaab, Montgomery form with R = 2^384                                   */
+/* ------------------------------------------------------------------------------------------ */
+static const uint64_t PL[6] = {0xb9feffffffffaaabULL, 0x1eabfffeb153ffffULL, 0x6730d2a0f6b0f624ULL,
+                               0x64774b84f38512bfULL, 0x4b1ba7b6434bacd7ULL, 0x1a0111ea397fe69aULL};
+static uint64_t PINV;           /* -p^-1 mod 2^64 */
+static fp FP_ONE, FP_R2, FP_ZERO;
+static uint64_t E_PM2[6], E_SQRT[6], E_HALF[6];  /* p-2, (p+1)/4, (p-1)/2 */
+
+static int cmp6(const uint64_t* a, const uint64_t* b) {
+  for (int i = 5; i >= 0; --i) { if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1; }
+  return 0;
+}
+static uint64_t add6(uint64_t* r, const uint64_t* a, const uint64_t* b) {
+  u128 c = 0;
+  for (int i = 0; i < 6; ++i) { c += (u128)a[i] + b[i]; r[i] = (uint64_t)c; c >>= 64; }
+  return (uint64_t)c;
+}
+static uint64_t sub6(uint64_t* r, const uint64_t* a, const uint64_t* b) {
+  uint64_t br = 0;
+  for (int i = 0; i < 6; ++i) {
+    u128 d = (u128)a[i] - b[i] - br;
+    r[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  return br;
+}
+static void fp_add(fp* r, const fp* a, const fp* b) {
+  uint64_t t[6];
+  add6(t, a->l, b->l);  /* a, b < p < 2^381: no carry out */
+  if (cmp6(t, PL) >= 0) sub6(t, t, PL);
+  memcpy(r->l, t, 48);
+}
+static void fp_sub(fp* r, const fp* a, const fp* b) {
+  uint64_t t[6];
+  if (sub6(t, a->l, b->l)) add6(t, t, PL);
+  memcpy(r->l, t, 48);
+}
+static void fp_neg(fp* r, const fp* a) { fp_sub(r, &FP_ZERO, a); }
+static void fp_mul(fp* r, const fp* a, const fp* b) {  /* CIOS, unrolled (scalar temporaries) */
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0, t6 = 0, t7, m;
+  u128 c;
+  const uint64_t a0 = a->l[0], a1 = a->l[1], a2 = a->l[2], a3 = a->l[3], a4 = a->l[4], a5 = a->l[5];
+  { const uint64_t bi = b->l[0];
+    c = (u128)a0 * bi + t0; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)a1 * bi + t1; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)a2 * bi + t2; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)a3 * bi + t3; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)a4 * bi + t4; t4 = (uint64_t)c; c >>= 64;
+    c += (u128)a5 * bi + t5; t5 = (uint64_t)c; c >>= 64;
+    c += t6; t6 = (uint64_t)c; t7 = (uint64_t)(c >> 64);
+    m = t0 * PINV;
+    c = (u128)m * PL[0] + t0; c >>= 64;
+    c += (u128)m * PL[1] + t1; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[2] + t2; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[3] + t3; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[4] + t4; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[5] + t5; t4 = (uint64_t)c; c >>= 64;
+    c += t6; t5 = (uint64_t)c; t6 = t7 + (uint64_t)(c >> 64); }
+  { const uint64_t bi = b->l[1];
+    c = (u128)a0 * bi + t0; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)a1 * bi + t1; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)a2 * bi + t2; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)a3 * bi + t3; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)a4 * bi + t4; t4 = (uint64_t)c; c >>= 64;
+    c += (u128)a5 * bi + t5; t5 = (uint64_t)c; c >>= 64;
+    c += t6; t6 = (uint64_t)c; t7 = (uint64_t)(c >> 64);
+    m = t0 * PINV;
+    c = (u128)m * PL[0] + t0; c >>= 64;
+    c += (u128)m * PL[1] + t1; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[2] + t2; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[3] + t3; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[4] + t4; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[5] + t5; t4 = (uint64_t)c; c >>= 64;
+    c += t6; t5 = (uint64_t)c; t6 = t7 + (uint64_t)(c >> 64); }
+  { const uint64_t bi = b->l[2];
+    c = (u128)a0 * bi + t0; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)a1 * bi + t1; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)a2 * bi + t2; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)a3 * bi + t3; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)a4 * bi + t4; t4 = (uint64_t)c; c >>= 64;
+    c += (u128)a5 * bi + t5; t5 = (uint64_t)c; c >>= 64;
+    c += t6; t6 = (uint64_t)c; t7 = (uint64_t)(c >> 64);
+    m = t0 * PINV;
+    c = (u128)m * PL[0] + t0; c >>= 64;
+    c += (u128)m * PL[1] + t1; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[2] + t2; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[3] + t3; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[4] + t4; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[5] + t5; t4 = (uint64_t)c; c >>= 64;
+    c += t6; t5 = (uint64_t)c; t6 = t7 + (uint64_t)(c >> 64); }
+  { const uint64_t bi = b->l[3];
+    c = (u128)a0 * bi + t0; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)a1 * bi + t1; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)a2 * bi + t2; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)a3 * bi + t3; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)a4 * bi + t4; t4 = (uint64_t)c; c >>= 64;
+    c += (u128)a5 * bi + t5; t5 = (uint64_t)c; c >>= 64;
+    c += t6; t6 = (uint64_t)c; t7 = (uint64_t)(c >> 64);
+    m = t0 * PINV;
+    c = (u128)m * PL[0] + t0; c >>= 64;
+    c += (u128)m * PL[1] + t1; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[2] + t2; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[3] + t3; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[4] + t4; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[5] + t5; t4 = (uint64_t)c; c >>= 64;
+    c += t6; t5 = (uint64_t)c; t6 = t7 + (uint64_t)(c >> 64); }
+  { const uint64_t bi = b->l[4];
+    c = (u128)a0 * bi + t0; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)a1 * bi + t1; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)a2 * bi + t2; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)a3 * bi + t3; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)a4 * bi + t4; t4 = (uint64_t)c; c >>= 64;
+    c += (u128)a5 * bi + t5; t5 = (uint64_t)c; c >>= 64;
+    c += t6; t6 = (uint64_t)c; t7 = (uint64_t)(c >> 64);
+    m = t0 * PINV;
+    c = (u128)m * PL[0] + t0; c >>= 64;
+    c += (u128)m * PL[1] + t1; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[2] + t2; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[3] + t3; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[4] + t4; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[5] + t5; t4 = (uint64_t)c; c >>= 64;
+    c += t6; t5 = (uint64_t)c; t6 = t7 + (uint64_t)(c >> 64); }
+  { const uint64_t bi = b->l[5];
+    c = (u128)a0 * bi + t0; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)a1 * bi + t1; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)a2 * bi + t2; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)a3 * bi + t3; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)a4 * bi + t4; t4 = (uint64_t)c; c >>= 64;
+    c += (u128)a5 * bi + t5; t5 = (uint64_t)c; c >>= 64;
+    c += t6; t6 = (uint64_t)c; t7 = (uint64_t)(c >> 64);
+    m = t0 * PINV;
+    c = (u128)m * PL[0] + t0; c >>= 64;
+    c += (u128)m * PL[1] + t1; t0 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[2] + t2; t1 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[3] + t3; t2 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[4] + t4; t3 = (uint64_t)c; c >>= 64;
+    c += (u128)m * PL[5] + t5; t4 = (uint64_t)c; c >>= 64;
+    c += t6; t5 = (uint64_t)c; t6 = t7 + (uint64_t)(c >> 64); }
+  uint64_t t[6] = {t0, t1, t2, t3, t4, t5};
+  if (t6 || cmp6(t, PL) >= 0) sub6(t, t, PL);
+  memcpy(r->l, t, 48);
+}
+static void fp_sqr(fp* r, const fp* a) { fp_mul(r, a, a); }
+static int fp_is_zero(const fp* a) { uint64_t o = 0; for (int i = 0; i < 6; ++i) o |= a->l[i]; return o == 0; }
+static int fp_eq(const fp* a, const fp* b) { return memcmp(a->l, b->l, 48) == 0; }
+static void fp_pow(fp* r, const fp* a, const uint64_t* e, int nl) {
+  fp acc = FP_ONE, base = *a;
+  for (int i = 64 * nl - 1; i >= 0; --i) {
+    fp_sqr(&acc, &acc);
+    if ((e[i >> 6] >> (i & 63)) & 1) fp_mul(&acc, &acc, &base);
+  }
+  *r = acc;
+}
+static void fp_to_mont(fp* r, const uint64_t* canon);
+static void fp_from_mont(uint64_t* canon, const fp* a);
+static void fp_inv_fermat(fp* r, const fp* a) { fp_pow(r, a, E_PM2, 6); }  /* inv(0) = 0 */
+/* binary extended Euclid on the canonical value: u = a, v = p, x1 = 1, x2 = 0; invariant
+ * x1 * a = u, x2 * a = v (mod p).  Result converted back to Montgomery form. */
+static void half_mod(uint64_t* x) {
+  uint64_t c = 0;
+  if (x[0] & 1) c = add6(x, x, PL);
+  for (int i = 0; i < 6; ++i) x[i] = (x[i] >> 1) | (i < 5 ? x[i + 1] << 63 : c << 63);
+}
+static void fp_inv(fp* r, const fp* a) {
+  if (fp_is_zero(a)) { *r = *a; return; }
+  uint64_t u[6], v[6], x1[6] = {1, 0, 0, 0, 0, 0}, x2[6] = {0};
+  fp_from_mont(u, a);
+  memcpy(v, PL, 48);
+  static const uint64_t ONE6[6] = {1, 0, 0, 0, 0, 0};
+  while (cmp6(u, ONE6) != 0 && cmp6(v, ONE6) != 0) {
+    while (!(u[0] & 1)) { for (int i = 0; i < 6; ++i) u[i] = (u[i] >> 1) | (i < 5 ? u[i + 1] << 63 : 0); half_mod(x1); }
+    while (!(v[0] & 1)) { for (int i = 0; i < 6; ++i) v[i] = (v[i] >> 1) | (i < 5 ? v[i + 1] << 63 : 0); half_mod(x2); }
+    if (cmp6(u, v) >= 0) { sub6(u, u, v); if (sub6(x1, x1, x2)) add6(x1, x1, PL); }
+    else { sub6(v, v, u); if (sub6(x2, x2, x1)) add6(x2, x2, PL); }
+  }
+  /* canonical inverse (< p) -> Montgomery: x * R2 * R^-1 = x R */
+  fp_to_mont(r, cmp6(u, ONE6) == 0 ? x1 : x2);
+}
+static int fp_sqrt(fp* r, const fp* a) {
+  fp s, c;
+  fp_pow(&s, a, E_SQRT, 6);
+  fp_sqr(&c, &s);
+  if (!fp_eq(&c, a)) return 0;
+  *r = s;
+  return 1;
+}
+static void fp_to_mont(fp* r, const uint64_t* canon) { fp t; memcpy(t.l, canon, 48); fp_mul(r, &t, &FP_R2); }
+static void fp_from_mont(uint64_t* canon, const fp* a) {
+  fp one = {{1, 0, 0, 0, 0, 0}}, t;
+  fp_mul(&t, a, &one);
+  memcpy(canon, t.l, 48);
+}
+static void fp_from_u64(fp* r, uint64_t v) { uint64_t c[6] = {v, 0, 0, 0, 0, 0}; fp_to_mont(r, c); }
+static int fp_is_lex_largest(const fp* a) { uint64_t c[6]; fp_from_mont(c, a); return cmp6(c, E_HALF) > 0; }
+static int fp_sgn0(const fp* a) { uint64_t c[6]; fp_from_mont(c, a); return (int)(c[0] & 1); }
+/* big-endian 48 bytes -> canonical limbs; returns 0 if >= p */
+static int be48_to_limbs(uint64_t* l, const uint8_t* b) {
+  for (int i = 0; i < 6; ++i) {
+    uint64_t v = 0;
+    for (int k = 0; k < 8; ++k) v = (v << 8) | b[(5 - i) * 8 + k];
+    l[i] = v;
+  }
+  return cmp6(l, PL) < 0;
+}
+static void limbs_to_be48(uint8_t* b, const uint64_t* l) {
+  for (int i = 0; i < 6; ++i)
+    for (int k = 0; k < 8; ++k) b[(5 - i) * 8 + k] = (uint8_t)(l[i] >> (56 - 8 * k));
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fp2 = Fp[u]/(u^2 + 1)                                                                       */
+/* ------------------------------------------------------------------------------------------ */
+static fp2 F2_ZERO, F2_ONE;
+static void f2_add(fp2* r, const fp2* a, const fp2* b) { fp_add(&r->c0, &a->c0, &b->c0); fp_add(&r->c1, &a->c1, &b->c1); }
+static void f2_sub(fp2* r, const fp2* a, const fp2* b) { fp_sub(&r->c0, &a->c0, &b->c0); fp_sub(&r->c1, &a->c1, &b->c1); }
+static void f2_neg(fp2* r, const fp2* a) { fp_neg(&r->c0, &a->c0); fp_neg(&r->c1, &a->c1); }
+static void f2_conj(fp2* r, const fp2* a) { r->c0 = a->c0; fp_neg(&r->c1, &a->c1); }
+static void f2_mul(fp2* r, const fp2* a, const fp2* b) {
+  fp t0, t1, t2, s0, s1;
+  fp_mul(&t0, &a->c0, &b->c0);
+  fp_mul(&t1, &a->c1, &b->c1);
+  fp_add(&s0, &a->c0, &a->c1);
+  fp_add(&s1, &b->c0, &b->c1);
+  fp_mul(&t2, &s0, &s1);
+  fp_sub(&r->c0, &t0, &t1);
+  fp_sub(&t2, &t2, &t0);
+  fp_sub(&r->c1, &t2, &t1);
+}
+static void f2_sqr(fp2* r, const fp2* a) { f2_mul(r, a, a); }
+static void f2_mul_fp(fp2* r, const fp2* a, const fp* b) { fp_mul(&r->c0, &a->c0, b); fp_mul(&r->c1, &a->c1, b); }
+static void f2_mul_xi(fp2* r, const fp2* a) {  /* (a0 + a1 u)(1 + u) */
+  fp t0, t1;
+  fp_sub(&t0, &a->c0, &a->c1);
+  fp_add(&t1, &a->c0, &a->c1);
+  r->c0 = t0; r->c1 = t1;
+}
+static int f2_is_zero(const fp2* a) { return fp_is_zero(&a->c0) && fp_is_zero(&a->c1); }
+static int f2_eq(const fp2* a, const fp2* b) { return fp_eq(&a->c0, &b->c0) && fp_eq(&a->c1, &b->c1); }
+static void f2_inv(fp2* r, const fp2* a) {
+  fp n, t;
+  fp_sqr(&n, &a->c0); fp_sqr(&t, &a->c1); fp_add(&n, &n, &t);
+  fp_inv(&n, &n);
+  fp_mul(&r->c0, &a->c0, &n);
+  fp_mul(&t, &a->c1, &n); fp_neg(&r->c1, &t);
+}
+static void f2_pow(fp2* r, const fp2* a, const uint64_t* e, int nl) {
+  fp2 acc = F2_ONE, base = *a;
+  for (int i = 64 * nl - 1; i >= 0; --i) {
+    f2_sqr(&acc, &acc);
+    if ((e[i >> 6] >> (i & 63)) & 1) f2_mul(&acc, &acc, &base);
+  }
+  *r = acc;
+}
+/* a square root of a (any of the two), or 0: the norm method of oracle/bls12_381.py:f2_sqrt */
+static int f2_sqrt(fp2* r, const fp2* a) {
+  if (f2_is_zero(a)) { *r = F2_ZERO; return 1; }
+  if (fp_is_zero(&a->c1)) {
+    fp s;
+    if (fp_sqrt(&s, &a->c0)) { r->c0 = s; r->c1 = FP_ZERO; return 1; }
+    fp na; fp_neg(&na, &a->c0);
+    if (!fp_sqrt(&s, &na)) return 0;
+    r->c0 = FP_ZERO; r->c1 = s; return 1;
+  }
+  fp n, t, s, c, x0, inv2, two;
+  fp_sqr(&n, &a->c0); fp_sqr(&t, &a->c1); fp_add(&n, &n, &t);
+  if (!fp_sqrt(&s, &n)) return 0;
+  fp_from_u64(&two, 2); fp_inv(&inv2, &two);
+  fp_add(&c, &a->c0, &s); fp_mul(&c, &c, &inv2);
+  if (!fp_sqrt(&x0, &c)) {
+    fp_sub(&c, &a->c0, &s); fp_mul(&c, &c, &inv2);
+    if (!fp_sqrt(&x0, &c)) return 0;
+  }
+  fp d; fp_add(&d, &x0, &x0); fp_inv(&d, &d);
+  fp2 rr; rr.c0 = x0; fp_mul(&rr.c1, &a->c1, &d);
+  fp2 chk; f2_sqr(&chk, &rr);
+  if (!f2_eq(&chk, a)) return 0;
+  *r = rr;
+  return 1;
+}
+static int f2_sgn0(const fp2* a) {
+  int s0 = fp_sgn0(&a->c0), z0 = fp_is_zero(&a->c0), s1 = fp_sgn0(&a->c1);
+  return s0 | (z0 & s1);
+}
+static int f2_is_lex_largest(const fp2* a) {
+  if (!fp_is_zero(&a->c1)) return fp_is_lex_largest(&a->c1);
+  return fp_is_lex_largest(&a->c0);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fp6 = Fp2[v]/(v^3 - xi), Fp12 = Fp6[w]/(w^2 - v), xi = 1 + u                                */
+/* ------------------------------------------------------------------------------------------ */
+static void f6_add(fp6* r, const fp6* a, const fp6* b) { f2_add(&r->c0, &a->c0, &b->c0); f2_add(&r->c1, &a->c1, &b->c1); f2_add(&r->c2, &a->c2, &b->c2); }
+static void f6_sub(fp6* r, const fp6* a, const fp6* b) { f2_sub(&r->c0, &a->c0, &b->c0); f2_sub(&r->c1, &a->c1, &b->c1); f2_sub(&r->c2, &a->c2, &b->c2); }
+static void f6_neg(fp6* r, const fp6* a) { f2_neg(&r->c0, &a->c0); f2_neg(&r->c1, &a->c1); f2_neg(&r->c2, &a->c2); }
+static void f6_mul(fp6* r, const fp6* a, const fp6* b) {  /* Karatsuba (6 Fp2 products), v^3 = xi */
+  fp2 v0, v1, v2, t0, t1, c0, c1, c2;
+  f2_mul(&v0, &a->c0, &b->c0);
+  f2_mul(&v1, &a->c1, &b->c1);
+  f2_mul(&v2, &a->c2, &b->c2);
+  f2_add(&t0, &a->c1, &a->c2); f2_add(&t1, &b->c1, &b->c2); f2_mul(&c0, &t0, &t1);
+  f2_sub(&c0, &c0, &v1); f2_sub(&c0, &c0, &v2); f2_mul_xi(&c0, &c0); f2_add(&c0, &c0, &v0);
+  f2_add(&t0, &a->c0, &a->c1); f2_add(&t1, &b->c0, &b->c1); f2_mul(&c1, &t0, &t1);
+  f2_sub(&c1, &c1, &v0); f2_sub(&c1, &c1, &v1); f2_mul_xi(&t0, &v2); f2_add(&c1, &c1, &t0);
+  f2_add(&t0, &a->c0, &a->c2); f2_add(&t1, &b->c0, &b->c2); f2_mul(&c2, &t0, &t1);
+  f2_sub(&c2, &c2, &v0); f2_sub(&c2, &c2, &v2); f2_add(&c2, &c2, &v1);
+  r->c0 = c0; r->c1 = c1; r->c2 = c2;
+}
+static void f6_mul_v(fp6* r, const fp6* a) { fp2 t; f2_mul_xi(&t, &a->c2); r->c2 = a->c1; r->c1 = a->c0; r->c0 = t; }
+static void f6_inv(fp6* r, const fp6* a) {
+  fp2 t0, t1, t2, t, d;
+  f2_sqr(&t0, &a->c0); f2_mul(&t, &a->c1, &a->c2); f2_mul_xi(&t, &t); f2_sub(&t0, &t0, &t);
+  f2_sqr(&t1, &a->c2); f2_mul_xi(&t1, &t1); f2_mul(&t, &a->c0, &a->c1); f2_sub(&t1, &t1, &t);
+  f2_sqr(&t2, &a->c1); f2_mul(&t, &a->c0, &a->c2); f2_sub(&t2, &t2, &t);
+  f2_mul(&d, &a->c0, &t0);
+  f2_mul(&t, &a->c2, &t1); f2_mul_xi(&t, &t); f2_add(&d, &d, &t);
+  f2_mul(&t, &a->c1, &t2); f2_mul_xi(&t, &t); f2_add(&d, &d, &t);
+  f2_inv(&d, &d);
+  f2_mul(&r->c0, &t0, &d); f2_mul(&r->c1, &t1, &d); f2_mul(&r->c2, &t2, &d);
+}
+static fp12 F12_ONE;
+static void f12_mul(fp12* r, const fp12* a, const fp12* b) {
+  fp6 t0, t1, t2, s0, s1;
+  f6_mul(&t0, &a->c0, &b->c0);
+  f6_mul(&t1, &a->c1, &b->c1);
+  f6_add(&s0, &a->c0, &a->c1);
+  f6_add(&s1, &b->c0, &b->c1);
+  f6_mul(&t2, &s0, &s1);
+  f6_sub(&t2, &t2, &t0); f6_sub(&r->c1, &t2, &t1);
+  f6_mul_v(&t1, &t1); f6_add(&r->c0, &t0, &t1);
+}
+static void f12_sqr(fp12* r, const fp12* a) {  /* complex squaring: (a0 + a1 w)^2, w^2 = v */
+  fp6 t0, t1, t2;
+  f6_mul(&t0, &a->c0, &a->c1);
+  f6_add(&t1, &a->c0, &a->c1);
+  f6_mul_v(&t2, &a->c1); f6_add(&t2, &a->c0, &t2);
+  f6_mul(&t1, &t1, &t2);
+  f6_sub(&t1, &t1, &t0);
+  f6_mul_v(&t2, &t0); f6_sub(&r->c0, &t1, &t2);
+  f6_add(&r->c1, &t0, &t0);
+}
+static void f12_conj(fp12* r, const fp12* a) { r->c0 = a->c0; f6_neg(&r->c1, &a->c1); }
+static void f12_inv(fp12* r, const fp12* a) {
+  fp6 t0, t1;
+  f6_mul(&t0, &a->c0, &a->c0);
+  f6_mul(&t1, &a->c1, &a->c1); f6_mul_v(&t1, &t1);
+  f6_sub(&t0, &t0, &t1);
+  f6_inv(&t0, &t0);
+  f6_mul(&r->c0, &a->c0, &t0);
+  f6_mul(&t1, &a->c1, &t0); f6_neg(&r->c1, &t1);
+}
+static int f12_is_one(const fp12* a) {
+  return f2_eq(&a->c0.c0, &F2_ONE) && f2_is_zero(&a->c0.c1) && f2_is_zero(&a->c0.c2) &&
+         f2_is_zero(&a->c1.c0) && f2_is_zero(&a->c1.c1) && f2_is_zero(&a->c1.c2);
+}
+/* Frobenius: a = sum_k a_k w^k (a_k in Fp2; w^0,w^2,w^4 = c0 slots, w^1,w^3,w^5 = c1 slots);
+ * a^p = sum_k conj(a_k) xi^(k (p-1)/6) w^k */
+static fp2 GAMMA[6];
+static fp2* wslot(fp12* a, int k) {
+  fp6* h = (k & 1) ? &a->c1 : &a->c0;
+  int i = k >> 1;
+  return i == 0 ? &h->c0 : (i == 1 ? &h->c1 : &h->c2);
+}
+static void f12_frob(fp12* r, const fp12* a) {
+  fp12 t = *a;
+  for (int k = 0; k < 6; ++k) { fp2* s = wslot(&t, k); fp2 c; f2_conj(&c, s); f2_mul(s, &c, &GAMMA[k]); }
+  *r = t;
+}
+static void f12_pow(fp12* r, const fp12* a, const uint64_t* e, int nl) {
+  fp12 acc = F12_ONE, base = *a;
+  int started = 0;
+  for (int i = 64 * nl - 1; i >= 0; --i) {
+    if (started) f12_sqr(&acc, &acc);
+    if ((e[i >> 6] >> (i & 63)) & 1) { f12_mul(&acc, &acc, &base); started = 1; }
+  }
+  *r = acc;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Curves in Jacobian coordinates: E1: y^2 = x^3 + 4 over Fp, E2: y^2 = x^3 + 4(1+u) over Fp2  */
+/* (complete with the doubling / opposite / infinity special cases)                            */
+/* ------------------------------------------------------------------------------------------ */
+#define DEFINE_CURVE(P, F, ADD, SUB, MUL, SQR, ISZ, EQ, INV, ONE, ZERO)                             \
+  typedef struct { F x, y; int inf; } P##_aff;                                                     \
+  typedef struct { F x, y, z; } P##_jac;                                                           \
+  static void P##_set_inf(P##_jac* r) { r->x = ONE; r->y = ONE; r->z = ZERO; }                     \
+  static int P##_is_inf(const P##_jac* p) { return ISZ(&p->z); }                                   \
+  static void P##_from_aff(P##_jac* r, const P##_aff* a) {                                         \
+    if (a->inf) { P##_set_inf(r); return; }                                                        \
+    r->x = a->x; r->y = a->y; r->z = ONE;                                                           \
+  }                                                                                                \
+  static void P##_dbl(P##_jac* r, const P##_jac* p) {                                              \
+    F A, B, C, D, E, G, t, x3, y3, z3;                                                             \
+    SQR(&A, &p->x); SQR(&B, &p->y); SQR(&C, &B);                                                   \
+    ADD(&t, &p->x, &B); SQR(&t, &t); SUB(&t, &t, &A); SUB(&t, &t, &C); ADD(&D, &t, &t);             \
+    ADD(&E, &A, &A); ADD(&E, &E, &A); SQR(&G, &E);                                                 \
+    ADD(&t, &D, &D); SUB(&x3, &G, &t);                                                             \
+    MUL(&z3, &p->y, &p->z); ADD(&z3, &z3, &z3);                                                    \
+    SUB(&t, &D, &x3); MUL(&y3, &E, &t);                                                            \
+    ADD(&C, &C, &C); ADD(&C, &C, &C); ADD(&C, &C, &C); SUB(&y3, &y3, &C);                           \
+    r->x = x3; r->y = y3; r->z = z3;                                                               \
+  }                                                                                                \
+  static void P##_add(P##_jac* r, const P##_jac* p, const P##_jac* q) {                            \
+    if (P##_is_inf(p)) { *r = *q; return; }                                                        \
+    if (P##_is_inf(q)) { *r = *p; return; }                                                        \
+    F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t, x3, y3, z3;                                    \
+    SQR(&z1z1, &p->z); SQR(&z2z2, &q->z);                                                          \
+    MUL(&u1, &p->x, &z2z2); MUL(&u2, &q->x, &z1z1);                                                \
+    MUL(&s1, &p->y, &q->z); MUL(&s1, &s1, &z2z2);                                                  \
+    MUL(&s2, &q->y, &p->z); MUL(&s2, &s2, &z1z1);                                                  \
+    SUB(&h, &u2, &u1); SUB(&rr, &s2, &s1);                                                         \
+    if (ISZ(&h)) { if (ISZ(&rr)) P##_dbl(r, p); else P##_set_inf(r); return; }                      \
+    ADD(&rr, &rr, &rr);                                                                            \
+    ADD(&i, &h, &h); SQR(&i, &i); MUL(&j, &h, &i); MUL(&v, &u1, &i);                               \
+    SQR(&x3, &rr); SUB(&x3, &x3, &j); ADD(&t, &v, &v); SUB(&x3, &x3, &t);                           \
+    SUB(&t, &v, &x3); MUL(&y3, &rr, &t); MUL(&t, &s1, &j); ADD(&t, &t, &t); SUB(&y3, &y3, &t);      \
+    ADD(&z3, &p->z, &q->z); SQR(&z3, &z3); SUB(&z3, &z3, &z1z1); SUB(&z3, &z3, &z2z2);              \
+    MUL(&z3, &z3, &h);                                                                             \
+    r->x = x3; r->y = y3; r->z = z3;                                                               \
+  }                                                                                                \
+  static void P##_neg(P##_jac* r, const P##_jac* p) { r->x = p->x; SUB(&r->y, &ZERO, &p->y); r->z = p->z; } \
+  static void P##_to_aff(P##_aff* r, const P##_jac* p) {                                           \
+    if (P##_is_inf(p)) { r->x = ZERO; r->y = ZERO; r->inf = 1; return; }                            \
+    F zi, zi2, zi3;                                                                                \
+    INV(&zi, &p->z); SQR(&zi2, &zi); MUL(&zi3, &zi2, &zi);                                        \
+    MUL(&r->x, &p->x, &zi2); MUL(&r->y, &p->y, &zi3); r->inf = 0;                                  \
+  }                                                                                                \
+  /* [k]P, k as little-endian 64-bit limbs, binary MSB first */                                    \
+  static void P##_mul(P##_jac* r, const P##_jac* p, const uint64_t* k, int nl) {                   \
+    P##_jac acc; P##_set_inf(&acc);                                                                \
+    for (int i = 64 * nl - 1; i >= 0; --i) {                                                       \
+      P##_dbl(&acc, &acc);                                                                         \
+      if ((k[i >> 6] >> (i & 63)) & 1) P##_add(&acc, &acc, p);                                     \
+    }                                                                                              \
+    *r = acc;                                                                                      \
+  }                                                                                                \
+  static int P##_eq(const P##_jac* a, const P##_jac* b) { /* projective equality */                \
+    if (P##_is_inf(a) || P##_is_inf(b)) return P##_is_inf(a) && P##_is_inf(b);                    \
+    F za, zb, t1, t2;                                                                              \
+    SQR(&za, &a->z); SQR(&zb, &b->z);                                                              \
+    MUL(&t1, &a->x, &zb); MUL(&t2, &b->x, &za); if (!EQ(&t1, &t2)) return 0;                        \
+    MUL(&za, &za, &a->z); MUL(&zb, &zb, &b->z);                                                    \
+    MUL(&t1, &a->y, &zb); MUL(&t2, &b->y, &za); return EQ(&t1, &t2);                               \
+  }
+
+DEFINE_CURVE(g1, fp, fp_add, fp_sub, fp_mul, fp_sqr, fp_is_zero, fp_eq, fp_inv, FP_ONE, FP_ZERO)
+DEFINE_CURVE(g2, fp2, f2_add, f2_sub, f2_mul, f2_sqr, f2_is_zero, f2_eq, f2_inv, F2_ONE, F2_ZERO)
+
+static const uint64_t X_ABS = 0xd201000000010000ULL;  /* x = -X_ABS */
+static fp B1;          /* 4 */
+static fp2 B2;         /* 4(1 + u) */
+static fp2 PSI_CX, PSI_CY;
+static g1_aff G1_GEN;
+
+static void g2_psi(g2_jac* r, const g2_jac* p) {  /* on Jacobian coordinates: (conj(X) cx, conj(Y) cy, conj(Z)) */
+  fp2 t;
+  f2_conj(&t, &p->x); f2_mul(&r->x, &t, &PSI_CX);
+  f2_conj(&t, &p->y); f2_mul(&r->y, &t, &PSI_CY);
+  f2_conj(&r->z, &p->z);
+}
+static void g2_mul_x(g2_jac* r, const g2_jac* p) {  /* [x]P, x < 0 */
+  uint64_t k[1] = {X_ABS};
+  g2_mul(r, p, k, 1);
+  g2_neg(r, r);
+}
+static int g2_in_subgroup(const g2_aff* a) {  /* psi(P) == [x]P */
+  if (a->inf) return 1;
+  g2_jac p, xp, ps;
+  g2_from_aff(&p, a);
+  g2_mul_x(&xp, &p);
+  g2_psi(&ps, &p);
+  return g2_eq(&xp, &ps);
+}
+
+/* ---- ZCash serialisation (blst *_compress / *_uncompress) ---- */
+static int g1_decompress(g1_aff* r, const uint8_t* b) {
+  uint8_t b0 = b[0];
+  if (!(b0 & 0x80)) return 0;
+  if (b0 & 0x40) {
+    if (b0 & 0x3f) return 0;
+    for (int i = 1; i < 48; ++i) if (b[i]) return 0;
+    r->inf = 1; r->x = FP_ZERO; r->y = FP_ZERO; return 1;
+  }
+  uint8_t t[48]; memcpy(t, b, 48); t[0] &= 0x1f;
+  uint64_t l[6];
+  if (!be48_to_limbs(l, t)) return 0;
+  fp x, y, rhs;
+  fp_to_mont(&x, l);
+  fp_sqr(&rhs, &x); fp_mul(&rhs, &rhs, &x); fp_add(&rhs, &rhs, &B1);
+  if (!fp_sqrt(&y, &rhs)) return 0;
+  if (fp_is_lex_largest(&y) != !!(b0 & 0x20)) fp_neg(&y, &y);
+  r->x = x; r->y = y; r->inf = 0;
+  return 1;
+}
+static int g2_decompress(g2_aff* r, const uint8_t* b) {
+  uint8_t b0 = b[0];
+  if (!(b0 & 0x80)) return 0;
+  if (b0 & 0x40) {
+    if (b0 & 0x3f) return 0;
+    for (int i = 1; i < 96; ++i) if (b[i]) return 0;
+    r->inf = 1; r->x = F2_ZERO; r->y = F2_ZERO; return 1;
+  }
+  uint8_t t[48]; memcpy(t, b, 48); t[0] &= 0x1f;
+  uint64_t l1[6], l0[6];
+  if (!be48_to_limbs(l1, t) || !be48_to_limbs(l0, b + 48)) return 0;
+  fp2 x, y, rhs;
+  fp_to_mont(&x.c0, l0); fp_to_mont(&x.c1, l1);
+  f2_sqr(&rhs, &x); f2_mul(&rhs, &rhs, &x); f2_add(&rhs, &rhs, &B2);
+  if (!f2_sqrt(&y, &rhs)) return 0;
+  if (f2_is_lex_largest(&y) != !!(b0 & 0x20)) f2_neg(&y, &y);
+  r->x = x; r->y = y; r->inf = 0;
+  return 1;
+}
+static void g2_compress(uint8_t* out, const g2_aff* a) {
+  if (a->inf) { memset(out, 0, 96); out[0] = 0xc0; return; }
+  uint64_t l[6];
+  fp_from_mont(l, &a->x.c1); limbs_to_be48(out, l);
+  fp_from_mont(l, &a->x.c0); limbs_to_be48(out + 48, l);
+  out[0] |= 0x80;
+  if (f2_is_lex_largest(&a->y)) out[0] |= 0x20;
+}
+static void g2_serialize(uint8_t* out, const g2_aff* a) {
+  if (a->inf) { memset(out, 0, 192); out[0] = 0x40; return; }
+  uint64_t l[6];
+  fp_from_mont(l, &a->x.c1); limbs_to_be48(out, l);
+  fp_from_mont(l, &a->x.c0); limbs_to_be48(out + 48, l);
+  fp_from_mont(l, &a->y.c1); limbs_to_be48(out + 96, l);
+  fp_from_mont(l, &a->y.c0); limbs_to_be48(out + 144, l);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SHA-256 (FIPS 180-4) and expand_message_xmd (RFC 9380 §5.3.1)                               */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { uint32_t h[8]; uint8_t buf[64]; uint64_t len; size_t fill; } sha256;
+static const uint32_t SK[64] = {
+  0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98, 0x12835b01,
+  0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc,
+  0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147,
+  0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+  0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116, 0x1e376c08,
+  0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208,
+  0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+#define ROR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+static void sha_block(sha256* s, const uint8_t* p) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; ++i) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+  for (int i = 16; i < 64; ++i) {
+    uint32_t s0 = ROR(w[i - 15], 7) ^ ROR(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = ROR(w[i - 2], 17) ^ ROR(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = s->h[0], b = s->h[1], c = s->h[2], d = s->h[3], e = s->h[4], f = s->h[5], g = s->h[6], h = s->h[7];
+  for (int i = 0; i < 64; ++i) {
+    uint32_t t1 = h + (ROR(e, 6) ^ ROR(e, 11) ^ ROR(e, 25)) + ((e & f) ^ (~e & g)) + SK[i] + w[i];
+    uint32_t t2 = (ROR(a, 2) ^ ROR(a, 13) ^ ROR(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  s->h[0] += a; s->h[1] += b; s->h[2] += c; s->h[3] += d; s->h[4] += e; s->h[5] += f; s->h[6] += g; s->h[7] += h;
+}
+static void sha_init(sha256* s) {
+  static const uint32_t H0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  memcpy(s->h, H0, 32); s->len = 0; s->fill = 0;
+}
+static void sha_update(sha256* s, const uint8_t* p, size_t n) {
+  s->len += n;
+  while (n) {
+    size_t k = 64 - s->fill < n ? 64 - s->fill : n;
+    memcpy(s->buf + s->fill, p, k); s->fill += k; p += k; n -= k;
+    if (s->fill == 64) { sha_block(s, s->buf); s->fill = 0; }
+  }
+}
+static void sha_final(sha256* s, uint8_t* out) {
+  uint64_t bits = s->len * 8;
+  uint8_t pad = 0x80, z = 0;
+  sha_update(s, &pad, 1);
+  while (s->fill != 56) sha_update(s, &z, 1);
+  uint8_t lb[8];
+  for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
+  sha_update(s, lb, 8);
+  for (int i = 0; i < 8; ++i) { out[4 * i] = s->h[i] >> 24; out[4 * i + 1] = s->h[i] >> 16; out[4 * i + 2] = s->h[i] >> 8; out[4 * i + 3] = s->h[i]; }
+}
+static void expand_message_xmd(uint8_t* out, size_t len, const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen) {
+  const size_t ell = (len + 31) / 32;
+  uint8_t b0[32], bi[32], zeros[64] = {0}, lib[3] = {(uint8_t)(len >> 8), (uint8_t)len, 0}, dl = (uint8_t)dlen;
+  sha256 s;
+  sha_init(&s); sha_update(&s, zeros, 64); sha_update(&s, msg, mlen); sha_update(&s, lib, 3);
+  sha_update(&s, dst, dlen); sha_update(&s, &dl, 1); sha_final(&s, b0);
+  uint8_t one = 1;
+  sha_init(&s); sha_update(&s, b0, 32); sha_update(&s, &one, 1); sha_update(&s, dst, dlen); sha_update(&s, &dl, 1); sha_final(&s, bi);
+  for (size_t i = 1; i <= ell; ++i) {
+    size_t k = (i - 1) * 32, n = len - k < 32 ? len - k : 32;
+    memcpy(out + k, bi, n);
+    if (i == ell) break;
+    uint8_t x[32], idx = (uint8_t)(i + 1);
+    for (int j = 0; j < 32; ++j) x[j] = b0[j] ^ bi[j];
+    sha_init(&s); sha_update(&s, x, 32); sha_update(&s, &idx, 1); sha_update(&s, dst, dlen); sha_update(&s, &dl, 1); sha_final(&s, bi);
+  }
+}
+/* 64 big-endian bytes mod p -> Montgomery: value = hi * 2^256 + lo, reduced via R2 */
+static void fp_from_be64(fp* r, const uint8_t* b) {
+  uint8_t t[48];
+  uint64_t hi[6], lo[6];
+  memset(t, 0, 48); memcpy(t + 16, b, 32); be48_to_limbs(hi, t);       /* < 2^256 < p */
+  memset(t, 0, 48); memcpy(t + 16, b + 32, 32); be48_to_limbs(lo, t);
+  fp h, l, s256;
+  fp_to_mont(&h, hi); fp_to_mont(&l, lo);
+  uint64_t c256[6] = {0, 0, 0, 0, 1, 0};  /* 2^256 */
+  fp_to_mont(&s256, c256);
+  fp_mul(&h, &h, &s256); fp_add(r, &h, &l);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* hash_to_G2: SSWU on E2' (A' = 240u, B' = 1012(1+u), Z = -(2+u)), 3-isogeny, h_eff clearing  */
+/* ------------------------------------------------------------------------------------------ */
+static fp2 SSWU_A, SSWU_B, SSWU_Z;
+static fp2 ISO_XNUM[4], ISO_XDEN[3], ISO_YNUM[4], ISO_YDEN[4];
+static const char* ISO_HEX[15][2] = {
+  {"5c759507e8e333ebb5b7a9a47d7ed8532c52d39fd3a042a88b58423c50ae15d5c2638e343d9c71c6238aaaaaaaa97d6",
+   "5c759507e8e333ebb5b7a9a47d7ed8532c52d39fd3a042a88b58423c50ae15d5c2638e343d9c71c6238aaaaaaaa97d6"},
+  {"0", "11560bf17baa99bc32126fced787c88f984f87adf7ae0c7f9a208c6b4f20a4181472aaa9cb8d555526a9ffffffffc71a"},
+  {"11560bf17baa99bc32126fced787c88f984f87adf7ae0c7f9a208c6b4f20a4181472aaa9cb8d555526a9ffffffffc71e",
+   "8ab05f8bdd54cde190937e76bc3e447cc27c3d6fbd7063fcd104635a790520c0a395554e5c6aaaa9354ffffffffe38d"},
+  {"171d6541fa38ccfaed6dea691f5fb614cb14b4e7f4e810aa22d6108f142b85757098e38d0f671c7188e2aaaaaaaa5ed1", "0"},
+  {"0", "1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaa63"},
+  {"c", "1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaa9f"},
+  {"1", "0"},
+  {"1530477c7ab4113b59a4c18b076d11930f7da5d4a07f649bf54439d87d27e500fc8c25ebf8c92f6812cfc71c71c6d706",
+   "1530477c7ab4113b59a4c18b076d11930f7da5d4a07f649bf54439d87d27e500fc8c25ebf8c92f6812cfc71c71c6d706"},
+  {"0", "5c759507e8e333ebb5b7a9a47d7ed8532c52d39fd3a042a88b58423c50ae15d5c2638e343d9c71c6238aaaaaaaa97be"},
+  {"11560bf17baa99bc32126fced787c88f984f87adf7ae0c7f9a208c6b4f20a4181472aaa9cb8d555526a9ffffffffc71c",
+   "8ab05f8bdd54cde190937e76bc3e447cc27c3d6fbd7063fcd104635a790520c0a395554e5c6aaaa9354ffffffffe38f"},
+  {"124c9ad43b6cf79bfbf7043de3811ad0761b0f37a1e26286b0e977c69aa274524e79097a56dc4bd9e1b371c71c718b10", "0"},
+  {"1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffa8fb",
+   "1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffa8fb"},
+  {"0", "1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffa9d3"},
+  {"12", "1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaa99"},
+  {"1", "0"}};
+static void hex_to_limbs(uint64_t* l, const char* h) {
+  memset(l, 0, 48);
+  size_t n = strlen(h);
+  for (size_t i = 0; i < n; ++i) {
+    char c = h[n - 1 - i];
+    uint64_t v = (c >= '0' && c <= '9') ? (uint64_t)(c - '0') : (uint64_t)((c | 32) - 'a' + 10);
+    l[i / 16] |= v << (4 * (i % 16));
+  }
+}
+static void fp_from_hex(fp* r, const char* h) { uint64_t l[6]; hex_to_limbs(l, h); fp_to_mont(r, l); }
+static void f2_poly(fp2* r, const fp2* c, int n, const fp2* x) {
+  fp2 acc = F2_ZERO;
+  for (int i = n - 1; i >= 0; --i) { f2_mul(&acc, &acc, x); f2_add(&acc, &acc, &c[i]); }
+  *r = acc;
+}
+static void map_to_curve_sswu(fp2* xo, fp2* yo, const fp2* u) {
+  fp2 zu2, den, x1, t, gx, y, x;
+  f2_sqr(&t, u); f2_mul(&zu2, &SSWU_Z, &t);
+  f2_sqr(&den, &zu2); f2_add(&den, &den, &zu2);
+  if (f2_is_zero(&den)) {
+    f2_mul(&t, &SSWU_Z, &SSWU_A); f2_inv(&t, &t); f2_mul(&x1, &SSWU_B, &t);
+  } else {
+    fp2 nb, ia, id;
+    f2_neg(&nb, &SSWU_B); f2_inv(&ia, &SSWU_A); f2_inv(&id, &den);
+    f2_add(&id, &F2_ONE, &id);
+    f2_mul(&x1, &nb, &ia); f2_mul(&x1, &x1, &id);
+  }
+#define GX(r, x) do { fp2 x2_; f2_sqr(&x2_, x); f2_mul(&x2_, &x2_, x); fp2 ax_; f2_mul(&ax_, &SSWU_A, x); f2_add(&x2_, &x2_, &ax_); f2_add(r, &x2_, &SSWU_B); } while (0)
+  GX(&gx, &x1);
+  if (f2_sqrt(&y, &gx)) x = x1;
+  else { f2_mul(&x, &zu2, &x1); GX(&gx, &x); f2_sqrt(&y, &gx); }
+#undef GX
+  if (f2_sgn0(u) != f2_sgn0(&y)) f2_neg(&y, &y);
+  *xo = x; *yo = y;
+}
+static int iso3_map(g2_aff* r, const fp2* xp, const fp2* yp) {
+  fp2 xn, xd, yn, yd;
+  f2_poly(&xn, ISO_XNUM, 4, xp); f2_poly(&xd, ISO_XDEN, 3, xp);
+  f2_poly(&yn, ISO_YNUM, 4, xp); f2_poly(&yd, ISO_YDEN, 4, xp);
+  if (f2_is_zero(&xd) || f2_is_zero(&yd)) { r->inf = 1; return 0; }
+  f2_inv(&xd, &xd); f2_inv(&yd, &yd);
+  f2_mul(&r->x, &xn, &xd);
+  f2_mul(&yn, &yn, &yd); f2_mul(&r->y, yp, &yn);
+  r->inf = 0;
+  return 1;
+}
+static void clear_cofactor_g2(g2_jac* r, const g2_jac* p) {  /* [x^2-x-1]P + [x-1]psi(P) + psi^2(2P) */
+  g2_jac t1, t2, t3, n;
+  g2_mul_x(&t1, p);
+  g2_psi(&t2, p);
+  g2_dbl(&t3, p); g2_psi(&t3, &t3); g2_psi(&t3, &t3);
+  g2_neg(&n, &t2); g2_add(&t3, &t3, &n);
+  g2_add(&t2, &t1, &t2);
+  g2_mul_x(&t2, &t2);
+  g2_add(&t3, &t3, &t2);
+  g2_neg(&n, &t1); g2_add(&t3, &t3, &n);
+  g2_neg(&n, p); g2_add(r, &t3, &n);
+}
+static void hash_to_g2(g2_aff* out, const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen) {
+  uint8_t buf[256];
+  expand_message_xmd(buf, 256, msg, mlen, dst, dlen);
+  fp2 u[2];
+  for (int i = 0; i < 2; ++i) { fp_from_be64(&u[i].c0, buf + 128 * i); fp_from_be64(&u[i].c1, buf + 128 * i + 64); }
+  g2_jac q[2];
+  for (int i = 0; i < 2; ++i) {
+    fp2 x, y; g2_aff a;
+    map_to_curve_sswu(&x, &y, &u[i]);
+    iso3_map(&a, &x, &y);
+    g2_from_aff(&q[i], &a);
+  }
+  g2_jac s, h;
+  g2_add(&s, &q[0], &q[1]);
+  clear_cofactor_g2(&h, &s);
+  g2_to_aff(out, &h);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Pairing: Miller loop with affine tangent/chord lines on E'(Fp2), the line through the      */
+/* untwisted T evaluated at P and scaled by w^3 (an Fp4 factor the final exponentiation        */
+/* removes):  l = (lambda x_T - y_T) + (-lambda x_P) v + y_P v w.                              */
+/* Final exponentiation f^((p^12 - 1)/r) = ((f^(p^6-1))^(p^2+1))^((p^4-p^2+1)/r).              */
+/* ------------------------------------------------------------------------------------------ */
+static uint64_t E_HARD[20];  /* (p^4 - p^2 + 1)/r, 1269 bits */
+static void line_mul(fp12* f, const fp2* lam, const fp2* xt, const fp2* yt, const fp* xp, const fp* yp) {
+  fp12 l;
+  memset(&l, 0, sizeof l);
+  fp2 t;
+  f2_mul(&t, lam, xt); f2_sub(&l.c0.c0, &t, yt);
+  f2_mul_fp(&t, lam, xp); f2_neg(&l.c0.c1, &t);
+  l.c1.c1.c0 = *yp;
+  /* sparse product: l = (l0 + l1 v) + (l4 v) w */
+  fp6 b0, b1, t0, t1, s0;
+  const fp6* a0 = &f->c0; const fp6* a1 = &f->c1;
+  { /* t0 = a0 * (l0 + l1 v) */
+    fp2 v0, v1, u, q; f2_mul(&v0, &a0->c0, &l.c0.c0); f2_mul(&v1, &a0->c1, &l.c0.c1);
+    f2_add(&u, &a0->c1, &a0->c2); f2_mul(&q, &u, &l.c0.c1); f2_sub(&q, &q, &v1); f2_mul_xi(&q, &q); f2_add(&t0.c0, &q, &v0);
+    f2_add(&u, &a0->c0, &a0->c1); { fp2 w; f2_add(&w, &l.c0.c0, &l.c0.c1); f2_mul(&q, &u, &w); } f2_sub(&q, &q, &v0); f2_sub(&t0.c1, &q, &v1);
+    f2_mul(&q, &a0->c2, &l.c0.c0); f2_add(&t0.c2, &q, &v1);
+  }
+  { /* t1 = a1 * (l4 v): (c0, c1, c2) v = (xi c2, c0, c1) times l4 */
+    fp2 q; f2_mul(&q, &a1->c2, &l.c1.c1); f2_mul_xi(&t1.c0, &q);
+    f2_mul(&t1.c1, &a1->c0, &l.c1.c1); f2_mul(&t1.c2, &a1->c1, &l.c1.c1);
+  }
+  { /* (a0 + a1)(l0 + (l1 + l4) v) */
+    fp6 sa; f6_add(&sa, a0, a1);
+    fp2 m0 = l.c0.c0, m1; f2_add(&m1, &l.c0.c1, &l.c1.c1);
+    fp2 v0, v1, u, q; f2_mul(&v0, &sa.c0, &m0); f2_mul(&v1, &sa.c1, &m1);
+    f2_add(&u, &sa.c1, &sa.c2); f2_mul(&q, &u, &m1); f2_sub(&q, &q, &v1); f2_mul_xi(&q, &q); f2_add(&s0.c0, &q, &v0);
+    f2_add(&u, &sa.c0, &sa.c1); { fp2 w; f2_add(&w, &m0, &m1); f2_mul(&q, &u, &w); } f2_sub(&q, &q, &v0); f2_sub(&s0.c1, &q, &v1);
+    f2_mul(&q, &sa.c2, &m0); f2_add(&s0.c2, &q, &v1);
+  }
+  f6_sub(&b1, &s0, &t0); f6_sub(&b1, &b1, &t1);
+  f6_mul_v(&b0, &t1); f6_add(&b0, &b0, &t0);
+  f->c0 = b0; f->c1 = b1;
+}
+static void miller_loop(fp12* out, const g1_aff* P, const g2_aff* Q) {
+  if (P->inf || Q->inf) { *out = F12_ONE; return; }
+  fp12 f = F12_ONE;
+  fp2 xt = Q->x, yt = Q->y, lam, t, three, x3;
+  fp_from_u64(&three.c0, 3); three.c1 = FP_ZERO;
+  for (int i = 62; i >= 0; --i) {
+    f12_sqr(&f, &f);
+    /* tangent at T: lambda = 3 x^2 / (2 y) */
+    f2_sqr(&t, &xt); f2_mul(&lam, &t, &three);
+    f2_add(&t, &yt, &yt); f2_inv(&t, &t); f2_mul(&lam, &lam, &t);
+    line_mul(&f, &lam, &xt, &yt, &P->x, &P->y);
+    f2_sqr(&x3, &lam); f2_sub(&x3, &x3, &xt); f2_sub(&x3, &x3, &xt);
+    f2_sub(&t, &xt, &x3); f2_mul(&t, &lam, &t); f2_sub(&yt, &t, &yt); xt = x3;
+    if ((X_ABS >> i) & 1) {
+      /* chord through T and Q */
+      fp2 d;
+      f2_sub(&lam, &Q->y, &yt); f2_sub(&d, &Q->x, &xt); f2_inv(&d, &d); f2_mul(&lam, &lam, &d);
+      line_mul(&f, &lam, &xt, &yt, &P->x, &P->y);
+      f2_sqr(&x3, &lam); f2_sub(&x3, &x3, &xt); f2_sub(&x3, &x3, &Q->x);
+      f2_sub(&t, &xt, &x3); f2_mul(&t, &lam, &t); f2_sub(&yt, &t, &yt); xt = x3;
+    }
+  }
+  f12_conj(out, &f);  /* x < 0 */
+}
+static void final_exp_easy(fp12* a, const fp12* f) {
+  fp12 b;
+  f12_inv(a, f); f12_conj(&b, f); f12_mul(a, &b, a);    /* f^(p^6 - 1) */
+  f12_frob(&b, a); f12_frob(&b, &b); f12_mul(a, &b, a);  /* ^(p^2 + 1) */
+}
+/* textbook: f^((p^12 - 1)/r) */
+static void final_exp_slow(fp12* r, const fp12* f) {
+  fp12 a;
+  final_exp_easy(&a, f);
+  f12_pow(r, &a, E_HARD, 20);
+}
+/* a^x for a cyclotomic a (after the easy part): a^-|x| = conj(a^|x|) */
+static void cyc_pow_x(fp12* r, const fp12* a) {
+  uint64_t k[1] = {X_ABS};
+  fp12 t;
+  f12_pow(&t, a, k, 1);
+  f12_conj(r, &t);
+}
+/* f^(3 (p^12 - 1)/r): 3 (p^4 - p^2 + 1)/r = (x - 1)^2 (x + p) (x^2 + p^2 - 1) + 3 (Hayashida,
+ * Hayasaka, Teruya 2020).  The cube is a bijection on the order-r group, so the pairing check
+ * (== 1) is the same; final_exp_slow pins it in tests/test_oracle_c.py. */
+static void final_exp(fp12* r, const fp12* f) {
+  fp12 a, b, c, t, m;
+  final_exp_easy(&m, f);
+  f12_conj(&t, &m);                               /* m^-1 */
+  cyc_pow_x(&a, &m); f12_mul(&a, &a, &t);         /* m^(x-1) */
+  cyc_pow_x(&b, &a); f12_conj(&t, &a); f12_mul(&a, &b, &t);  /* m^((x-1)^2) */
+  cyc_pow_x(&b, &a); f12_frob(&t, &a); f12_mul(&b, &b, &t);  /* ^(x + p) */
+  cyc_pow_x(&c, &b); cyc_pow_x(&c, &c);           /* b^(x^2) */
+  f12_frob(&t, &b); f12_frob(&t, &t); f12_mul(&c, &c, &t);   /* * b^(p^2) */
+  f12_conj(&t, &b); f12_mul(&c, &c, &t);          /* * b^-1 */
+  f12_sqr(&t, &m); f12_mul(&t, &t, &m);           /* m^3 */
+  f12_mul(r, &c, &t);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fr (scalars, r = 0x73eda753...00000001), plain modular arithmetic on 4 x 64-bit limbs       */
+/* ------------------------------------------------------------------------------------------ */
+static const uint64_t RL[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL, 0x73eda753299d7d48ULL};
+static void fr_mulmod(uint64_t* r, const uint64_t* a, const uint64_t* b) {  /* schoolbook + bitwise reduction */
+  uint64_t t[8] = {0};
+  for (int i = 0; i < 4; ++i) {
+    u128 c = 0;
+    for (int j = 0; j < 4; ++j) { c += (u128)a[i] * b[j] + t[i + j]; t[i + j] = (uint64_t)c; c >>= 64; }
+    t[i + 4] = (uint64_t)c;
+  }
+  uint64_t rem[5] = {0};
+  for (int bit = 511; bit >= 0; --bit) {  /* rem = (rem << 1 | bit) mod r */
+    uint64_t carry = rem[3] >> 63;
+    for (int k = 3; k > 0; --k) rem[k] = (rem[k] << 1) | (rem[k - 1] >> 63);
+    rem[0] = (rem[0] << 1) | ((t[bit >> 6] >> (bit & 63)) & 1);
+    int ge = carry;
+    if (!ge) { ge = 1; for (int k = 3; k >= 0; --k) { if (rem[k] != RL[k]) { ge = rem[k] > RL[k]; break; } } }
+    if (ge) { uint64_t br = 0; for (int k = 0; k < 4; ++k) { u128 d = (u128)rem[k] - RL[k] - br; rem[k] = (uint64_t)d; br = (uint64_t)(d >> 64) & 1; } }
+  }
+  memcpy(r, rem, 32);
+}
+static void fr_from_u64(uint64_t* r, uint64_t v) {  /* v mod r (v < 2^64 < r) */
+  r[0] = v; r[1] = r[2] = r[3] = 0;
+}
+static void fr_sub(uint64_t* r, const uint64_t* a, const uint64_t* b) {
+  uint64_t br = 0, t[4];
+  for (int k = 0; k < 4; ++k) { u128 d = (u128)a[k] - b[k] - br; t[k] = (uint64_t)d; br = (uint64_t)(d >> 64) & 1; }
+  if (br) { u128 c = 0; for (int k = 0; k < 4; ++k) { c += (u128)t[k] + RL[k]; t[k] = (uint64_t)c; c >>= 64; } }
+  memcpy(r, t, 32);
+}
+static void fr_pow(uint64_t* r, const uint64_t* a, const uint64_t* e) {
+  uint64_t acc[4] = {1, 0, 0, 0};
+  for (int i = 255; i >= 0; --i) {
+    fr_mulmod(acc, acc, acc);
+    if ((e[i >> 6] >> (i & 63)) & 1) fr_mulmod(acc, acc, a);
+  }
+  memcpy(r, acc, 32);
+}
+static int fr_is_zero(const uint64_t* a) { return !(a[0] | a[1] | a[2] | a[3]); }
+
+/* lambda_i = prod_{j != i} x_j (x_j - x_i)^-1 mod r, inverse(0) = 0 */
+static void lagrange(uint64_t (*lam)[4], const uint64_t* ids, int t) {
+  uint64_t rm2[4];
+  memcpy(rm2, RL, 32); rm2[0] -= 2;
+  for (int i = 0; i < t; ++i) {
+    uint64_t acc[4] = {1, 0, 0, 0}, xi[4], xj[4], d[4], di[4];
+    fr_from_u64(xi, ids[i]);
+    for (int j = 0; j < t; ++j) {
+      if (i == j) continue;
+      fr_from_u64(xj, ids[j]);
+      fr_sub(d, xj, xi);
+      if (fr_is_zero(d)) memset(di, 0, 32); else fr_pow(di, d, rm2);
+      fr_mulmod(acc, acc, xj);
+      fr_mulmod(acc, acc, di);
+    }
+    memcpy(lam[i], acc, 32);
+  }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* init                                                                                        */
+/* ------------------------------------------------------------------------------------------ */
+static void f2_pow_big(fp2* r, const fp2* a, const uint64_t* e, int nl) { f2_pow(r, a, e, nl); }
+static void mp_divsmall(uint64_t* q, const uint64_t* a, int n, uint64_t d) {
+  u128 rem = 0;
+  for (int i = n - 1; i >= 0; --i) { rem = (rem << 64) | a[i]; q[i] = (uint64_t)(rem / d); rem %= d; }
+}
+static int g_init = 0;
+static pthread_mutex_t g_init_mu = PTHREAD_MUTEX_INITIALIZER;
+int bls_oracle_init(void) {
+  pthread_mutex_lock(&g_init_mu);
+  if (g_init) { pthread_mutex_unlock(&g_init_mu); return 0; }
+  uint64_t inv = 1;
+  for (int i = 0; i < 7; ++i) inv *= 2 - PL[0] * inv;
+  PINV = ~inv + 1;
+  memset(&FP_ZERO, 0, sizeof FP_ZERO);
+  /* R mod p and R^2 mod p by doubling 1 */
+  fp t = {{1, 0, 0, 0, 0, 0}};
+  for (int i = 0; i < 384; ++i) { uint64_t s[6]; add6(s, t.l, t.l); if (cmp6(s, PL) >= 0) sub6(s, s, PL); memcpy(t.l, s, 48); }
+  FP_ONE = t;
+  for (int i = 0; i < 384; ++i) { uint64_t s[6]; add6(s, t.l, t.l); if (cmp6(s, PL) >= 0) sub6(s, s, PL); memcpy(t.l, s, 48); }
+  FP_R2 = t;
+  uint64_t two[6] = {2, 0, 0, 0, 0, 0}, one[6] = {1, 0, 0, 0, 0, 0};
+  sub6(E_PM2, PL, two);
+  add6(E_SQRT, PL, one); for (int i = 0; i < 6; ++i) E_SQRT[i] = (E_SQRT[i] >> 2) | (i < 5 ? E_SQRT[i + 1] << 62 : 0);
+  sub6(E_HALF, PL, one); for (int i = 0; i < 6; ++i) E_HALF[i] = (E_HALF[i] >> 1) | (i < 5 ? E_HALF[i + 1] << 63 : 0);
+  F2_ZERO.c0 = FP_ZERO; F2_ZERO.c1 = FP_ZERO;
+  F2_ONE.c0 = FP_ONE; F2_ONE.c1 = FP_ZERO;
+  memset(&F12_ONE, 0, sizeof F12_ONE); F12_ONE.c0.c0 = F2_ONE;
+  fp_from_u64(&B1, 4);
+  fp_from_u64(&B2.c0, 4); fp_from_u64(&B2.c1, 4);
+  /* psi constants: 1/xi^((p-1)/3), 1/xi^((p-1)/2); Frobenius gammas xi^(k(p-1)/6) */
+  fp2 xi; fp_from_u64(&xi.c0, 1); fp_from_u64(&xi.c1, 1);
+  uint64_t pm1[6], e3[6], e2[6], e6[6];
+  sub6(pm1, PL, one);
+  mp_divsmall(e3, pm1, 6, 3); mp_divsmall(e2, pm1, 6, 2); mp_divsmall(e6, pm1, 6, 6);
+  f2_pow_big(&PSI_CX, &xi, e3, 6); f2_inv(&PSI_CX, &PSI_CX);
+  f2_pow_big(&PSI_CY, &xi, e2, 6); f2_inv(&PSI_CY, &PSI_CY);
+  fp2 g1; f2_pow_big(&g1, &xi, e6, 6);
+  GAMMA[0] = F2_ONE;
+  for (int k = 1; k < 6; ++k) f2_mul(&GAMMA[k], &GAMMA[k - 1], &g1);
+  /* hard exponent (p^4 - p^2 + 1) / r, by schoolbook big-int arithmetic on 64-bit limbs */
+  {
+    uint64_t p2[12] = {0}, p4[24] = {0}, num[24] = {0};
+    for (int i = 0; i < 6; ++i) { u128 c = 0; for (int j = 0; j < 6; ++j) { c += (u128)PL[i] * PL[j] + p2[i + j]; p2[i + j] = (uint64_t)c; c >>= 64; } p2[i + 6] = (uint64_t)c; }
+    for (int i = 0; i < 12; ++i) { u128 c = 0; for (int j = 0; j < 12; ++j) { c += (u128)p2[i] * p2[j] + p4[i + j]; p4[i + j] = (uint64_t)c; c >>= 64; } if (i + 12 < 24) p4[i + 12] = (uint64_t)c; }
+    uint64_t br = 0;
+    for (int i = 0; i < 24; ++i) { u128 d = (u128)p4[i] - (i < 12 ? p2[i] : 0) - br; num[i] = (uint64_t)d; br = (uint64_t)(d >> 64) & 1; }
+    u128 c = 1; for (int i = 0; i < 24 && c; ++i) { c += num[i]; num[i] = (uint64_t)c; c >>= 64; }
+    /* long division by r (256 bits): bitwise */
+    uint64_t q[24] = {0}, rem[5] = {0};
+    for (int bit = 24 * 64 - 1; bit >= 0; --bit) {
+      uint64_t carry = rem[3] >> 63;
+      for (int k = 3; k > 0; --k) rem[k] = (rem[k] << 1) | (rem[k - 1] >> 63);
+      rem[0] = (rem[0] << 1) | ((num[bit >> 6] >> (bit & 63)) & 1);
+      int ge = carry;
+      if (!ge) { ge = 1; for (int k = 3; k >= 0; --k) { if (rem[k] != RL[k]) { ge = rem[k] > RL[k]; break; } } }
+      if (ge) { uint64_t b2 = 0; for (int k = 0; k < 4; ++k) { u128 d = (u128)rem[k] - RL[k] - b2; rem[k] = (uint64_t)d; b2 = (uint64_t)(d >> 64) & 1; } q[bit >> 6] |= 1ULL << (bit & 63); }
+    }
+    memcpy(E_HARD, q, sizeof E_HARD);
+  }
+  /* SSWU and isogeny constants */
+  fp_from_u64(&SSWU_A.c0, 0); fp_from_u64(&SSWU_A.c1, 240);
+  fp_from_u64(&SSWU_B.c0, 1012); fp_from_u64(&SSWU_B.c1, 1012);
+  fp2 z; fp_from_u64(&z.c0, 2); fp_from_u64(&z.c1, 1); f2_neg(&SSWU_Z, &z);
+  fp2* dst[15] = {&ISO_XNUM[0], &ISO_XNUM[1], &ISO_XNUM[2], &ISO_XNUM[3], &ISO_XDEN[0], &ISO_XDEN[1], &ISO_XDEN[2],
+                  &ISO_YNUM[0], &ISO_YNUM[1], &ISO_YNUM[2], &ISO_YNUM[3], &ISO_YDEN[0], &ISO_YDEN[1], &ISO_YDEN[2], &ISO_YDEN[3]};
+  for (int i = 0; i < 15; ++i) { fp_from_hex(&dst[i]->c0, ISO_HEX[i][0]); fp_from_hex(&dst[i]->c1, ISO_HEX[i][1]); }
+  fp_from_hex(&G1_GEN.x, "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb");
+  fp_from_hex(&G1_GEN.y, "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1");
+  G1_GEN.inf = 0;
+  g_init = 1;
+  pthread_mutex_unlock(&g_init_mu);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* exported API (ctypes)                                                                       */
+/* ------------------------------------------------------------------------------------------ */
+void bls_oracle_hash_to_g2(const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen, uint8_t* out192) {
+  bls_oracle_init();
+  g2_aff h;
+  hash_to_g2(&h, msg, mlen, dst, dlen);
+  g2_serialize(out192, &h);
+}
+
+static int verify_points(const g1_aff* pk, const g2_aff* sig, const g2_aff* h) {
+  if (pk->inf) return 0;
+  if (!g2_in_subgroup(sig)) return 0;
+  fp12 f1, f2, e;
+  g1_aff ng = G1_GEN; fp_neg(&ng.y, &ng.y);
+  miller_loop(&f1, pk, h);
+  miller_loop(&f2, &ng, sig);
+  f12_mul(&f1, &f1, &f2);
+  final_exp(&e, &f1);
+  return f12_is_one(&e);
+}
+
+/* Signature::verify(pk, msg) (blst, sig_groupcheck = true, pk_validate = false) */
+int bls_oracle_verify(const uint8_t* pk48, const uint8_t* sig96, const uint8_t* msg, size_t mlen, const uint8_t* dst,
+                      size_t dlen) {
+  bls_oracle_init();
+  g1_aff pk; g2_aff sig, h;
+  if (!g1_decompress(&pk, pk48) || !g2_decompress(&sig, sig96)) return 0;
+  hash_to_g2(&h, msg, mlen, dst, dlen);
+  return verify_points(&pk, &sig, &h);
+}
+
+/* threshold_aggregate of one job (src/crypto/generic_threshold.rs:132-175); returns the DvfError
+ * tag (0 ok), err[2] the error fields, out96 the combined signature.  h: H(msg) if precomputed. */
+/* verify_all: verify every share (verdicts[i]) and combine the first t valid ones -- the same work
+ * as the device engine per job (the reference stops verifying at the t-th valid share; the
+ * combined signature is identical). */
+static int threshold_job(uint32_t t, uint32_t n, const uint8_t* sigs96, const uint8_t* pks48, const uint64_t* ids,
+                         const g2_aff* h, uint8_t* out96, uint64_t* err, uint8_t* verdicts, int verify_all) {
+  if (n < t) { err[0] = n; err[1] = t; return 2; }
+  uint64_t sel_ids[64]; g2_aff sel[64]; uint32_t got = 0;
+  if (t > 64) { err[0] = n; err[1] = t; return 2; }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (ids[i] == 0) { err[0] = 0; err[1] = 0; return 3; }
+    int dup = 0;
+    for (uint32_t k = 0; k < got; ++k) dup |= sel_ids[k] == ids[i];
+    if (dup && !verify_all) continue;
+    g1_aff pk; g2_aff sig;
+    int ok = g1_decompress(&pk, pks48 + 48 * (size_t)i) && g2_decompress(&sig, sigs96 + 96 * (size_t)i) &&
+             verify_points(&pk, &sig, h);
+    if (verdicts) verdicts[i] = (uint8_t)ok;
+    if (ok && !dup && got < t) { sel[got] = sig; sel_ids[got] = ids[i]; ++got; if (got >= t && !verify_all) break; }
+  }
+  if (got < t) { err[0] = got; err[1] = t; return 4; }
+  uint64_t lam[64][4];
+  lagrange(lam, sel_ids, (int)t);
+  g2_jac acc; g2_set_inf(&acc);
+  for (uint32_t i = 0; i < t; ++i) {
+    g2_jac p, q;
+    g2_from_aff(&p, &sel[i]);
+    g2_mul(&q, &p, lam[i], 4);
+    g2_add(&acc, &acc, &q);
+  }
+  g2_aff a;
+  g2_to_aff(&a, &acc);
+  g2_compress(out96, &a);
+  err[0] = err[1] = 0;
+  return 0;
+}
+
+int bls_oracle_threshold_aggregate(uint32_t t, uint32_t n, const uint8_t* sigs96, const uint8_t* pks48,
+                                   const uint64_t* ids, const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen,
+                                   uint8_t* out96, uint64_t* err) {
+  bls_oracle_init();
+  g2_aff h;
+  hash_to_g2(&h, msg, mlen, dst, dlen);
+  return threshold_job(t, n, sigs96, pks48, ids, &h, out96, err, NULL, 0);
+}
+
+/* Batched jobs over `threads` POSIX threads (the CPU baseline): job j = shares
+ * [share_off[j], share_off[j+1]), threshold t[j], root roots32[job_root[j]] (32-byte messages).
+ * H(root) is computed once per distinct root, like the device engine. */
+typedef struct {
+  size_t lo, hi; const uint32_t* off; const uint32_t* t; const uint8_t* sigs; const uint8_t* pks; const uint64_t* ids;
+  const uint32_t* jr; const g2_aff* H; uint8_t* out; int32_t* st; uint64_t* err; uint8_t* verdicts; int verify_all;
+} job_args;
+static void* job_worker(void* p) {
+  job_args* a = (job_args*)p;
+  for (size_t j = a->lo; j < a->hi; ++j) {
+    const uint32_t b = a->off[j], e = a->off[j + 1];
+    a->st[j] = threshold_job(a->t[j], e - b, a->sigs + 96 * (size_t)b, a->pks + 48 * (size_t)b, a->ids + b, &a->H[a->jr[j]],
+                             a->out + 96 * j, a->err + 2 * j, a->verdicts ? a->verdicts + b : NULL, a->verify_all);
+  }
+  return NULL;
+}
+typedef struct { size_t lo, hi; const uint8_t* roots; const uint8_t* dst; size_t dlen; g2_aff* H; } hash_args;
+static void* hash_worker(void* p) {
+  hash_args* a = (hash_args*)p;
+  for (size_t r = a->lo; r < a->hi; ++r) hash_to_g2(&a->H[r], a->roots + 32 * r, 32, a->dst, a->dlen);
+  return NULL;
+}
+int bls_oracle_threshold_batch(size_t n_jobs, const uint32_t* share_off, const uint32_t* t, const uint8_t* sigs96,
+                               const uint8_t* pks48, const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                               const uint8_t* roots32, const uint8_t* dst, size_t dlen, uint8_t* out96, int32_t* status,
+                               uint64_t* err, uint8_t* verdicts, int verify_all, int threads) {
+  bls_oracle_init();
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  g2_aff* H = (g2_aff*)malloc(sizeof(g2_aff) * (n_roots ? n_roots : 1));
+  if (!H) return -3;
+  pthread_t th[256];
+  hash_args ha[256];
+  job_args ja[256];
+  int nt = (size_t)threads < n_roots ? threads : (int)n_roots;
+  for (int i = 0; i < nt; ++i) {
+    ha[i] = (hash_args){n_roots * i / nt, n_roots * (i + 1) / nt, roots32, dst, dlen, H};
+    pthread_create(&th[i], NULL, hash_worker, &ha[i]);
+  }
+  for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+  nt = (size_t)threads < n_jobs ? threads : (int)n_jobs;
+  for (int i = 0; i < nt; ++i) {
+    ja[i] = (job_args){n_jobs * i / nt, n_jobs * (i + 1) / nt, share_off, t, sigs96, pks48, ids, job_root, H, out96, status, err,
+                       verdicts, verify_all};
+    pthread_create(&th[i], NULL, job_worker, &ja[i]);
+  }
+  for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+  free(H);
+  return 0;
+}
+
+/* self-test: the x-chain final exponentiation equals the cube of the textbook exponent */
+int bls_oracle_selftest_final_exp(void) {
+  bls_oracle_init();
+  g2_aff h; uint8_t m[3] = {1, 2, 3};
+  hash_to_g2(&h, m, 3, (const uint8_t*)"T", 1);
+  fp12 f, a, b, c;
+  miller_loop(&f, &G1_GEN, &h);
+  final_exp(&a, &f);
+  final_exp_slow(&b, &f);
+  f12_sqr(&c, &b); f12_mul(&c, &c, &b);
+  fp12 d; f12_conj(&d, &c); f12_mul(&d, &d, &a);   /* a * c^-1 (cyclotomic inverse) */
+  return f12_is_one(&d) && !f12_is_one(&a) ? 0 : 1;
+}
+
+/* self-test of the internal constants: the generators are on their curves and in their groups */
+int bls_oracle_selftest(void) {
+  bls_oracle_init();
+  fp y2, x3;
+  fp_sqr(&y2, &G1_GEN.y); fp_sqr(&x3, &G1_GEN.x); fp_mul(&x3, &x3, &G1_GEN.x); fp_add(&x3, &x3, &B1);
+  if (!fp_eq(&y2, &x3)) return 1;
+  g1_jac g; g1_from_aff(&g, &G1_GEN);
+  uint64_t r[4]; memcpy(r, RL, 32);
+  g1_jac z; g1_mul(&z, &g, r, 4);
+  if (!g1_is_inf(&z)) return 2;
+  return 0;
+}
