@@ -98,6 +98,18 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
                      const uint32_t* root_idx, size_t n_roots, const uint8_t* roots32,
                      const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* verdicts);
 
+/* Same, device pointers, enqueued on the next pipeline slot after `stream` (hipStream_t; NULL =
+ * default); the verdicts are ready when `stream` reaches them.  Root indices >= n_roots give
+ * verdict 0.  The _cached variant takes per-share indices into the ssb_pk_cache_set table.  With
+ * the validators' master keys and the combined signatures this is the combined-signature
+ * verify (a-8), batched across validators by RLC. */
+int ssb_verify_batch_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t* sig96, const uint32_t* root_idx,
+                         size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
+                         uint8_t* verdicts, void* stream);
+int ssb_verify_batch_cached_dev(ssb_ctx* ctx, size_t n, const uint32_t* pk_index, const uint8_t* sig96,
+                                const uint32_t* root_idx, size_t n_roots, const uint8_t* roots32, const uint8_t* dst,
+                                size_t dst_len, uint64_t rlc_seed, uint8_t* verdicts, void* stream);
+
 /* Batched threshold_aggregate.  Job j owns shares [share_off[j], share_off[j+1]) of sig96 /
  * pk48 / ids (input order = the reference's scan order), threshold t[j], and signs
  * roots32[job_root[j]].  Per job: out_status[j] (SSB_DVF_*), out_err[2j..2j+1] (error fields),

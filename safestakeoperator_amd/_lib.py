@@ -35,6 +35,12 @@ SIGNATURES = {
                                                          ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "ssb_pk_cache_set": (ctypes.c_int, [_ctx, _sz, _u8p]),
+    "ssb_verify_batch_dev": (ctypes.c_int, [_ctx, _sz, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz,
+                                            ctypes.c_void_p, _u8p, _sz, ctypes.c_uint64, ctypes.c_void_p,
+                                            ctypes.c_void_p]),
+    "ssb_verify_batch_cached_dev": (ctypes.c_int, [_ctx, _sz, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz,
+                                                   ctypes.c_void_p, _u8p, _sz, ctypes.c_uint64, ctypes.c_void_p,
+                                                   ctypes.c_void_p]),
     "ssb_threshold_aggregate_batch_cached_dev": (ctypes.c_int, [_ctx, _sz, _sz, ctypes.c_void_p, ctypes.c_void_p,
                                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                                 ctypes.c_void_p, _sz, ctypes.c_void_p, _u8p, _sz,

@@ -110,9 +110,13 @@ __global__ void __launch_bounds__(64) k_check_rlc(int n, uint64_t seed, const ui
 }
 
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
-                        const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags) {
+                        const uint32_t* __restrict__ gflags, const uint32_t* __restrict__ share_root, uint32_t n_roots,
+                        uint32_t* __restrict__ flags) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) flags[s] = combine_flags(sflags[s], pflags[s], gflags[s]);
+  if (s >= n) return;
+  uint32_t f = combine_flags(sflags[s], pflags[s], gflags[s]);
+  if (share_root[s] >= n_roots) f &= ~FLAG_CANDIDATE;  // no H(root): the share cannot verify
+  flags[s] = f;
 }
 __global__ void __launch_bounds__(SUM_THREADS) k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
                                                                 const uint32_t* __restrict__ flags,

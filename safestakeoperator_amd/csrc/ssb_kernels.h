@@ -51,7 +51,8 @@ __global__ void k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ s
                             const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
                             g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk);
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
-                        const uint32_t* __restrict__ gflags, uint32_t* __restrict__ flags);
+                        const uint32_t* __restrict__ gflags, const uint32_t* __restrict__ share_root, uint32_t n_roots,
+                        uint32_t* __restrict__ flags);
 __global__ void k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
                                                                 const uint32_t* __restrict__ flags,
                                                                 const g1_jac* __restrict__ rpk,

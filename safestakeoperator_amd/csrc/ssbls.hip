@@ -320,7 +320,8 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, seed, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent, w.order); }
   if (n) {
     { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags); }
-    hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, w.flags);
+    hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, d_share_root,
+                       (uint32_t)n_roots, w.flags);
   }
   SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));
   // G1 sums (per root) on side[1] -- then the caller's speculative combine, off the critical path --
@@ -593,6 +594,36 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   return SSB_OK;
 }
 
+// the body of ssb_verify_batch_dev / _cached_dev: verdicts of (pk, sig, root) triples, device
+// pointers, enqueued on the next pipeline slot (a-2; a-8 with the validators' master keys)
+int verify_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint32_t* pk_index, const uint8_t* sig96,
+               const uint32_t* root_idx, size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+               uint64_t rlc_seed, uint8_t* verdicts, void* stream) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!(pk48 || pk_index) || !sig96 || !root_idx || !roots32 || !verdicts || n_roots == 0) {
+    ctx->err = "null pointer or no roots"; return SSB_EINVAL;
+  }
+  if (pk_index && !ctx->pkc_aff) { ctx->err = "no public-key cache (ssb_pk_cache_set)"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  ctx->cur = &ctx->sl[ctx->next];
+  ctx->next = (ctx->next + 1) % ctx->nslots;
+  dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
+  if ((rc = ensure_ws(ctx, verify_ws_bytes(n, n_roots)))) return rc;
+  hipStream_t user = (hipStream_t)stream, st = ctx->cur->stream;
+  SSB_HIP(hipEventRecord(ctx->cur->ev_user, user));
+  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_user, 0));
+  carve c{(char*)ctx->cur->ws};
+  verify_ws w = carve_verify(c, n, n_roots);
+  // root indices >= n_roots: those shares are skipped by the sums and get verdict 0
+  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, root_idx, roots32, d, rlc_seed, verdicts, [] {},
+                       ctx->tail))) return rc;
+  SSB_HIP(hipEventRecord(ctx->cur->ev_out, ctx->tail));
+  ctx->cur->out_pending = true;
+  SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
+  return SSB_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -616,6 +647,20 @@ int ssb_threshold_aggregate_batch_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t
   if (ctx && n_shares && !pk_index) { ctx->err = "null pk_index"; return SSB_EINVAL; }
   return aggregate_dev(ctx, n_jobs, n_shares, share_off, t, sig96, nullptr, pk_index, ids, job_root, n_roots, roots32, dst,
                        dst_len, rlc_seed, out_sig96, out_status, out_err, share_verdicts, stream);
+}
+
+int ssb_verify_batch_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t* sig96, const uint32_t* root_idx,
+                         size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
+                         uint8_t* verdicts, void* stream) {
+  if (ctx && n && !pk48) { ctx->err = "null pk48"; return SSB_EINVAL; }
+  return verify_dev(ctx, n, pk48, nullptr, sig96, root_idx, n_roots, roots32, dst, dst_len, rlc_seed, verdicts, stream);
+}
+
+int ssb_verify_batch_cached_dev(ssb_ctx* ctx, size_t n, const uint32_t* pk_index, const uint8_t* sig96,
+                                const uint32_t* root_idx, size_t n_roots, const uint8_t* roots32, const uint8_t* dst,
+                                size_t dst_len, uint64_t rlc_seed, uint8_t* verdicts, void* stream) {
+  if (ctx && n && !pk_index) { ctx->err = "null pk_index"; return SSB_EINVAL; }
+  return verify_dev(ctx, n, nullptr, pk_index, sig96, root_idx, n_roots, roots32, dst, dst_len, rlc_seed, verdicts, stream);
 }
 
 int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {

@@ -280,3 +280,36 @@ def test_large_configs_properties(engine, V, t, n):
     sample = list(range(0, V, V // 512))
     msig = engine.sign_batch([master[v] for v in sample], [jr[v] for v in sample], roots)
     assert all(out[v].tobytes() == msig[k] for k, v in enumerate(sample))
+
+
+def test_combined_verify_on_device(engine):
+    """a-8 on device: the combined signatures of an aggregate batch verified against the
+    validators' master keys with ssb_verify_batch_dev (RLC across validators sharing a root),
+    including swapped signatures and an out-of-range root index (verdict 0)."""
+    import ctypes
+    import torch
+    from safestakeoperator_amd import _lib
+    V, t, n = 512, 3, 4
+    roots, master, sigs, pks, ids, jr, msig = _gen_committees(engine, V, t, n, 8, seed=23)
+    offs = list(range(0, V * n + 1, n))
+    out, st, err, ver = engine.threshold_aggregate_batch_raw([t] * V, offs, b"".join(sigs), b"".join(pks), ids, jr, roots)
+    assert (st == 0).all()
+    mpk = engine.sk_to_pk_batch(master)
+    comb = [out[v].tobytes() for v in range(V)]
+    comb[10], comb[11] = comb[11], comb[10]            # both invalid now (different roots/keys)
+    jr2 = list(jr)
+    jr2[20] = len(roots) + 5                           # no such root
+    lib = engine._lib
+    dev = torch.device("cuda", 0)
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_pk, d_sig, d_roots = u8(b"".join(mpk)), u8(b"".join(comb)), u8(b"".join(roots))
+    d_jr = torch.tensor(jr2, dtype=torch.int32, device=dev)
+    d_ver = torch.zeros((V,), dtype=torch.uint8, device=dev)
+    dst = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
+    rc = lib.ssb_verify_batch_dev(engine.handle, V, d_pk.data_ptr(), d_sig.data_ptr(), d_jr.data_ptr(), len(roots),
+                                  d_roots.data_ptr(), ctypes.cast(dst, _lib._u8p), len(DST), 99, d_ver.data_ptr(), None)
+    assert rc == 0, lib.ssb_last_error(engine.handle)
+    torch.cuda.synchronize()
+    expect = np.ones(V, dtype=np.uint8)
+    expect[[10, 11, 20]] = 0
+    assert (d_ver.cpu().numpy() == expect).all()
