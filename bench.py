@@ -127,9 +127,11 @@ def pmc_traffic(kernel):
         return None
 
 
-def make_workload(engine, V, t, n, n_roots, rank):
+def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0):
     """Synthetic committees: deterministic keys (seed 0x5AFE57A4E, rank), Shamir shares, partial
-    signatures from the engine's batched signer (H(m)*sk), public keys sk*g1."""
+    signatures from the engine's batched signer (H(m)*sk), public keys sk*g1.  invalid_rate: that
+    fraction of the shares (deterministic choice) signs the NEXT root instead -- a valid G2 point
+    that fails verification (SURVEY.md §8d C2/C4 invalid variants)."""
     seed = b"ssbls-bench" + (0x5AFE57A4E).to_bytes(8, "little") + rank.to_bytes(4, "little")
     roots = [hashlib.sha256(seed + b"root" + i.to_bytes(4, "little")).digest() for i in range(n_roots)]
 
@@ -149,10 +151,19 @@ def make_workload(engine, V, t, n, n_roots, rank):
             ids.append(i)
             share_root.append(v % n_roots)
         jr.append(v % n_roots)
-    sigs = engine.sign_batch(share_sk, share_root, roots)
+    bad = [i for i in range(len(share_sk))
+           if invalid_rate > 0 and int.from_bytes(hashlib.sha256(seed + b"bad" + i.to_bytes(4, "little")).digest()[:8],
+                                                   "little") < invalid_rate * 2.0 ** 64]
+    sign_root = list(share_root)
+    for i in bad:
+        sign_root[i] = (share_root[i] + 1) % n_roots
+    sigs = engine.sign_batch(share_sk, sign_root, roots)
     pks = engine.sk_to_pk_batch(share_sk)
+    valid = [1] * len(share_sk)
+    for i in bad:
+        valid[i] = 0
     return dict(roots=roots, sigs=b"".join(sigs), pks=b"".join(pks), ids=ids, job_root=jr, master=master,
-                share_sigs=sigs, share_pks=pks)
+                share_sigs=sigs, share_pks=pks, valid=valid, n_bad=len(bad))
 
 
 def cpu_baseline(wl, t, n, gpu_out=None, n_val=1024, threads=None):
@@ -198,6 +209,9 @@ def main():
     ap.add_argument("--compressed-pk", action="store_true",
                     help="headline on the compressed-public-key entry point (default: keys decompressed once, "
                          "ssb_pk_cache_set, as lighthouse's PublicKey holds them; the other variant is reported beside)")
+    ap.add_argument("--invalid-rate", type=float, default=0.0,
+                    help="fraction of shares signed over the wrong root (the RLC batch fails; exact verdicts "
+                         "come from the per-share fallback).  The headline is the all-valid C2 batch.")
     args = ap.parse_args()
     set_hw_queues(args.pipeline * args.slot_streams + 4)
 
@@ -226,7 +240,9 @@ def main():
     V, t, n, n_roots = args.validators, args.threshold, args.operators, args.roots
     N = V * n
     eng = Engine(local)
-    wl = make_workload(eng, V, t, n, n_roots, rank)
+    wl = make_workload(eng, V, t, n, n_roots, rank, args.invalid_rate)
+    valid = np.asarray(wl["valid"], dtype=np.uint8)
+    job_ok = valid.reshape(V, n).sum(axis=1) >= t
 
     # inputs resident in HBM before the timed region
     def dt8(b):
@@ -311,9 +327,10 @@ def main():
         torch.cuda.synchronize(dev)
         ok_st = ok_comb = True
         for o in outs:
-            ok_st = ok_st and bool((o["st"] == 0).all().item()) and bool((o["ver"] == 1).all().item())
+            st_host = o["st"].cpu().numpy()
+            ok_st = ok_st and bool(((st_host == 0) == job_ok).all()) and bool((o["ver"].cpu().numpy() == valid).all())
             out_host = o["out"].cpu().numpy()
-            ok_comb = ok_comb and all(out_host[v].tobytes() == msig[v] for v in range(min(64, V)))
+            ok_comb = ok_comb and all(out_host[v].tobytes() == msig[v] for v in range(min(64, V)) if job_ok[v])
         return ok_st and ok_comb
 
     def timed_run():
@@ -390,6 +407,7 @@ def main():
                 round(N * world * args.steps / elapsed_other, 1),
             "combined_sigs_per_s": round(combined, 1),
             "results_ok": ok_all,
+            "invalid_shares_per_batch": wl["n_bad"],
             "roofline": {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),
                          "peak": round(peak, 2), "unit": "TMAD/s", "frac": round(achieved / peak, 5),
                          "traffic": pmc_traffic(dom), "mads_per_launch": km[dom], "avg_launch_ms": round(avg[dom], 4),
@@ -399,7 +417,7 @@ def main():
                               "frac": round(step_mads * world * args.steps / elapsed / MAD_PEAK_MEASURED / world, 5)},
             "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not wl["n_bad"]:
             rec["cpu_baseline"] = cpu_baseline(wl, t, n, gpu_out=outs[0]["out"].cpu().numpy(),
                                                n_val=min(1024, V))
         print(json.dumps(rec), flush=True)

@@ -5,7 +5,9 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libssbls.so")
+# SSB_LIB_VARIANT=name loads the experiment build libssbls_<name>.so (safestakeoperator_amd/build.py)
+_VARIANT = os.environ.get("SSB_LIB_VARIANT", "")
+LIB_PATH = os.path.join(HERE, "libssbls%s.so" % ("_" + _VARIANT if _VARIANT else ""))
 HEADER = os.path.join(HERE, "..", "include", "ssbls.h")
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)

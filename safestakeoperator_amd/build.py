@@ -14,14 +14,19 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "libssbls.so")
+# SSB_VARIANT=name builds an experiment variant (extra -D flags from SSB_VARIANT_DEFS) into
+# libssbls_<name>.so with its own object directory; the product library is libssbls.so.
+VARIANT = os.environ.get("SSB_VARIANT", "")
+LIB = os.path.join(HERE, "libssbls%s.so" % ("_" + VARIANT if VARIANT else ""))
 SOURCES = ["ssbls.hip", "ssb_k_lane.hip", "ssb_k_verify.hip", "ssb_k_pair.hip", "ssb_k_hash.hip",
            "ssb_k_combine.hip", "ssb_k_msm.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SSB_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]
+if VARIANT:
+    FLAGS += os.environ.get("SSB_VARIANT_DEFS", "").split()
 STAMP = LIB + ".srchash"
-OBJDIR = os.path.join(HERE, "build")
+OBJDIR = os.path.join(HERE, "build" + ("_" + VARIANT if VARIANT else ""))
 
 
 def _inputs():

@@ -16,6 +16,13 @@
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define SSB_INL __host__ __device__ __forceinline__
+// Kernel launch bounds: workgroup size n and a minimum of SSB_WAVES_PER_EU waves per SIMD, which
+// caps every kernel of the TU (and, through the attributor, its out-of-line callees) at
+// 512 / SSB_WAVES_PER_EU registers per lane (VGPR + AGPR).
+#ifndef SSB_WAVES_PER_EU
+#define SSB_WAVES_PER_EU 1
+#endif
+#define SSB_LB(n) __attribute__((amdgpu_flat_work_group_size(1, n), amdgpu_waves_per_eu(SSB_WAVES_PER_EU)))
 #ifdef SSB_FN_INLINE  // experiment: every routine inlined (code size explodes; microbenchmarks only)
 #define SSB_FN __host__ __device__ __forceinline__
 #else

@@ -60,7 +60,7 @@ __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const u
   for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
   unit_lagrange(lam + b, x, t);
 }
-__global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
+__global__ void SSB_LB(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                                       const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                                       const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64) k_combine_terms(int n, const uint32_t* __r
   unit_combine_term(r, sig_aff[sel[s]], l.l);  // blst_p2_mult(.., 255 bits)
   term[s] = r;
 }
-__global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
+__global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
                                                     const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96) {
@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(64) k_combine_sum(int n_jobs, const uint32_t* 
 // Small-integer Lagrange fast path (unit_lagrange_small): every selected share is a verified
 // (hence order-r) point, so sum c_i sig_i with the integer c_i == lambda_i mod r is the reference's
 // combination.  fast[j] = 1 when the job was finished here; the 255-bit path skips those jobs.
-__global__ void __launch_bounds__(64) k_combine_fast(int n_jobs, const uint32_t* __restrict__ off,
+__global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                      const uint32_t* __restrict__ sel, const uint64_t* __restrict__ ids,
                                                      const g2_aff* __restrict__ sig_aff,

@@ -7,7 +7,7 @@
 namespace ssb {
 namespace k {
 
-__global__ void __launch_bounds__(64) k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
+__global__ void SSB_LB(64) k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
                                                    g2_aff* __restrict__ out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -19,7 +19,7 @@ __global__ void __launch_bounds__(64) k_hash_to_g2(int n, const uint8_t* __restr
 }
 // ---- staged hash_to_G2 (same result as k_hash_to_g2, shorter critical path) ----
 // 1: expand_message_xmd + the two field elements, one lane per root
-__global__ void __launch_bounds__(64) k_h2c_u(int n, const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
+__global__ void SSB_LB(64) k_h2c_u(int n, const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t m[32];
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(64) k_h2c_u(int n, const uint8_t* __restrict__
 
 // 2: simplified SWU, one lane per (root, u_j, candidate x1 / x2): both square roots run at once
 // instead of one after the other; then the 3-isogeny.  Lanes 4i+2j+c, 16 roots per block.
-__global__ void __launch_bounds__(64) k_h2c_map(int n, const fp2* __restrict__ u, g2_aff* __restrict__ q) {
+__global__ void SSB_LB(64) k_h2c_map(int n, const fp2* __restrict__ u, g2_aff* __restrict__ q) {
   struct cand_t { fp2 x, y; uint32_t ok; };
   __shared__ cand_t cs[64];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(64) k_h2c_map(int n, const fp2* __restrict__ u
 // 3: q0 + q1 and the cofactor clearing as lane-group programs (8 lanes per root)
 constexpr int H2C_S0 = lane::G2_ADD_SCRATCH > lane::G2_MADD_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G2_MADD_SCRATCH;
 constexpr int H2C_GS = H2C_S0 + 6 + 4 + 6 + 30;
-__global__ void __launch_bounds__(64) k_h2c_clear(int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
+__global__ void SSB_LB(64) k_h2c_clear(int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
                                                   uint32_t* __restrict__ exc_out) {
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + 8 * H2C_GS];
@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(64) k_h2c_clear(int n, const g2_aff* __restric
 }
 
 // 4: affine output; a root whose lane-group stage met an exceptional addition is redone exactly
-__global__ void __launch_bounds__(64) k_h2c_affine(int n, const g2_aff* __restrict__ q, const g2_jac* __restrict__ hj,
+__global__ void SSB_LB(64) k_h2c_affine(int n, const g2_aff* __restrict__ q, const g2_jac* __restrict__ hj,
                                                    const uint32_t* __restrict__ exc, g2_aff* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(64) k_h2c_affine(int n, const g2_aff* __restri
   out[i] = a;
 }
 
-__global__ void __launch_bounds__(64) k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
+__global__ void SSB_LB(64) k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
                                              const g2_aff* __restrict__ H, uint8_t* __restrict__ out96) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(64) k_sign(int n, const uint8_t* __restrict__ 
   g2_compress(o, a);
   for (int b = 0; b < 96; ++b) out96[96 * (size_t)i + b] = o[b];
 }
-__global__ void __launch_bounds__(64) k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48) {
+__global__ void SSB_LB(64) k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8];

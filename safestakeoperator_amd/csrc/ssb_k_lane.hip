@@ -30,7 +30,7 @@ SSB_INL g2_aff dummy_g2() {  // any curve point: the results of inactive groups 
 
 // subgroup check: user slots P(4) acc(6) tmp(10)
 constexpr int SG_GS = G2S0 + 20;
-__global__ void __launch_bounds__(64) k_lane_subgroup(int n, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(64) k_lane_subgroup(int n, const uint32_t* __restrict__ sflags,
                                                       const g2_aff* __restrict__ sig, uint32_t* __restrict__ gflags,
                                                       uint32_t* __restrict__ exc_out) {
   __shared__ fp lds[LP_NCODE_CONST + G2NG * SG_GS];
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(64) k_lane_subgroup(int n, const uint32_t* __r
 
 // RLC on G2: user slots P(4) table(48) acc(6) tmp(6)
 constexpr int R2_GS = G2S0 + 64;
-__global__ void __launch_bounds__(64) k_lane_rlc_g2(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(64) k_lane_rlc_g2(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
                                                     const g2_aff* __restrict__ sig, g2_jac* __restrict__ rsig,
                                                     uint32_t* __restrict__ exc_out) {
   __shared__ fp lds[LP_NCODE_CONST + G2NG * R2_GS];
@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(64) k_lane_rlc_g2(int n, uint64_t seed, const 
 
 // RLC on G1: user slots P(2) table(24) acc(3) tmp(3)
 constexpr int R1_GS = G1S0 + 32;
-__global__ void __launch_bounds__(64) k_lane_rlc_g1(int n, uint64_t seed, const uint32_t* __restrict__ pflags,
+__global__ void SSB_LB(64) k_lane_rlc_g1(int n, uint64_t seed, const uint32_t* __restrict__ pflags,
                                                     const g1_aff* __restrict__ pk, g1_jac* __restrict__ rpk,
                                                     uint32_t* __restrict__ exc_out) {
   __shared__ fp lds[LP_NCODE_CONST + G1NG * R1_GS];
@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(64) k_lane_rlc_g1(int n, uint64_t seed, const 
   }
 }
 
-__global__ void __launch_bounds__(64) k_lane_fixup(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(64) k_lane_fixup(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
                                                    const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig,
                                                    const g1_aff* __restrict__ pk, const uint32_t* __restrict__ exc_g2,
                                                    const uint32_t* __restrict__ exc_rlc2, const uint32_t* __restrict__ exc_rlc1,

@@ -42,7 +42,7 @@ SSB_INL void msm_entries(int i, uint64_t k, uint32_t g, const msm_cfg& c, uint32
 
 // cnt[key] += 1 per (share, window) entry (SCATTER: ent[cursor[key]++] = share)
 template <bool SCATTER>
-__global__ void __launch_bounds__(256) k_msm_sort(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(256) k_msm_sort(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
                                                   const uint32_t* __restrict__ pflags,
                                                   const uint32_t* __restrict__ share_root, msm_cfg c2, msm_cfg c1,
                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
@@ -71,7 +71,7 @@ SSB_INL uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   __syncthreads();
   return incl - v;
 }
-__global__ void __launch_bounds__(SCAN_T) k_scan_blocks(uint32_t K, const uint32_t* __restrict__ cnt,
+__global__ void SSB_LB(SCAN_T) k_scan_blocks(uint32_t K, const uint32_t* __restrict__ cnt,
                                                         uint32_t* __restrict__ start, uint32_t* __restrict__ bsum) {
   __shared__ uint32_t sh[SCAN_T];
   const uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_PER;
@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_blocks(uint32_t K, const uint32
   for (int q = 0; q < SCAN_PER; ++q) { if (base + q < K) start[base + q] = run; run += v[q]; }
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
-__global__ void __launch_bounds__(SCAN_T) k_scan_top(uint32_t nb, uint32_t* __restrict__ bsum) {
+__global__ void SSB_LB(SCAN_T) k_scan_top(uint32_t nb, uint32_t* __restrict__ bsum) {
   __shared__ uint32_t sh[SCAN_T];
   const uint32_t base = threadIdx.x * SCAN_PER;
   uint32_t v[SCAN_PER], s = 0;
@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_top(uint32_t nb, uint32_t* __re
   uint32_t run = block_excl_scan(s, sh, total);
   for (int q = 0; q < SCAN_PER; ++q) { if (base + q < nb) bsum[base + q] = run; run += v[q]; }
 }
-__global__ void __launch_bounds__(256) k_scan_add(uint32_t K, uint32_t* __restrict__ start,
+__global__ void SSB_LB(256) k_scan_add(uint32_t K, uint32_t* __restrict__ start,
                                                   const uint32_t* __restrict__ bsum, uint32_t* __restrict__ cur) {
   const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= K) return;
@@ -105,14 +105,14 @@ __global__ void __launch_bounds__(256) k_scan_add(uint32_t K, uint32_t* __restri
 // (Poisson-sized buckets in key order cost ~2x in divergence).  512 bins = 2 MSMs x counts 0..255
 // (larger counts share bin 255; only the convergence depends on the order, never the result).
 constexpr int ORDER_BINS = 512;
-__global__ void __launch_bounds__(256) k_order_hist(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
+__global__ void SSB_LB(256) k_order_hist(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
                                                     uint32_t* __restrict__ bins) {
   const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
   if (key >= K) return;
   const uint32_t c = cnt[key] < 255u ? cnt[key] : 255u;
   atomicAdd(&bins[(key >= K2 ? 256u : 0u) + 255u - c], 1u);
 }
-__global__ void __launch_bounds__(256) k_order_scatter(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
+__global__ void SSB_LB(256) k_order_scatter(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
                                                        uint32_t* __restrict__ bins, uint32_t* __restrict__ order) {
   const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
   if (key >= K) return;
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256) k_order_scatter(uint32_t K, uint32_t K2, 
 
 // ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
+__global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
                                                    const uint32_t* __restrict__ start,
                                                    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ flags, const aff<F>* __restrict__ pts,
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(64) k_msm_bucket(uint32_t nb, uint32_t base, i
 // G1: out_jac[gw] (Jacobian, for the Horner combine).  G2: the window is affine pair gw of the
 // multi-pairing: out_q[gw] = W_gw, out_p[gw] = [2^(c gw)](-g1) from negg1_pow.
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
+__global__ void SSB_LB(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
                                                    aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
                                                    const g1_aff* __restrict__ negg1_pow) {
   __shared__ jac<F> sh[64];
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(64) k_msm_window(int c, const jac<F>* __restri
 // ---- window sums for narrow windows (2^c <= 16 buckets): one lane per (group, window), the
 // sequential running sum  R += B_d, U += R  for d = 2^c - 1 .. 1  (2 (2^c - 1) additions) ----
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
+__global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
                                                        jac<F>* __restrict__ out_jac) {
   const uint32_t gw = blockIdx.x * blockDim.x + threadIdx.x;
   if (gw >= ngw) return;
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(64) k_msm_window_seq(uint32_t ngw, int c, cons
 }
 
 // ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
-__global__ void __launch_bounds__(64) k_msm_horner(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
+__global__ void SSB_LB(64) k_msm_horner(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
                                                    g1_aff* __restrict__ out) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngroups) return;
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(64) k_msm_horner(int ngroups, int c, int W, co
 
 // per-share G1 RLC product (the G1 side when the roots' groups are small: 64 doublings per share
 // beat a per-root bucket MSM whose window reduce / Horner overheads dominate at ~256 shares/root)
-__global__ void __launch_bounds__(64) k_rlc_pk(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(64) k_rlc_pk(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
                                                const uint32_t* __restrict__ pflags, const g1_aff* __restrict__ pk_aff,
                                                g1_jac* __restrict__ rpk) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(64) k_rlc_pk(int n, uint64_t seed, const uint3
 }
 
 // subgroup check of every decodable signature (psi(P) == [x]P, sig_groupcheck)
-__global__ void __launch_bounds__(64) k_subgroup(int n, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(64) k_subgroup(int n, const uint32_t* __restrict__ sflags,
                                                  const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;

@@ -9,7 +9,7 @@ namespace ssb {
 namespace k {
 
 constexpr int WAVE_MILLER_SLOTS = wave::S_USER + 30;
-__global__ void __launch_bounds__(64) k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
+__global__ void SSB_LB(64) k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
                                                     const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
                                                     fp12* __restrict__ f) {
   __shared__ fp slots[WAVE_MILLER_SLOTS];
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(64) k_miller_wave(int n_roots, const g1_aff* _
   if (lane == 0) { fp12 r; wave::load12(r, w, B); f[p] = r; }
 }
 constexpr int WAVE_FINAL_SLOTS = wave::S_USER + 12 * 10;
-__global__ void __launch_bounds__(64) k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok) {
+__global__ void SSB_LB(64) k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok) {
   __shared__ fp slots[WAVE_FINAL_SLOTS];
   const int lane = threadIdx.x;
   wave::ws w{slots};
@@ -54,7 +54,7 @@ constexpr int ML_S0 = lane::MILLER_ITER_SCRATCH > lane::MILLER_ADDSTEP_SCRATCH ?
                                                                                : lane::MILLER_ADDSTEP_SCRATCH;
 constexpr int ML_SLOTS = ML_S0 + 18 + 6;
 // pairs 0..n_roots-1: (sum_root r_i pk_i, H(root));  pair n_roots: (-g1, sum r_i sig_i)
-__global__ void __launch_bounds__(64) k_miller_lane(int n_roots, const g1_aff* __restrict__ root_sum,
+__global__ void SSB_LB(64) k_miller_lane(int n_roots, const g1_aff* __restrict__ root_sum,
                                                     const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
                                                     fp12* __restrict__ f) {
   using namespace ssb::lane;
@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(64) k_miller_lane(int n_roots, const g1_aff* _
 
 // one Miller loop per pair (P[p], Q[p]), one workgroup each: the roots' (S_r, H(root r)) and the
 // G2 MSM windows' ([2^(c w)](-g1), W_w)
-__global__ void __launch_bounds__(64) k_miller_pairs(int npairs, const g1_aff* __restrict__ Pa,
+__global__ void SSB_LB(64) k_miller_pairs(int npairs, const g1_aff* __restrict__ Pa,
                                                      const g2_aff* __restrict__ Qa, fp12* __restrict__ f) {
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + ML_SLOTS];
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(64) k_miller_pairs(int npairs, const g1_aff* _
 // on every hardware queue).
 constexpr int FB_S0 = ML_S0 > lane::FP12_MUL_SCRATCH ? ML_S0 : lane::FP12_MUL_SCRATCH;
 constexpr int FB_SLOTS = FB_S0 + 18 + 6 + 18 + 84;
-__global__ void __launch_bounds__(64) k_fallback_lane(int n, const uint32_t* __restrict__ ok,
+__global__ void SSB_LB(64) k_fallback_lane(int n, const uint32_t* __restrict__ ok,
                                                       const uint32_t* __restrict__ flags,
                                                       const uint32_t* __restrict__ share_root,
                                                       const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_aff,
@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(64) k_fallback_lane(int n, const uint32_t* __r
 }
 
 // out[w] = prod of in[8w .. 8w+7]
-__global__ void __launch_bounds__(64) k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out) {
+__global__ void SSB_LB(64) k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out) {
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + FP12_MUL_SCRATCH + 24];
   __shared__ uint32_t flg;
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(64) k_fp12_prod8(int n, const fp12* __restrict
 
 // product of the n values, then ONE final exponentiation -> batch verdict
 constexpr int FE_S0 = lane::FP12_MUL_SCRATCH;
-__global__ void __launch_bounds__(64) k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok) {
+__global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok) {
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + FE_S0 + 12 + 12 + 84];
   __shared__ uint32_t flg;

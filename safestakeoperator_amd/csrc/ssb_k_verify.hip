@@ -17,7 +17,7 @@ __global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const 
     if (share_root) share_root[s] = r;
   }
 }
-__global__ void __launch_bounds__(64) k_decode(int n, const uint8_t* __restrict__ sig96,
+__global__ void SSB_LB(64) k_decode(int n, const uint8_t* __restrict__ sig96,
                                                const uint8_t* __restrict__ pk48, int group_check,
                                                g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
                                                uint32_t* __restrict__ flags) {
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(64) k_decode(int n, const uint8_t* __restrict_
   if (pk48) pk_aff[s] = pk;
   flags[s] = fl;
 }
-__global__ void __launch_bounds__(64) k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
+__global__ void SSB_LB(64) k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
                                                 g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
                                                 uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(64) k_decode2(int n, const uint8_t* __restrict
 // decoded-public-key path (ssb_pk_cache_set): n lanes decode the signatures, the public keys are
 // gathered from the context's table of points decompressed once (lighthouse's PublicKey holds the
 // decompressed point too: the reference never decompresses a key per verification)
-__global__ void __launch_bounds__(64) k_decode_sig(int n, const uint8_t* __restrict__ sig96, g2_aff* __restrict__ sig_aff,
+__global__ void SSB_LB(64) k_decode_sig(int n, const uint8_t* __restrict__ sig96, g2_aff* __restrict__ sig_aff,
                                                    uint32_t* __restrict__ sflags) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(64) k_decode_sig(int n, const uint8_t* __restr
   sflags[g] = unit_decode_sig(sig, b);
   sig_aff[g] = sig;
 }
-__global__ void __launch_bounds__(256) k_pk_gather(int n, const uint32_t* __restrict__ pk_index, uint32_t n_cache,
+__global__ void SSB_LB(256) k_pk_gather(int n, const uint32_t* __restrict__ pk_index, uint32_t n_cache,
                                                    const g1_aff* __restrict__ cache_aff, const uint32_t* __restrict__ cache_flags,
                                                    g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ pflags) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(256) k_pk_gather(int n, const uint32_t* __rest
   if (i < n_cache) { pk_aff[s] = cache_aff[i]; pflags[s] = cache_flags[i]; }
   else pflags[s] = 0u;  // out-of-range index: the share cannot verify
 }
-__global__ void __launch_bounds__(64) k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
+__global__ void SSB_LB(64) k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
                                                   uint32_t* __restrict__ pflags) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(64) k_decode_pk(int n, const uint8_t* __restri
 // threads [0, n): G2 subgroup check; [n, 2n): r_i * sig_i; [2n, 3n): r_i * pk_i  (single lane each:
 // at C2 size the chip has spare waves, so the per-share chains run one per lane; the lane-group
 // versions in ssb_k_lane.hip cost ~6x the instructions for ~2x lower latency)
-__global__ void __launch_bounds__(64) k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(64) k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
                                                   const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
                                                   const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
                                                   g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
@@ -118,7 +118,7 @@ __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32
   if (share_root[s] >= n_roots) f &= ~FLAG_CANDIDATE;  // no H(root): the share cannot verify
   flags[s] = f;
 }
-__global__ void __launch_bounds__(SUM_THREADS) k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
+__global__ void SSB_LB(SUM_THREADS) k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
                                                                 const uint32_t* __restrict__ flags,
                                                                 const g1_jac* __restrict__ rpk,
                                                                 g1_aff* __restrict__ root_sum) {
@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(SUM_THREADS) k_sum_g1_by_root(int n, const uin
   }
   if (threadIdx.x == 0) { g1_aff a; jac_to_aff(a, acc); root_sum[b] = a; }
 }
-__global__ void __launch_bounds__(SUM_THREADS) k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
+__global__ void SSB_LB(SUM_THREADS) k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
                                                                 const g2_jac* __restrict__ rsig,
                                                                 g2_jac* __restrict__ part) {
   __shared__ g2_jac sh[SUM_THREADS];
@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(SUM_THREADS) k_sum_g2_partial(int n, const uin
   }
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
-__global__ void __launch_bounds__(64) k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
+__global__ void SSB_LB(64) k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
                                                      g2_aff* __restrict__ out) {
   __shared__ g2_jac sh[64];
   g2_jac acc; jac_set_inf(acc);
@@ -193,7 +193,7 @@ __global__ void k_root_scatter(int n, int n_roots, const uint32_t* __restrict__ 
 // blocks [n_roots, 2 n_roots): T_r = sum r_i sig_i (G2).  Affine outputs (infinity if none).
 // The summation order inside a segment is whatever the scatter produced: the affine sum is the
 // same group element either way, and jac_add is exact for every input.
-__global__ void __launch_bounds__(SEG_THREADS) k_sum_seg(int n_roots, const uint32_t* __restrict__ start,
+__global__ void SSB_LB(SEG_THREADS) k_sum_seg(int n_roots, const uint32_t* __restrict__ start,
                                                          const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
                                                          const uint32_t* __restrict__ flags, const g1_jac* __restrict__ rpk,
                                                          const g2_jac* __restrict__ rsig, g1_aff* __restrict__ s1,
