@@ -213,7 +213,9 @@ def main():
                     help="fraction of shares signed over the wrong root (the RLC batch fails; exact verdicts "
                          "come from the per-share fallback).  The headline is the all-valid C2 batch.")
     args = ap.parse_args()
-    set_hw_queues(args.pipeline * args.slot_streams + 4)
+    # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 3)
+    # + one for torch's own stream
+    set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "3") or 3))
 
     import numpy as np
     import torch

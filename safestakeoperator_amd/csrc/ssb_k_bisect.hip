@@ -1,0 +1,230 @@
+// ssb_k_bisect.hip -- kernels (gfx950): exact per-share verdicts after a failed RLC batch check,
+// by group testing instead of one pairing check per share.
+//
+// "on batch failure, bisect deterministically until each share's verdict equals
+// the single-verify result".  The shares of a failed batch are ordered by signing root (counting
+// sort) and tested in root-aligned groups on a 4-ary tree: level 0 holds groups of Gs_0 = 4^(L-1)
+// >= n shares (one group per root), level l groups of Gs_0 / 4^l, the last level single shares.
+// A group g of root r passes when
+//     e(sum_{i in g} k_i pk_i, H(r)) * e(-g1, sum_{i in g} k_i sig_i) == 1
+// with the batch's own odd 64-bit RLC scalars k_i: every candidate of a passing group gets verdict 1
+// (the batch check's soundness, 2^-63 per group); a failing single-share group is exactly the
+// reference's verify (k_i != 0 mod r), so it gets verdict 0.  Children of a passing group are not
+// tested; a group whose share range equals its failed parent's inherits the failure untested.
+// Work at 1% invalid shares (C2: 64 roots x 256): ~2.1k group checks instead of 16,384 per-share
+// checks.  Every kernel here is a no-op (uniform early exit) when the batch passed.
+#include "ssb_kernels.h"
+#include "ssb_wave.h"
+#include "ssb_lane_ops.h"
+
+namespace ssb {
+namespace k {
+
+// One workgroup: counting sort of the shares by root (cnt, start, perm) and the group starts of
+// every level (gst[l][r], n_roots + 1 words per level).  Phases separated by workgroup barriers
+// (global atomics and stores of one workgroup are ordered by them).
+constexpr int PREP_THREADS = 1024;
+__global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, int L, const uint32_t* __restrict__ ok,
+                                                        const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt,
+                                                        uint32_t* __restrict__ start, uint32_t* __restrict__ cursor,
+                                                        uint32_t* __restrict__ gst, uint32_t* __restrict__ perm) {
+  if (*ok) return;
+  const int t = threadIdx.x;
+  for (int r = t; r < n_roots; r += PREP_THREADS) cnt[r] = 0u;
+  __syncthreads();
+  for (int s = t; s < n; s += PREP_THREADS)
+    if (share_root[s] < (uint32_t)n_roots) atomicAdd(&cnt[share_root[s]], 1u);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (int r = 0; r < n_roots; ++r) { start[r] = acc; cursor[r] = acc; acc += cnt[r]; }
+  } else if (t <= L) {
+    const int l = t - 1;
+    const uint32_t lg = 2u * (uint32_t)(L - 1 - l);     // Gs_l = 2^lg
+    uint32_t* g = gst + (size_t)l * (n_roots + 1);
+    uint32_t acc = 0;
+    for (int r = 0; r < n_roots; ++r) {
+      g[r] = acc;
+      acc += (uint32_t)(((uint64_t)cnt[r] + (1ull << lg) - 1) >> lg);
+    }
+    g[n_roots] = acc;
+  }
+  __syncthreads();
+  for (int s = t; s < n; s += PREP_THREADS)
+    if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
+}
+// threads [0, n): rsig[s] = k_s sig_s;  [n, 2n): rpk[s] = k_s pk_s  (candidates only)
+__global__ void SSB_LB(64) k_fb_rlc(int n, uint64_t seed, const uint32_t* __restrict__ ok,
+                                   const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig_aff,
+                                   const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
+                                   g1_jac* __restrict__ rpk) {
+  if (*ok) return;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) {
+    if (flags[g] & FLAG_CANDIDATE) { g2_jac r; unit_rlc_sig(r, sig_aff[g], rlc_scalar_odd(seed, (uint64_t)g)); rsig[g] = r; }
+  } else if (g < 2 * n) {
+    const int s = g - n;
+    if (flags[s] & FLAG_CANDIDATE) { g1_jac r; unit_rlc_pk(r, pk_aff[s], rlc_scalar_odd(seed, (uint64_t)s)); rpk[s] = r; }
+  }
+}
+
+constexpr int BS_ML0 = lane::MILLER_ITER_SCRATCH > lane::MILLER_ADDSTEP_SCRATCH ? lane::MILLER_ITER_SCRATCH
+                                                                               : lane::MILLER_ADDSTEP_SCRATCH;
+constexpr int BS_S0 = BS_ML0 > lane::FP12_MUL_SCRATCH ? BS_ML0 : lane::FP12_MUL_SCRATCH;
+constexpr int BS_SLOTS = BS_S0 + 18 + 6 + 18 + 84;
+
+// One level of the group tree.  Workgroups (one wave) stride over the level's groups (control
+// flow uniform per group): sums of the group's k_i pk_i and k_i sig_i (lane-strided, LDS tree),
+// affine, then the two lane-program Miller loops, product, final exponentiation.  (A two-wave
+// variant running both Miller loops at once halved the resident workgroups and measured slower.)
+// gv_prev / gv_cur: per-group results of the previous / this level (1 pass, 0 fail).
+constexpr int LV_THREADS = 64;
+__global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int n_roots, const uint32_t* __restrict__ ok,
+                                              const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                                              const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst,
+                                              const uint32_t* __restrict__ flags, const g2_jac* __restrict__ rsig,
+                                              const g1_jac* __restrict__ rpk, const g2_aff* __restrict__ H,
+                                              const uint8_t* __restrict__ gv_prev, uint8_t* __restrict__ gv_cur,
+                                              uint8_t* __restrict__ verdict) {
+  using namespace ssb::lane;
+  if (*ok) return;  // uniform: the batch passed
+  __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
+  __shared__ g2_jac red[64];
+  __shared__ g1_aff sP;
+  __shared__ g2_aff sQ;
+  __shared__ uint32_t flg, ncand;
+  const int lane_ = threadIdx.x;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  lp_init_consts(g);
+  const int F1 = BS_S0, B = F1 + 18, F2 = B + 6, TMP = F2 + 18;
+  const uint32_t lg = 2u * (uint32_t)(L - 1 - l);
+  const uint64_t Gs = 1ull << lg;
+  const uint32_t* gl = gst + (size_t)l * (n_roots + 1);
+  const uint32_t ngroups = gl[n_roots];
+  for (uint32_t gid = blockIdx.x; gid < ngroups; gid += gridDim.x) {
+    // root of the group: the last r with gl[r] <= gid
+    int lo = 0, hi = n_roots;                  // invariant: gl[lo] <= gid < gl[hi]
+    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (gl[m] <= gid) lo = m; else hi = m; }
+    const int r = lo;
+    const uint32_t j = gid - gl[r];
+    const uint64_t seg_b = start[r], seg_e = seg_b + cnt[r];
+    const uint64_t a = seg_b + (uint64_t)j * Gs, b = a + Gs < seg_e ? a + Gs : seg_e;
+    if (l > 0) {
+      const uint32_t* gp = gst + (size_t)(l - 1) * (n_roots + 1);
+      const uint8_t pv = gv_prev[gp[r] + (j >> 2)];
+      if (pv) { if (lane_ == 0) gv_cur[gid] = 1; continue; }   // parent passed: verdicts written
+      // parent range [seg_b + (j/4) 4Gs, +4Gs) equals [a, b): inherit the failure untested
+      const uint64_t pa = seg_b + (uint64_t)(j >> 2) * (Gs << 2);
+      const uint64_t pb = pa + (Gs << 2) < seg_e ? pa + (Gs << 2) : seg_e;
+      if (pa == a && pb == b) {
+        if (lane_ == 0) gv_cur[gid] = 0;
+        if (lg == 0)
+          for (uint64_t k = a + lane_; k < b; k += 64) { const uint32_t s = perm[k]; if (flags[s] & FLAG_CANDIDATE) verdict[s] = 0; }
+        continue;
+      }
+    }
+    // sums over the group's candidates
+    if (lane_ == 0) ncand = 0u;
+    __syncthreads();
+    g2_jac acc2; jac_set_inf(acc2);
+    g1_jac acc1; jac_set_inf(acc1);
+    uint32_t nc = 0;
+    for (uint64_t k = a + lane_; k < b; k += 64) {
+      const uint32_t s = perm[k];
+      if (flags[s] & FLAG_CANDIDATE) { jac_add(acc2, acc2, rsig[s]); jac_add(acc1, acc1, rpk[s]); ++nc; }
+    }
+    if (nc) atomicAdd(&ncand, nc);
+    red[lane_] = acc2;
+    __syncthreads();
+    for (int w = 32; w > 0; w >>= 1) {
+      if (lane_ < w) { g2_jac o = red[lane_ + w]; jac_add(acc2, acc2, o); red[lane_] = acc2; }
+      __syncthreads();
+    }
+    if (lane_ == 0) { g2_aff q; jac_to_aff(q, acc2); sQ = q; }
+    __syncthreads();
+    g1_jac* red1 = (g1_jac*)red;
+    red1[lane_] = acc1;
+    __syncthreads();
+    for (int w = 32; w > 0; w >>= 1) {
+      if (lane_ < w) { g1_jac o = red1[lane_ + w]; jac_add(acc1, acc1, o); red1[lane_] = acc1; }
+      __syncthreads();
+    }
+    if (lane_ == 0) { g1_aff p; jac_to_aff(p, acc1); sP = p; }
+    __syncthreads();
+    bool pass = true;
+    if (ncand) {
+      const g1_aff P = sP;
+      const g2_aff Q = sQ;
+      if (!P.inf) {                            // e(S_pk, H(r)) before the final exponentiation
+        const g2_aff h = H[r];
+        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&h)[lane_];
+        if (lane_ == 4) g.s[B + 4] = P.x;
+        if (lane_ == 5) g.s[B + 5] = P.y;
+        __syncthreads();
+        f12_miller(g, F1, B);
+      } else {
+        const fp12 one = fp12_one();
+        if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&one)[lane_];
+        __syncthreads();
+      }
+      if (!Q.inf) {                            // e(-g1, S_sig)
+        const g1_aff ng = g1_neg_generator();
+        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
+        if (lane_ == 4) g.s[B + 4] = ng.x;
+        if (lane_ == 5) g.s[B + 5] = ng.y;
+        __syncthreads();
+        f12_miller(g, F2, B);
+        f12_mul(g, F1, F2, F1);
+      }
+      f12_final_exp(g, F1, TMP);
+      __syncthreads();
+      fp12 e;
+      ld12(e, g.s + F1);
+      pass = fp12_is_one(e);
+    }
+    if (lane_ == 0) gv_cur[gid] = pass ? 1 : 0;
+    if (pass || lg == 0)
+      for (uint64_t k = a + lane_; k < b; k += 64) {
+        const uint32_t s = perm[k];
+        if (flags[s] & FLAG_CANDIDATE) verdict[s] = pass ? 1 : 0;
+      }
+    __syncthreads();
+  }
+}
+
+}  // namespace k
+
+namespace launch {
+
+int fallback_levels(size_t n) {
+  int L = 1;
+  uint64_t gs = 1;
+  while (gs < n) { gs <<= 2; ++L; }
+  return L;
+}
+
+void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const uint32_t* ok, const uint32_t* flags,
+                     const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
+                     uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
+                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict) {
+  using namespace ssb::k;
+  if (n <= 0 || n_roots <= 0) return;
+  const int L = fallback_levels((size_t)n);
+  auto nb = [](size_t x, unsigned b) { return (unsigned)((x + b - 1) / b); };
+  hipLaunchKernelGGL(k_fb_prep, dim3(1), dim3(PREP_THREADS), 0, st, n, n_roots, L, ok, share_root, cnt, start, cursor,
+                     gst, perm);
+  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, seed, ok, flags, sig, pk, rsig, rpk);
+  for (int l = 0; l < L; ++l) {
+    const uint64_t gs = 1ull << (2 * (L - 1 - l));
+    const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;
+    const unsigned grid = (unsigned)(bound < 2048 ? bound : 2048);
+    uint8_t* cur = (l & 1) ? gv1 : gv0;
+    const uint8_t* prev = (l & 1) ? gv0 : gv1;
+    hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, n_roots, ok, (const uint32_t*)start,
+                       (const uint32_t*)cnt, (const uint32_t*)perm, (const uint32_t*)gst, flags, (const g2_jac*)rsig,
+                       (const g1_jac*)rpk, H, prev, cur, verdict);
+  }
+}
+
+}  // namespace launch
+}  // namespace ssb

@@ -144,6 +144,14 @@ void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
             const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum);
 // gflags[s] = DEC_IN_GROUP when signature s (decodable, not infinity) passes psi(P) == [x]P
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags);
+// Exact verdicts of a failed batch by group testing on a 4-ary tree of root-aligned share groups
+// (ssb_k_bisect.hip); no-op when *ok.  Workspace: cnt/start/cursor n_roots words, perm n words,
+// gst fallback_levels(n) * (n_roots + 1) words, rsig/rpk n points, gv0/gv1 n + n_roots bytes.
+int fallback_levels(size_t n);
+void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const uint32_t* ok, const uint32_t* flags,
+                     const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
+                     uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
+                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict);
 // exact single-lane recomputation of the shares whose lane-group stage raised exc
 void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
                 const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,

@@ -77,6 +77,11 @@ struct ssb_ctx {
   // hardware queue for the largest kernel it has run, so these stay on two queues instead of
   // every slot's.  spec: the speculative combines; tail: verdicts, exact fallback, exact combine.
   hipStream_t spec = nullptr, tail = nullptr;
+  // tail streams: slot i uses tails[i % ntails] (tails[0] == tail).  More than one lets the exact
+  // fallbacks of failed batches on different slots run concurrently (SSB_TAILS, default 3; a caller must give the process enough hardware queues -- slots + 5 -- or streams share queues and serialise).
+  static constexpr int MAX_TAILS = 4;
+  hipStream_t tails[MAX_TAILS] = {nullptr, nullptr, nullptr, nullptr};
+  int ntails = 3;
   // decoded public keys (ssb_pk_cache_set): affine points + DEC_* flags, indexed by the caller
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0;
 };
@@ -115,6 +120,8 @@ int ensure_ws(ssb_ctx* ctx, size_t bytes) {
   ctx->cur->ws_bytes = want;
   return SSB_OK;
 }
+
+hipStream_t slot_tail(ssb_ctx* ctx) { return ctx->tails[(int)(ctx->cur - ctx->sl) % ctx->ntails]; }
 
 int ensure_io(ssb_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->io_bytes) return SSB_OK;
@@ -214,6 +221,16 @@ bool g1_use_msm(size_t n, size_t n_roots) {
   if (e && !strcmp(e, "share")) return false;
   return n >= 128 * (n_roots ? n_roots : 1);
 }
+// Exact verdicts of a failed batch: group tests (default) or SSB_FALLBACK=share, one pairing check
+// per candidate share (kept for the tests and as the measured comparison).
+bool fallback_per_share() {
+  const char* e = getenv("SSB_FALLBACK");
+  return e && !strcmp(e, "share");
+}
+bool fallback_on_tail() {
+  const char* e = getenv("SSB_FB_STREAM");
+  return !(e && !strcmp(e, "slot"));
+}
 msm_plan plan_msm(size_t n, size_t n_roots) {
   msm_plan p;
   const size_t g1n = n_roots ? n_roots : 1;
@@ -241,6 +258,7 @@ struct verify_ws {
   uint32_t* order;                                                                 // buckets by count
   g2_jac* b2; g1_jac* b1; g1_jac* w1;                                              // MSM buckets / windows
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
+  g2_jac* rsig; uint32_t* gst; uint8_t* gv0; uint8_t* gv1;                         // failed-batch group tests
   size_t npairs;
 };
 // Miller values of the pairs plus the levels of the 8-ary product tree
@@ -259,7 +277,8 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up(p.n_ent * 4) + align_up(((size_t)p.g2.W << p.g2.c) * sizeof(g2_jac)) +
          align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
          align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
-         3 * align_up(n_roots * 4) + align_up(n * 4);
+         3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(n * sizeof(g2_jac)) +
+         align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
@@ -280,6 +299,9 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.rpk = c.take<g1_jac>(n);
   w.rcnt = c.take<uint32_t>(n_roots); w.rstart = c.take<uint32_t>(n_roots); w.rcur = c.take<uint32_t>(n_roots);
   w.perm = c.take<uint32_t>(n);
+  w.rsig = c.take<g2_jac>(n);
+  w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
+  w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
@@ -352,16 +374,29 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     }
     hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok);
   }
-  // verdicts (+ the exact per-share fallback when the batch failed) on the tail stream
-  if (tail != st) {
+  // verdicts (+ the exact fallback when the batch failed) on the slot's tail stream: its kernels
+  // have the largest private segments, and the runtime reserves scratch per hardware queue for the
+  // largest kernel the queue has run (on every slot stream, 12 slots ran out of resources).
+  // SSB_FB_STREAM=slot puts them on the slot's own stream (few slots only).
+  const bool fb_tail = fallback_on_tail();
+  hipStream_t fbs = fb_tail ? tail : st;
+  if (fb_tail && tail != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
     SSB_HIP(hipStreamWaitEvent(tail, ctx->cur->ev_fin, 0));
   }
   if (n) {
-    timed t(ctx, "k_fallback_verify", tail);
-    hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, tail, (int)n, w.ok, w.flags, d_verdict);
-    hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, tail, (int)n, w.ok, w.flags,
-                       d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
+    timed t(ctx, "k_fallback_verify", fbs);
+    hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, fbs, (int)n, w.ok, w.flags, d_verdict);
+    if (fallback_per_share())
+      hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, fbs, (int)n, w.ok, w.flags,
+                         d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
+    else
+      launch::fallback_bisect(fbs, (int)n, (int)n_roots, seed, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff,
+                              w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict);
+  }
+  if (!fb_tail && tail != st) {
+    SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
+    SSB_HIP(hipStreamWaitEvent(tail, ctx->cur->ev_fin, 0));
   }
   SSB_HIP(hipGetLastError());
   return SSB_OK;
@@ -384,6 +419,10 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   if (init_slot(ctx->sl[0], ctx->slot_streams) != SSB_OK) { delete ctx; return SSB_EHIP; }
   if (hipStreamCreateWithFlags(&ctx->spec, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx->sl[0]); delete ctx; return SSB_EHIP; }
+  ctx->tails[0] = ctx->tail;
+  if (const char* e = getenv("SSB_TAILS")) ctx->ntails = std::max(1, std::min(ssb_ctx::MAX_TAILS, atoi(e)));
+  for (int i = 1; i < ctx->ntails; ++i)
+    if (hipStreamCreateWithFlags(&ctx->tails[i], hipStreamNonBlocking) != hipSuccess) { ctx->ntails = i; break; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
@@ -408,6 +447,7 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->negg1_pow) hipFree(ctx->negg1_pow);
   if (ctx->pkc_aff) hipFree(ctx->pkc_aff);
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
+  for (int i = 1; i < ctx->ntails; ++i) if (ctx->tails[i]) { hipStreamSynchronize(ctx->tails[i]); hipStreamDestroy(ctx->tails[i]); }
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
@@ -550,7 +590,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
                 align_up(n * sizeof(g2_jac)) + align_up(n_jobs * 4);
   if ((rc = ensure_ws(ctx, need))) return rc;
   hipStream_t user = (hipStream_t)stream;
-  hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = ctx->tail;
+  hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = slot_tail(ctx);
   // order the engine's streams after the caller's stream, and the caller's stream after them
   hipEvent_t e_user;
   SSB_HIP(hipEventCreateWithFlags(&e_user, hipEventDisableTiming));
@@ -616,9 +656,10 @@ int verify_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint32_t* pk_i
   carve c{(char*)ctx->cur->ws};
   verify_ws w = carve_verify(c, n, n_roots);
   // root indices >= n_roots: those shares are skipped by the sums and get verdict 0
+  hipStream_t tl = slot_tail(ctx);
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, root_idx, roots32, d, rlc_seed, verdicts, [] {},
-                       ctx->tail))) return rc;
-  SSB_HIP(hipEventRecord(ctx->cur->ev_out, ctx->tail));
+                       tl))) return rc;
+  SSB_HIP(hipEventRecord(ctx->cur->ev_out, tl));
   ctx->cur->out_pending = true;
   SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
   return SSB_OK;
@@ -669,6 +710,7 @@ int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) SSB_HIP(hipStreamSynchronize(x));
+  for (int i = 1; i < ctx->ntails; ++i) SSB_HIP(hipStreamSynchronize(ctx->tails[i]));
   if (ctx->pkc_aff) { hipFree(ctx->pkc_aff); ctx->pkc_aff = nullptr; }
   if (ctx->pkc_flags) { hipFree(ctx->pkc_flags); ctx->pkc_flags = nullptr; }
   ctx->pkc_n = 0;

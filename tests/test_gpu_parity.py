@@ -163,11 +163,13 @@ def test_c2_full_size_properties(engine, g1_path, monkeypatch):
         assert B.verify(pks[v * n], sigs[v * n], roots[jr[v]])
 
 
-@pytest.mark.parametrize("g1_path", ["share", "msm"])
-def test_c2_invalid_injection_exact_verdicts(engine, g1_path, monkeypatch):
+@pytest.mark.parametrize("g1_path,fallback", [("share", "bisect"), ("msm", "bisect"), ("share", "share")])
+def test_c2_invalid_injection_exact_verdicts(engine, g1_path, fallback, monkeypatch):
     """1% invalid shares (signature over another root): the RLC batch fails, the fallback gives
-    exact per-share verdicts, and jobs still combine from the first t valid shares."""
+    exact per-share verdicts (group tests on the 4-ary root-aligned tree, or SSB_FALLBACK=share:
+    one pairing check per share), and jobs still combine from the first t valid shares."""
     monkeypatch.setenv("SSB_G1_PATH", g1_path)
+    monkeypatch.setenv("SSB_FALLBACK", fallback)
     V, t, n = 512, 3, 4
     roots, master, sigs, pks, ids, jr, msig = _gen_committees(engine, V, t, n, 8, seed=11)
     rng = np.random.default_rng(5)
@@ -181,6 +183,53 @@ def test_c2_invalid_injection_exact_verdicts(engine, g1_path, monkeypatch):
     expect = np.ones(V * n, dtype=np.uint8)
     expect[bad] = 0
     assert (ver == expect).all()
+    for v in range(V):
+        valid = int(expect[v * n:(v + 1) * n].sum())
+        if valid >= t:
+            assert st[v] == 0 and out[v].tobytes() == msig[v]
+        else:
+            assert st[v] == 4 and list(err[v]) == [valid, t]
+
+
+@pytest.mark.parametrize("pattern", ["all_invalid", "one_root_invalid", "adjacent_pairs", "mixed_garbage", "last_share"])
+def test_bisect_fallback_patterns(engine, pattern, monkeypatch):
+    """Group-test fallback (ssb_k_bisect.hip) on the patterns that stress the tree: every share
+    invalid (every group fails down to single shares), one whole root invalid (its subtree only),
+    adjacent invalid pairs (siblings in one 4-group), undecodable / infinity / swapped
+    shares mixed in (non-candidates never enter a group sum), a single invalid last share.
+    Verdicts must equal the per-share truth exactly."""
+    monkeypatch.setenv("SSB_FALLBACK", "bisect")
+    V, t, n, R = 300, 3, 4, 5                                   # ragged roots: 300 % 5 == 0 but n*V/R = 240
+    roots, master, sigs, pks, ids, jr, msig = _gen_committees(engine, V, t, n, R, seed=31)
+    N = V * n
+    share_root = [jr[v] for v in range(V) for _ in range(n)]
+    other = [hashlib.sha256(b"other%d" % r).digest() for r in range(R)]
+    expect = np.ones(N, dtype=np.uint8)
+    if pattern == "all_invalid":
+        bad = list(range(N))
+    elif pattern == "one_root_invalid":
+        bad = [i for i in range(N) if share_root[i] == 2]
+    elif pattern == "adjacent_pairs":
+        bad = [i for i in range(0, N, 97)] + [i + 1 for i in range(0, N - 1, 97)]
+    elif pattern == "last_share":
+        bad = [N - 1]
+    else:
+        bad = list(range(5, N, 151))
+    sigs = list(sigs)
+    if bad:
+        wrong = engine.sign_batch([7 + i for i in range(len(bad))], [share_root[i] for i in bad], other)
+        for k, i in enumerate(bad):
+            sigs[i] = wrong[k]
+            expect[i] = 0
+    jr2 = list(jr)
+    if pattern == "mixed_garbage":
+        sigs[17] = b"\xff" * 96                                   # does not decode
+        sigs[40] = bytes([0xc0]) + bytes(95)                       # infinity
+        sigs[41] = sigs[44]                                        # valid point, wrong key: invalid
+        expect[[17, 40, 41]] = 0
+    offs = list(range(0, N + 1, n))
+    out, st, err, ver = engine.threshold_aggregate_batch_raw([t] * V, offs, b"".join(sigs), b"".join(pks), ids, jr2, roots)
+    assert (ver == expect).all(), np.nonzero(ver != expect)[0][:20]
     for v in range(V):
         valid = int(expect[v * n:(v + 1) * n].sum())
         if valid >= t:
