@@ -41,6 +41,20 @@ MAD_PEAK_MEASURED = 3.8235e13  # v_mad_u64_u32/s, profiles/r01_madpeak.json (16 
 MAD_PEAK_ISSUE = 256 * 4 * 16 * 2.4e9  # 16 lanes/clk/SIMD (wave64 mad = 4 cycles) x 1024 SIMDs x 2.4 GHz
 
 
+# Per-GPU workloads of BASELINE.json's configs.  One step = one batch of the config.
+#   C2  configs[1]: 4,096 validators x 4 shares (3-of-4), 64 roots -- the headline
+#   C3  configs[2]: 65,536 validators, 3-of-4 and 5-of-7, one batch
+#   C4  configs[3]: 1,048,576 attestation shares over 8 GPUs -> 131,072 shares (32,768 x 4) per GPU
+#   C5  configs[4]: 1M validators x 13 shares (10-of-13) over 8 GPUs -> 131,072 validators per GPU
+CONFIGS = {
+    "C2": dict(validators=4096, threshold=3, operators=4, roots=64, pipeline=12),
+    "C3_3of4": dict(validators=65536, threshold=3, operators=4, roots=64, pipeline=3),
+    "C3_5of7": dict(validators=65536, threshold=5, operators=7, roots=64, pipeline=3),
+    "C4_per_gpu": dict(validators=32768, threshold=3, operators=4, roots=64, pipeline=4),
+    "C5_per_gpu": dict(validators=131072, threshold=10, operators=13, roots=64, pipeline=2),
+}
+
+
 def opcount_mads():
     with open(os.path.join(ROOT, "bench_tools", "opcount.json")) as f:
         oc = json.load(f)
@@ -138,19 +152,25 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0):
     def h(*parts):
         return int.from_bytes(hashlib.sha256(seed + b"".join(parts)).digest(), "little") % R_ORDER
 
-    share_sk, ids, share_root, jr, master = [], [], [], [], []
+    import numpy as np
+    # Shamir shares by Horner over r, vectorised over validators (object arrays of Python ints)
+    coef = np.empty((V, t), dtype=object)
     for v in range(V):
         vb = v.to_bytes(4, "little")
-        coeffs = [h(b"sk", vb)] + [h(b"c", vb, k.to_bytes(4, "little")) for k in range(1, t)]
-        master.append(coeffs[0])
-        for i in range(1, n + 1):
-            acc = 0
-            for c in reversed(coeffs):
-                acc = (acc * i + c) % R_ORDER
-            share_sk.append(acc)
-            ids.append(i)
-            share_root.append(v % n_roots)
-        jr.append(v % n_roots)
+        coef[v, 0] = h(b"sk", vb)
+        for k in range(1, t):
+            coef[v, k] = h(b"c", vb, k.to_bytes(4, "little"))
+    master = coef[:, 0].tolist()
+    shares = np.empty((V, n), dtype=object)
+    for i in range(1, n + 1):
+        acc = coef[:, t - 1].copy()
+        for k in range(t - 2, -1, -1):
+            acc = (acc * i + coef[:, k]) % R_ORDER
+        shares[:, i - 1] = acc
+    share_sk = shares.reshape(-1).tolist()
+    ids = list(range(1, n + 1)) * V
+    jr = [v % n_roots for v in range(V)]
+    share_root = [r for r in jr for _ in range(n)]
     bad = [i for i in range(len(share_sk))
            if invalid_rate > 0 and int.from_bytes(hashlib.sha256(seed + b"bad" + i.to_bytes(4, "little")).digest()[:8],
                                                    "little") < invalid_rate * 2.0 ** 64]
@@ -198,11 +218,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--validators", type=int, default=4096)
-    ap.add_argument("--threshold", type=int, default=3)
-    ap.add_argument("--operators", type=int, default=4)
-    ap.add_argument("--roots", type=int, default=64)
-    ap.add_argument("--pipeline", type=int, default=12, help="independent batches in flight (engine pipeline slots)")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                    help="BASELINE.json workload per GPU (the headline is C2; the others are reported under profiles/)")
+    ap.add_argument("--validators", type=int, default=None)
+    ap.add_argument("--threshold", type=int, default=None)
+    ap.add_argument("--operators", type=int, default=None)
+    ap.add_argument("--roots", type=int, default=None)
+    ap.add_argument("--pipeline", type=int, default=None, help="independent batches in flight (engine pipeline slots)")
     ap.add_argument("--slot-streams", type=int, default=1, choices=(1, 3),
                     help="streams per slot (1: batch in order on one queue; 3: hash / G1 side overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -213,6 +235,10 @@ def main():
                     help="fraction of shares signed over the wrong root (the RLC batch fails; exact verdicts "
                          "come from the per-share fallback).  The headline is the all-valid C2 batch.")
     args = ap.parse_args()
+    preset = CONFIGS[args.config]
+    for k in ("validators", "threshold", "operators", "roots", "pipeline"):
+        if getattr(args, k) is None:
+            setattr(args, k, preset[k])
     # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 3)
     # + one for torch's own stream
     set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "3") or 3))
@@ -396,8 +422,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u32-limb modular integer (BLS12-381 Fp/Fr)",
             "data": "synthetic (deterministic keys, GPU-signed shares)",
-            "config": {"workload": "C2: %d validators x %d shares (%d-of-%d), %d roots per GPU; verify + combine"
-                                   % (V, n, t, n, n_roots),
+            "config": {"workload": "%s: %d validators x %d shares (%d-of-%d), %d roots per GPU; verify + combine"
+                                   % (args.config, V, n, t, n, n_roots),
                        "validators_per_gpu": V, "threshold": t, "operators": n, "roots": n_roots,
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
                        "batches_in_flight": S, "streams_per_slot": args.slot_streams},
