@@ -7,3 +7,4 @@ from .threshold import (  # noqa: F401
     DST, INFINITY_SIGNATURE, DvfError, DifferentLength, InsufficientSignatures, InvalidOperatorId,
     InsufficientValidSignatures, BadSignatureEncoding, Engine, ThresholdJob, ThresholdSignature,
 )
+from .collector import SlotCollector  # noqa: F401,E402
