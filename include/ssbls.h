@@ -17,6 +17,10 @@
  *   ssb_hash_to_g2                 <- the hash_to_G2 blst runs inside verify/sign with the DST of
  *                                     src/crypto/impls/blst.rs:11
  *   ssb_lagrange_coeffs            <- lagrange_coeffs (src/crypto/impls/blst.rs:19-39)
+ *   ssb_decode_wire_sigs           <- bincode::deserialize::<Signature>(&data) on a received
+ *                                     partial signature (src/validation/operator.rs:108; the
+ *                                     records are written by bincode::serialize(&sig),
+ *                                     src/node/dvfcore.rs:245-251), batched
  *
  * Conventions
  *   - Signatures are 96-byte compressed G2 points, public keys 48-byte compressed G1 points
@@ -90,6 +94,18 @@ int ssb_kernel_timing(ssb_ctx* ctx, int on);
 int ssb_kernel_time(ssb_ctx* ctx, const char* kernel_name, float* total_ms, int* launches);
 
 /* hash_to_G2 of n 32-byte messages; out: n x 192 bytes (blst_p2_serialize layout). */
+/* Wire-format partial signatures -> 96-byte compressed signatures.  Record i (at wire + i*stride,
+ * stride >= 202) is bincode(bls::Signature): u64 LE length 194, then "0x" and 192 hex digits of the
+ * compressed point.  status[i]: 0 ok, 1 length field is not 194, 2 no "0x" prefix, 3 a non-hex
+ * digit (out96[i] is then meaningless; the reference drops such a record -- "Deserialize failed",
+ * operator.rs:113 -- so a caller leaves that share out of its job).  The point itself is checked
+ * later, by the verify/aggregate entry points (decompression, subgroup check). */
+int ssb_decode_wire_sigs(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96,
+                         int32_t* status);
+/* device pointers, enqueued on `stream` (hipStream_t as void*), no synchronisation */
+int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96,
+                             int32_t* status, void* stream);
+
 int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* dst, size_t dst_len,
                    uint8_t* out192);
 

@@ -825,3 +825,25 @@ def poly_eval(coeffs, x):
 def key_split(sk: int, coeffs_tail, ids):
     coeffs = [sk] + list(coeffs_tail)
     return {i: poly_eval(coeffs, i) for i in ids}
+
+
+# ---- wire format of a partial signature ----
+# bincode::serialize(&sig) (src/node/dvfcore.rs:245-251) of lighthouse's bls::Signature, whose serde
+# form is the string "0x" + lowercase hex of the 96-byte compressed point; bincode 1.x (fixint,
+# little endian) writes a string as a u64 length and the bytes.  (The lighthouse serde macro is
+# upstream, not in the reference tree: this layout follows SURVEY.md §8a-6.)
+def bincode_signature(sig96: bytes) -> bytes:
+    s = b"0x" + sig96.hex().encode()
+    return len(s).to_bytes(8, "little") + s
+
+
+def bincode_signature_decode(rec: bytes):
+    """(status, sig96 or None): 0 ok, 1 length field not 194, 2 no "0x", 3 non-hex digit."""
+    if int.from_bytes(rec[:8], "little") != 194:
+        return 1, None
+    if rec[8:10] != b"0x":
+        return 2, None
+    try:
+        return 0, bytes.fromhex(rec[10:204].decode("ascii"))
+    except ValueError:
+        return 3, None

@@ -152,6 +152,9 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const ui
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
                      uint8_t* gv0, uint8_t* gv1, uint8_t* verdict);
+// wire-format records bincode(bls::Signature) -> 96-byte compressed signatures (ssb_k_wire.hip)
+constexpr size_t WIRE_SIG_BYTES = 202;
+void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status);
 // exact single-lane recomputation of the shares whose lane-group stage raised exc
 void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
                 const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,

@@ -539,6 +539,40 @@ int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t*
   return SSB_OK;
 }
 
+int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status,
+                             void* stream) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!wire || !out96 || !status || stride < launch::WIRE_SIG_BYTES || n > (size_t)INT32_MAX) {
+    ctx->err = "null pointer, stride < 202 or n too large"; return SSB_EINVAL;
+  }
+  SSB_HIP(hipSetDevice(ctx->device));
+  launch::wire_sig((hipStream_t)stream, (int)n, wire, stride, out96, status);
+  SSB_HIP(hipGetLastError());
+  return SSB_OK;
+}
+
+int ssb_decode_wire_sigs(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!wire || !out96 || !status || stride < launch::WIRE_SIG_BYTES || n > (size_t)INT32_MAX) {
+    ctx->err = "null pointer, stride < 202 or n too large"; return SSB_EINVAL;
+  }
+  SSB_HIP(hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = ensure_ws(ctx, align_up(n * stride) + align_up(n * 96) + align_up(n * 4)))) return rc;
+  carve c{(char*)ctx->cur->ws};
+  uint8_t* d_in = c.take<uint8_t>(n * stride); uint8_t* d_out = c.take<uint8_t>(n * 96); int32_t* d_st = c.take<int32_t>(n);
+  hipStream_t st = ctx->cur->stream;
+  SSB_HIP(hipMemcpyAsync(d_in, wire, n * stride, hipMemcpyHostToDevice, st));
+  { timed t(ctx, "k_wire_sig"); launch::wire_sig(st, (int)n, d_in, stride, d_out, d_st); }
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(out96, d_out, n * 96, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipMemcpyAsync(status, d_st, n * 4, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
 int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t* sig96, const uint32_t* root_idx,
                      size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
                      uint8_t* verdicts) {

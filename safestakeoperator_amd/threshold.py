@@ -25,6 +25,7 @@ import numpy as np
 
 from . import _lib
 
+WIRE_SIG_BYTES = 202   # bincode(bls::Signature): u64 length 194 + "0x" + 192 hex digits
 DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"  # src/crypto/impls/blst.rs:11
 INFINITY_SIGNATURE = bytes([0xC0]) + bytes(95)          # bls::INFINITY_SIGNATURE
 
@@ -166,6 +167,23 @@ class Engine:
         self._check(self._lib.ssb_hash_to_g2(self._h, n, m.ctypes.data_as(_lib._u8p), dp, len(dst),
                                              out.ctypes.data_as(_lib._u8p)), "ssb_hash_to_g2")
         return [out[192 * i:192 * (i + 1)].tobytes() for i in range(n)]
+
+    def decode_wire_sigs(self, records: Sequence[bytes]) -> List[Optional[bytes]]:
+        """bincode(bls::Signature) records (202 bytes each, src/node/dvfcore.rs:245-251) -> the
+        96-byte compressed signatures, None where the record does not parse (the reference's
+        "Deserialize failed" at src/validation/operator.rs:113 drops that share)."""
+        n = len(records)
+        if n == 0:
+            return []
+        if any(len(r) != WIRE_SIG_BYTES for r in records):
+            raise ValueError("wire records are %d bytes" % WIRE_SIG_BYTES)
+        w = np.frombuffer(b"".join(records), dtype=np.uint8)
+        out = np.zeros(96 * n, dtype=np.uint8)
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self._lib.ssb_decode_wire_sigs(self._h, n, w.ctypes.data_as(_lib._u8p), WIRE_SIG_BYTES,
+                                                   out.ctypes.data_as(_lib._u8p), st.ctypes.data_as(_lib._i32p)),
+                    "ssb_decode_wire_sigs")
+        return [out[96 * i:96 * (i + 1)].tobytes() if st[i] == 0 else None for i in range(n)]
 
     def verify_batch(self, pks: Sequence[bytes], sigs: Sequence[bytes], root_idx: Sequence[int],
                      roots: Sequence[bytes], seed: int = 0x5AFE57A4E, dst: bytes = DST) -> np.ndarray:

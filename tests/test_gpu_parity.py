@@ -362,3 +362,31 @@ def test_combined_verify_on_device(engine):
     expect = np.ones(V, dtype=np.uint8)
     expect[[10, 11, 20]] = 0
     assert (d_ver.cpu().numpy() == expect).all()
+
+
+def test_wire_decode_matches_oracle(engine):
+    """§8f-2: bincode(bls::Signature) records decoded on the GPU == the oracle's codec, including
+    upper-case hex, a wrong length field, a missing prefix and a non-hex digit; the decoded bytes
+    feed the aggregate and give the golden combine."""
+    from oracle import bls12_381 as B
+    cases = [c for c in _load("threshold_cases.json")["cases"] if c["expected_status"] == 0]
+    c = cases[0]
+    sigs = [bytes.fromhex(s) for s in c["sigs"]]
+    recs = [B.bincode_signature(s) for s in sigs]
+    up = bytearray(recs[0]); up[10:] = up[10:].upper()
+    bad_len = bytearray(recs[0]); bad_len[0] = 193
+    bad_pre = bytearray(recs[0]); bad_pre[9] = ord("X")
+    bad_hex = bytearray(recs[0]); bad_hex[50] = ord("g")
+    extra = [bytes(up), bytes(bad_len), bytes(bad_pre), bytes(bad_hex)]
+    out = engine.decode_wire_sigs(recs + extra)
+    for r, o in zip(recs + extra, out):
+        st, want = B.bincode_signature_decode(r)
+        assert (o is None) == (st != 0) and (st != 0 or o == want)
+    assert out[:len(sigs)] == sigs and out[len(sigs)] == sigs[0]
+    ts = ThresholdSignature(c["t"], engine)
+    got = ts.threshold_aggregate(out[:len(sigs)], [bytes.fromhex(p) for p in c["pks"]], c["ids"], bytes.fromhex(c["root"]))
+    assert got.hex() == c["master_sig"]
+    # full C2-size batch of records
+    rng = np.random.default_rng(9)
+    many = [bytes(rng.integers(0, 256, 96, dtype=np.uint8)) for _ in range(16384)]
+    assert engine.decode_wire_sigs([B.bincode_signature(s) for s in many]) == many

@@ -100,3 +100,16 @@ def test_decode_rejections():
     assert pytest.raises(B.DecodeError, B.g2_decompress, bytes(96))           # no compression flag
     assert pytest.raises(B.DecodeError, B.g2_decompress, bytes([0xE0]) + bytes(95))  # infinity + sign
     assert B.g2_decompress(bytes([0xC0]) + bytes(95)) is None
+
+
+def test_wire_codec_roundtrip():
+    """bincode(bls::Signature) layout (SURVEY.md §8a-6): 8-byte LE length 194, "0x", 192 hex digits."""
+    from oracle import bls12_381 as B
+    sig = bytes(range(96))
+    rec = B.bincode_signature(sig)
+    assert len(rec) == 202 and rec[:8] == (194).to_bytes(8, "little") and rec[8:10] == b"0x"
+    assert B.bincode_signature_decode(rec) == (0, sig)
+    assert B.bincode_signature_decode(rec[:10] + rec[10:].upper()) == (0, sig)
+    assert B.bincode_signature_decode(b"\x00" + rec[1:])[0] == 1
+    assert B.bincode_signature_decode(rec[:9] + b"X" + rec[10:])[0] == 2
+    assert B.bincode_signature_decode(rec[:20] + b"z" + rec[21:])[0] == 3
