@@ -239,6 +239,12 @@ def main():
     for k in ("validators", "threshold", "operators", "roots", "pipeline"):
         if getattr(args, k) is None:
             setattr(args, k, preset[k])
+    # Hardware queues: on one MI355X, 17 queues ran at full speed, 19 lost a third of the throughput
+    # and 21 collapsed (the firmware time-slices queues beyond what it maps at once).  With N > 1
+    # the process group adds a stream of its own, so multi-GPU runs use one tail stream (the exact
+    # fallback's concurrency across slots is not exercised by all-valid batches).
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "SSB_TAILS" not in os.environ:
+        os.environ["SSB_TAILS"] = "1"
     # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 3)
     # + one for torch's own stream
     set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "3") or 3))
