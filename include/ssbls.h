@@ -17,6 +17,9 @@
  *   ssb_hash_to_g2                 <- the hash_to_G2 blst runs inside verify/sign with the DST of
  *                                     src/crypto/impls/blst.rs:11
  *   ssb_lagrange_coeffs            <- lagrange_coeffs (src/crypto/impls/blst.rs:19-39)
+ *   ssb_feldman_verify_batch       <- DKG::share_verification (src/crypto/dkg.rs:433-450):
+ *                                     blst_p1_mult(h, s) == CommittedPoly::eval(party)
+ *                                     (src/math/polynomial.rs:68-81), batched
  *   ssb_decode_wire_sigs           <- bincode::deserialize::<Signature>(&data) on a received
  *                                     partial signature (src/validation/operator.rs:108; the
  *                                     records are written by bincode::serialize(&sig),
@@ -94,6 +97,15 @@ int ssb_kernel_timing(ssb_ctx* ctx, int on);
 int ssb_kernel_time(ssb_ctx* ctx, const char* kernel_name, float* total_ms, int* launches);
 
 /* hash_to_G2 of n 32-byte messages; out: n x 192 bytes (blst_p2_serialize layout). */
+/* DKG / VSS share verification: verdicts[i] = ([s_i]h == C_{i,0} + sum_{k>=1} [ids[i]^k mod r] C_{i,k}).
+ * commitments48: n * t compressed G1 points (check i's polynomial commitments C_{i,0..t-1}, as
+ * CommittedPoly::to_bytes without its u32 count); shares32: n 32-byte LITTLE-endian scalars
+ * (bytes_to_blst_scalar; the low 255 bits are used, as blst_p1_mult(.., 255)); h48: the
+ * commitment base (the reference's another_p1_generator(), hash_to_G1 of "dvf another
+ * generator"), compressed.  A commitment or h that does not decode gives verdict 0. */
+int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* commitments48, const uint64_t* ids,
+                             const uint8_t* shares32, const uint8_t* h48, uint8_t* verdicts);
+
 /* Wire-format partial signatures -> 96-byte compressed signatures.  Record i (at wire + i*stride,
  * stride >= 202) is bincode(bls::Signature): u64 LE length 194, then "0x" and 192 hex digits of the
  * compressed point.  status[i]: 0 ok, 1 length field is not 194, 2 no "0x" prefix, 3 a non-hex

@@ -847,3 +847,21 @@ def bincode_signature_decode(rec: bytes):
         return 0, bytes.fromhex(rec[10:204].decode("ascii"))
     except ValueError:
         return 3, None
+
+
+# ---- DKG / VSS share verification ----
+def committed_poly_eval(commitments, x: int):
+    """CommittedPoly::eval (src/math/polynomial.rs:68-81): C_0 + sum_{i>=1} [x^i mod r] C_i with
+    x^i accumulated by blst_sk_mul_n_check (mod r)."""
+    y = commitments[0]
+    xp = x % R
+    for c in commitments[1:]:
+        y = g1_add(y, g1_mul(c, xp))
+        xp = xp * x % R
+    return y
+
+
+def feldman_share_verify(h, share: int, commitments, party: int) -> bool:
+    """DKG share_verification (src/crypto/dkg.rs:433-450): blst_p1_mult(h, s) (255-bit scalar, s
+    from LE bytes; blst reads its low 255 bits) == committed_poly.eval(party)."""
+    return g1_mul(h, share & ((1 << 255) - 1)) == committed_poly_eval(commitments, party)

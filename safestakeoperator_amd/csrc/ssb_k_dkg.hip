@@ -1,0 +1,80 @@
+// ssb_k_dkg.hip -- kernels (gfx950): batched DKG / VSS share verification.
+//
+// DKG::share_verification (src/crypto/dkg.rs:433-450) checks, per received share,
+//     blst_p1_mult(h, s) == CommittedPoly::eval(party)
+// with eval = C_0 + sum_{i>=1} [x^i mod r] C_i (src/math/polynomial.rs:68-81).  Here one thread
+// per check: [s]h by a 4-bit fixed window over the low 255 bits of s (blst_p1_mult's nbits = 255),
+// and the evaluation by Horner in the group, acc = [x] acc + C_i for i = t-1 .. 0 -- the same
+// group element, since every C_i has order r and the integer x^i equals x^i mod r on it.
+// Commitments arrive compressed (CommittedPoly::to_bytes, polynomial.rs:88-99 without the count
+// prefix); one that does not decode makes the check fail.  Registration-time work, rare: plain
+// single-lane code.
+#include "ssb_kernels.h"
+
+namespace ssb {
+namespace k {
+
+// [x]P for a Jacobian P and a 64-bit x (binary, from the top set bit)
+SSB_FN void g1_mul_u64_jac(g1_jac& r, const g1_jac& p, uint64_t x) {
+  g1_jac acc; jac_set_inf(acc);
+  for (int i = 63; i >= 0; --i) {
+    if (!jac_is_inf(acc)) jac_dbl(acc, acc);
+    if ((x >> i) & 1ull) jac_add(acc, acc, p);
+  }
+  r = acc;
+}
+
+SSB_INL bool g1_jac_eq(const g1_jac& a, const g1_jac& b) {
+  const bool ia = jac_is_inf(a), ib = jac_is_inf(b);
+  if (ia || ib) return ia && ib;
+  fp za2, zb2, za3, zb3, l, r;
+  fp_sqr(za2, a.z); fp_sqr(zb2, b.z);
+  fp_mul(l, a.x, zb2); fp_mul(r, b.x, za2);
+  if (!fp_eq(l, r)) return false;
+  fp_mul(za3, za2, a.z); fp_mul(zb3, zb2, b.z);
+  fp_mul(l, a.y, zb3); fp_mul(r, b.y, za3);
+  return fp_eq(l, r);
+}
+
+__global__ void SSB_LB(64) k_feldman_share(int n, int t, const uint8_t* __restrict__ comm48, const uint64_t* __restrict__ x,
+                                          const uint8_t* __restrict__ s32le, const g1_aff* __restrict__ h,
+                                          const uint32_t* __restrict__ hflags, uint8_t* __restrict__ verdict) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t hf = *hflags;
+  if (!(hf & DEC_OK)) { verdict[i] = 0; return; }
+  bool ok = true;
+  g1_jac acc; jac_set_inf(acc);
+  for (int c = t - 1; c >= 0 && ok; --c) {
+    uint8_t b[48];
+    const uint8_t* src = comm48 + ((size_t)i * t + c) * 48;
+    for (int k2 = 0; k2 < 48; ++k2) b[k2] = src[k2];
+    g1_aff C;
+    const uint32_t st = g1_decompress(C, b);
+    if (!(st & DEC_OK)) { ok = false; break; }
+    if (c != t - 1) g1_mul_u64_jac(acc, acc, x[i]);
+    if (!C.inf) jac_add_aff(acc, acc, C);
+  }
+  if (!ok) { verdict[i] = 0; return; }
+  uint32_t k[8];
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* q = s32le + 32 * (size_t)i + 4 * w;
+    k[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  k[7] &= 0x7fffffffu;                          // 255 bits, as blst_p1_mult(.., 255)
+  g1_jac y;
+  if (hf & DEC_INF) jac_set_inf(y); else jac_mul_w4(y, *h, k, 8);
+  verdict[i] = g1_jac_eq(y, acc) ? 1 : 0;
+}
+
+}  // namespace k
+
+namespace launch {
+void feldman_share(hipStream_t st, int n, int t, const uint8_t* comm48, const uint64_t* x, const uint8_t* s32le,
+                   const g1_aff* h, const uint32_t* hflags, uint8_t* verdict) {
+  if (n > 0)
+    hipLaunchKernelGGL(k::k_feldman_share, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, t, comm48, x, s32le, h,
+                       hflags, verdict);
+}
+}  // namespace launch
+}  // namespace ssb

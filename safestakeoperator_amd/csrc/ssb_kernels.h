@@ -155,6 +155,9 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const ui
 // wire-format records bincode(bls::Signature) -> 96-byte compressed signatures (ssb_k_wire.hip)
 constexpr size_t WIRE_SIG_BYTES = 202;
 void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status);
+// DKG share verification (ssb_k_dkg.hip): verdict[i] = ([s_i]h == sum_k [x_i^k] C_{i,k})
+void feldman_share(hipStream_t st, int n, int t, const uint8_t* comm48, const uint64_t* x, const uint8_t* s32le,
+                   const g1_aff* h, const uint32_t* hflags, uint8_t* verdict);
 // exact single-lane recomputation of the shares whose lane-group stage raised exc
 void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
                 const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,

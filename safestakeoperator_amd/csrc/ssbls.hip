@@ -539,6 +539,34 @@ int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t*
   return SSB_OK;
 }
 
+int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* commitments48, const uint64_t* ids,
+                             const uint8_t* shares32, const uint8_t* h48, uint8_t* verdicts) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!commitments48 || !ids || !shares32 || !h48 || !verdicts || t == 0 || t > 1024 || n > (size_t)INT32_MAX) {
+    ctx->err = "null pointer, t not in [1, 1024] or n too large"; return SSB_EINVAL;
+  }
+  SSB_HIP(hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = ensure_ws(ctx, align_up(n * t * 48) + align_up(n * 8) + align_up(n * 32) + align_up(48) +
+                               align_up(sizeof(g1_aff)) + align_up(4) + align_up(n)))) return rc;
+  carve c{(char*)ctx->cur->ws};
+  uint8_t* d_c = c.take<uint8_t>(n * t * 48); uint64_t* d_x = c.take<uint64_t>(n); uint8_t* d_s = c.take<uint8_t>(n * 32);
+  uint8_t* d_h48 = c.take<uint8_t>(48); g1_aff* d_h = c.take<g1_aff>(1); uint32_t* d_hf = c.take<uint32_t>(1);
+  uint8_t* d_v = c.take<uint8_t>(n);
+  hipStream_t st = ctx->cur->stream;
+  SSB_HIP(hipMemcpyAsync(d_c, commitments48, n * t * 48, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_x, ids, n * 8, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_s, shares32, n * 32, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_h48, h48, 48, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_decode_pk, dim3(1), dim3(64), 0, st, 1, (const uint8_t*)d_h48, d_h, d_hf);
+  { timed tm(ctx, "k_feldman_share"); launch::feldman_share(st, (int)n, (int)t, d_c, d_x, d_s, d_h, d_hf, d_v); }
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
 int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status,
                              void* stream) {
   if (!ctx) return SSB_EINVAL;

@@ -168,6 +168,27 @@ class Engine:
                                              out.ctypes.data_as(_lib._u8p)), "ssb_hash_to_g2")
         return [out[192 * i:192 * (i + 1)].tobytes() for i in range(n)]
 
+    def feldman_verify_batch(self, commitments: Sequence[Sequence[bytes]], ids: Sequence[int],
+                             shares: Sequence[int], h48: bytes) -> List[bool]:
+        """DKG share_verification (src/crypto/dkg.rs:433-450) for n received shares: check i has
+        its dealer's t compressed commitments, this party's id and the decrypted share scalar."""
+        n = len(ids)
+        if n == 0:
+            return []
+        t = len(commitments[0])
+        if len(commitments) != n or len(shares) != n or any(len(c) != t for c in commitments):
+            raise ValueError("one commitment vector (all of length t) and one share per check")
+        cm = np.frombuffer(b"".join(b"".join(c) for c in commitments), dtype=np.uint8)
+        x = np.asarray(ids, dtype=np.uint64)
+        sv = np.frombuffer(b"".join(int(s).to_bytes(32, "little") for s in shares), dtype=np.uint8)
+        hp = np.frombuffer(bytes(h48), dtype=np.uint8)
+        v = np.zeros(n, dtype=np.uint8)
+        self._check(self._lib.ssb_feldman_verify_batch(self._h, n, t, cm.ctypes.data_as(_lib._u8p),
+                                                       x.ctypes.data_as(_lib._u64p), sv.ctypes.data_as(_lib._u8p),
+                                                       hp.ctypes.data_as(_lib._u8p), v.ctypes.data_as(_lib._u8p)),
+                    "ssb_feldman_verify_batch")
+        return [bool(b) for b in v]
+
     def decode_wire_sigs(self, records: Sequence[bytes]) -> List[Optional[bytes]]:
         """bincode(bls::Signature) records (202 bytes each, src/node/dvfcore.rs:245-251) -> the
         96-byte compressed signatures, None where the record does not parse (the reference's

@@ -390,3 +390,23 @@ def test_wire_decode_matches_oracle(engine):
     rng = np.random.default_rng(9)
     many = [bytes(rng.integers(0, 256, 96, dtype=np.uint8)) for _ in range(16384)]
     assert engine.decode_wire_sigs([B.bincode_signature(s) for s in many]) == many
+
+
+def test_feldman_share_verification_golden(engine):
+    """§8f-4: DKG share verification on the GPU == the oracle's verdicts (tests/golden/feldman.json:
+    t = 1, 3, 5; wrong share, wrong party, undecodable commitment, an infinity commitment, a 64-bit
+    id), one batch per t."""
+    d = _load("feldman.json")
+    h48 = bytes.fromhex(d["h"])
+    by_t = {}
+    for c in d["cases"]:
+        by_t.setdefault(c["t"], []).append(c)
+    for t, cs in by_t.items():
+        got = engine.feldman_verify_batch([[bytes.fromhex(x) for x in c["commitments"]] for c in cs],
+                                          [c["id"] for c in cs], [c["share"] for c in cs], h48)
+        assert got == [c["expect"] for c in cs], (t, got)
+    # larger batch: the valid t = 3 cases repeated 5,000 times
+    cs = [c for c in by_t[3] if c["kind"] == "valid"] * 5000
+    got = engine.feldman_verify_batch([[bytes.fromhex(x) for x in c["commitments"]] for c in cs],
+                                      [c["id"] for c in cs], [c["share"] for c in cs], h48)
+    assert all(got)

@@ -113,3 +113,19 @@ def test_wire_codec_roundtrip():
     assert B.bincode_signature_decode(b"\x00" + rec[1:])[0] == 1
     assert B.bincode_signature_decode(rec[:9] + b"X" + rec[10:])[0] == 2
     assert B.bincode_signature_decode(rec[:20] + b"z" + rec[21:])[0] == 3
+
+
+def test_feldman_fixture_consistent():
+    """tests/golden/feldman.json (make_feldman.py): valid shares verify, altered ones do not, and
+    the oracle's [s]h == CommittedPoly::eval(id) reproduces two cases from scratch."""
+    import json
+    import os
+    from oracle import bls12_381 as B
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "feldman.json")))
+    for c in d["cases"]:
+        # (a degree-0 polynomial verifies at every party)
+        assert c["expect"] == (c["kind"] in ("valid", "big_id") or (c["kind"] == "wrong_party" and c["t"] == 1))
+    h = B.g1_decompress(bytes.fromhex(d["h"]))
+    for c in (d["cases"][0], d["cases"][1]):
+        pts = [B.g1_decompress(bytes.fromhex(x)) for x in c["commitments"]]
+        assert B.feldman_share_verify(h, c["share"], pts, c["id"]) == c["expect"]
