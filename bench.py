@@ -228,6 +228,8 @@ def main():
     ap.add_argument("--slot-streams", type=int, default=1, choices=(1, 3),
                     help="streams per slot (1: batch in order on one queue; 3: hash / G1 side overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (RCCL, the measured path) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--compressed-pk", action="store_true",
                     help="headline on the compressed-public-key entry point (default: keys decompressed once, "
                          "ssb_pk_cache_set, as lighthouse's PublicKey holds them; the other variant is reported beside)")
@@ -255,13 +257,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # --dist-backend gloo: rehearsal of the N > 1 path on fewer GPUs than ranks (ranks share
+    # devices round robin, the collectives run on host copies); the measured path is RCCL.
+    gpu = local % max(1, torch.cuda.device_count()) if args.dist_backend == "gloo" else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
     else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")   # where collectives run
+    local = gpu
 
     from safestakeoperator_amd.build import build
     if rank == 0 or world == 1:
@@ -324,7 +334,8 @@ def main():
             if rc != 0:
                 raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
             if dist is not None:
-                exchange(o["ver"], o["out"], o["st"])  # RCCL all-gather over xGMI: the one exchange step
+                # RCCL all-gather over xGMI: the one exchange step
+                exchange(o["ver"].to(cdev), o["out"].to(cdev), o["st"].to(cdev))
 
     # phase 1: single-batch latency and per-kernel times (depth 1, no overlap between batches)
     # (latency configuration: 3 streams per slot, hash_to_G2 and the G1 side beside the main chain)
@@ -393,10 +404,10 @@ def main():
     elapsed = timed_run()
     ok_st = ok_comb = ok_head and ok_other
     if dist is not None:
-        tt = torch.tensor([elapsed, elapsed_other], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, elapsed_other], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, elapsed_other = float(tt[0].item()), float(tt[1].item())
-        okt = torch.tensor([1 if (ok_st and ok_comb) else 0], dtype=torch.int32, device=dev)
+        okt = torch.tensor([1 if (ok_st and ok_comb) else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_all = bool(okt.item())
     else:
