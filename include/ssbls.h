@@ -20,6 +20,7 @@
  *   ssb_feldman_verify_batch       <- DKG::share_verification (src/crypto/dkg.rs:433-450):
  *                                     blst_p1_mult(h, s) == CommittedPoly::eval(party)
  *                                     (src/math/polynomial.rs:68-81), batched
+ *   ssb_dleq_verify_batch          <- DKG::dleq_verify (src/crypto/dkg.rs:674-692), batched
  *   ssb_decode_wire_sigs           <- bincode::deserialize::<Signature>(&data) on a received
  *                                     partial signature (src/validation/operator.rs:108; the
  *                                     records are written by bincode::serialize(&sig),
@@ -105,6 +106,14 @@ int ssb_kernel_time(ssb_ctx* ctx, const char* kernel_name, float* total_ms, int*
  * generator"), compressed.  A commitment or h that does not decode gives verdict 0. */
 int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* commitments48, const uint64_t* ids,
                              const uint8_t* shares32, const uint8_t* h48, uint8_t* verdicts);
+
+/* DLEQ (Chaum-Pedersen) proof verification: verdicts[i] = 1 iff c_i equals hash_points_to_blst_scalar
+ * (x1, y1, x2, y2, t1, t2) with t_h = [r_i] x_h + [c_i] y_h -- the reference's "hash" is the 288-byte
+ * concatenation of the compressed points read as one little-endian integer mod r
+ * (src/utils/blst_utils.rs:273-278).  points48: n x (x1, y1, x2, y2), 48-byte compressed G1 each;
+ * c32 / r32: the proof scalars, 32 bytes little endian (compared byte for byte, as blst_scalar ==). */
+int ssb_dleq_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* points48, const uint8_t* c32, const uint8_t* r32,
+                          uint8_t* verdicts);
 
 /* Wire-format partial signatures -> 96-byte compressed signatures.  Record i (at wire + i*stride,
  * stride >= 202) is bincode(bls::Signature): u64 LE length 194, then "0x" and 192 hex digits of the

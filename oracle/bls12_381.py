@@ -865,3 +865,26 @@ def feldman_share_verify(h, share: int, commitments, party: int) -> bool:
     """DKG share_verification (src/crypto/dkg.rs:433-450): blst_p1_mult(h, s) (255-bit scalar, s
     from LE bytes; blst reads its low 255 bits) == committed_poly.eval(party)."""
     return g1_mul(h, share & ((1 << 255) - 1)) == committed_poly_eval(commitments, party)
+
+
+def hash_points_to_scalar(points) -> int:
+    """hash_points_to_blst_scalar (src/utils/blst_utils.rs:273-278): the compressed points
+    concatenated, read as ONE little-endian integer and reduced mod r (blst_scalar_from_le_bytes)."""
+    return int.from_bytes(b"".join(g1_compress(p) for p in points), "little") % R
+
+
+def dleq_prove(x1, x2, alpha: int, w: int):
+    """DKG::dleq_prove (src/crypto/dkg.rs:649-672) with a given nonce w: (y1, y2, c, r)."""
+    y1, y2 = g1_mul(x1, alpha), g1_mul(x2, alpha)
+    t1, t2 = g1_mul(x1, w), g1_mul(x2, w)
+    c = hash_points_to_scalar([x1, y1, x2, y2, t1, t2])
+    return y1, y2, c, (w - alpha * c) % R
+
+
+def dleq_verify(x1, y1, x2, y2, c: int, r: int) -> bool:
+    """DKG::dleq_verify (src/crypto/dkg.rs:674-692): t_i = [r]x_i + [c]y_i (255-bit scalars),
+    accept iff c == hash_points_to_scalar(x1, y1, x2, y2, t1, t2)."""
+    m = (1 << 255) - 1
+    t1 = g1_add(g1_mul(x1, r & m), g1_mul(y1, c & m))
+    t2 = g1_add(g1_mul(x2, r & m), g1_mul(y2, c & m))
+    return c == hash_points_to_scalar([x1, y1, x2, y2, t1, t2])

@@ -53,6 +53,7 @@ SIGNATURES = {
     "ssb_sk_to_pk_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p]),
     "ssb_lagrange_coeffs": (ctypes.c_int, [_ctx, _sz, _u64p, _u8p]),
     "ssb_feldman_verify_batch": (ctypes.c_int, [_ctx, _sz, _sz, _u8p, _u64p, _u8p, _u8p, _u8p]),
+    "ssb_dleq_verify_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _u8p, _u8p]),
     "ssb_decode_wire_sigs": (ctypes.c_int, [_ctx, _sz, _u8p, _sz, _u8p, _i32p]),
     "ssb_decode_wire_sigs_dev": (ctypes.c_int, [_ctx, _sz, ctypes.c_void_p, _sz, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_void_p]),

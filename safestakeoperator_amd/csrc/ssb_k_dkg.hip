@@ -8,7 +8,7 @@
 // group element, since every C_i has order r and the integer x^i equals x^i mod r on it.
 // Commitments arrive compressed (CommittedPoly::to_bytes, polynomial.rs:88-99 without the count
 // prefix); one that does not decode makes the check fail.  Registration-time work, rare: plain
-// single-lane code.
+// single-lane code.  k_dleq_verify: the Chaum-Pedersen proofs of exchange_group_public_keys.
 #include "ssb_kernels.h"
 
 namespace ssb {
@@ -67,9 +67,78 @@ __global__ void SSB_LB(64) k_feldman_share(int n, int t, const uint8_t* __restri
   verdict[i] = g1_jac_eq(y, acc) ? 1 : 0;
 }
 
+// ---- DLEQ proof verification: DKG::dleq_verify (src/crypto/dkg.rs:674-692) ----
+SSB_INL void load_scalar255(uint32_t* k, const uint8_t* b32) {
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* q = b32 + 4 * w;
+    k[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  k[7] &= 0x7fffffffu;                          // blst_p1_mult(.., 255)
+}
+// a 256-bit little-endian chunk reduced mod r (chunk < 2^256 < 3r: at most two subtractions)
+SSB_INL void fr_reduce256(uint32_t* v) {
+  for (int pass = 0; pass < 2; ++pass) {
+    uint32_t t[8], br = 0;
+    for (int i = 0; i < 8; ++i) t[i] = subb(v[i], R_LIMBS[i], br, br);
+    if (!br) for (int i = 0; i < 8; ++i) v[i] = t[i];
+  }
+}
+// hash_points_to_blst_scalar (src/utils/blst_utils.rs:273-278): the 288-byte concatenation read as a
+// little-endian integer mod r (blst_scalar_from_le_bytes): Horner over 32-byte chunks from the top,
+// acc = acc * 2^256 + chunk (acc * 2^256 mod r = MontMul(acc, 2^512 mod r))
+SSB_INL void le_bytes_mod_r(uint32_t* acc, const uint8_t* b, int nchunks) {
+  for (int i = 0; i < 8; ++i) acc[i] = 0;
+  for (int k = nchunks - 1; k >= 0; --k) {
+    uint32_t c[8];
+    for (int w = 0; w < 8; ++w) {
+      const uint8_t* q = b + 32 * k + 4 * w;
+      c[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+    }
+    fr_reduce256(c);
+    uint32_t t[8];
+    mp_mont_mul<8>(t, acc, R_R2, R_LIMBS, R_INV32);
+    mp_add_mod<8>(acc, t, c, R_LIMBS);
+  }
+}
+
+__global__ void SSB_LB(64) k_dleq_verify(int n, const uint8_t* __restrict__ pts48, const uint8_t* __restrict__ c32,
+                                        const uint8_t* __restrict__ r32, uint8_t* __restrict__ verdict) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t buf[288];                             // x1 y1 x2 y2 t1 t2, compressed
+  for (int k = 0; k < 192; ++k) buf[k] = pts48[192 * (size_t)i + k];
+  g1_aff P[4];
+  for (int q = 0; q < 4; ++q)
+    if (!(g1_decompress(P[q], buf + 48 * q) & DEC_OK)) { verdict[i] = 0; return; }
+  uint32_t rk[8], ck[8];
+  load_scalar255(rk, r32 + 32 * (size_t)i);
+  load_scalar255(ck, c32 + 32 * (size_t)i);
+  for (int h = 0; h < 2; ++h) {                 // t_h = [r] x_h + [c] y_h
+    g1_jac a, b;
+    if (P[2 * h].inf) jac_set_inf(a); else jac_mul_w4(a, P[2 * h], rk, 8);
+    if (P[2 * h + 1].inf) jac_set_inf(b); else jac_mul_w4(b, P[2 * h + 1], ck, 8);
+    jac_add(a, a, b);
+    g1_aff t; jac_to_aff(t, a);
+    g1_compress(buf + 192 + 48 * h, t);
+  }
+  uint32_t e[8];
+  le_bytes_mod_r(e, buf, 9);
+  bool ok = true;                               // proof.c == c_ (the 32 scalar bytes)
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* q = c32 + 32 * (size_t)i + 4 * w;
+    const uint32_t cw = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+    ok = ok && cw == e[w];
+  }
+  verdict[i] = ok ? 1 : 0;
+}
+
 }  // namespace k
 
 namespace launch {
+void dleq_verify(hipStream_t st, int n, const uint8_t* pts48, const uint8_t* c32, const uint8_t* r32, uint8_t* verdict) {
+  if (n > 0)
+    hipLaunchKernelGGL(k::k_dleq_verify, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, pts48, c32, r32, verdict);
+}
 void feldman_share(hipStream_t st, int n, int t, const uint8_t* comm48, const uint64_t* x, const uint8_t* s32le,
                    const g1_aff* h, const uint32_t* hflags, uint8_t* verdict) {
   if (n > 0)

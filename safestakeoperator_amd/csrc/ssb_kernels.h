@@ -158,6 +158,8 @@ void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t
 // DKG share verification (ssb_k_dkg.hip): verdict[i] = ([s_i]h == sum_k [x_i^k] C_{i,k})
 void feldman_share(hipStream_t st, int n, int t, const uint8_t* comm48, const uint64_t* x, const uint8_t* s32le,
                    const g1_aff* h, const uint32_t* hflags, uint8_t* verdict);
+// DLEQ verification (ssb_k_dkg.hip): pts48 = n x (x1, y1, x2, y2) compressed, c32 / r32 LE scalars
+void dleq_verify(hipStream_t st, int n, const uint8_t* pts48, const uint8_t* c32, const uint8_t* r32, uint8_t* verdict);
 // exact single-lane recomputation of the shares whose lane-group stage raised exc
 void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
                 const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,

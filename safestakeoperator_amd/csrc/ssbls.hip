@@ -567,6 +567,28 @@ int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* co
   return SSB_OK;
 }
 
+int ssb_dleq_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* points48, const uint8_t* c32, const uint8_t* r32,
+                          uint8_t* verdicts) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!points48 || !c32 || !r32 || !verdicts || n > (size_t)INT32_MAX) { ctx->err = "null pointer or n too large"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = ensure_ws(ctx, align_up(n * 192) + 2 * align_up(n * 32) + align_up(n)))) return rc;
+  carve c{(char*)ctx->cur->ws};
+  uint8_t* d_p = c.take<uint8_t>(n * 192); uint8_t* d_c = c.take<uint8_t>(n * 32); uint8_t* d_r = c.take<uint8_t>(n * 32);
+  uint8_t* d_v = c.take<uint8_t>(n);
+  hipStream_t st = ctx->cur->stream;
+  SSB_HIP(hipMemcpyAsync(d_p, points48, n * 192, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_c, c32, n * 32, hipMemcpyHostToDevice, st));
+  SSB_HIP(hipMemcpyAsync(d_r, r32, n * 32, hipMemcpyHostToDevice, st));
+  { timed tm(ctx, "k_dleq_verify"); launch::dleq_verify(st, (int)n, d_p, d_c, d_r, d_v); }
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
 int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status,
                              void* stream) {
   if (!ctx) return SSB_EINVAL;

@@ -19,7 +19,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Union
+from typing import List, Optional, Sequence, Union, Tuple
 
 import numpy as np
 
@@ -187,6 +187,24 @@ class Engine:
                                                        x.ctypes.data_as(_lib._u64p), sv.ctypes.data_as(_lib._u8p),
                                                        hp.ctypes.data_as(_lib._u8p), v.ctypes.data_as(_lib._u8p)),
                     "ssb_feldman_verify_batch")
+        return [bool(b) for b in v]
+
+    def dleq_verify_batch(self, proofs: Sequence[Tuple[bytes, bytes, bytes, bytes, bytes, bytes]]) -> List[bool]:
+        """DKG::dleq_verify (src/crypto/dkg.rs:674-692) per proof (x1, y1, x2, y2 compressed G1; c, r
+        32-byte little-endian scalars)."""
+        n = len(proofs)
+        if n == 0:
+            return []
+        for pr in proofs:
+            if [len(x) for x in pr] != [48, 48, 48, 48, 32, 32]:
+                raise ValueError("proof = (x1, y1, x2, y2: 48 bytes, c, r: 32 bytes)")
+        pts = np.frombuffer(b"".join(b"".join(pr[:4]) for pr in proofs), dtype=np.uint8)
+        cs = np.frombuffer(b"".join(pr[4] for pr in proofs), dtype=np.uint8)
+        rs = np.frombuffer(b"".join(pr[5] for pr in proofs), dtype=np.uint8)
+        v = np.zeros(n, dtype=np.uint8)
+        self._check(self._lib.ssb_dleq_verify_batch(self._h, n, pts.ctypes.data_as(_lib._u8p), cs.ctypes.data_as(_lib._u8p),
+                                                    rs.ctypes.data_as(_lib._u8p), v.ctypes.data_as(_lib._u8p)),
+                    "ssb_dleq_verify_batch")
         return [bool(b) for b in v]
 
     def decode_wire_sigs(self, records: Sequence[bytes]) -> List[Optional[bytes]]:

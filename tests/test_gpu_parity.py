@@ -410,3 +410,12 @@ def test_feldman_share_verification_golden(engine):
     got = engine.feldman_verify_batch([[bytes.fromhex(x) for x in c["commitments"]] for c in cs],
                                       [c["id"] for c in cs], [c["share"] for c in cs], h48)
     assert all(got)
+
+
+def test_dleq_verify_golden(engine):
+    """§8f-4: DLEQ proof verification (dkg.rs:674-692) on the GPU == the oracle (tests/golden/dleq.json:
+    valid proofs, wrong c / r / y2, a non-canonical c), plus a 6,000-proof batch."""
+    d = _load("dleq.json")
+    proofs = [tuple(bytes.fromhex(c[k]) for k in ("x1", "y1", "x2", "y2", "c", "r")) for c in d["cases"]]
+    assert engine.dleq_verify_batch(proofs) == [c["expect"] for c in d["cases"]]
+    assert engine.dleq_verify_batch(proofs * 200) == [c["expect"] for c in d["cases"]] * 200

@@ -129,3 +129,18 @@ def test_feldman_fixture_consistent():
     for c in (d["cases"][0], d["cases"][1]):
         pts = [B.g1_decompress(bytes.fromhex(x)) for x in c["commitments"]]
         assert B.feldman_share_verify(h, c["share"], pts, c["id"]) == c["expect"]
+
+
+def test_dleq_fixture_consistent():
+    """tests/golden/dleq.json: valid proofs verify, altered ones (c, r, y2, non-canonical c bytes)
+    do not; one valid and one altered case re-verified by the oracle."""
+    import json
+    import os
+    from oracle import bls12_381 as B
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "dleq.json")))
+    for c in d["cases"]:
+        assert c["expect"] == (c["kind"] == "valid")
+    for c in d["cases"][:2]:
+        pts = [B.g1_decompress(bytes.fromhex(c[k])) for k in ("x1", "y1", "x2", "y2")]
+        assert B.dleq_verify(*pts, int.from_bytes(bytes.fromhex(c["c"]), "little"),
+                             int.from_bytes(bytes.fromhex(c["r"]), "little")) == c["expect"]
