@@ -217,7 +217,7 @@ def cpu_baseline(wl, t, n, gpu_out=None, n_val=1024, threads=None, reps=1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
                     help="BASELINE.json workload per GPU (the headline is C2; the others are reported under profiles/)")

@@ -88,7 +88,9 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth);
  * throughput with many batches in flight).  Re-creates the slots' streams. */
 int ssb_set_slot_streams(ssb_ctx* ctx, int streams);
 /* The main stream of pipeline slot `slot` (hipStream_t as void*), e.g. to pass it back as the
- * `stream` of ssb_threshold_aggregate_batch_dev so a caller adds no hardware queue of its own. */
+ * `stream` of ssb_threshold_aggregate_batch_dev so a caller adds no hardware queue of its own.
+ * A *_dev call whose `stream` is a slot's main stream runs on THAT slot; any other stream gets the
+ * next slot round robin. */
 void* ssb_slot_stream(ssb_ctx* ctx, int slot);
 /* Device-side kernel timing with hipEvents recorded on the engine's stream around each launch.
  * ssb_last_kernel_ms: the last launch of `kernel_name`.  ssb_kernel_timing(ctx, 1) clears and
