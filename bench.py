@@ -141,7 +141,7 @@ def pmc_traffic(kernel):
         return None
 
 
-def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0):
+def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_count=0):
     """Synthetic committees: deterministic keys (seed 0x5AFE57A4E, rank), Shamir shares, partial
     signatures from the engine's batched signer (H(m)*sk), public keys sk*g1.  invalid_rate: that
     fraction of the shares (deterministic choice) signs the NEXT root instead -- a valid G2 point
@@ -174,6 +174,9 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0):
     bad = [i for i in range(len(share_sk))
            if invalid_rate > 0 and int.from_bytes(hashlib.sha256(seed + b"bad" + i.to_bytes(4, "little")).digest()[:8],
                                                    "little") < invalid_rate * 2.0 ** 64]
+    if invalid_count:                                  # exactly that many, spread over the batch
+        N = len(share_sk)
+        bad = sorted(set(bad) | {(k * (N // invalid_count) + 4099 * (k + 1)) % N for k in range(invalid_count)})
     sign_root = list(share_root)
     for i in bad:
         sign_root[i] = (share_root[i] + 1) % n_roots
@@ -234,6 +237,8 @@ def main():
     ap.add_argument("--compressed-pk", action="store_true",
                     help="headline on the compressed-public-key entry point (default: keys decompressed once, "
                          "ssb_pk_cache_set, as lighthouse's PublicKey holds them; the other variant is reported beside)")
+    ap.add_argument("--invalid-count", type=int, default=0,
+                    help="exactly this many invalid shares per batch (e.g. 2 ~ C4's 1e-4 rate at C2 size)")
     ap.add_argument("--invalid-rate", type=float, default=0.0,
                     help="fraction of shares signed over the wrong root (the RLC batch fails; exact verdicts "
                          "come from the per-share fallback).  The headline is the all-valid C2 batch.")
@@ -285,7 +290,7 @@ def main():
     V, t, n, n_roots = args.validators, args.threshold, args.operators, args.roots
     N = V * n
     eng = Engine(local)
-    wl = make_workload(eng, V, t, n, n_roots, rank, args.invalid_rate)
+    wl = make_workload(eng, V, t, n, n_roots, rank, args.invalid_rate, args.invalid_count)
     valid = np.asarray(wl["valid"], dtype=np.uint8)
     job_ok = valid.reshape(V, n).sum(axis=1) >= t
 

@@ -3,16 +3,19 @@
 //
 // "on batch failure, bisect deterministically until each share's verdict equals
 // the single-verify result".  The shares of a failed batch are ordered by signing root (counting
-// sort) and tested in root-aligned groups on a 4-ary tree: level 0 holds groups of Gs_0 = 4^(L-1)
-// >= n shares (one group per root), level l groups of Gs_0 / 4^l, the last level single shares.
+// sort) and tested in root-aligned groups on a B-ary tree (B = 16 by default): level 0 holds groups of
+// Gs_0 = B^(L-1) >= n shares (one group per root), level l groups of Gs_0 / B^l, the last level single
+// shares.  B = 16 rather than 4: the fallback runs on a shared tail stream and is latency bound
+// (each level is one pairing check deep), so fewer, wider levels win -- at one invalid share per C2
+// batch 3 tested levels instead of 5.
 // A group g of root r passes when
 //     e(sum_{i in g} k_i pk_i, H(r)) * e(-g1, sum_{i in g} k_i sig_i) == 1
 // with the batch's own odd 64-bit RLC scalars k_i: every candidate of a passing group gets verdict 1
 // (the batch check's soundness, 2^-63 per group); a failing single-share group is exactly the
 // reference's verify (k_i != 0 mod r), so it gets verdict 0.  Children of a passing group are not
 // tested; a group whose share range equals its failed parent's inherits the failure untested.
-// Work at 1% invalid shares (C2: 64 roots x 256): ~2.1k group checks instead of 16,384 per-share
-// checks.  Every kernel here is a no-op (uniform early exit) when the batch passed.
+// Work at 1% invalid shares (C2: 64 roots x 256): ~3.5k group checks (4-ary: ~2.1k, in 5 levels)
+// instead of 16,384 per-share checks; at one invalid share, 96.  Every kernel here is a no-op (uniform early exit) when the batch passed.
 #include "ssb_kernels.h"
 #include "ssb_wave.h"
 #include "ssb_lane_ops.h"
@@ -24,7 +27,7 @@ namespace k {
 // every level (gst[l][r], n_roots + 1 words per level).  Phases separated by workgroup barriers
 // (global atomics and stores of one workgroup are ordered by them).
 constexpr int PREP_THREADS = 1024;
-__global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, int L, const uint32_t* __restrict__ ok,
+__global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, int L, int lb, const uint32_t* __restrict__ ok,
                                                         const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt,
                                                         uint32_t* __restrict__ start, uint32_t* __restrict__ cursor,
                                                         uint32_t* __restrict__ gst, uint32_t* __restrict__ perm) {
@@ -40,7 +43,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, in
     for (int r = 0; r < n_roots; ++r) { start[r] = acc; cursor[r] = acc; acc += cnt[r]; }
   } else if (t <= L) {
     const int l = t - 1;
-    const uint32_t lg = 2u * (uint32_t)(L - 1 - l);     // Gs_l = 2^lg
+    const uint32_t lg = (uint32_t)(lb * (L - 1 - l));   // Gs_l = 2^lg
     uint32_t* g = gst + (size_t)l * (n_roots + 1);
     uint32_t acc = 0;
     for (int r = 0; r < n_roots; ++r) {
@@ -79,7 +82,7 @@ constexpr int BS_SLOTS = BS_S0 + 18 + 6 + 18 + 84;
 // variant running both Miller loops at once halved the resident workgroups and measured slower.)
 // gv_prev / gv_cur: per-group results of the previous / this level (1 pass, 0 fail).
 constexpr int LV_THREADS = 64;
-__global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int n_roots, const uint32_t* __restrict__ ok,
+__global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots, const uint32_t* __restrict__ ok,
                                               const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
                                               const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst,
                                               const uint32_t* __restrict__ flags, const g2_jac* __restrict__ rsig,
@@ -97,7 +100,7 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int n_roots, const u
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
   lp_init_consts(g);
   const int F1 = BS_S0, B = F1 + 18, F2 = B + 6, TMP = F2 + 18;
-  const uint32_t lg = 2u * (uint32_t)(L - 1 - l);
+  const uint32_t lg = (uint32_t)(lb * (L - 1 - l));
   const uint64_t Gs = 1ull << lg;
   const uint32_t* gl = gst + (size_t)l * (n_roots + 1);
   const uint32_t ngroups = gl[n_roots];
@@ -111,11 +114,11 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int n_roots, const u
     const uint64_t a = seg_b + (uint64_t)j * Gs, b = a + Gs < seg_e ? a + Gs : seg_e;
     if (l > 0) {
       const uint32_t* gp = gst + (size_t)(l - 1) * (n_roots + 1);
-      const uint8_t pv = gv_prev[gp[r] + (j >> 2)];
+      const uint8_t pv = gv_prev[gp[r] + (j >> lb)];
       if (pv) { if (lane_ == 0) gv_cur[gid] = 1; continue; }   // parent passed: verdicts written
-      // parent range [seg_b + (j/4) 4Gs, +4Gs) equals [a, b): inherit the failure untested
-      const uint64_t pa = seg_b + (uint64_t)(j >> 2) * (Gs << 2);
-      const uint64_t pb = pa + (Gs << 2) < seg_e ? pa + (Gs << 2) : seg_e;
+      // parent range [seg_b + (j/B) B Gs, + B Gs) equals [a, b): inherit the failure untested
+      const uint64_t pa = seg_b + (uint64_t)(j >> lb) * (Gs << lb);
+      const uint64_t pb = pa + (Gs << lb) < seg_e ? pa + (Gs << lb) : seg_e;
       if (pa == a && pb == b) {
         if (lane_ == 0) gv_cur[gid] = 0;
         if (lg == 0)
@@ -196,10 +199,22 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int n_roots, const u
 
 namespace launch {
 
+// log2 of the tree's branching factor B: 4 (16-ary, default) or SSB_FB_BRANCH=4 / 16 / 2 / ...
+int fallback_log2_branch() {
+  static const int lb = [] {
+    const char* e = getenv("SSB_FB_BRANCH");
+    const int b = e ? atoi(e) : 16;
+    int l = 1;
+    while ((1 << l) < b && l < 8) ++l;
+    return l;
+  }();
+  return lb;
+}
 int fallback_levels(size_t n) {
+  const int lb = fallback_log2_branch();
   int L = 1;
   uint64_t gs = 1;
-  while (gs < n) { gs <<= 2; ++L; }
+  while (gs < n) { gs <<= lb; ++L; }
   return L;
 }
 
@@ -211,16 +226,17 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const ui
   if (n <= 0 || n_roots <= 0) return;
   const int L = fallback_levels((size_t)n);
   auto nb = [](size_t x, unsigned b) { return (unsigned)((x + b - 1) / b); };
-  hipLaunchKernelGGL(k_fb_prep, dim3(1), dim3(PREP_THREADS), 0, st, n, n_roots, L, ok, share_root, cnt, start, cursor,
+  const int lb = fallback_log2_branch();
+  hipLaunchKernelGGL(k_fb_prep, dim3(1), dim3(PREP_THREADS), 0, st, n, n_roots, L, lb, ok, share_root, cnt, start, cursor,
                      gst, perm);
   hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, seed, ok, flags, sig, pk, rsig, rpk);
   for (int l = 0; l < L; ++l) {
-    const uint64_t gs = 1ull << (2 * (L - 1 - l));
+    const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;
     const unsigned grid = (unsigned)(bound < 2048 ? bound : 2048);
     uint8_t* cur = (l & 1) ? gv1 : gv0;
     const uint8_t* prev = (l & 1) ? gv0 : gv1;
-    hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, n_roots, ok, (const uint32_t*)start,
+    hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, lb, n_roots, ok, (const uint32_t*)start,
                        (const uint32_t*)cnt, (const uint32_t*)perm, (const uint32_t*)gst, flags, (const g2_jac*)rsig,
                        (const g1_jac*)rpk, H, prev, cur, verdict);
   }

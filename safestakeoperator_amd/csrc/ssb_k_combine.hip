@@ -78,17 +78,39 @@ __global__ void SSB_LB(64) k_combine_terms(int n, const uint32_t* __restrict__ s
   unit_combine_term(r, sig_aff[sel[s]], l.l);  // blst_p2_mult(.., 255 bits)
   term[s] = r;
 }
+// verified candidates only: four lanes per share, one base-u digit each (unit_combine_term_gls);
+// term[4 s + q]
+__global__ void SSB_LB(64) k_combine_terms_gls(int n, const uint32_t* __restrict__ share_job,
+                                              const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                                              const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                                              const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
+                                              const uint32_t* __restrict__ skip_if_ok, const uint32_t* __restrict__ fast,
+                                              g2_jac* __restrict__ term) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 4 * n) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  const int s = g >> 2, q = g & 3;
+  const uint32_t j = share_job[s];
+  if (fast && fast[j]) return;
+  const uint32_t k = (uint32_t)s - off[j];
+  if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
+  const fr l = lam[s];
+  g2_jac r;
+  unit_combine_term_gls(r, sig_aff[sel[s]], l.l, q);
+  term[4 * (size_t)s + q] = r;
+}
+// stride: terms per share (1: k_combine_terms, 4: k_combine_terms_gls)
 __global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
-                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96) {
+                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
   if (fast && fast[j]) return;
   uint8_t o[96];
   if (status[j] == SSB_DVF_OK) {
-    unit_combine_sum(o, term + off[j], tt[j]);  // infinity(t) start (src/crypto/impls/blst.rs:74)
+    unit_combine_sum(o, term + (size_t)stride * off[j], (uint32_t)stride * tt[j]);  // infinity(t) start (blst.rs:74)
   } else {
     for (int k = 0; k < 96; ++k) o[k] = 0;
   }

@@ -101,10 +101,15 @@ __global__ void k_combine_terms(int n, const uint32_t* __restrict__ share_job,
                                                       const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
                                                       const uint32_t* __restrict__ skip_if_ok, const uint32_t* __restrict__ fast,
                                                       g2_jac* __restrict__ term);
+__global__ void k_combine_terms_gls(int n, const uint32_t* __restrict__ share_job, const uint32_t* __restrict__ off,
+                                    const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
+                                    const uint32_t* __restrict__ sel, const fr* __restrict__ lam,
+                                    const g2_aff* __restrict__ sig_aff, const uint32_t* __restrict__ skip_if_ok,
+                                    const uint32_t* __restrict__ fast, g2_jac* __restrict__ term);
 __global__ void k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
-                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96);
+                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride);
 __global__ void k_combine_fast(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
@@ -144,9 +149,10 @@ void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
             const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum);
 // gflags[s] = DEC_IN_GROUP when signature s (decodable, not infinity) passes psi(P) == [x]P
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags);
-// Exact verdicts of a failed batch by group testing on a 4-ary tree of root-aligned share groups
+// Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups
 // (ssb_k_bisect.hip); no-op when *ok.  Workspace: cnt/start/cursor n_roots words, perm n words,
 // gst fallback_levels(n) * (n_roots + 1) words, rsig/rpk n points, gv0/gv1 n + n_roots bytes.
+int fallback_log2_branch();
 int fallback_levels(size_t n);
 void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,

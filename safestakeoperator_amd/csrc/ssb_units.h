@@ -91,6 +91,40 @@ SSB_FN void unit_combine_term(g2_jac& r, const g2_aff& sig, const uint32_t* lam8
   if (even) { g2_aff n = sig; fp2_neg(n.y, n.y); jac_add_aff(r, r, n); }
 }
 
+// GLS split of a combine term for a signature KNOWN to lie in G2 (a verified candidate): on G2,
+// psi acts as [x] with x = -u, u = |x| = 0xd201000000010000, and r = u^4 - u^2 + 1 < u^4, so a
+// canonical scalar k < r has four base-u digits, k = d0 + d1 u + d2 u^2 + d3 u^3 (d_q < 2^64), and
+//     [k] sig = [d0] sig + [d1] (-psi(sig)) + [d2] psi^2(sig) + [d3] (-psi^3(sig)).
+// Each digit's 64-bit product runs on its own lane (a quarter of the 255-bit chain's latency); the
+// group element is the same as blst_p2_mult(sig, k, 255), so the compressed sum is bit-identical.
+// (unsafe_aggregate's shares are not group-checked: it keeps the 255-bit unit_combine_term.)
+constexpr uint64_t GLS_U = 0xd201000000010000ull;
+SSB_INL uint64_t gls_digit(const uint32_t* k8, int q) {
+  uint64_t w[4];
+  for (int i = 0; i < 4; ++i) w[i] = (uint64_t)k8[2 * i] | ((uint64_t)k8[2 * i + 1] << 32);
+  uint64_t rem = 0;
+  for (int step = 0; step <= q; ++step) {       // (w, rem) = divmod(w, u), q + 1 times
+    uint64_t qt[4] = {0, 0, 0, 0};
+    rem = 0;
+    for (int i = 255; i >= 0; --i) {
+      const uint64_t hi = rem >> 63;
+      rem = (rem << 1) | ((w[i >> 6] >> (i & 63)) & 1ull);
+      if (hi || rem >= GLS_U) { rem -= GLS_U; qt[i >> 6] |= 1ull << (i & 63); }
+    }
+    for (int i = 0; i < 4; ++i) w[i] = qt[i];
+  }
+  return rem;
+}
+SSB_FN void unit_combine_term_gls(g2_jac& r, const g2_aff& sig, const uint32_t* lam8, int q) {
+  if (sig.inf) { jac_set_inf(r); return; }
+  const uint64_t d = gls_digit(lam8, q);
+  g2_aff p = sig;
+  for (int i = 0; i < q; ++i) g2_psi_aff(p, p);
+  if (q & 1) fp2_neg(p.y, p.y);
+  const uint32_t dw[2] = {(uint32_t)d, (uint32_t)(d >> 32)};
+  jac_mul_aff(r, p, dw, 2);
+}
+
 // unit "combine_sum": sum of t terms, affine, compressed (src/crypto/impls/blst.rs:74-86)
 SSB_FN void unit_combine_sum(uint8_t* out96, const g2_jac* terms, uint32_t t) {
   g2_jac acc; jac_set_inf(acc);

@@ -15,7 +15,7 @@
 //   k_fallback_verify exact per-share verify, only if the batch failed
 //   k_select          reference scan order / error semantics per job      (a-1)
 //   k_lagrange        Lagrange coefficients, Montgomery batch inversion    (a-5)
-//   k_combine_terms   lambda_i * sig_i  (255-bit, 4-bit window)            (a-4)
+//   k_combine_terms   lambda_i * sig_i  (verified shares: GLS, 4 digits on 4 lanes; a-4 unsafe: 255-bit)
 //   k_combine_sum     sum, affine, compress                                 (a-4)
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -685,7 +685,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   const size_t n = n_shares;
   size_t need = verify_ws_bytes(n, n_roots) + align_up(n * 4) * 3 + align_up(n) + align_up(n * sizeof(fr)) +
-                align_up(n * sizeof(g2_jac)) + align_up(n_jobs * 4);
+                align_up(4 * n * sizeof(g2_jac)) + align_up(n_jobs * 4);
   if ((rc = ensure_ws(ctx, need))) return rc;
   hipStream_t user = (hipStream_t)stream;
   hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = slot_tail(ctx);
@@ -701,7 +701,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   uint32_t* sel = c.take<uint32_t>(n);
   uint8_t* verdict = share_verdicts ? share_verdicts : c.take<uint8_t>(n);
   fr* lam = c.take<fr>(n);
-  g2_jac* term = c.take<g2_jac>(n);
+  g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
   hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, job_root, share_job, share_root);
   // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
@@ -710,8 +710,8 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     { timed tm(ctx, "k_select", sc); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err); }
     { timed tm(ctx, "k_combine_fast", sc); hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)nullptr, fast, out_sig96); }
     { timed tm(ctx, "k_lagrange", sc); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)nullptr, (const uint32_t*)fast, lam); }
-    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
-    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96); }
+    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
+    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict, spec, tl))) return rc;
@@ -722,8 +722,8 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
   hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)w.ok, fast, out_sig96);
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, (const uint32_t*)fast, lam);
-  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, (const uint32_t*)fast, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, (const uint32_t*)fast, out_sig96);
+  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, (const uint32_t*)fast, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, (const uint32_t*)fast, out_sig96, 4);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
   ctx->cur->out_pending = true;
@@ -916,7 +916,7 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   // unsafe_aggregate does not subgroup-check its inputs (blst.rs:77-84): always the exact 255-bit path
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, (const uint32_t*)nullptr, (const uint32_t*)nullptr, lam);
   if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, (const uint32_t*)nullptr, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out, 1);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
