@@ -47,7 +47,7 @@ MAD_PEAK_ISSUE = 256 * 4 * 16 * 2.4e9  # 16 lanes/clk/SIMD (wave64 mad = 4 cycle
 #   C4  configs[3]: 1,048,576 attestation shares over 8 GPUs -> 131,072 shares (32,768 x 4) per GPU
 #   C5  configs[4]: 1M validators x 13 shares (10-of-13) over 8 GPUs -> 131,072 validators per GPU
 CONFIGS = {
-    "C2": dict(validators=4096, threshold=3, operators=4, roots=64, pipeline=12),
+    "C2": dict(validators=4096, threshold=3, operators=4, roots=64, pipeline=14),
     "C3_3of4": dict(validators=65536, threshold=3, operators=4, roots=64, pipeline=3),
     "C3_5of7": dict(validators=65536, threshold=5, operators=7, roots=64, pipeline=3),
     "C4_per_gpu": dict(validators=32768, threshold=3, operators=4, roots=64, pipeline=4),

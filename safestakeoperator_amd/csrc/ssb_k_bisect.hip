@@ -63,11 +63,21 @@ __global__ void SSB_LB(64) k_fb_rlc(int n, uint64_t seed, const uint32_t* __rest
                                    g1_jac* __restrict__ rpk) {
   if (*ok) return;
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  // binary double-and-add (no window table): the private segment stays small -- every tail queue
+  // reserves scratch for the largest kernel it has run, and this one is launched on every batch
   if (g < n) {
-    if (flags[g] & FLAG_CANDIDATE) { g2_jac r; unit_rlc_sig(r, sig_aff[g], rlc_scalar_odd(seed, (uint64_t)g)); rsig[g] = r; }
+    if (flags[g] & FLAG_CANDIDATE) {
+      const uint64_t k = rlc_scalar_odd(seed, (uint64_t)g);
+      const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+      g2_jac r; jac_mul_aff(r, sig_aff[g], kw, 2); rsig[g] = r;
+    }
   } else if (g < 2 * n) {
     const int s = g - n;
-    if (flags[s] & FLAG_CANDIDATE) { g1_jac r; unit_rlc_pk(r, pk_aff[s], rlc_scalar_odd(seed, (uint64_t)s)); rpk[s] = r; }
+    if (flags[s] & FLAG_CANDIDATE) {
+      const uint64_t k = rlc_scalar_odd(seed, (uint64_t)s);
+      const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+      g1_jac r; jac_mul_aff(r, pk_aff[s], kw, 2); rpk[s] = r;
+    }
   }
 }
 
