@@ -189,6 +189,33 @@ SSB_FN void clear_cofactor_g2(g2_jac& r, const g2_jac& P) {
   jac_add(r, t3, n);
 }
 
+// h_eff * (q0 + q1), the same element as clear_cofactor_g2(q0 + q1), with at most three Jacobian
+// points live: h_eff P = [x]u - u + psi^2(2P) - P where u = [x]P + psi(P); u and [x]u - u go
+// through *tmp (memory), P is recomputed from q0, q1.  The hash pipeline's exact redo of a root
+// whose lane-group stage met an exceptional addition; its private segment is what the batch
+// streams reserve per queue, so it is kept below the per-share kernels'.
+#define SSB_MEM_FENCE() __asm__ volatile("" ::: "memory")
+SSB_FN void h2c_clear_exact(g2_jac& r, const g2_aff& q0, const g2_aff& q1, g2_jac* tmp) {
+  g2_jac p, a;
+  jac_from_aff(p, q0); jac_add_aff(p, p, q1);          // P
+  jac_mul_x_abs(a, p); jac_neg(a, a);                  // [x]P
+  g2_psi_jac(p, p);
+  jac_add(a, a, p);                                    // u = [x]P + psi(P)
+  *tmp = a;
+  SSB_MEM_FENCE();
+  jac_mul_x_abs(p, a); jac_neg(p, p);                  // [x]u
+  a = *tmp; jac_neg(a, a);
+  jac_add(p, p, a);                                    // [x]u - u
+  *tmp = p;
+  SSB_MEM_FENCE();
+  jac_from_aff(p, q0); jac_add_aff(p, p, q1);          // P again
+  jac_dbl(a, p); g2_psi_jac(a, a); g2_psi_jac(a, a);   // psi^2(2P)
+  jac_neg(p, p);
+  jac_add(a, a, p);                                    // psi^2(2P) - P
+  p = *tmp;
+  jac_add(r, p, a);
+}
+
 // ---- the same hash split into the stages of the batched pipeline (ssb_k_hash.hip) ----
 // stage 1: u0, u1 from expand_message_xmd
 SSB_FN void h2c_field(fp2& u0, fp2& u1, const uint8_t* msg32, const uint8_t* dst, int dst_len) {

@@ -82,16 +82,15 @@ __global__ void SSB_LB(64) k_h2c_clear(int n, const g2_aff* __restrict__ q, g2_j
   }
 }
 
-// 4: affine output; a root whose lane-group stage met an exceptional addition is redone exactly
-__global__ void SSB_LB(64) k_h2c_affine(int n, const g2_aff* __restrict__ q, const g2_jac* __restrict__ hj,
-                                                   const uint32_t* __restrict__ exc, g2_aff* __restrict__ out) {
+// 4: affine output; a root whose lane-group stage met an exceptional addition (or every root,
+// with exact_all: the test knob SSB_H2C_EXACT) is redone exactly, hj[i] serving as its temporary
+__global__ void SSB_LB(64) k_h2c_affine(int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
+                                                   const uint32_t* __restrict__ exc, int exact_all, g2_aff* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2_jac s;
-  if (exc[i]) {
-    jac_from_aff(s, q[2 * i]);
-    jac_add_aff(s, s, q[2 * i + 1]);
-    clear_cofactor_g2(s, s);
+  if (exc[i] || exact_all) {
+    h2c_clear_exact(s, q[2 * i], q[2 * i + 1], &hj[i]);
   } else {
     s = hj[i];
   }
@@ -155,7 +154,9 @@ void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst,
   hipLaunchKernelGGL(k::k_h2c_u, dim3((n + 63) / 64), dim3(64), 0, st, n, roots, dst, u);
   hipLaunchKernelGGL(k::k_h2c_map, dim3((4 * n + 63) / 64), dim3(64), 0, st, n, u, q);
   hipLaunchKernelGGL(k::k_h2c_clear, dim3((n + 7) / 8), dim3(64), 0, st, n, q, hj, exc);
-  hipLaunchKernelGGL(k::k_h2c_affine, dim3((n + 63) / 64), dim3(64), 0, st, n, q, hj, exc, out);
+  const char* ex = getenv("SSB_H2C_EXACT");
+  const int exact_all = (ex && atoi(ex) != 0) ? 1 : 0;
+  hipLaunchKernelGGL(k::k_h2c_affine, dim3((n + 63) / 64), dim3(64), 0, st, n, q, hj, exc, exact_all, out);
 }
 }  // namespace launch
 }  // namespace ssb

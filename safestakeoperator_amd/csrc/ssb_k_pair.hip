@@ -186,10 +186,13 @@ __global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint
     f12_mul(g, ACC, IN, ACC);
   }
   f12_final_exp(g, ACC, TMP);
-  if (threadIdx.x == 0) {
-    fp12 e;
-    ld12(e, g.s + ACC);
-    *ok = fp12_is_one(e) ? 1u : 0u;
+  if (threadIdx.x == 0) {  // == 1, read slot by slot (an fp12 local would sit in scratch)
+    bool one = true;
+    for (int k = 0; k < 12; ++k) {
+      const fp v = g.s[ACC + k];
+      one = one && (k == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v));
+    }
+    *ok = one ? 1u : 0u;
   }
 }
 

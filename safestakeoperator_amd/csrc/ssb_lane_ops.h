@@ -224,15 +224,23 @@ template <class GR> SSB_INL void f12_cyc_exp_x(GR& g, int r, int f) {
 template <class GR> SSB_INL void f12_final_exp(GR& g, int f, int tmp) {
   const int t0 = tmp, t1 = tmp + 12, t2 = tmp + 24, t3 = tmp + 36, t4 = tmp + 48, t5 = tmp + 60, t6 = tmp + 72;
   f12_conj(g, f, t0);
+  // f^-1 = conj(f) / N with N = f conj(f) = c0^2 - v c1^2 in Fp6: the two Fp12 products run as
+  // lane programs, only the Fp6 inversion of N stays on one lane (an Fp12 inversion there held
+  // ~2 KB of private segment per lane, the largest on the batch streams).
+  f12_mul(g, f, t0, t2);  // N: slots t2 .. t2+5 (the w-half is zero)
   LP_FOR(1) {
-    if (role == 0) {  // one Fp12 inversion, on one lane
-      fp12 x, xi;
-      ld12(x, g.s + f);
-      fp12_inv(xi, x);
-      st12(g.s + t1, xi);
+    if (role == 0) {
+      fp6 x, xi;
+      fp2* v[3] = {&x.c0, &x.c1, &x.c2};
+      for (int k = 0; k < 3; ++k) { v[k]->c0 = g.s[t2 + 2 * k]; v[k]->c1 = g.s[t2 + 2 * k + 1]; }
+      fp6_inv(xi, x);
+      const fp2 w[3] = {xi.c0, xi.c1, xi.c2};
+      for (int k = 0; k < 3; ++k) { g.s[t1 + 2 * k] = w[k].c0; g.s[t1 + 2 * k + 1] = w[k].c1; }
+      for (int k = 6; k < 12; ++k) g.s[t1 + k] = fp_zero();
     }
   }
   LP_SYNC();
+  f12_mul(g, t1, t0, t1);  // f^-1
   f12_mul(g, t0, t1, t2);
   lg_copy<64>(g, t2, t1, 12);
   f12_frob(g, 2, t2, t2);

@@ -130,6 +130,12 @@ static void lane_selftest(const uint8_t* seed32) {
   { uint32_t e = 0; g2_jac S; jac_from_aff(S, Hraw); jac_add_aff(S, S, Q);
     put_jac(h, 0, S); lane::g2_clear_cofactor(g, h.U(0), h.U(6), h.U(12), e);
     g2_jac R; clear_cofactor_g2(R, S); ok += same_point(h, 6, R) && e == 0; ++n;
+    // the exact redo (three live points, temporaries through memory) == clear_cofactor_g2
+    { auto same = [](const g2_jac& a, const g2_jac& b) { g2_aff x, y; jac_to_aff(x, a); jac_to_aff(y, b);
+        uint8_t ca[96], cb[96]; g2_compress(ca, x); g2_compress(cb, y); return memcmp(ca, cb, 96) == 0; };
+      g2_jac tmp, X; h2c_clear_exact(X, Hraw, Q, &tmp); ok += same(X, R); ++n;
+      g2_aff Qn = Q; fp2_neg(Qn.y, Q.y); h2c_clear_exact(X, Q, Qn, &tmp); ok += jac_is_inf(X) != 0; ++n;  // q0 = -q1
+      g2_jac D; jac_from_aff(D, Q); jac_dbl(D, D); clear_cofactor_g2(D, D); h2c_clear_exact(X, Q, Q, &tmp); ok += same(X, D); ++n; }  // q0 = q1
     // staged hash == hash_to_g2
     fp2 u0, u1; h2c_field(u0, u1, m, (const uint8_t*)DST, (int)strlen(DST));
     g2_aff q[2]; const fp2* us[2] = {&u0, &u1};

@@ -89,6 +89,15 @@ def test_hash_to_g2_golden(engine):
     assert [o.hex() for o in out] == [c["out192"] for c in hc]
 
 
+def test_hash_to_g2_exact_redo_golden(engine, monkeypatch):
+    """Every root through k_h2c_affine's exact redo (the path a root takes when its lane-group
+    cofactor clearing met an exceptional addition): same bytes as the golden hash vectors."""
+    hc = _load("hash_to_g2.json")["cases"]
+    monkeypatch.setenv("SSB_H2C_EXACT", "1")
+    out = engine.hash_to_g2([bytes.fromhex(c["msg"]) for c in hc])
+    assert [o.hex() for o in out] == [c["out192"] for c in hc]
+
+
 def test_known_answers(engine):
     ka = _load("known_answers.json")
     # Ethereum consensus `sign` vector with the PoP DST (the reference's DST)
