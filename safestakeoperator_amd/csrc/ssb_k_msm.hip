@@ -262,6 +262,15 @@ __global__ void SSB_LB(64) k_subgroup(int n, const uint32_t* __restrict__ sflags
   gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
 }
 
+// exact single-lane redo of the shares whose lane-group subgroup check met an exceptional addition
+__global__ void SSB_LB(64) k_subgroup_fix(int n, const uint32_t* __restrict__ sflags, const g2_aff* __restrict__ sig_aff,
+                                          const uint32_t* __restrict__ exc, uint32_t* __restrict__ gflags) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n || !exc[s]) return;
+  const uint32_t sf = sflags[s];
+  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+}
+
 }  // namespace k
 
 namespace launch {
@@ -310,8 +319,16 @@ void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
                      (const g1_jac*)wsum, root_sum);
 }
 
-void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags) {
-  if (n) hipLaunchKernelGGL(k_subgroup, dim3((n + 63) / 64), dim3(64), 0, st, n, sflags, sig, gflags);
+void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc) {
+  if (!n) return;
+  const char* sg = getenv("SSB_SUBGROUP");
+  const bool lane_path = sg && sg[0] == 'l';  // "lane"
+  if (lane_path) {
+    lane_subgroup(st, n, sflags, sig, gflags, exc);
+    hipLaunchKernelGGL(k_subgroup_fix, dim3((n + 63) / 64), dim3(64), 0, st, n, sflags, sig, (const uint32_t*)exc, gflags);
+  } else {
+    hipLaunchKernelGGL(k_subgroup, dim3((n + 63) / 64), dim3(64), 0, st, n, sflags, sig, gflags);
+  }
 }
 
 }  // namespace launch

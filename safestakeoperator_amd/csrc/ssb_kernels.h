@@ -148,7 +148,8 @@ void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
 void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
             const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum);
 // gflags[s] = DEC_IN_GROUP when signature s (decodable, not infinity) passes psi(P) == [x]P
-void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags);
+// subgroup checks: single-lane (default) or SSB_SUBGROUP=lane (8-lane groups + exact redo of exceptional shares)
+void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups
 // (ssb_k_bisect.hip); no-op when *ok.  Workspace: cnt/start/cursor n_roots words, perm n words,
 // gst fallback_levels(n) * (n_roots + 1) words, rsig/rpk n points, gv0/gv1 n + n_roots bytes.

@@ -266,7 +266,7 @@ struct verify_ws {
   msm_plan plan;
   g2_aff* H;          // pair Q points: H(root r) for r < n_roots, then the G2 MSM windows
   g1_aff* pair_p;     // pair P points: root sums, then [2^(c w)](-g1)
-  g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags;
+  g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags; uint32_t* gexc;
   fp12* f; uint32_t* ok;
   char* hws;          // staged hash_to_G2 workspace
   uint32_t* cnt; uint32_t* start; uint32_t* cur; uint32_t* sbsum; uint32_t* ent;   // MSM counting sort
@@ -287,7 +287,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
   const msm_plan p = plan_msm(n, n_roots);
   const size_t np = n_roots + MSM_WMAX;
   return align_up(np * sizeof(g2_aff)) + align_up(np * sizeof(g1_aff)) + align_up(n * sizeof(g2_aff)) +
-         align_up(n * sizeof(g1_aff)) + align_up(n * 4) * 4 + align_up(fp12_slots(np) * sizeof(fp12)) + align_up(4) +
+         align_up(n * sizeof(g1_aff)) + align_up(n * 4) * 5 + align_up(fp12_slots(np) * sizeof(fp12)) + align_up(4) +
          align_up(launch::hash_ws_bytes(n_roots)) + 4 * align_up((size_t)p.K * 4) + align_up(1024 * 4) +
          align_up(p.n_ent * 4) + align_up(((size_t)p.g2.W << p.g2.c) * sizeof(g2_jac)) +
          align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
@@ -303,7 +303,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.H = c.take<g2_aff>(np); w.pair_p = c.take<g1_aff>(np);
   w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
   w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
-  w.gflags = c.take<uint32_t>(n);
+  w.gflags = c.take<uint32_t>(n); w.gexc = c.take<uint32_t>(n);
   w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   w.cnt = c.take<uint32_t>(w.plan.K); w.start = c.take<uint32_t>(w.plan.K); w.cur = c.take<uint32_t>(w.plan.K);
@@ -356,7 +356,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, seed, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent, w.order); }
   if (n) {
-    { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags); }
+    { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags, w.gexc); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, d_share_root,
                        (uint32_t)n_roots, w.flags);
   }

@@ -42,8 +42,11 @@ def test_threshold_golden_cases_one_by_one(engine):
             assert ei.value == _expected_error(c)(), c["name"]
 
 
-def test_threshold_golden_cases_one_batch(engine):
-    """All fixture jobs (mixed t, roots, errors) in ONE device batch, with every share verdict."""
+@pytest.mark.parametrize("subgroup", ["single", "lane"])
+def test_threshold_golden_cases_one_batch(engine, subgroup, monkeypatch):
+    """All fixture jobs (mixed t, roots, errors) in ONE device batch, with every share verdict;
+    subgroup checks single-lane or as 8-lane groups (SSB_SUBGROUP=lane)."""
+    monkeypatch.setenv("SSB_SUBGROUP", subgroup)
     cases = _load("threshold_cases.json")["cases"]
     roots, t, offs, sigs, pks, ids, jr = [], [], [0], [], [], [], []
     for c in cases:
@@ -66,7 +69,9 @@ def test_threshold_golden_cases_one_batch(engine):
         assert [bool(v) for v in ver[offs[k]:offs[k + 1]]] == c["share_verdicts"], c["name"]
 
 
-def test_verify_batch_matches_oracle_verdicts(engine):
+@pytest.mark.parametrize("subgroup", ["single", "lane"])
+def test_verify_batch_matches_oracle_verdicts(engine, subgroup, monkeypatch):
+    monkeypatch.setenv("SSB_SUBGROUP", subgroup)
     cases = _load("threshold_cases.json")["cases"]
     roots, pks, sigs, ri, want = [], [], [], [], []
     for c in cases:
