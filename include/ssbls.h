@@ -34,9 +34,14 @@
  *     decodes to infinity, makes its share invalid (verdict 0).
  *   - A signature that does not decode (blst BAD_ENCODING / POINT_NOT_ON_CURVE), is not in G2,
  *     or is the point at infinity yields verdict 0, exactly as blst verify returns false.
- *   - Verification is by random linear combination (64-bit non-zero scalars derived from
- *     `rlc_seed`, one final exponentiation per batch); a failing batch falls back to exact
- *     per-share verification, so every verdict equals the single-signature verify result.
+ *   - Verification is by random linear combination, as lighthouse's verify_signature_sets
+ *     (RAND_BITS = 64, src/crypto/impls/blst.rs:12): one final exponentiation per batch, a failing
+ *     batch is resolved by exact group tests, so every verdict equals the single-signature verify
+ *     result.  The 64-bit scalars come from a 256-bit key drawn from the OS CSPRNG (getrandom) for
+ *     EVERY call, inside the library, after the inputs are handed over (ChaCha12 of the key and the
+ *     share index); `rlc_seed` is only XORed into that key.  The key never leaves the library, so a
+ *     sender cannot craft shares whose errors cancel in the combination (see
+ *     ssb_set_rlc_deterministic for the one exception).
  *   - Host-pointer functions copy inputs to the device and results back; they are synchronous.
  *     The *_dev variants take DEVICE pointers and a hipStream_t (as void*), enqueue everything
  *     on that stream and return without synchronising.
@@ -67,6 +72,10 @@ extern "C" {
 #define SSB_DVF_INSUFFICIENT_VALID_SIGNATURES 4 /* err = {got, expected} */
 #define SSB_DVF_BAD_SIGNATURE_ENCODING 5      /* unsafe_aggregate only: a share does not decode
                                                  (the reference's unwrap() would panic) */
+#define SSB_DVF_INVALID_JOB 6                 /* *_dev entry points only: t[j] == 0, t[j] > SSB_MAX_T,
+                                                 share_off[j+1] < share_off[j] or > n_shares;
+                                                 err = {t, share count}.  The host-pointer entry
+                                                 points refuse such a batch with SSB_EINVAL. */
 
 /* Maximum threshold t supported per job, and maximum DST length. */
 #define SSB_MAX_T 64
@@ -87,6 +96,11 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth);
  * queue per slot and more slots within the HIP runtime's per-queue scratch reservations (highest
  * throughput with many batches in flight).  Re-creates the slots' streams. */
 int ssb_set_slot_streams(ssb_ctx* ctx, int streams);
+/* TESTS / REPRODUCIBLE PROFILING ONLY.  on = 1: the RLC key of every later call is expanded from
+ * the caller's rlc_seed alone (splitmix64), so the scalars are a public function of the seed and
+ * crafted shares CAN cancel -- never use this on untrusted input.  on = 0 (the default): a fresh
+ * getrandom() key per call. */
+int ssb_set_rlc_deterministic(ssb_ctx* ctx, int on);
 /* The main stream of pipeline slot `slot` (hipStream_t as void*), e.g. to pass it back as the
  * `stream` of ssb_threshold_aggregate_batch_dev so a caller adds no hardware queue of its own.
  * A *_dev call whose `stream` is a slot's main stream runs on THAT slot; any other stream gets the
@@ -105,7 +119,10 @@ int ssb_kernel_time(ssb_ctx* ctx, const char* kernel_name, float* total_ms, int*
  * CommittedPoly::to_bytes without its u32 count); shares32: n 32-byte LITTLE-endian scalars
  * (bytes_to_blst_scalar; the low 255 bits are used, as blst_p1_mult(.., 255)); h48: the
  * commitment base (the reference's another_p1_generator(), hash_to_G1 of "dvf another
- * generator"), compressed.  A commitment or h that does not decode gives verdict 0. */
+ * generator"), compressed.  A commitment that does not decode counts as the identity (the
+ * reference ignores blst_p1_uncompress's error and keeps the zeroed point, polynomial.rs:109-111);
+ * one that decodes to a point outside G1 gives verdict 0 (blst_p1_mult's GLV result on such a point
+ * is implementation-defined); an h that does not decode gives verdict 0. */
 int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* commitments48, const uint64_t* ids,
                              const uint8_t* shares32, const uint8_t* h48, uint8_t* verdicts);
 
@@ -120,9 +137,11 @@ int ssb_dleq_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* points48, const
 /* Wire-format partial signatures -> 96-byte compressed signatures.  Record i (at wire + i*stride,
  * stride >= 202) is bincode(bls::Signature): u64 LE length 194, then "0x" and 192 hex digits of the
  * compressed point.  status[i]: 0 ok, 1 length field is not 194, 2 no "0x" prefix, 3 a non-hex
- * digit (out96[i] is then meaningless; the reference drops such a record -- "Deserialize failed",
- * operator.rs:113 -- so a caller leaves that share out of its job).  The point itself is checked
- * later, by the verify/aggregate entry points (decompression, subgroup check). */
+ * digit, 4 the bytes do not decompress to a curve point (bad flags, x >= p, off the curve; the
+ * infinity encoding IS a valid Signature).  Any non-zero status is a record the reference drops --
+ * bincode::deserialize::<Signature> fails, "Deserialize failed", operator.rs:108-113 -- so a caller
+ * leaves that share out of its job (out96[i] is then meaningless).  The subgroup check stays with
+ * verify (sig_groupcheck), as in the reference. */
 int ssb_decode_wire_sigs(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96,
                          int32_t* status);
 /* device pointers, enqueued on `stream` (hipStream_t as void*), no synchronisation */
@@ -162,7 +181,11 @@ int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* s
                                   uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
                                   uint64_t* out_err, uint8_t* share_verdicts);
 
-/* Same, all array arguments are device pointers; `stream` is a hipStream_t (NULL = default). */
+/* Same, all array arguments are device pointers; `stream` is a hipStream_t (NULL = default).
+ * The caller owns the job shapes: share_off must be non-decreasing with share_off[n_jobs] ==
+ * n_shares and 1 <= t[j] <= SSB_MAX_T; a job that breaks this (the library cannot check device
+ * arrays without a synchronisation) gets status SSB_DVF_INVALID_JOB and no output, and never makes
+ * a kernel index outside the batch. */
 int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares,
                                       const uint32_t* share_off, const uint32_t* t,
                                       const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids,

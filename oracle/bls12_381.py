@@ -838,18 +838,39 @@ def bincode_signature(sig96: bytes) -> bytes:
 
 
 def bincode_signature_decode(rec: bytes):
-    """(status, sig96 or None): 0 ok, 1 length field not 194, 2 no "0x", 3 non-hex digit."""
+    """(status, sig96 or None): 0 ok, 1 length field not 194, 2 no "0x", 3 non-hex digit, 4 the
+    point does not decompress (bincode::deserialize::<Signature> runs Signature::deserialize, i.e.
+    blst uncompress: flags, x < p, on the curve; src/validation/operator.rs:108-113 drops the
+    record on any of these)."""
     if int.from_bytes(rec[:8], "little") != 194:
         return 1, None
     if rec[8:10] != b"0x":
         return 2, None
     try:
-        return 0, bytes.fromhex(rec[10:204].decode("ascii"))
+        sig = bytes.fromhex(rec[10:204].decode("ascii"))
     except ValueError:
         return 3, None
+    try:
+        g2_decompress(sig)
+    except DecodeError:
+        return 4, None
+    return 0, sig
 
 
 # ---- DKG / VSS share verification (SURVEY.md §8f-4) ----
+def committed_poly_from_bytes(comm48):
+    """CommittedPoly::from_bytes (src/math/polynomial.rs:101-118): blst_p1_uncompress's return
+    code is ignored, so bytes that do not decode leave the zeroed affine point, which
+    blst_p1_from_affine maps to the identity (None here)."""
+    out = []
+    for b in comm48:
+        try:
+            out.append(g1_decompress(b))
+        except DecodeError:
+            out.append(None)
+    return out
+
+
 def committed_poly_eval(commitments, x: int):
     """CommittedPoly::eval (src/math/polynomial.rs:68-81): C_0 + sum_{i>=1} [x^i mod r] C_i with
     x^i accumulated by blst_sk_mul_n_check (mod r)."""
@@ -863,7 +884,12 @@ def committed_poly_eval(commitments, x: int):
 
 def feldman_share_verify(h, share: int, commitments, party: int) -> bool:
     """DKG share_verification (src/crypto/dkg.rs:433-450): blst_p1_mult(h, s) (255-bit scalar, s
-    from LE bytes; blst reads its low 255 bits) == committed_poly.eval(party)."""
+    from LE bytes; blst reads its low 255 bits) == committed_poly.eval(party).
+    PARITY UNPINNED for a commitment outside G1: blst_p1_mult uses GLV for 255-bit scalars, which
+    is [k]P only on G1, so the reference's result there is blst-defined; like the engine, this
+    restatement rejects such a commitment (an honest dealer never sends one)."""
+    if any(c is not None and not g1_in_subgroup_slow(c) for c in commitments):
+        return False
     return g1_mul(h, share & ((1 << 255) - 1)) == committed_poly_eval(commitments, party)
 
 

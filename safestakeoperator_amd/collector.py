@@ -15,14 +15,16 @@ oldest pending job has waited `window_s` (the aggregation window), or on `flush(
 resolves to exactly what `threshold_aggregate` returns for that job alone: the 96-byte combined
 signature, or the reference's `DvfError` raised from `Future.result()`.  Batching changes nothing
 observable per job: every job's verify-then-combine is independent, and the RLC batch check falls
-back to exact per-share verdicts when any share in the batch is invalid.
+back to exact per-share verdicts when any share in the batch is invalid.  The batch's random
+linear combination is keyed by a secret the library draws per call (include/ssbls.h), so shares
+from different validators' committees cannot be crafted to cancel each other out in one batch.
 """
 import threading
 import time
 from concurrent.futures import Future
 from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
 
-from .threshold import DvfError, Engine, ThresholdJob, ThresholdSignature
+from .threshold import MAX_T, DvfError, Engine, ThresholdJob, ThresholdSignature, job_shape_error
 
 BatchFn = Callable[[int, Sequence[ThresholdJob]], List[Union[bytes, DvfError]]]
 
@@ -49,7 +51,19 @@ class SlotCollector:
 
     # -- the replacement for ThresholdSignature::new(t).threshold_aggregate(...) per task --
     def submit(self, threshold: int, job: ThresholdJob) -> Future:
+        """A future of this job's result.  A job the engine cannot take (threshold outside
+        [1, MAX_T], a malformed message / signature / key) fails alone, at once, and never joins
+        a batch: the other validators of the slot are unaffected."""
         fut: Future = Future()
+        bad = None
+        if not 1 <= int(threshold) <= MAX_T:
+            bad = "threshold must be in [1, %d]" % MAX_T
+        elif len(job.sigs) == len(job.pks) == len(job.ids):   # DifferentLength: the engine's own error
+            bad = job_shape_error(job)
+        if bad:
+            fut.set_running_or_notify_cancel()
+            fut.set_exception(ValueError(bad))
+            return fut
         with self._cv:
             if self._closed:
                 raise RuntimeError("collector closed")
@@ -129,7 +143,7 @@ class SlotCollector:
                         f.set_exception(e)
                     continue
                 for (_, f), r in zip(live, res):
-                    if isinstance(r, DvfError):
+                    if isinstance(r, (DvfError, ValueError)):
                         f.set_exception(r)
                     else:
                         f.set_result(r)

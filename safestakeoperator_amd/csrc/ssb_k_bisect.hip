@@ -17,7 +17,6 @@
 // Work at 1% invalid shares (C2: 64 roots x 256): ~3.5k group checks (4-ary: ~2.1k, in 5 levels)
 // instead of 16,384 per-share checks; at one invalid share, 96.  Every kernel here is a no-op (uniform early exit) when the batch passed.
 #include "ssb_kernels.h"
-#include "ssb_wave.h"
 #include "ssb_lane_ops.h"
 
 namespace ssb {
@@ -57,7 +56,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, in
     if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
 }
 // threads [0, n): rsig[s] = k_s sig_s;  [n, 2n): rpk[s] = k_s pk_s  (candidates only)
-__global__ void SSB_LB(64) k_fb_rlc(int n, uint64_t seed, const uint32_t* __restrict__ ok,
+__global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restrict__ ok,
                                    const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig_aff,
                                    const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
                                    g1_jac* __restrict__ rpk) {
@@ -67,14 +66,14 @@ __global__ void SSB_LB(64) k_fb_rlc(int n, uint64_t seed, const uint32_t* __rest
   // reserves scratch for the largest kernel it has run, and this one is launched on every batch
   if (g < n) {
     if (flags[g] & FLAG_CANDIDATE) {
-      const uint64_t k = rlc_scalar_odd(seed, (uint64_t)g);
+      const uint64_t k = rlc_scalar_odd(key, (uint64_t)g);
       const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
       g2_jac r; jac_mul_aff(r, sig_aff[g], kw, 2); rsig[g] = r;
     }
   } else if (g < 2 * n) {
     const int s = g - n;
     if (flags[s] & FLAG_CANDIDATE) {
-      const uint64_t k = rlc_scalar_odd(seed, (uint64_t)s);
+      const uint64_t k = rlc_scalar_odd(key, (uint64_t)s);
       const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
       g1_jac r; jac_mul_aff(r, pk_aff[s], kw, 2); rpk[s] = r;
     }
@@ -228,7 +227,7 @@ int fallback_levels(size_t n) {
   return L;
 }
 
-void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const uint32_t* ok, const uint32_t* flags,
+void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
                      uint8_t* gv0, uint8_t* gv1, uint8_t* verdict) {
@@ -239,7 +238,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const ui
   const int lb = fallback_log2_branch();
   hipLaunchKernelGGL(k_fb_prep, dim3(1), dim3(PREP_THREADS), 0, st, n, n_roots, L, lb, ok, share_root, cnt, start, cursor,
                      gst, perm);
-  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, seed, ok, flags, sig, pk, rsig, rpk);
+  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, key, ok, flags, sig, pk, rsig, rpk);
   for (int l = 0; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;

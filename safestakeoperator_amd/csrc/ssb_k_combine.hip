@@ -2,12 +2,18 @@
 // Launched from ssbls.hip (declarations in ssb_kernels.h); one TU per kernel family so the
 // library compiles in parallel.
 #include "ssb_kernels.h"
-#include "ssb_wave.h"
 
 namespace ssb {
 namespace k {
 
-__global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+// A job the engine cannot run -- t == 0, t > SSB_MAX_T, share_off[j + 1] < share_off[j] or past the
+// batch's n_shares (only the *_dev entry points can pass one: the host wrapper refuses them) --
+// gets SSB_DVF_INVALID_JOB and is never selected, so no later kernel indexes its fixed t-arrays or
+// its share range.  (k_share_map clamps the ranges the same way.)
+SSB_INL bool job_ok(uint32_t b, uint32_t e, uint32_t t, uint32_t n_shares) {
+  return t >= 1 && t <= SSB_MAX_T && b <= e && e <= n_shares;
+}
+__global__ void k_select(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                          const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
                          const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
                          uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err) {
@@ -15,6 +21,7 @@ __global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uin
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
   const uint32_t b = off[j], e = off[j + 1], t = tt[j];
+  if (!job_ok(b, e, t, n_shares)) { status[j] = SSB_DVF_INVALID_JOB; err[2 * j] = t; err[2 * j + 1] = e - b; return; }
   const uint32_t n = e - b;
   if (n < t) { status[j] = SSB_DVF_INSUFFICIENT_SIGNATURES; err[2 * j] = n; err[2 * j + 1] = t; return; }
   uint32_t cnt = 0;

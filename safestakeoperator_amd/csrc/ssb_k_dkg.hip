@@ -5,10 +5,16 @@
 // with eval = C_0 + sum_{i>=1} [x^i mod r] C_i (src/math/polynomial.rs:68-81).  Here one thread
 // per check: [s]h by a 4-bit fixed window over the low 255 bits of s (blst_p1_mult's nbits = 255),
 // and the evaluation by Horner in the group, acc = [x] acc + C_i for i = t-1 .. 0 -- the same
-// group element, since every C_i has order r and the integer x^i equals x^i mod r on it.
+// group element, since every C_i used has order r and the integer x^i equals x^i mod r on it.
 // Commitments arrive compressed (CommittedPoly::to_bytes, polynomial.rs:88-99 without the count
-// prefix); one that does not decode makes the check fail.  Registration-time work, rare: plain
-// single-lane code.  k_dleq_verify: the Chaum-Pedersen proofs of exchange_group_public_keys.
+// prefix).  Decoding follows CommittedPoly::from_bytes (polynomial.rs:101-118): the return code of
+// blst_p1_uncompress is ignored, so a commitment that does not decode leaves the all-zero affine
+// point, which blst_p1_from_affine turns into the identity -- here too it counts as infinity.
+// A commitment that decodes to a curve point OUTSIDE G1 fails the check: blst_p1_mult multiplies
+// 255-bit scalars by GLV, which equals [k]P only on G1, so the reference's result for such a point
+// is blst-implementation-defined (and unequal to [s]h unless crafted); the engine rejects it
+// (documented deviation).  Registration-time work, rare: plain single-lane code.
+// k_dleq_verify: the Chaum-Pedersen proofs of exchange_group_public_keys.
 #include "ssb_kernels.h"
 
 namespace ssb {
@@ -22,6 +28,13 @@ SSB_FN void g1_mul_u64_jac(g1_jac& r, const g1_jac& p, uint64_t x) {
     if ((x >> i) & 1ull) jac_add(acc, acc, p);
   }
   r = acc;
+}
+
+// [r]P == O: membership in the order-r subgroup G1 (r from ssb_consts.h)
+SSB_FN bool g1_in_subgroup(const g1_aff& p) {
+  g1_jac q;
+  jac_mul_aff(q, p, R_LIMBS, 8);
+  return jac_is_inf(q);
 }
 
 SSB_INL bool g1_jac_eq(const g1_jac& a, const g1_jac& b) {
@@ -51,9 +64,10 @@ __global__ void SSB_LB(64) k_feldman_share(int n, int t, const uint8_t* __restri
     for (int k2 = 0; k2 < 48; ++k2) b[k2] = src[k2];
     g1_aff C;
     const uint32_t st = g1_decompress(C, b);
-    if (!(st & DEC_OK)) { ok = false; break; }
     if (c != t - 1) g1_mul_u64_jac(acc, acc, x[i]);
-    if (!C.inf) jac_add_aff(acc, acc, C);
+    if (!(st & DEC_OK) || C.inf) continue;      // undecodable: the identity, as the reference
+    if (!g1_in_subgroup(C)) { ok = false; break; }
+    jac_add_aff(acc, acc, C);
   }
   if (!ok) { verdict[i] = 0; return; }
   uint32_t k[8];

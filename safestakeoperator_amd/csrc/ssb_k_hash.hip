@@ -7,17 +7,7 @@
 namespace ssb {
 namespace k {
 
-__global__ void SSB_LB(64) k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
-                                                   g2_aff* __restrict__ out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t m[32];
-  for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
-  g2_aff h;
-  hash_to_g2(h, m, dst.b, dst.len);
-  out[i] = h;
-}
-// ---- staged hash_to_G2 (same result as k_hash_to_g2, shorter critical path) ----
+// ---- staged hash_to_G2 (the RFC 9380 hash_to_curve of ssb_h2c.h, split into stages) ----
 // 1: expand_message_xmd + the two field elements, one lane per root
 __global__ void SSB_LB(64) k_h2c_u(int n, const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;

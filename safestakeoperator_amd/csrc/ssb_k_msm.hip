@@ -3,7 +3,7 @@
 //
 // The batch check  prod_r e(sum_{i in r} k_i pk_i, H_r) == e(g1, sum_i k_i sig_i)  needs, over the
 // candidate shares, one G1 sum per signing root and one G2 sum, with the 64-bit RLC scalars
-// k_i = rlc_scalar_odd(seed, i).  Both are computed as Pippenger bucket MSMs:
+// k_i = rlc_scalar_odd(key, i) (secret per-call key, ssb_units.h).  Both are computed as Pippenger bucket MSMs:
 //   - W = ceil(64 / c) windows of c bits; entry (i, w) lands in bucket (group, w, digit), digit 0
 //     dropped.  k_msm_sort<false> (count) / k_scan_* / k_msm_sort<true> (scatter) counting-sort the entries by bucket key
 //     (order inside a bucket is irrelevant: the group law is exact).
@@ -42,7 +42,7 @@ SSB_INL void msm_entries(int i, uint64_t k, uint32_t g, const msm_cfg& c, uint32
 
 // cnt[key] += 1 per (share, window) entry (SCATTER: ent[cursor[key]++] = share)
 template <bool SCATTER>
-__global__ void SSB_LB(256) k_msm_sort(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(256) k_msm_sort(int n, rlc_key key, const uint32_t* __restrict__ sflags,
                                                   const uint32_t* __restrict__ pflags,
                                                   const uint32_t* __restrict__ share_root, msm_cfg c2, msm_cfg c1,
                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
@@ -50,7 +50,7 @@ __global__ void SSB_LB(256) k_msm_sort(int n, uint64_t seed, const uint32_t* __r
   if (i >= n || !share_decodable(sflags[i], pflags[i])) return;
   const uint32_t g = share_root[i];
   if (g >= c1.ngroups) return;  // out-of-range root index: the share cannot enter the batch
-  const uint64_t k = rlc_scalar_odd(seed, (uint64_t)i);
+  const uint64_t k = rlc_scalar_odd(key, (uint64_t)i);
   msm_entries<SCATTER>(i, k, 0u, c2, cnt, ent);
   msm_entries<SCATTER>(i, k, g, c1, cnt, ent);
 }
@@ -242,13 +242,13 @@ __global__ void SSB_LB(64) k_msm_horner(int ngroups, int c, int W, const g1_jac*
 
 // per-share G1 RLC product (the G1 side when the roots' groups are small: 64 doublings per share
 // beat a per-root bucket MSM whose window reduce / Horner overheads dominate at ~256 shares/root)
-__global__ void SSB_LB(64) k_rlc_pk(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
+__global__ void SSB_LB(64) k_rlc_pk(int n, rlc_key key, const uint32_t* __restrict__ sflags,
                                                const uint32_t* __restrict__ pflags, const g1_aff* __restrict__ pk_aff,
                                                g1_jac* __restrict__ rpk) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   g1_jac r;
-  if (share_decodable(sflags[s], pflags[s])) unit_rlc_pk(r, pk_aff[s], rlc_scalar_odd(seed, (uint64_t)s));
+  if (share_decodable(sflags[s], pflags[s])) unit_rlc_pk(r, pk_aff[s], rlc_scalar_odd(key, (uint64_t)s));
   else jac_set_inf(r);
   rpk[s] = r;
 }
@@ -277,16 +277,16 @@ namespace launch {
 
 using namespace ssb::k;
 
-void msm_sort(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
+void msm_sort(hipStream_t st, int n, const rlc_key& key, const uint32_t* sflags, const uint32_t* pflags,
               const uint32_t* share_root, const msm_cfg& c2, const msm_cfg& c1, uint32_t K, uint32_t* cnt,
               uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent, uint32_t* order) {
   hipMemsetAsync(cnt, 0, (size_t)K * 4, st);
   const unsigned g = (unsigned)((n + 255) / 256), nb = (K + SCAN_BLOCK - 1) / SCAN_BLOCK;
-  if (n) hipLaunchKernelGGL(k_msm_sort<false>, dim3(g), dim3(256), 0, st, n, seed, sflags, pflags, share_root, c2, c1, cnt, ent);
+  if (n) hipLaunchKernelGGL(k_msm_sort<false>, dim3(g), dim3(256), 0, st, n, key, sflags, pflags, share_root, c2, c1, cnt, ent);
   hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(SCAN_T), 0, st, K, cnt, start, bsum);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, nb, bsum);
   hipLaunchKernelGGL(k_scan_add, dim3((K + 255) / 256), dim3(256), 0, st, K, start, bsum, cur);
-  if (n) hipLaunchKernelGGL(k_msm_sort<true>, dim3(g), dim3(256), 0, st, n, seed, sflags, pflags, share_root, c2, c1, cur, ent);
+  if (n) hipLaunchKernelGGL(k_msm_sort<true>, dim3(g), dim3(256), 0, st, n, key, sflags, pflags, share_root, c2, c1, cur, ent);
   // bucket order by count (bsum reused for the 512 bins)
   hipMemsetAsync(bsum, 0, ORDER_BINS * 4, st);
   hipLaunchKernelGGL(k_order_hist, dim3((K + 255) / 256), dim3(256), 0, st, K, c1.base, cnt, bsum);

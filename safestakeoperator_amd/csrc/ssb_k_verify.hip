@@ -1,18 +1,20 @@
-// ssb_k_verify.hip -- kernels (gfx950): share map, decompression, flags, RLC sums, exact fallback verify.
+// ssb_k_verify.hip -- kernels (gfx950): share map, decompression, flags, verdicts, per-root segment sums.
 // Launched from ssbls.hip (declarations in ssb_kernels.h); one TU per kernel family so the
 // library compiles in parallel.
 #include "ssb_kernels.h"
-#include "ssb_wave.h"
 
 namespace ssb {
 namespace k {
 
-__global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
+// share -> job and share -> root; a job range past n_shares is clipped (k_select marks that job
+// SSB_DVF_INVALID_JOB), so a bad _dev argument never writes outside the batch
+__global__ void k_share_map(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
                             uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   const uint32_t r = job_root ? job_root[j] : 0u;
-  for (uint32_t s = off[j]; s < off[j + 1]; ++s) {
+  const uint32_t e = off[j + 1] < n_shares ? off[j + 1] : n_shares;
+  for (uint32_t s = off[j]; s < e; ++s) {
     share_job[s] = (uint32_t)j;
     if (share_root) share_root[s] = r;
   }
@@ -83,32 +85,6 @@ __global__ void SSB_LB(64) k_decode_pk(int n, const uint8_t* __restrict__ pk48, 
   pflags[s] = unit_decode_pk(pk, b);
   pk_aff[s] = pk;
 }
-// threads [0, n): G2 subgroup check; [n, 2n): r_i * sig_i; [2n, 3n): r_i * pk_i  (single lane each:
-// at C2 size the chip has spare waves, so the per-share chains run one per lane; the lane-group
-// versions in ssb_k_lane.hip cost ~6x the instructions for ~2x lower latency)
-__global__ void SSB_LB(64) k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
-                                                  const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
-                                                  const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
-                                                  g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) {
-    const uint32_t sf = sflags[g];
-    gflags[g] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[g]) : 0u;
-  } else if (g < 2 * n) {
-    const int s = g - n;
-    const uint32_t sf = sflags[s];
-    g2_jac r;
-    if ((sf & DEC_OK) && !(sf & DEC_INF)) unit_rlc_sig(r, sig_aff[s], rlc_scalar_odd(seed, (uint64_t)s)); else jac_set_inf(r);
-    rsig[s] = r;
-  } else if (g < 3 * n) {
-    const int s = g - 2 * n;
-    const uint32_t pf = pflags[s];
-    g1_jac r;
-    if ((pf & DEC_OK) && !(pf & DEC_INF)) unit_rlc_pk(r, pk_aff[s], rlc_scalar_odd(seed, (uint64_t)s)); else jac_set_inf(r);
-    rpk[s] = r;
-  }
-}
-
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
                         const uint32_t* __restrict__ gflags, const uint32_t* __restrict__ share_root, uint32_t n_roots,
                         uint32_t* __restrict__ flags) {
@@ -117,51 +93,6 @@ __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32
   uint32_t f = combine_flags(sflags[s], pflags[s], gflags[s]);
   if (share_root[s] >= n_roots) f &= ~FLAG_CANDIDATE;  // no H(root): the share cannot verify
   flags[s] = f;
-}
-__global__ void SSB_LB(SUM_THREADS) k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
-                                                                const uint32_t* __restrict__ flags,
-                                                                const g1_jac* __restrict__ rpk,
-                                                                g1_aff* __restrict__ root_sum) {
-  __shared__ g1_jac sh[SUM_THREADS];
-  const uint32_t b = blockIdx.x;
-  g1_jac acc; jac_set_inf(acc);
-  for (int s = threadIdx.x; s < n; s += SUM_THREADS)
-    if ((flags[s] & FLAG_CANDIDATE) && share_root[s] == b) jac_add(acc, acc, rpk[s]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) { g1_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) { g1_aff a; jac_to_aff(a, acc); root_sum[b] = a; }
-}
-__global__ void SSB_LB(SUM_THREADS) k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
-                                                                const g2_jac* __restrict__ rsig,
-                                                                g2_jac* __restrict__ part) {
-  __shared__ g2_jac sh[SUM_THREADS];
-  g2_jac acc; jac_set_inf(acc);
-  for (int s = blockIdx.x * SUM_THREADS + threadIdx.x; s < n; s += gridDim.x * SUM_THREADS)
-    if (flags[s] & FLAG_CANDIDATE) jac_add(acc, acc, rsig[s]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = SUM_THREADS / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[blockIdx.x] = acc;
-}
-__global__ void SSB_LB(64) k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
-                                                     g2_aff* __restrict__ out) {
-  __shared__ g2_jac sh[64];
-  g2_jac acc; jac_set_inf(acc);
-  for (int i = threadIdx.x; i < nparts; i += 64) jac_add(acc, acc, part[i]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = 32; w > 0; w >>= 1) {
-    if (threadIdx.x < w) { g2_jac o = sh[threadIdx.x + w]; jac_add(acc, acc, o); sh[threadIdx.x] = acc; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) { g2_aff a; jac_to_aff(a, acc); *out = a; }
 }
 // Verdicts when the RLC batch check passed (every candidate is valid) and for non-candidates; the
 // candidates of a failed batch are left to k_fallback_lane (ssb_k_pair.hip).

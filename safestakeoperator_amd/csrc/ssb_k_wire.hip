@@ -22,7 +22,7 @@ __device__ __forceinline__ int hexval(uint32_t c) {
   return -1;
 }
 
-__global__ void k_wire_sig(int n, const uint8_t* __restrict__ wire, size_t stride, uint8_t* __restrict__ out96,
+__global__ void SSB_LB(64) k_wire_sig(int n, const uint8_t* __restrict__ wire, size_t stride, uint8_t* __restrict__ out96,
                            int32_t* __restrict__ status) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -38,6 +38,15 @@ __global__ void k_wire_sig(int n, const uint8_t* __restrict__ wire, size_t strid
     if ((hi | lo) < 0) st = st ? st : 3;
     o[b] = (uint8_t)(((hi & 15) << 4) | (lo & 15));
   }
+  // bincode::deserialize::<Signature> also decompresses the point (blst uncompress: flags, x < p,
+  // on the curve; infinity is a valid Signature) -- a record that fails is dropped by the reference
+  // (operator.rs:108-113), so it is reported here instead of failing later as an invalid share
+  if (!st) {
+    uint8_t b[96];
+    for (int k = 0; k < 96; ++k) b[k] = o[k];
+    g2_aff pt;
+    if (!(g2_decompress(pt, b) & DEC_OK)) st = 4;
+  }
   status[i] = st;
 }
 
@@ -45,7 +54,7 @@ __global__ void k_wire_sig(int n, const uint8_t* __restrict__ wire, size_t strid
 
 namespace launch {
 void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status) {
-  if (n > 0) hipLaunchKernelGGL(k::k_wire_sig, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, wire, stride, out96, status);
+  if (n > 0) hipLaunchKernelGGL(k::k_wire_sig, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, wire, stride, out96, status);
 }
 }  // namespace launch
 }  // namespace ssb

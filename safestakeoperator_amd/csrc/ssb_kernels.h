@@ -22,15 +22,15 @@ __global__ void k_root_scan(int n_roots, const uint32_t* __restrict__ cnt, uint3
                             uint32_t* __restrict__ cursor);
 __global__ void k_root_scatter(int n, int n_roots, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cursor,
                                uint32_t* __restrict__ perm);
-// rpk[s] = rlc_scalar_odd(seed, s) * pk[s] for every decodable share (infinity otherwise)
-__global__ void k_rlc_pk(int n, uint64_t seed, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
+// rpk[s] = rlc_scalar_odd(key, s) * pk[s] for every decodable share (infinity otherwise)
+__global__ void k_rlc_pk(int n, rlc_key key, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
                          const g1_aff* __restrict__ pk_aff, g1_jac* __restrict__ rpk);
 __global__ void k_sum_seg(int n_roots, const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
                           const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
                           const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ rsig, g1_aff* __restrict__ s1,
                           g2_aff* __restrict__ s2);
 
-__global__ void k_share_map(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
+__global__ void k_share_map(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
                             uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root);
 __global__ void k_decode(int n, const uint8_t* __restrict__ sig96,
                                                const uint8_t* __restrict__ pk48, int group_check,
@@ -46,45 +46,24 @@ __global__ void k_pk_gather(int n, const uint32_t* __restrict__ pk_index, uint32
                             g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ pflags);
 __global__ void k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
                             uint32_t* __restrict__ pflags);
-__global__ void k_check_rlc(int n, uint64_t seed, const uint32_t* __restrict__ sflags,
-                            const uint32_t* __restrict__ pflags, const g2_aff* __restrict__ sig_aff,
-                            const g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ gflags,
-                            g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk);
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
                         const uint32_t* __restrict__ gflags, const uint32_t* __restrict__ share_root, uint32_t n_roots,
                         uint32_t* __restrict__ flags);
-__global__ void k_sum_g1_by_root(int n, const uint32_t* __restrict__ share_root,
-                                                                const uint32_t* __restrict__ flags,
-                                                                const g1_jac* __restrict__ rpk,
-                                                                g1_aff* __restrict__ root_sum);
-__global__ void k_sum_g2_partial(int n, const uint32_t* __restrict__ flags,
-                                                                const g2_jac* __restrict__ rsig,
-                                                                g2_jac* __restrict__ part);
-__global__ void k_sum_g2_final(int nparts, const g2_jac* __restrict__ part,
-                                                     g2_aff* __restrict__ out);
 __global__ void k_verdict_fast(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
                                uint8_t* __restrict__ verdict);
 __global__ void k_fallback_lane(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
                                 const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ H,
                                 const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
                                 uint8_t* __restrict__ verdict);
-__global__ void k_miller_wave(int n_roots, const g1_aff* __restrict__ root_sum,
-                                                    const g2_aff* __restrict__ H, const g2_aff* __restrict__ sig_sum,
-                                                    fp12* __restrict__ f);
-__global__ void k_final_wave(int npairs, const fp12* __restrict__ f, uint32_t* __restrict__ ok);
-__global__ void k_miller_lane(int n_roots, const g1_aff* __restrict__ root_sum, const g2_aff* __restrict__ H,
-                              const g2_aff* __restrict__ sig_sum, fp12* __restrict__ f);
 __global__ void k_miller_pairs(int npairs, const g1_aff* __restrict__ P, const g2_aff* __restrict__ Q,
                                fp12* __restrict__ f);
 __global__ void k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out);
 __global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok);
-__global__ void k_hash_to_g2(int n, const uint8_t* __restrict__ roots, dst_arg dst,
-                                                   g2_aff* __restrict__ out);
 __global__ void k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
                                              const g2_aff* __restrict__ H, uint8_t* __restrict__ out96);
 __global__ void k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48);
 __global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* __restrict__ out192);
-__global__ void k_select(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+__global__ void k_select(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                          const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
                          const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
                          uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err);
@@ -126,12 +105,6 @@ namespace launch {
 //   signatures: sflags[s] has DEC_OK and not DEC_INF);  exc[s] |= 1 when an addition was
 //   exceptional (the share is then recomputed by the exact single-lane fallback).
 void lane_subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
-//   rsig[s] = rlc_scalar_odd(seed, s) * sig[s]   (or infinity when the signature is not decodable)
-void lane_rlc_g2(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const g2_aff* sig, g2_jac* rsig,
-                 uint32_t* exc);
-//   rpk[s] = rlc_scalar_odd(seed, s) * pk[s]      (exc bit 1)
-void lane_rlc_g1(hipStream_t st, int n, uint64_t seed, const uint32_t* pflags, const g1_aff* pk, g1_jac* rpk,
-                 uint32_t* exc);
 // staged hash_to_G2 of n roots into out (ssb_k_hash.hip); ws: hash_ws_bytes(n) device bytes
 size_t hash_ws_bytes(size_t n);
 void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws);
@@ -139,7 +112,7 @@ void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst,
 // entries of both MSMs by bucket key (K keys; cnt/start/cur: K words, bsum: 1024 words, ent: one
 // word per entry).  msm_g2: window sums of sum_i k_i sig_i as multi-pairing pairs
 // (pair_q[w] = W_w affine, pair_p[w] = [2^(c w)](-g1)).  msm_g1: root_sum[r] = sum_{i in r} k_i pk_i.
-void msm_sort(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
+void msm_sort(hipStream_t st, int n, const rlc_key& key, const uint32_t* sflags, const uint32_t* pflags,
               const uint32_t* share_root, const msm_cfg& c2, const msm_cfg& c1, uint32_t K, uint32_t* cnt,
               uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent, uint32_t* order);
 void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
@@ -155,7 +128,7 @@ void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, 
 // gst fallback_levels(n) * (n_roots + 1) words, rsig/rpk n points, gv0/gv1 n + n_roots bytes.
 int fallback_log2_branch();
 int fallback_levels(size_t n);
-void fallback_bisect(hipStream_t st, int n, int n_roots, uint64_t seed, const uint32_t* ok, const uint32_t* flags,
+void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
                      uint8_t* gv0, uint8_t* gv1, uint8_t* verdict);
@@ -167,10 +140,6 @@ void feldman_share(hipStream_t st, int n, int t, const uint8_t* comm48, const ui
                    const g1_aff* h, const uint32_t* hflags, uint8_t* verdict);
 // DLEQ verification (ssb_k_dkg.hip): pts48 = n x (x1, y1, x2, y2) compressed, c32 / r32 LE scalars
 void dleq_verify(hipStream_t st, int n, const uint8_t* pts48, const uint8_t* c32, const uint8_t* r32, uint8_t* verdict);
-// exact single-lane recomputation of the shares whose lane-group stage raised exc
-void lane_fixup(hipStream_t st, int n, uint64_t seed, const uint32_t* sflags, const uint32_t* pflags,
-                const g2_aff* sig, const g1_aff* pk, const uint32_t* exc, uint32_t* gflags, g2_jac* rsig,
-                g1_jac* rpk);
 
 }  // namespace launch
 }  // namespace ssb

@@ -10,18 +10,61 @@ namespace ssb {
 
 enum : uint32_t { FLAG_CANDIDATE = 1u << 16 };
 
-SSB_INL uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
-  // splitmix64(seed ^ golden*i), forced non-zero
-  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (i + 1));
+// ---- random-linear-combination scalars -------------------------------------------------------
+// lighthouse's verify_signature_sets draws one fresh non-zero 64-bit scalar per signature set from
+// rand::thread_rng() (ChaCha12 keyed from the OS; RAND_BITS = 64, src/crypto/impls/blst.rs:12).
+// Here: a 256-bit key drawn from getrandom() by the host for EVERY batch call (after the caller has
+// handed the inputs over), passed to the kernels by value; share i's scalar is the first 64 bits
+// of ChaCha12(key, counter = i, nonce = "SSB-RLC1").  The key never leaves the library, so a sender
+// cannot predict k_i and cannot build shares whose errors cancel in the sums (sig_a + [k_b]D,
+// sig_b - [k_a]D).  ssb_set_rlc_deterministic() switches a context to a key expanded from the
+// caller's seed (reproducible runs and the forgery test only: NOT sound against chosen shares).
+struct rlc_key { uint32_t w[8]; };
+
+SSB_INL uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+#define SSB_QR(a, b, c, d)                     \
+  a += b; d ^= a; d = rotl32(d, 16);           \
+  c += d; b ^= c; b = rotl32(b, 12);           \
+  a += b; d ^= a; d = rotl32(d, 8);            \
+  c += d; b ^= c; b = rotl32(b, 7);
+// words 0 and 1 of the ChaCha12 block (key, 64-bit block counter i, 64-bit nonce "SSB-RLC1")
+SSB_INL uint64_t chacha12_u64(const rlc_key& key, uint64_t i) {
+  const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                           key.w[0], key.w[1], key.w[2], key.w[3], key.w[4], key.w[5], key.w[6], key.w[7],
+                           (uint32_t)i, (uint32_t)(i >> 32), 0x2d425353u /* "SSB-" */, 0x31434c52u /* "RLC1" */};
+  uint32_t x[16];
+  for (int q = 0; q < 16; ++q) x[q] = in[q];
+#pragma unroll 1
+  for (int r = 0; r < 6; ++r) {             // 6 double rounds = 12 rounds
+    SSB_QR(x[0], x[4], x[8], x[12]) SSB_QR(x[1], x[5], x[9], x[13])
+    SSB_QR(x[2], x[6], x[10], x[14]) SSB_QR(x[3], x[7], x[11], x[15])
+    SSB_QR(x[0], x[5], x[10], x[15]) SSB_QR(x[1], x[6], x[11], x[12])
+    SSB_QR(x[2], x[7], x[8], x[13]) SSB_QR(x[3], x[4], x[9], x[14])
+  }
+  return (uint64_t)(x[0] + in[0]) | ((uint64_t)(x[1] + in[1]) << 32);
+}
+#undef SSB_QR
+
+// the RLC scalars: odd, so the regular signed-window recoding applies and k != 0
+// (63 secret random bits per share; lighthouse draws 64: the batch soundness error stays 2^-63)
+SSB_INL uint64_t rlc_scalar_odd(const rlc_key& key, uint64_t i) { return chacha12_u64(key, i) | 1ull; }
+
+// deterministic mode: key words = splitmix64 outputs 0..3 of the caller's seed
+SSB_INL uint64_t splitmix64_at(uint64_t seed, uint64_t j) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (j + 1);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return z ? z : 1ull;
+  return z ^ (z >> 31);
 }
-
-// the RLC scalars the lane-group stage uses: odd, so the regular signed-window recoding applies
-// (63 random bits per share; lighthouse draws 64: the batch soundness error stays 2^-63)
-SSB_INL uint64_t rlc_scalar_odd(uint64_t seed, uint64_t i) { return rlc_scalar(seed, i) | 1ull; }
+SSB_INL rlc_key rlc_key_from_seed(uint64_t seed) {
+  rlc_key k;
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t z = splitmix64_at(seed, (uint64_t)j);
+    k.w[2 * j] = (uint32_t)z;
+    k.w[2 * j + 1] = (uint32_t)(z >> 32);
+  }
+  return k;
+}
 
 SSB_INL g1_aff g1_neg_generator() {
   g1_aff ng; ng.x = fp_from_c(G1_GEN_X); ng.y = fp_from_c(G1_GEN_NEG_Y); ng.inf = 0;

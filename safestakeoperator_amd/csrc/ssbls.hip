@@ -26,9 +26,10 @@
 #include <mutex>
 #include <algorithm>
 #include <cmath>
+#include <cerrno>
+#include <sys/random.h>
 
 #include "ssb_units.h"
-#include "ssb_wave.h"
 #include "ssb_kernels.h"
 #include "../../include/ssbls.h"
 
@@ -84,6 +85,9 @@ struct ssb_ctx {
   int ntails = 3;
   // decoded public keys (ssb_pk_cache_set): affine points + DEC_* flags, indexed by the caller
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0;
+  // RLC key of each batch: fresh from getrandom() per call (default), or expanded from the caller's
+  // seed (ssb_set_rlc_deterministic: reproducible runs / tests only)
+  bool rlc_deterministic = false;
 };
 
 namespace {
@@ -199,6 +203,27 @@ int fill_dst(ssb_ctx* ctx, dst_arg& d, const uint8_t* dst, size_t dst_len) {
   memset(&d, 0, sizeof(d));
   if (dst_len) memcpy(d.b, dst, dst_len);
   d.len = (int)dst_len;
+  return SSB_OK;
+}
+
+// The batch's RLC key (ssb_units.h): 256 bits from the OS CSPRNG for every call, drawn after the
+// caller has handed the inputs over, so no sender can know its shares' scalars; the caller's
+// rlc_seed is XORed in (it can only add entropy).  Deterministic mode: the seed alone.
+int draw_rlc_key(ssb_ctx* ctx, uint64_t seed, rlc_key& key) {
+  if (ctx->rlc_deterministic) { key = rlc_key_from_seed(seed); return SSB_OK; }
+  uint8_t* p = (uint8_t*)key.w;
+  size_t got = 0;
+  while (got < sizeof(key.w)) {
+    const ssize_t r = getrandom(p + got, sizeof(key.w) - got, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      ctx->err = "getrandom failed: no entropy for the RLC scalars";
+      return SSB_EINVAL;
+    }
+    got += (size_t)r;
+  }
+  key.w[0] ^= (uint32_t)seed;
+  key.w[1] ^= (uint32_t)(seed >> 32);
   return SSB_OK;
 }
 
@@ -323,8 +348,10 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
 
 template <class F>
 int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
-               const uint32_t* d_pk_index, const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t seed,
+               const uint32_t* d_pk_index, const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t rlc_seed,
                uint8_t* d_verdict, F on_decoded, hipStream_t tail) {
+  rlc_key key;
+  if (int rc = draw_rlc_key(ctx, rlc_seed, key)) return rc;
   hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
   SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
@@ -348,13 +375,13 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_sdec, 0));
   if (!P.g1_msm) {
     timed t(ctx, "k_rlc_pk", s1);
-    if (n) hipLaunchKernelGGL(k_rlc_pk, dim3(nblk(n, 64)), dim3(64), 0, s1, (int)n, seed, w.sflags, w.pflags, w.pk_aff, w.rpk);
+    if (n) hipLaunchKernelGGL(k_rlc_pk, dim3(nblk(n, 64)), dim3(64), 0, s1, (int)n, key, w.sflags, w.pflags, w.pk_aff, w.rpk);
     SSB_HIP(hipMemsetAsync(w.rcnt, 0, n_roots * 4, s1));
     if (n) hipLaunchKernelGGL(k_root_hist, dim3(nblk(n, 256)), dim3(256), 0, s1, (int)n, (int)n_roots, d_share_root, w.rcnt);
     hipLaunchKernelGGL(k_root_scan, dim3(1), dim3(64), 0, s1, (int)n_roots, w.rcnt, w.rstart, w.rcur);
     if (n) hipLaunchKernelGGL(k_root_scatter, dim3(nblk(n, 256)), dim3(256), 0, s1, (int)n, (int)n_roots, d_share_root, w.rcur, w.perm);
   }
-  { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, seed, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent, w.order); }
+  { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, key, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent, w.order); }
   if (n) {
     { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags, w.gexc); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, d_share_root,
@@ -406,7 +433,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
       hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, fbs, (int)n, w.ok, w.flags,
                          d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
     else
-      launch::fallback_bisect(fbs, (int)n, (int)n_roots, seed, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff,
+      launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff,
                               w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict);
   }
   if (!fb_tail && tail != st) {
@@ -491,6 +518,12 @@ int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
     if (init_slot(ctx->sl[i], streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
   ctx->next = 0;
   ctx->cur = &ctx->sl[0];
+  return SSB_OK;
+}
+
+int ssb_set_rlc_deterministic(ssb_ctx* ctx, int on) {
+  if (!ctx) return SSB_EINVAL;
+  ctx->rlc_deterministic = on != 0;
   return SSB_OK;
 }
 
@@ -703,11 +736,11 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
-  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, job_root, share_job, share_root);
+  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, job_root, share_job, share_root);
   // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
   auto spec = [&] {
     hipStreamWaitEvent(sc, ctx->cur->ev_dec, 0);
-    { timed tm(ctx, "k_select", sc); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err); }
+    { timed tm(ctx, "k_select", sc); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, (uint32_t)n, share_off, t, ids, (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err); }
     { timed tm(ctx, "k_combine_fast", sc); hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)nullptr, fast, out_sig96); }
     { timed tm(ctx, "k_lagrange", sc); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)nullptr, (const uint32_t*)fast, lam); }
     if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
@@ -719,7 +752,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   // exact path, only if the RLC batch failed (every kernel is a no-op when w.ok == 1)
   SSB_HIP(hipStreamWaitEvent(tl, ctx->cur->ev_comb, 0));
   st = tl;
-  hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
+  hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
   hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)w.ok, fast, out_sig96);
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, (const uint32_t*)fast, lam);
   if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, (const uint32_t*)fast, term);
@@ -910,7 +943,7 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
     SSB_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, st));
   }
   SSB_HIP(hipMemcpyAsync(d_off, share_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, (const uint32_t*)nullptr, share_job, (uint32_t*)nullptr);
+  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, d_off, (const uint32_t*)nullptr, share_job, (uint32_t*)nullptr);
   if (n) hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, (const uint8_t*)nullptr, 0, sig_aff, (g1_aff*)nullptr, flags);
   hipLaunchKernelGGL(k_select_all, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, flags, sel, tt, d_st, err);
   // unsafe_aggregate does not subgroup-check its inputs (blst.rs:77-84): always the exact 255-bit path

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import secrets
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Union, Tuple
 
@@ -31,8 +32,16 @@ INFINITY_SIGNATURE = bytes([0xC0]) + bytes(95)          # bls::INFINITY_SIGNATUR
 
 SSB_OK = 0
 DVF_OK, DVF_DIFFERENT_LENGTH, DVF_INSUFFICIENT_SIGNATURES, DVF_INVALID_OPERATOR_ID, \
-    DVF_INSUFFICIENT_VALID_SIGNATURES, DVF_BAD_SIGNATURE_ENCODING = range(6)
+    DVF_INSUFFICIENT_VALID_SIGNATURES, DVF_BAD_SIGNATURE_ENCODING, DVF_INVALID_JOB = range(7)
 MAX_T = 64
+
+
+def _rlc_seed(seed: Optional[int]) -> int:
+    """The rlc_seed argument: a fresh random value unless the caller passes one.  The library
+    draws its own 256-bit key per call from getrandom() and only XORs this in (include/ssbls.h),
+    so the scalars stay secret either way; a fixed seed matters only on an engine switched to
+    set_rlc_deterministic(True) (tests, reproducible profiling)."""
+    return (secrets.randbits(64) if seed is None else int(seed)) & (2**64 - 1)
 
 
 # ------------------------------------------------------------------------------------------
@@ -98,6 +107,8 @@ def _error_from(status: int, e0: int, e1: int) -> Optional[DvfError]:
         return BadSignatureEncoding()
     if status == DVF_DIFFERENT_LENGTH:
         return DifferentLength(e0, e1)
+    if status == DVF_INVALID_JOB:      # _dev callers only (t or share range outside the limits)
+        return ValueError("job outside the engine's limits: t = %d, %d shares" % (e0, e1))
     raise RuntimeError("unknown status %d" % status)
 
 
@@ -139,6 +150,12 @@ class Engine:
         if rc != SSB_OK:
             msg = self._lib.ssb_last_error(self._h)
             raise RuntimeError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def set_rlc_deterministic(self, on: bool):
+        """TESTS ONLY: derive the RLC scalars from the caller's seed alone (ssb_set_rlc_deterministic).
+        Scalars that are a public function of the seed let two colluding senders cancel errors in
+        the batch sums; the default (off) draws a secret key from the OS for every call."""
+        self._check(self._lib.ssb_set_rlc_deterministic(self._h, 1 if on else 0), "ssb_set_rlc_deterministic")
 
     def last_kernel_ms(self, name: str) -> float:
         ms = ctypes.c_float()
@@ -209,8 +226,9 @@ class Engine:
 
     def decode_wire_sigs(self, records: Sequence[bytes]) -> List[Optional[bytes]]:
         """bincode(bls::Signature) records (202 bytes each, src/node/dvfcore.rs:245-251) -> the
-        96-byte compressed signatures, None where the record does not parse (the reference's
-        "Deserialize failed" at src/validation/operator.rs:113 drops that share)."""
+        96-byte compressed signatures, None where the record does not parse or its point does not
+        decompress (the reference's "Deserialize failed" at src/validation/operator.rs:113 drops
+        that share)."""
         n = len(records)
         if n == 0:
             return []
@@ -225,7 +243,7 @@ class Engine:
         return [out[96 * i:96 * (i + 1)].tobytes() if st[i] == 0 else None for i in range(n)]
 
     def verify_batch(self, pks: Sequence[bytes], sigs: Sequence[bytes], root_idx: Sequence[int],
-                     roots: Sequence[bytes], seed: int = 0x5AFE57A4E, dst: bytes = DST) -> np.ndarray:
+                     roots: Sequence[bytes], seed: Optional[int] = None, dst: bytes = DST) -> np.ndarray:
         n = len(sigs)
         out = np.zeros(n, dtype=np.uint8)
         if n == 0:
@@ -237,7 +255,7 @@ class Engine:
         d, dp = _lib.buf(dst)
         self._check(self._lib.ssb_verify_batch(
             self._h, n, pk.ctypes.data_as(_lib._u8p), sg.ctypes.data_as(_lib._u8p), ri.ctypes.data_as(_lib._u32p),
-            len(roots), rt.ctypes.data_as(_lib._u8p), dp, len(dst), seed & (2**64 - 1),
+            len(roots), rt.ctypes.data_as(_lib._u8p), dp, len(dst), _rlc_seed(seed),
             out.ctypes.data_as(_lib._u8p)), "ssb_verify_batch")
         return out
 
@@ -278,7 +296,7 @@ class Engine:
 
     def threshold_aggregate_batch_raw(self, t: Sequence[int], share_off: Sequence[int], sigs: bytes, pks: bytes,
                                       ids: Sequence[int], job_root: Sequence[int], roots: Sequence[bytes],
-                                      seed: int = 0x5AFE57A4E, dst: bytes = DST):
+                                      seed: Optional[int] = None, dst: bytes = DST):
         """Packed form: returns (out_sig96[J,96], status[J], err[J,2], share_verdicts[N])."""
         J = len(t)
         off = np.ascontiguousarray(np.asarray(share_off, dtype=np.uint32))
@@ -297,7 +315,7 @@ class Engine:
         self._check(self._lib.ssb_threshold_aggregate_batch(
             self._h, J, off.ctypes.data_as(_lib._u32p), tt.ctypes.data_as(_lib._u32p), sg.ctypes.data_as(_lib._u8p),
             pk.ctypes.data_as(_lib._u8p), idv.ctypes.data_as(_lib._u64p), jr.ctypes.data_as(_lib._u32p), len(roots),
-            rt.ctypes.data_as(_lib._u8p), dp, len(dst), seed & (2**64 - 1), out.ctypes.data_as(_lib._u8p),
+            rt.ctypes.data_as(_lib._u8p), dp, len(dst), _rlc_seed(seed), out.ctypes.data_as(_lib._u8p),
             st.ctypes.data_as(_lib._i32p), err.ctypes.data_as(_lib._u64p), ver.ctypes.data_as(_lib._u8p)),
             "ssb_threshold_aggregate_batch")
         return out[:J], st[:J], err[:J], ver[:N]
@@ -338,6 +356,18 @@ class ThresholdJob:
     msg: bytes
 
 
+def job_shape_error(job: ThresholdJob) -> Optional[str]:
+    """Why a job's arguments could not come from the reference's types, or None: msg is a Hash256
+    (32 bytes), a Signature serialises to 96 bytes, a PublicKey to 48, an id is a u64."""
+    if len(job.msg) != 32:
+        return "msg must be a 32-byte Hash256"
+    if any(len(s) != 96 for s in job.sigs) or any(len(p) != 48 for p in job.pks):
+        return "signatures are 96 bytes, public keys 48 bytes"
+    if any(not 0 <= int(i) < 2**64 for i in job.ids):
+        return "operator ids are u64"
+    return None
+
+
 class ThresholdSignature:
     """GenericThresholdSignature<HipThresholdSignature> (src/crypto/generic_threshold.rs:25-180)."""
 
@@ -364,13 +394,17 @@ class ThresholdSignature:
                             msg: bytes) -> bytes:
         """Returns the 96-byte combined signature or raises the DvfError the reference returns."""
         r = self.threshold_aggregate_batch([ThresholdJob(sigs, pks, ids, msg)])[0]
-        if isinstance(r, DvfError):
+        if isinstance(r, (DvfError, ValueError)):
             raise r
         return r
 
-    def threshold_aggregate_batch(self, jobs: Sequence[ThresholdJob], seed: int = 0x5AFE57A4E
-                                  ) -> List[Union[bytes, DvfError]]:
-        results: List[Union[bytes, DvfError, None]] = [None] * len(jobs)
+    def threshold_aggregate_batch(self, jobs: Sequence[ThresholdJob], seed: Optional[int] = None
+                                  ) -> List[Union[bytes, DvfError, ValueError]]:
+        """One result per job: the combined signature, the DvfError the reference returns, or a
+        ValueError for a job whose arguments the reference's types could not hold (a message that
+        is not a 32-byte Hash256, a signature / public key of the wrong length).  A malformed job
+        fails alone; the rest of the batch is aggregated."""
+        results: List[Union[bytes, DvfError, ValueError, None]] = [None] * len(jobs)
         t = self._t
         if t < 1 or t > MAX_T:
             raise ValueError("threshold must be in [1, %d]" % MAX_T)
@@ -384,8 +418,10 @@ class ThresholdSignature:
             if len(job.sigs) != len(job.ids):
                 results[j] = DifferentLength(len(job.sigs), len(job.ids))
                 continue
-            if len(job.msg) != 32:
-                raise ValueError("msg must be a 32-byte Hash256")
+            bad = job_shape_error(job)
+            if bad:
+                results[j] = ValueError(bad)
+                continue
             dev_jobs.append(j)
             roots.setdefault(bytes(job.msg), len(roots))
         if dev_jobs:
@@ -394,8 +430,6 @@ class ThresholdSignature:
             for j in dev_jobs:
                 job = jobs[j]
                 for s, p, i in zip(job.sigs, job.pks, job.ids):
-                    if len(s) != 96 or len(p) != 48:
-                        raise ValueError("signatures are 96 bytes, public keys 48 bytes")
                     sigs.append(bytes(s)); pks.append(bytes(p)); ids.append(int(i))
                 offs.append(len(sigs))
                 jr.append(roots[bytes(job.msg)])

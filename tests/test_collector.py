@@ -127,3 +127,22 @@ def test_collector_on_engine(engine):
         futs = [(col.submit(c["t"], _job(c)), _expected(c)) for c in cases for _ in range(3)]
         for f, want in futs:
             _check(f, want)
+
+
+def test_malformed_job_fails_alone():
+    """A job with a short message, a wrong-length signature or an out-of-range threshold fails
+    its own future at submit and never joins the batch; the slot's other jobs aggregate."""
+    calls = []
+    cases = [c for c in _cases() if c["expected_status"] == 0][:3]
+    with SlotCollector(max_jobs=64, window_s=0.01, batch_fn=_golden_batch_fn(calls)) as col:
+        good = [col.submit(c["t"], _job(c)) for c in cases]
+        j = _job(cases[0])
+        bad_msg = col.submit(cases[0]["t"], ThresholdJob(j.sigs, j.pks, j.ids, b"\0" * 31))
+        bad_sig = col.submit(cases[0]["t"], ThresholdJob([s[:95] for s in j.sigs], j.pks, j.ids, j.msg))
+        bad_t = col.submit(0, j)
+        for f in (bad_msg, bad_sig, bad_t):
+            with pytest.raises(ValueError):
+                f.result(1)
+        for c, f in zip(cases, good):
+            _check(f, _expected(c))
+    assert sum(n for _, n in calls) == len(cases)

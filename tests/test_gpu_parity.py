@@ -380,8 +380,8 @@ def test_combined_verify_on_device(engine):
 
 def test_wire_decode_matches_oracle(engine):
     """§8f-2: bincode(bls::Signature) records decoded on the GPU == the oracle's codec, including
-    upper-case hex, a wrong length field, a missing prefix and a non-hex digit; the decoded bytes
-    feed the aggregate and give the golden combine."""
+    upper-case hex, a wrong length field, a missing prefix, a non-hex digit and points that do not
+    decompress; the decoded bytes feed the aggregate and give the golden combine."""
     from oracle import bls12_381 as B
     cases = [c for c in _load("threshold_cases.json")["cases"] if c["expected_status"] == 0]
     c = cases[0]
@@ -400,9 +400,17 @@ def test_wire_decode_matches_oracle(engine):
     ts = ThresholdSignature(c["t"], engine)
     got = ts.threshold_aggregate(out[:len(sigs)], [bytes.fromhex(p) for p in c["pks"]], c["ids"], bytes.fromhex(c["root"]))
     assert got.hex() == c["master_sig"]
-    # full C2-size batch of records
+    # records whose hex is fine but whose point does not decompress (random bytes, an x >= p, an
+    # off-curve x; the infinity encoding is a valid Signature): status 4 exactly where the oracle
     rng = np.random.default_rng(9)
-    many = [bytes(rng.integers(0, 256, 96, dtype=np.uint8)) for _ in range(16384)]
+    junk = [bytes(rng.integers(0, 256, 96, dtype=np.uint8)) for _ in range(384)]
+    junk += [bytes([0x9a]) + b"\xff" * 95, bytes([0x80]) + bytes(94) + b"\x01", bytes([0xC0]) + bytes(95)]
+    got = engine.decode_wire_sigs([B.bincode_signature(s) for s in junk])
+    want = [B.bincode_signature_decode(B.bincode_signature(s))[1] for s in junk]
+    assert got == want
+    assert want[-1] is not None and want[-3] is None and sum(w is None for w in want) > 300
+    # full C2-size batch of records
+    many = [sigs[k % len(sigs)] for k in range(16384)]
     assert engine.decode_wire_sigs([B.bincode_signature(s) for s in many]) == many
 
 

@@ -77,21 +77,20 @@ def test_opcount_is_current():
     assert make_opcount.measure() == committed
 
 
-def test_wave_programs_match_single_lane(host_exe):
-    """The generated lane-parallel programs (Fp12 mul/sqr/frobenius/conj/sparse line/cyclotomic
-    square, final exponentiation, Miller loop) reproduce the single-lane functions exactly."""
-    c = _load("threshold_cases.json")["cases"][0]
-    ok, n = _run(host_exe, ["wave %s %s %s" % (c["pks"][0], c["sigs"][0], c["root"])])[0].split()
-    assert ok == n == "12"
-
-
-def test_wave_tables_are_current():
-    import subprocess, sys
-    gen = os.path.join(HERE, "..", "safestakeoperator_amd", "csrc", "gen_wave_tables.py")
-    hdr = os.path.join(HERE, "..", "safestakeoperator_amd", "csrc", "ssb_wave_tables.h")
-    before = open(hdr).read()
-    subprocess.run([sys.executable, gen], check=True, capture_output=True)
-    assert open(hdr).read() == before
+def test_rlc_scalars_match_restatement(host_exe):
+    """The device's RLC scalar derivation (ssb_units.h: ChaCha12 of the batch key and the share
+    index, odd) compiled for the host == oracle/rlc.py, for seed-expanded and explicit keys."""
+    from oracle import rlc
+    lines, want = [], []
+    for seed in (0, 1, 0x5AFE57A4E, 2**64 - 1):
+        for i in (0, 1, 2, 16383, 2**32 + 5):
+            lines.append("rlc %d %d" % (seed, i))
+            want.append(rlc.rlc_scalar_odd(rlc.key_from_seed(seed), i))
+    key = [0x03020100 + 0x04040404 * k for k in range(8)]
+    for i in (0, 7, 2**40):
+        lines.append("rlc 0 %d %s" % (i, " ".join("%08x" % w for w in key)))
+        want.append(rlc.rlc_scalar_odd(key, i))
+    assert [int(x) for x in _run(host_exe, lines)] == want
 
 
 def test_lane_programs_match_single_lane(host_exe):

@@ -105,7 +105,7 @@ def test_decode_rejections():
 def test_wire_codec_roundtrip():
     """bincode(bls::Signature) layout (SURVEY.md §8a-6): 8-byte LE length 194, "0x", 192 hex digits."""
     from oracle import bls12_381 as B
-    sig = bytes(range(96))
+    sig = B.g2_compress(B.g2_mul(B.G2_GEN, 12345))
     rec = B.bincode_signature(sig)
     assert len(rec) == 202 and rec[:8] == (194).to_bytes(8, "little") and rec[8:10] == b"0x"
     assert B.bincode_signature_decode(rec) == (0, sig)
@@ -113,6 +113,9 @@ def test_wire_codec_roundtrip():
     assert B.bincode_signature_decode(b"\x00" + rec[1:])[0] == 1
     assert B.bincode_signature_decode(rec[:9] + b"X" + rec[10:])[0] == 2
     assert B.bincode_signature_decode(rec[:20] + b"z" + rec[21:])[0] == 3
+    assert B.bincode_signature_decode(B.bincode_signature(bytes(range(96))))[0] == 4   # no compression flag
+    inf = bytes([0xC0]) + bytes(95)
+    assert B.bincode_signature_decode(B.bincode_signature(inf)) == (0, inf)
 
 
 def test_feldman_fixture_consistent():
@@ -124,10 +127,15 @@ def test_feldman_fixture_consistent():
     d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "feldman.json")))
     for c in d["cases"]:
         # (a degree-0 polynomial verifies at every party)
-        assert c["expect"] == (c["kind"] in ("valid", "big_id") or (c["kind"] == "wrong_party" and c["t"] == 1))
+        # (a degree-0 polynomial verifies at every party; an undecodable commitment is the identity,
+        # so it breaks the check unless it replaced the identity commitment of a zero coefficient)
+        assert c["expect"] == (c["kind"] in ("valid", "big_id", "undecodable_zero_commitment")
+                               or (c["kind"] == "wrong_party" and c["t"] == 1)), c["kind"]
     h = B.g1_decompress(bytes.fromhex(d["h"]))
-    for c in (d["cases"][0], d["cases"][1]):
-        pts = [B.g1_decompress(bytes.fromhex(x)) for x in c["commitments"]]
+    kinds = {c["kind"]: c for c in d["cases"] if c["t"] == 5}
+    for c in [d["cases"][0], d["cases"][1], kinds["bad_commitment"], kinds["undecodable_zero_commitment"],
+              kinds["non_g1_commitment"]]:
+        pts = B.committed_poly_from_bytes([bytes.fromhex(x) for x in c["commitments"]])
         assert B.feldman_share_verify(h, c["share"], pts, c["id"]) == c["expect"]
 
 
