@@ -150,6 +150,10 @@ int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t
 
 int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* dst, size_t dst_len,
                    uint8_t* out192);
+/* Same for messages shorter than a root: message i is the first msg_len[i] <= 32 bytes of the
+ * 32-byte slot msgs32 + 32 i (RFC 9380's test vectors, e.g. the empty message of Appendix K.2). */
+int ssb_hash_to_g2_msgs(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* msg_len, const uint8_t* dst,
+                        size_t dst_len, uint8_t* out192);
 
 /* verdicts[i] = Signature::verify(pk48[i], roots32[root_idx[i]]) for sig96[i]  (1/0). */
 int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t* sig96,

@@ -29,6 +29,7 @@ SIGNATURES = {
     "ssb_kernel_timing": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_kernel_time": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]),
     "ssb_hash_to_g2": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _sz, _u8p]),
+    "ssb_hash_to_g2_msgs": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _u8p, _sz, _u8p]),
     "ssb_verify_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _u32p, _sz, _u8p, _u8p, _sz, ctypes.c_uint64, _u8p]),
     "ssb_threshold_aggregate_batch": (ctypes.c_int, [_ctx, _sz, _u32p, _u32p, _u8p, _u8p, _u64p, _u32p, _sz, _u8p,
                                                      _u8p, _sz, ctypes.c_uint64, _u8p, _i32p, _u64p, _u8p]),
@@ -74,6 +75,13 @@ def load():
     global _LIB
     if _LIB is not None:
         return _LIB
+    # One HIP runtime per process: PyTorch (device memory, streams, RCCL for the callers) ships its
+    # own libamdhip64; load it first so libssbls.so binds to the same runtime.  (With the library
+    # loaded first, a later torch.cuda init in the same process finds "No HIP GPUs".)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libssbls.so is not built (run `python -m safestakeoperator_amd.build`); "
                            "there is no CPU fallback")

@@ -64,12 +64,13 @@ SSB_FN void sha256(uint8_t* out, const uint8_t* msg, int len) {
   }
 }
 
-// expand_message_xmd(msg[32], DST, 256) -> 256 bytes   (RFC 9380 §5.3.1)
-SSB_FN void expand_message_xmd_256(uint8_t* out, const uint8_t* msg32, const uint8_t* dst, int dst_len) {
+// expand_message_xmd(msg, DST, 256) -> 256 bytes   (RFC 9380 §5.3.1); msg_len <= 32 (a signing
+// root is 32 bytes; shorter messages are for the RFC's own test vectors)
+SSB_FN void expand_message_xmd_256(uint8_t* out, const uint8_t* msg32, const uint8_t* dst, int dst_len, int msg_len = 32) {
   uint8_t buf[64 + 32 + 3 + 256 + 1];
   int n = 0;
   for (int i = 0; i < 64; ++i) buf[n++] = 0;         // Z_pad
-  for (int i = 0; i < 32; ++i) buf[n++] = msg32[i];  // msg
+  for (int i = 0; i < msg_len; ++i) buf[n++] = msg32[i];  // msg
   buf[n++] = 1; buf[n++] = 0;                         // I2OSP(256, 2)
   buf[n++] = 0;                                       // I2OSP(0, 1)
   for (int i = 0; i < dst_len; ++i) buf[n++] = dst[i];
@@ -218,9 +219,9 @@ SSB_FN void h2c_clear_exact(g2_jac& r, const g2_aff& q0, const g2_aff& q1, g2_ja
 
 // ---- the same hash split into the stages of the batched pipeline (ssb_k_hash.hip) ----
 // stage 1: u0, u1 from expand_message_xmd
-SSB_FN void h2c_field(fp2& u0, fp2& u1, const uint8_t* msg32, const uint8_t* dst, int dst_len) {
+SSB_FN void h2c_field(fp2& u0, fp2& u1, const uint8_t* msg32, const uint8_t* dst, int dst_len, int msg_len = 32) {
   uint8_t uni[256];
-  expand_message_xmd_256(uni, msg32, dst, dst_len);
+  expand_message_xmd_256(uni, msg32, dst, dst_len, msg_len);
   fp_from_be64_mod(u0.c0, uni);
   fp_from_be64_mod(u0.c1, uni + 64);
   fp_from_be64_mod(u1.c0, uni + 128);
@@ -256,9 +257,9 @@ SSB_FN void sswu_finish(g2_aff& q, const fp2& u, const fp2& x, const fp2& y_in) 
   iso3_map(q, x, y);
 }
 
-SSB_FN void hash_to_g2(g2_aff& out, const uint8_t* msg32, const uint8_t* dst, int dst_len) {
+SSB_FN void hash_to_g2(g2_aff& out, const uint8_t* msg32, const uint8_t* dst, int dst_len, int msg_len = 32) {
   uint8_t uni[256];
-  expand_message_xmd_256(uni, msg32, dst, dst_len);
+  expand_message_xmd_256(uni, msg32, dst, dst_len, msg_len);
   fp2 u0, u1;
   fp_from_be64_mod(u0.c0, uni);
   fp_from_be64_mod(u0.c1, uni + 64);

@@ -8,14 +8,17 @@ namespace ssb {
 namespace k {
 
 // ---- staged hash_to_G2 (the RFC 9380 hash_to_curve of ssb_h2c.h, split into stages) ----
-// 1: expand_message_xmd + the two field elements, one lane per root
-__global__ void SSB_LB(64) k_h2c_u(int n, const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
+// 1: expand_message_xmd + the two field elements, one lane per root (message i: 32 bytes, or
+// lens[i] <= 32 bytes at roots + 32 i when lens is given)
+__global__ void SSB_LB(64) k_h2c_u(int n, const uint8_t* __restrict__ roots, const uint8_t* __restrict__ lens, dst_arg dst,
+                                   fp2* __restrict__ u) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t m[32];
   for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
+  const int len = lens ? (lens[i] < 32 ? lens[i] : 32) : 32;
   fp2 u0, u1;
-  h2c_field(u0, u1, m, dst.b, dst.len);
+  h2c_field(u0, u1, m, dst.b, dst.len, len);
   u[2 * i] = u0;
   u[2 * i + 1] = u1;
 }
@@ -133,7 +136,7 @@ __global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* _
 
 namespace launch {
 size_t hash_ws_bytes(size_t n) { return n * (2 * sizeof(fp2) + 2 * sizeof(g2_aff) + sizeof(g2_jac) + 4) + 1024; }
-void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws) {
+void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws, const uint8_t* lens) {
   if (n <= 0) return;
   char* p = (char*)ws;
   auto take = [&](size_t b) { char* r = p; p += (b + 255) & ~(size_t)255; return r; };
@@ -141,7 +144,7 @@ void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst,
   g2_aff* q = (g2_aff*)take(2 * n * sizeof(g2_aff));
   g2_jac* hj = (g2_jac*)take(n * sizeof(g2_jac));
   uint32_t* exc = (uint32_t*)take(n * 4);
-  hipLaunchKernelGGL(k::k_h2c_u, dim3((n + 63) / 64), dim3(64), 0, st, n, roots, dst, u);
+  hipLaunchKernelGGL(k::k_h2c_u, dim3((n + 63) / 64), dim3(64), 0, st, n, roots, lens, dst, u);
   hipLaunchKernelGGL(k::k_h2c_map, dim3((4 * n + 63) / 64), dim3(64), 0, st, n, u, q);
   hipLaunchKernelGGL(k::k_h2c_clear, dim3((n + 7) / 8), dim3(64), 0, st, n, q, hj, exc);
   const char* ex = getenv("SSB_H2C_EXACT");

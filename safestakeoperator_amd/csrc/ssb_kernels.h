@@ -107,7 +107,9 @@ namespace launch {
 void lane_subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // staged hash_to_G2 of n roots into out (ssb_k_hash.hip); ws: hash_ws_bytes(n) device bytes
 size_t hash_ws_bytes(size_t n);
-void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws);
+// (lens: per-message lengths <= 32, or nullptr for 32-byte roots)
+void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws,
+                const uint8_t* lens = nullptr);
 // RLC sums as bucket MSMs (ssb_k_msm.hip).  msm_sort: counting sort of the (share, window)
 // entries of both MSMs by bucket key (K keys; cnt/start/cur: K words, bsum: 1024 words, ent: one
 // word per entry).  msm_g2: window sums of sum_i k_i sig_i as multi-pairing pairs

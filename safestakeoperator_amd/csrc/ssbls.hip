@@ -567,24 +567,41 @@ int ssb_kernel_time(ssb_ctx* ctx, const char* name, float* total_ms, int* launch
   return SSB_OK;
 }
 
-int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* dst, size_t dst_len, uint8_t* out192) {
+namespace {
+int hash_to_g2_impl(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* lens, const uint8_t* dst, size_t dst_len,
+                    uint8_t* out192) {
   if (!ctx) return SSB_EINVAL;
   if (n == 0) return SSB_OK;
   if (!msgs32 || !out192) { ctx->err = "null pointer"; return SSB_EINVAL; }
+  if (lens)
+    for (size_t i = 0; i < n; ++i) if (lens[i] > 32) { ctx->err = "message longer than 32 bytes"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
-  size_t need = align_up(n * 32) + align_up(n * sizeof(g2_aff)) + align_up(n * 192) + align_up(launch::hash_ws_bytes(n));
+  size_t need = align_up(n * 32) + align_up(n) + align_up(n * sizeof(g2_aff)) + align_up(n * 192) + align_up(launch::hash_ws_bytes(n));
   if ((rc = ensure_ws(ctx, need))) return rc;
   carve c{(char*)ctx->cur->ws};
-  uint8_t* d_msg = c.take<uint8_t>(n * 32); g2_aff* d_h = c.take<g2_aff>(n); uint8_t* d_out = c.take<uint8_t>(n * 192);
+  uint8_t* d_msg = c.take<uint8_t>(n * 32); uint8_t* d_len = c.take<uint8_t>(n); g2_aff* d_h = c.take<g2_aff>(n);
+  uint8_t* d_out = c.take<uint8_t>(n * 192);
   char* hws = c.take<char>(launch::hash_ws_bytes(n));
   SSB_HIP(hipMemcpyAsync(d_msg, msgs32, n * 32, hipMemcpyHostToDevice, ctx->cur->stream));
-  { timed t(ctx, "k_hash_to_g2"); launch::hash_to_g2(ctx->cur->stream, (int)n, d_msg, d, d_h, hws); }
+  if (lens) SSB_HIP(hipMemcpyAsync(d_len, lens, n, hipMemcpyHostToDevice, ctx->cur->stream));
+  { timed t(ctx, "k_hash_to_g2"); launch::hash_to_g2(ctx->cur->stream, (int)n, d_msg, d, d_h, hws, lens ? d_len : nullptr); }
   hipLaunchKernelGGL(k_serialize_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->cur->stream, (int)n, d_h, d_out);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out192, d_out, n * 192, hipMemcpyDeviceToHost, ctx->cur->stream));
   SSB_HIP(hipStreamSynchronize(ctx->cur->stream));
   return SSB_OK;
+}
+}  // namespace
+
+int ssb_hash_to_g2(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* dst, size_t dst_len, uint8_t* out192) {
+  return hash_to_g2_impl(ctx, n, msgs32, nullptr, dst, dst_len, out192);
+}
+
+int ssb_hash_to_g2_msgs(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* msg_len, const uint8_t* dst,
+                        size_t dst_len, uint8_t* out192) {
+  if (ctx && n && !msg_len) { ctx->err = "null msg_len"; return SSB_EINVAL; }
+  return hash_to_g2_impl(ctx, n, msgs32, msg_len, dst, dst_len, out192);
 }
 
 int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* commitments48, const uint64_t* ids,

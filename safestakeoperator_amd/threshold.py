@@ -174,15 +174,24 @@ class Engine:
 
     # --- primitives -------------------------------------------------------------------------
     def hash_to_g2(self, msgs: Sequence[bytes], dst: bytes = DST) -> List[bytes]:
+        """hash_to_G2 (RFC 9380 BLS12381G2_XMD:SHA-256_SSWU_RO_) of messages of at most 32 bytes
+        (signing roots are 32): 192-byte uncompressed points."""
         n = len(msgs)
         if n == 0:
             return []
-        m = np.frombuffer(b"".join(msgs), dtype=np.uint8)
-        assert m.size == 32 * n
+        if any(len(x) > 32 for x in msgs):
+            raise ValueError("messages are at most 32 bytes")
         out = np.zeros(192 * n, dtype=np.uint8)
         d, dp = _lib.buf(dst)
-        self._check(self._lib.ssb_hash_to_g2(self._h, n, m.ctypes.data_as(_lib._u8p), dp, len(dst),
-                                             out.ctypes.data_as(_lib._u8p)), "ssb_hash_to_g2")
+        if all(len(x) == 32 for x in msgs):
+            m = np.frombuffer(b"".join(msgs), dtype=np.uint8)
+            rc = self._lib.ssb_hash_to_g2(self._h, n, m.ctypes.data_as(_lib._u8p), dp, len(dst), out.ctypes.data_as(_lib._u8p))
+        else:
+            m = np.frombuffer(b"".join(bytes(x).ljust(32, b"\0") for x in msgs), dtype=np.uint8)
+            ln = np.asarray([len(x) for x in msgs], dtype=np.uint8)
+            rc = self._lib.ssb_hash_to_g2_msgs(self._h, n, m.ctypes.data_as(_lib._u8p), ln.ctypes.data_as(_lib._u8p), dp,
+                                               len(dst), out.ctypes.data_as(_lib._u8p))
+        self._check(rc, "ssb_hash_to_g2")
         return [out[192 * i:192 * (i + 1)].tobytes() for i in range(n)]
 
     def feldman_verify_batch(self, commitments: Sequence[Sequence[bytes]], ids: Sequence[int],

@@ -179,11 +179,13 @@ int main() {
   while (std::getline(std::cin, line)) {
     std::istringstream is(line);
     std::string cmd; is >> cmd;
-    if (cmd == "h2g2") {  // h2g2 <msg32hex> [dsthex]
+    if (cmd == "h2g2") {  // h2g2 <msghex, <= 32 bytes; "-" = empty> [dsthex]
       std::string m, d; is >> m >> d;
-      auto msg = unhex(m);
+      auto msg = m == "-" ? std::vector<uint8_t>() : unhex(m);
+      const int mlen = (int)msg.size();
+      msg.resize(32, 0);
       std::vector<uint8_t> dst = d.empty() ? std::vector<uint8_t>(DST, DST + strlen(DST)) : unhex(d);
-      g2_aff h; hash_to_g2(h, msg.data(), dst.data(), (int)dst.size());
+      g2_aff h; hash_to_g2(h, msg.data(), dst.data(), (int)dst.size(), mlen);
       uint8_t out[192]; g2_serialize(out, h);
       printf("%s\n", hex(out, 192).c_str());
     } else if (cmd == "g2dec") {

@@ -1,0 +1,162 @@
+"""GPU: every BASELINE.json config at its full per-GPU size, checked against INDEPENDENT
+references -- the plain-C oracle (oracle/bls_c.c: 64-bit-limb restatement of the reference's scan,
+exact per-share verify and Lagrange combine, tests/test_oracle_c.py pins it to the Python oracle and
+the published vectors) and the construction truth of the inputs (which shares were signed over the
+wrong root) -- not against the engine's own signer.
+
+  C2  4,096 validators x 4, 3-of-4, 64 roots; all valid and 1% invalid: EVERY verdict, status and
+      combined signature == the C oracle on the same bytes
+  C3  65,536 validators 3-of-4: the 65,536 combined signatures verified on the device with the
+      validators' master keys (a-8, ssb_verify_batch_cached_dev), plus swapped / out-of-range cases
+  C4  1,048,576 shares at invalid rates 1e-4 and 1e-2: exact verdicts, statuses, combines
+  C5  131,072 validators x 13, 10-of-13 (one GPU's slice of 1M): 64 roots and all-distinct roots
+and the RFC 9380 Appendix K.2 hash_to_G2 vector (QUUX DST) on the device.
+Reference test being generalised: tests/test_generic_threshold.rs:26-35 (combine == master
+signature, both verify).
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import bench
+from oracle import bls_c
+from safestakeoperator_amd import DST, _lib
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+THREADS = 16
+
+
+def _agg(engine, wl, V, t, n):
+    offs = list(range(0, V * n + 1, n))
+    return engine.threshold_aggregate_batch_raw([t] * V, offs, wl["sigs"], wl["pks"], wl["ids"], wl["job_root"],
+                                                wl["roots"])
+
+
+def _c_oracle(wl, jobs, t, n):
+    """C oracle on the listed jobs (every share verified): (out96, status, err, verdicts)."""
+    sig = b"".join(wl["sigs"][96 * n * v:96 * n * (v + 1)] for v in jobs)
+    pk = b"".join(wl["pks"][48 * n * v:48 * n * (v + 1)] for v in jobs)
+    ids = [i for v in jobs for i in wl["ids"][n * v:n * (v + 1)]]
+    used = sorted({wl["job_root"][v] for v in jobs})       # hash only the roots the sample signs
+    remap = {r: k for k, r in enumerate(used)}
+    jr = [remap[wl["job_root"][v]] for v in jobs]
+    off = list(range(0, len(jobs) * n + 1, n))
+    return bls_c.threshold_batch(off, [t] * len(jobs), sig, pk, ids, jr, [wl["roots"][r] for r in used], THREADS,
+                                 verify_all=True)
+
+
+def _check_against_truth(wl, V, t, n, out, st, err, ver):
+    valid = np.asarray(wl["valid"], dtype=np.uint8)
+    assert (ver == valid).all(), np.nonzero(ver != valid)[0][:20]
+    per_job = valid.reshape(V, n).sum(axis=1)
+    assert ((st == 0) == (per_job >= t)).all()
+    bad = np.nonzero(per_job < t)[0]
+    assert (st[bad] == 4).all() and (err[bad, 0] == per_job[bad]).all() and (err[bad, 1] == t).all()
+
+
+def test_rfc9380_k2_vector_on_gpu(engine):
+    """RFC 9380 Appendix K.2 (BLS12381G2_XMD:SHA-256_SSWU_RO_, QUUX DST, msg = ""), published
+    output point, through ssb_hash_to_g2_msgs."""
+    v = json.load(open(os.path.join(GOLD, "known_answers.json")))["rfc9380_g2"][0]
+    out = engine.hash_to_g2([v["msg"].encode()], dst=v["dst"].encode())[0].hex()
+    assert [out[0:96], out[96:192], out[192:288], out[288:384]] == [v["P_x"][1], v["P_x"][0], v["P_y"][1], v["P_y"][0]]
+    # the same message padded to a 32-byte root is a different input: a different point
+    assert engine.hash_to_g2([bytes(32)], dst=v["dst"].encode())[0].hex() != out
+
+
+@pytest.mark.parametrize("rate", [0.0, 0.01], ids=["valid", "invalid_1pct"])
+def test_c2_full_batch_matches_c_oracle(engine, rate):
+    V, t, n, R = 4096, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=0, invalid_rate=rate)
+    out, st, err, ver = _agg(engine, wl, V, t, n)
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
+    assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
+    assert (st == o_st).all()
+    assert (err == o_err).all()
+    ok = st == 0
+    assert (out[ok] == o_out[ok]).all()
+    _check_against_truth(wl, V, t, n, out, st, err, ver)
+    assert rate == 0 or wl["n_bad"] > 100
+
+
+def _verify_cached_dev(engine, cache_pk48, pk_index, sigs96, root_idx, roots, seed=None):
+    import torch
+    lib = engine._lib
+    dev = torch.device("cuda", 0)
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    cache = np.frombuffer(b"".join(cache_pk48), dtype=np.uint8)
+    assert lib.ssb_pk_cache_set(engine.handle, len(cache_pk48), cache.ctypes.data_as(_lib._u8p)) == 0
+    n = len(sigs96)
+    d_idx = torch.tensor(np.asarray(pk_index, dtype=np.uint32).view(np.int32), device=dev)
+    d_sig, d_roots = u8(b"".join(sigs96)), u8(b"".join(roots))
+    d_ri = torch.tensor(np.asarray(root_idx, dtype=np.uint32).view(np.int32), device=dev)
+    d_ver = torch.zeros((n,), dtype=torch.uint8, device=dev)
+    dst = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
+    rc = lib.ssb_verify_batch_cached_dev(engine.handle, n, d_idx.data_ptr(), d_sig.data_ptr(), d_ri.data_ptr(), len(roots),
+                                         d_roots.data_ptr(), ctypes.cast(dst, _lib._u8p), len(DST),
+                                         int.from_bytes(os.urandom(8), "little"), d_ver.data_ptr(), None)
+    assert rc == 0, lib.ssb_last_error(engine.handle)
+    torch.cuda.synchronize()
+    return d_ver.cpu().numpy()
+
+
+def test_c3_final_verify_65536(engine):
+    """a-8 at C3 size: combine 65,536 validators (3-of-4), then verify all 65,536 combined
+    signatures on the device against the master keys (RLC across validators sharing a root, keys
+    from the decoded-key cache).  Two swapped signatures, an out-of-range root and an out-of-range
+    key index must be the only verdicts 0; a sample re-verified by the C oracle."""
+    V, t, n, R = 65536, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=3)
+    out, st, err, ver = _agg(engine, wl, V, t, n)
+    assert (st == 0).all() and ver.all()
+    mpk = engine.sk_to_pk_batch(wl["master"])
+    comb = [out[v].tobytes() for v in range(V)]
+    comb[100], comb[4000] = comb[4000], comb[100]          # swapped: both invalid
+    ri = list(wl["job_root"])
+    ri[777] = R + 9                                        # no such root
+    pk_index = list(range(V))
+    pk_index[31337] = V + 5                                # no such key
+    got = _verify_cached_dev(engine, mpk, pk_index, comb, ri, wl["roots"])
+    want = np.ones(V, dtype=np.uint8)
+    want[[100, 4000, 777, 31337]] = 0
+    assert (got == want).all(), np.nonzero(got != want)[0]
+    for v in (0, 100, 4000, 65535):
+        assert bls_c.verify(mpk[v], comb[v], wl["roots"][wl["job_root"][v]]) == bool(want[v])
+
+
+@pytest.mark.parametrize("rate", [1e-4, 1e-2], ids=["1e-4", "1e-2"])
+def test_c4_invalid_rates_full_size(engine, rate):
+    """C4: 1,048,576 shares (262,144 validators x 4, 64 roots) in ONE batch at invalid rate 1e-4 /
+    1e-2: every verdict and status exact (construction truth), and every job that lost a share
+    combines to the same bytes as the C oracle (sampled: all such jobs up to 256)."""
+    V, t, n, R = 262144, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=5, invalid_rate=rate)
+    out, st, err, ver = _agg(engine, wl, V, t, n)
+    _check_against_truth(wl, V, t, n, out, st, err, ver)
+    valid = np.asarray(wl["valid"]).reshape(V, n)
+    hit = np.nonzero(valid.sum(axis=1) < n)[0][:256].tolist() + [0, V - 1]
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, hit, t, n)
+    assert (st[hit] == o_st).all()
+    assert all(out[v].tobytes() == o_out[k].tobytes() for k, v in enumerate(hit) if st[v] == 0)
+    assert wl["n_bad"] > (50 if rate < 1e-3 else 9000)
+
+
+@pytest.mark.parametrize("distinct_roots", [False, True], ids=["64_roots", "all_distinct_roots"])
+def test_c5_per_gpu_slice(engine, distinct_roots):
+    """C5, one GPU's slice of 1M validators over 8: 131,072 validators x 13 shares, 10-of-13, with
+    64 signing roots (one per committee) or every validator on its own root (hash_to_G2 of 131,072
+    roots, one Miller pair per root).  All statuses Ok, every share verified, a sample of 128
+    validators' combines == the C oracle's."""
+    V, t, n = 131072, 10, 13
+    R = V if distinct_roots else 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=7)
+    out, st, err, ver = _agg(engine, wl, V, t, n)
+    assert (st == 0).all() and ver.all()
+    sample = list(range(0, V, V // 128))
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, sample, t, n)
+    assert (o_st == 0).all() and o_ver[:len(sample) * n].all()
+    assert all(out[v].tobytes() == o_out[k].tobytes() for k, v in enumerate(sample))
