@@ -52,6 +52,8 @@ CONFIGS = {
     "C3_5of7": dict(validators=65536, threshold=5, operators=7, roots=64, pipeline=3),
     "C4_per_gpu": dict(validators=32768, threshold=3, operators=4, roots=64, pipeline=4),
     "C5_per_gpu": dict(validators=131072, threshold=10, operators=13, roots=64, pipeline=2),
+    # ONE global batch of 1,048,576 shares split over the ranks (--scaling strong)
+    "C4_global": dict(validators=262144, threshold=3, operators=4, roots=64, pipeline=2),
 }
 
 
@@ -141,11 +143,12 @@ def pmc_traffic(kernel):
         return None
 
 
-def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_count=0):
+def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_count=0, v0=0):
     """Synthetic committees: deterministic keys (seed 0x5AFE57A4E, rank), Shamir shares, partial
     signatures from the engine's batched signer (H(m)*sk), public keys sk*g1.  invalid_rate: that
     fraction of the shares (deterministic choice) signs the NEXT root instead -- a valid G2 point
-    that fails verification (SURVEY.md §8d C2/C4 invalid variants)."""
+    that fails verification (SURVEY.md §8d C2/C4 invalid variants).  v0: index of the first
+    validator (a rank's shard of one global batch: validators v0 .. v0+V-1 of seed `rank`)."""
     seed = b"ssbls-bench" + (0x5AFE57A4E).to_bytes(8, "little") + rank.to_bytes(4, "little")
     roots = [hashlib.sha256(seed + b"root" + i.to_bytes(4, "little")).digest() for i in range(n_roots)]
 
@@ -156,7 +159,7 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_coun
     # Shamir shares by Horner over r, vectorised over validators (object arrays of Python ints)
     coef = np.empty((V, t), dtype=object)
     for v in range(V):
-        vb = v.to_bytes(4, "little")
+        vb = (v0 + v).to_bytes(4, "little")
         coef[v, 0] = h(b"sk", vb)
         for k in range(1, t):
             coef[v, k] = h(b"c", vb, k.to_bytes(4, "little"))
@@ -169,10 +172,10 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_coun
         shares[:, i - 1] = acc
     share_sk = shares.reshape(-1).tolist()
     ids = list(range(1, n + 1)) * V
-    jr = [v % n_roots for v in range(V)]
+    jr = [(v0 + v) % n_roots for v in range(V)]
     share_root = [r for r in jr for _ in range(n)]
     bad = [i for i in range(len(share_sk))
-           if invalid_rate > 0 and int.from_bytes(hashlib.sha256(seed + b"bad" + i.to_bytes(4, "little")).digest()[:8],
+           if invalid_rate > 0 and int.from_bytes(hashlib.sha256(seed + b"bad" + (v0 * n + i).to_bytes(4, "little")).digest()[:8],
                                                    "little") < invalid_rate * 2.0 ** 64]
     if invalid_count:                                  # exactly that many, spread over the batch
         N = len(share_sk)
@@ -191,30 +194,44 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_coun
 
 def cpu_baseline(wl, t, n, gpu_out=None, n_val=1024, threads=None, reps=1):
     """The plain-C oracle (oracle/bls_c.c, multi-threaded, `kind: "port"`) on a bounded sample of
-    the same workload: the first n_val validators x n shares of rank 0's batch, every share
-    verified (blst verify semantics) and the first t valid combined, H(root) once per root --
-    the engine's work per job.  Threads: the GPU box's CPU share (16 per GPU), fewer if the host
-    has fewer.  Checked against the GPU's combined signatures for the same validators."""
+    the same workload: the first n_val validators x n shares of rank 0's batch, H(root) once per
+    root, two columns ("per-signature verify and RLC batch, both reported"):
+      * rlc (the `value`): the batch-verify algorithm family the engine and lighthouse's
+        verify_signature_sets use -- per share decompress + subgroup check + 64-bit [k]pk, [k]sig,
+        one multi-pairing and one final exponentiation, then the integer-Lagrange combine;
+      * per_share: every share verified on its own (2 Miller loops + final exponentiation each,
+        the reference's loop at generic_threshold.rs:149-169), 255-bit Lagrange combine.
+    Threads: the GPU box's CPU share (16 per GPU), fewer if the host has fewer.  Both columns are
+    checked against the GPU's combined signatures for the same validators."""
     from oracle import bls_c
     threads = threads or max(1, min(16, os.cpu_count() or 1))
     N = n_val * n
     off = list(range(0, N + 1, n))
     sigs = wl["sigs"][:96 * N]
     pks = wl["pks"][:48 * N]
+    args = (off, [t] * n_val, sigs, pks, wl["ids"][:N], wl["job_root"][:n_val], wl["roots"], threads)
     bls_c.load()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        out, st, _, ver = bls_c.threshold_batch(off, [t] * n_val, sigs, pks, wl["ids"][:N], wl["job_root"][:n_val],
-                                               wl["roots"], threads, verify_all=True)
-    dt = (time.perf_counter() - t0) / reps
-    ok = bool((st == 0).all()) and bool(ver[:N].all())
+
+    def timed(fn):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = fn()
+        return res, (time.perf_counter() - t0) / reps
+
+    (out, st, _, ver, batch_ok), dt_rlc = timed(lambda: bls_c.threshold_batch_rlc(*args))
+    (out2, st2, _, ver2), dt_share = timed(lambda: bls_c.threshold_batch(*args, verify_all=True))
+    ok = bool((st == 0).all()) and bool(ver[:N].all()) and batch_ok and bool((st2 == 0).all()) and bool(ver2[:N].all())
     if gpu_out is not None:
-        ok = ok and all(out[v].tobytes() == gpu_out[v].tobytes() for v in range(n_val))
-    return dict(value=round(N / dt, 1), unit="partial_sigs/s", cores=threads, kind="port",
-                combined_per_s=round(n_val / dt, 1), seconds=round(dt, 2), matches_gpu=bool(ok),
-                sample="%d validators x %d shares of the rank-0 C2 batch, %d passes (verify every share + %d-of-%d "
-                       "combine, H(root) once per root), oracle/bls_c.c (plain C, 64-bit limbs), %d threads"
-                       % (n_val, n, reps, t, n, threads), seconds_total=round(dt * reps, 2))
+        ok = ok and all(out[v].tobytes() == gpu_out[v].tobytes() == out2[v].tobytes() for v in range(n_val))
+    return dict(value=round(N / dt_rlc, 1), unit="partial_sigs/s", cores=threads, kind="port",
+                per_core=round(N / dt_rlc / threads, 1), combined_per_s=round(n_val / dt_rlc, 1),
+                seconds=round(dt_rlc, 2), matches_gpu=bool(ok),
+                per_share=dict(value=round(N / dt_share, 1), per_core=round(N / dt_share / threads, 1),
+                               combined_per_s=round(n_val / dt_share, 1), seconds=round(dt_share, 2)),
+                sample="%d validators x %d shares of the rank-0 C2 batch, %d passes per column (rlc: batch verify + "
+                       "%d-of-%d combine; per_share: every share verified on its own), H(root) once per root, "
+                       "oracle/bls_c.c (plain C, 64-bit limbs), %d threads"
+                       % (n_val, n, reps, t, n, threads), seconds_total=round((dt_rlc + dt_share) * reps, 2))
 
 
 def main():
@@ -222,8 +239,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
-                    help="BASELINE.json workload per GPU (the headline is C2; the others are reported under profiles/)")
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="BASELINE.json workload per GPU (the headline is C2; the others are reported under profiles/); "
+                         "default C2, or C4_global with --scaling strong")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: every rank runs its own batch (the headline); strong: ONE global batch (C4_global: "
+                         "1,048,576 shares) split over the ranks by shard_jobs, results all-gathered back in order")
     ap.add_argument("--validators", type=int, default=None)
     ap.add_argument("--threshold", type=int, default=None)
     ap.add_argument("--operators", type=int, default=None)
@@ -243,6 +264,9 @@ def main():
                     help="fraction of shares signed over the wrong root (the RLC batch fails; exact verdicts "
                          "come from the per-share fallback).  The headline is the all-valid C2 batch.")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "C4_global" if args.scaling == "strong" else "C2"
+    strong = args.scaling == "strong"
     preset = CONFIGS[args.config]
     for k in ("validators", "threshold", "operators", "roots", "pipeline"):
         if getattr(args, k) is None:
@@ -288,9 +312,21 @@ def main():
     from safestakeoperator_amd import _lib
 
     V, t, n, n_roots = args.validators, args.threshold, args.operators, args.roots
-    N = V * n
+    V_glob = V * (1 if strong else world)             # validators of the whole job (all ranks)
     eng = Engine(local)
-    wl = make_workload(eng, V, t, n, n_roots, rank, args.invalid_rate, args.invalid_count)
+    from safestakeoperator_amd.shard import exchange, exchange_var, shard_jobs, shard_sizes
+    sizes = None
+    if strong:
+        # this rank's contiguous, share-balanced slice of the ONE global batch (seed of rank 0, so the
+        # data of validator v does not depend on the number of ranks)
+        goff = list(range(0, V * n + 1, n))
+        j0, j1 = shard_jobs(goff, world, rank)
+        sizes = shard_sizes(goff, world)
+        V = j1 - j0
+        wl = make_workload(eng, V, t, n, n_roots, 0, args.invalid_rate, args.invalid_count, v0=j0)
+    else:
+        wl = make_workload(eng, V, t, n, n_roots, rank, args.invalid_rate, args.invalid_count)
+    N = V * n
     valid = np.asarray(wl["valid"], dtype=np.uint8)
     job_ok = valid.reshape(V, n).sum(axis=1) >= t
 
@@ -308,12 +344,12 @@ def main():
     outs = [dict(out=torch.empty((V, 96), dtype=torch.uint8, device=dev), st=torch.empty((V,), dtype=torch.int32, device=dev),
                  err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev))
             for _ in range(S)]
-    from safestakeoperator_amd.shard import exchange
     dst_arr = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
     lib = eng._lib
     seed_base = 0x5AFE57A4E ^ (rank << 40)
 
     streams = {}
+    pending = {}    # slot -> in-flight all-gather handles reading that slot's output buffers
 
     # validator registration (outside the timed region): every operator key decompressed once
     pk_host = np.frombuffer(wl["pks"], dtype=np.uint8)
@@ -332,6 +368,10 @@ def main():
         fn = lib.ssb_threshold_aggregate_batch_cached_dev if use_cache[0] else lib.ssb_threshold_aggregate_batch_dev
         pk_arg = d_pkidx if use_cache[0] else d_pk
         with torch.cuda.stream(s):
+            # the slot's output buffers are rewritten by this batch: order it after the all-gather
+            # of the slot's previous batch (a stream wait, the host does not block)
+            for w in pending.pop(k, []):
+                w.wait()
             rc = fn(
                 eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(), pk_arg.data_ptr(), d_ids.data_ptr(),
                 d_jr.data_ptr(), n_roots, d_roots.data_ptr(), ctypes.cast(dst_arr, _lib._u8p), len(DST),
@@ -340,8 +380,14 @@ def main():
             if rc != 0:
                 raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
             if dist is not None:
-                # RCCL all-gather over xGMI: the one exchange step
-                exchange(o["ver"].to(cdev), o["out"].to(cdev), o["st"].to(cdev))
+                # RCCL all-gather over xGMI, the one exchange step, asynchronous: RCCL's stream waits
+                # for this batch, the slot's stream does not wait for RCCL (only its next reuse does)
+                if strong:
+                    _, works = exchange_var(o["ver"].to(cdev), o["out"].to(cdev), o["st"].to(cdev), o["err"].to(cdev),
+                                            sizes=sizes, async_op=True)
+                else:
+                    _, works = exchange(o["ver"].to(cdev), o["out"].to(cdev), o["st"].to(cdev), async_op=True)
+                pending[k] = [w for w in works if w is not None]
 
     # phase 1: single-batch latency and per-kernel times (depth 1, no overlap between batches)
     # (latency configuration: 3 streams per slot, hash_to_G2 and the G1 side beside the main chain)
@@ -421,9 +467,9 @@ def main():
 
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
-        total_shares = N * world * args.steps
+        total_shares = V_glob * n * args.steps
         value = total_shares / elapsed
-        combined = V * world * args.steps / elapsed
+        combined = V_glob * args.steps / elapsed
         mads = opcount_mads()
         km = kernel_mads(mads, V, t, n, n_roots, pk_cached=not args.compressed_pk)
         avg = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in kt.items()}
@@ -441,21 +487,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u32-limb modular integer (BLS12-381 Fp/Fr)",
             "data": "synthetic (deterministic keys, GPU-signed shares)",
-            "config": {"workload": "%s: %d validators x %d shares (%d-of-%d), %d roots per GPU; verify + combine"
-                                   % (args.config, V, n, t, n, n_roots),
+            "config": {"workload": ("%s: %d validators x %d shares (%d-of-%d), %d roots, ONE batch split over %d GPU(s); "
+                                    "verify + combine" % (args.config, V_glob, n, t, n, n_roots, world)) if strong else
+                                   ("%s: %d validators x %d shares (%d-of-%d), %d roots per GPU; verify + combine"
+                                    % (args.config, V, n, t, n, n_roots)),
                        "validators_per_gpu": V, "threshold": t, "operators": n, "roots": n_roots,
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
-                       "batches_in_flight": S, "streams_per_slot": args.slot_streams},
+                       "batches_in_flight": S, "streams_per_slot": args.slot_streams,
+                       "tail_streams": int(os.environ.get("SSB_TAILS", "3") or 3)},
             "batch_latency_ms": round(latency_ms, 3),
             "public_keys": ("compressed per batch (ssb_threshold_aggregate_batch_dev)" if args.compressed_pk else
                             "decompressed once at registration (ssb_pk_cache_set + _cached_dev), as lighthouse's "
                             "PublicKey holds the point"),
             ("value_pk_cached" if args.compressed_pk else "value_compressed_pk"):
-                round(N * world * args.steps / elapsed_other, 1),
+                round(V_glob * n * args.steps / elapsed_other, 1),
             "combined_sigs_per_s": round(combined, 1),
             "results_ok": ok_all,
             "invalid_shares_per_batch": wl["n_bad"],
@@ -465,13 +514,13 @@ def main():
                          "timing": "hipEvents on the kernel's stream, pipeline depth 1"},
             "step_roofline": {"mads_per_step_per_gpu": step_mads,
                               "achieved_TMAD_s": round(step_mads * world * args.steps / elapsed / 1e12, 4),
-                              "frac": round(step_mads * world * args.steps / elapsed / MAD_PEAK_MEASURED / world, 5)},
+                              "frac": round(step_mads * args.steps / elapsed / MAD_PEAK_MEASURED, 5)},
             "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
         }
         if world == 1 and not args.no_cpu_baseline and not wl["n_bad"]:
-            # about 10 s of host CPU work: the whole C2 batch, three passes
+            # about 10 s of host CPU work: the whole C2 batch, two passes per column
             rec["cpu_baseline"] = cpu_baseline(wl, t, n, gpu_out=outs[0]["out"].cpu().numpy(),
-                                               n_val=min(4096, V), reps=3)
+                                               n_val=min(4096, V), reps=2)
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()

@@ -86,6 +86,14 @@ typedef struct ssb_ctx ssb_ctx;
 int ssb_create(ssb_ctx** out, int device_ordinal);
 void ssb_destroy(ssb_ctx* ctx);
 const char* ssb_last_error(const ssb_ctx* ctx);
+/* Slots x streams-per-slot limit: the HIP runtime reserves scratch on every hardware queue for the
+ * largest kernel that queue has run, and 8 slots x 3 streams exhausted it on an MI355X
+ * (HSA_STATUS_ERROR_OUT_OF_RESOURCES) while 16 one-stream slots run clean. */
+#define SSB_MAX_SLOT_STREAMS 16
+/* SSB_OK if `depth` slots of `streams` streams are a supported configuration (depth 1..16,
+ * streams 1 or 3, depth x streams <= SSB_MAX_SLOT_STREAMS), SSB_EINVAL otherwise.  No GPU needed;
+ * ssb_set_pipeline_depth / ssb_set_slot_streams refuse what this refuses. */
+int ssb_check_pipeline_config(int depth, int streams);
 /* Number of pipeline slots (1..16, default 1).  Each slot owns its streams and workspace; calls of
  * ssb_threshold_aggregate_batch_dev go to the slots round robin, so up to `depth` independent
  * batches are in flight and overlap on the device (e.g. the duties of consecutive slots).  Each

@@ -1018,35 +1018,51 @@ int bls_oracle_verify(const uint8_t* pk48, const uint8_t* sig96, const uint8_t* 
  * combined signature is identical). */
 static int threshold_job(uint32_t t, uint32_t n, const uint8_t* sigs96, const uint8_t* pks48, const uint64_t* ids,
                          const g2_aff* h, uint8_t* out96, uint64_t* err, uint8_t* verdicts, int verify_all) {
-  if (n < t) { err[0] = n; err[1] = t; return 2; }
+  uint8_t* vall = NULL;
+  if (verify_all) {     /* every share's verdict first (the engine's verify stage), then the scan */
+    vall = verdicts ? verdicts : (uint8_t*)malloc(n ? n : 1);
+    for (uint32_t i = 0; i < n; ++i) {
+      g1_aff pk; g2_aff sig;
+      vall[i] = (uint8_t)(g1_decompress(&pk, pks48 + 48 * (size_t)i) && g2_decompress(&sig, sigs96 + 96 * (size_t)i) &&
+                          verify_points(&pk, &sig, h));
+    }
+  }
+  int rc = 0;
   uint64_t sel_ids[64]; g2_aff sel[64]; uint32_t got = 0;
-  if (t > 64) { err[0] = n; err[1] = t; return 2; }
+  if (n < t || t > 64) { err[0] = n; err[1] = t; rc = 2; goto done; }
   for (uint32_t i = 0; i < n; ++i) {
-    if (ids[i] == 0) { err[0] = 0; err[1] = 0; return 3; }
+    if (ids[i] == 0) { err[0] = 0; err[1] = 0; rc = 3; goto done; }
     int dup = 0;
     for (uint32_t k = 0; k < got; ++k) dup |= sel_ids[k] == ids[i];
-    if (dup && !verify_all) continue;
+    if (dup) continue;
     g1_aff pk; g2_aff sig;
-    int ok = g1_decompress(&pk, pks48 + 48 * (size_t)i) && g2_decompress(&sig, sigs96 + 96 * (size_t)i) &&
-             verify_points(&pk, &sig, h);
-    if (verdicts) verdicts[i] = (uint8_t)ok;
-    if (ok && !dup && got < t) { sel[got] = sig; sel_ids[got] = ids[i]; ++got; if (got >= t && !verify_all) break; }
+    int ok;
+    if (vall) ok = vall[i] && g2_decompress(&sig, sigs96 + 96 * (size_t)i);
+    else {
+      ok = g1_decompress(&pk, pks48 + 48 * (size_t)i) && g2_decompress(&sig, sigs96 + 96 * (size_t)i) && verify_points(&pk, &sig, h);
+      if (verdicts) verdicts[i] = (uint8_t)ok;
+    }
+    if (ok) { sel[got] = sig; sel_ids[got] = ids[i]; ++got; if (got >= t) break; }
   }
-  if (got < t) { err[0] = got; err[1] = t; return 4; }
-  uint64_t lam[64][4];
-  lagrange(lam, sel_ids, (int)t);
-  g2_jac acc; g2_set_inf(&acc);
-  for (uint32_t i = 0; i < t; ++i) {
-    g2_jac p, q;
-    g2_from_aff(&p, &sel[i]);
-    g2_mul(&q, &p, lam[i], 4);
-    g2_add(&acc, &acc, &q);
+  if (got < t) { err[0] = got; err[1] = t; rc = 4; goto done; }
+  {
+    uint64_t lam[64][4];
+    lagrange(lam, sel_ids, (int)t);
+    g2_jac acc; g2_set_inf(&acc);
+    for (uint32_t i = 0; i < t; ++i) {
+      g2_jac p, q;
+      g2_from_aff(&p, &sel[i]);
+      g2_mul(&q, &p, lam[i], 4);
+      g2_add(&acc, &acc, &q);
+    }
+    g2_aff a;
+    g2_to_aff(&a, &acc);
+    g2_compress(out96, &a);
+    err[0] = err[1] = 0;
   }
-  g2_aff a;
-  g2_to_aff(&a, &acc);
-  g2_compress(out96, &a);
-  err[0] = err[1] = 0;
-  return 0;
+done:
+  if (vall && vall != verdicts) free(vall);
+  return rc;
 }
 
 int bls_oracle_threshold_aggregate(uint32_t t, uint32_t n, const uint8_t* sigs96, const uint8_t* pks48,
@@ -1107,6 +1123,180 @@ int bls_oracle_threshold_batch(size_t n_jobs, const uint32_t* share_off, const u
   for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
   free(H);
   return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * RLC-batched variant of the batch (the CPU baseline's second column, BASELINE.md §2: "per-signature
+ * verify and RLC batch, both reported").  The same algorithm family as the device engine and as
+ * lighthouse's verify_signature_sets: per share decompress + subgroup check + [k_i]pk_i, [k_i]sig_i
+ * (64-bit odd scalars); per root sum_i k_i pk_i; ONE multi-pairing
+ * prod_r e(P_r, H_r) * e(-g1, sum_i k_i sig_i) and ONE final exponentiation; if it fails, every
+ * share is verified on its own (the per-share path).  Combine: integer Lagrange coefficients when
+ * the ids give them (ids 1..t), else the 255-bit lambda_i (as threshold_job).  The scalars are a
+ * splitmix64 stream of `seed` -- a timing baseline, not a soundness claim (the engine's are secret).
+ * --------------------------------------------------------------------------------------------- */
+static uint64_t splitmix_at(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ULL * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+typedef struct {
+  size_t lo, hi; const uint8_t* sigs; const uint8_t* pks; uint64_t seed;
+  g1_jac* kpk; g2_jac* ksig; g2_aff* sig; uint8_t* cand;
+} rlc_args;
+static void* rlc_worker(void* p) {
+  rlc_args* a = (rlc_args*)p;
+  for (size_t i = a->lo; i < a->hi; ++i) {
+    g1_aff pk; g2_aff* sg = &a->sig[i];
+    int ok = g1_decompress(&pk, a->pks + 48 * i) && g2_decompress(sg, a->sigs + 96 * i) && !pk.inf && !sg->inf &&
+             g2_in_subgroup(sg);
+    a->cand[i] = (uint8_t)ok;
+    if (!ok) { g1_set_inf(&a->kpk[i]); g2_set_inf(&a->ksig[i]); continue; }
+    uint64_t k = splitmix_at(a->seed, i) | 1ULL;
+    g1_jac P; g1_from_aff(&P, &pk); g1_mul(&a->kpk[i], &P, &k, 1);
+    g2_jac Q; g2_from_aff(&Q, sg); g2_mul(&a->ksig[i], &Q, &k, 1);
+  }
+  return NULL;
+}
+typedef struct {
+  size_t lo, hi; size_t n; const uint32_t* share_root; const g1_jac* kpk; const g2_aff* H; fp12* f;
+} root_args;
+static void* root_worker(void* p) {   /* roots [lo, hi): P_r = sum k_i pk_i, f_r = Miller(P_r, H_r) */
+  root_args* a = (root_args*)p;
+  for (size_t r = a->lo; r < a->hi; ++r) {
+    g1_jac acc; g1_set_inf(&acc);
+    for (size_t i = 0; i < a->n; ++i) if (a->share_root[i] == r) g1_add(&acc, &acc, &a->kpk[i]);
+    if (g1_is_inf(&acc)) { a->f[r] = F12_ONE; continue; }
+    g1_aff P; g1_to_aff(&P, &acc);
+    miller_loop(&a->f[r], &P, &a->H[r]);
+  }
+  return NULL;
+}
+typedef struct { size_t lo, hi; const g2_jac* ksig; g2_jac part; } sum2_args;
+static void* sum2_worker(void* p) {
+  sum2_args* a = (sum2_args*)p;
+  g2_set_inf(&a->part);
+  for (size_t i = a->lo; i < a->hi; ++i) g2_add(&a->part, &a->part, &a->ksig[i]);
+  return NULL;
+}
+/* lambda_i as integers c_i (|c_i| < 2^62) when every one is an integer (same test as the device's
+ * unit_lagrange_small); returns 0 otherwise */
+static int64_t gcd64(int64_t a, int64_t b) { if (a < 0) a = -a; if (b < 0) b = -b; while (b) { int64_t t = a % b; a = b; b = t; } return a; }
+static int lagrange_small(int64_t* c, const uint64_t* x, uint32_t t) {
+  for (uint32_t i = 0; i < t; ++i) {
+    int64_t num = 1, den = 1;
+    for (uint32_t k = 0; k < t; ++k) {
+      if (k == i) continue;
+      if (x[k] >= (1ULL << 62) || x[i] >= (1ULL << 62)) return 0;
+      int64_t a = (int64_t)x[k], b = (int64_t)x[k] - (int64_t)x[i];
+      if (b == 0) return 0;
+      int64_t g = gcd64(a, b); a /= g; b /= g;
+      g = gcd64(a, den); a /= g; den /= g;
+      g = gcd64(num, b); num /= g; b /= g;
+      if (__builtin_mul_overflow(num, a, &num) || __builtin_mul_overflow(den, b, &den)) return 0;
+    }
+    if (den == -1) { num = -num; den = 1; }
+    if (den != 1 || num >= (1LL << 62) || num <= -(1LL << 62)) return 0;
+    c[i] = num;
+  }
+  return 1;
+}
+typedef struct {
+  size_t lo, hi; const uint32_t* off; const uint32_t* t; const uint64_t* ids; const g2_aff* sig; const uint8_t* ver;
+  uint8_t* out; int32_t* st; uint64_t* err;
+} comb_args;
+static void* comb_worker(void* p) {   /* the reference's scan over known verdicts, then the combine */
+  comb_args* a = (comb_args*)p;
+  for (size_t j = a->lo; j < a->hi; ++j) {
+    const uint32_t b = a->off[j], n = a->off[j + 1] - b, t = a->t[j];
+    uint64_t* err = a->err + 2 * j;
+    if (n < t || t > 64) { err[0] = n; err[1] = t; a->st[j] = 2; continue; }
+    uint64_t sel_ids[64]; uint32_t sel[64], got = 0; int st = 0;
+    for (uint32_t i = 0; i < n && got < t; ++i) {   /* stops at the t-th valid share, as the reference */
+      const uint64_t id = a->ids[b + i];
+      if (id == 0) { st = 3; break; }
+      int dup = 0;
+      for (uint32_t k = 0; k < got; ++k) dup |= sel_ids[k] == id;
+      if (dup || !a->ver[b + i]) continue;
+      sel[got] = b + i; sel_ids[got] = id; ++got;
+    }
+    if (st == 3) { err[0] = err[1] = 0; a->st[j] = 3; continue; }
+    if (got < t) { err[0] = got; err[1] = t; a->st[j] = 4; continue; }
+    g2_jac acc; g2_set_inf(&acc);
+    int64_t c[64];
+    if (lagrange_small(c, sel_ids, t)) {          /* sum c_i sig_i, interleaved signed binary */
+      int nb = 0;
+      for (uint32_t i = 0; i < t; ++i) { uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]); int bl = m ? 64 - __builtin_clzll(m) : 0; nb = bl > nb ? bl : nb; }
+      for (int bit = nb - 1; bit >= 0; --bit) {
+        g2_dbl(&acc, &acc);
+        for (uint32_t i = 0; i < t; ++i) {
+          uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
+          if ((m >> bit) & 1) { g2_jac q; g2_from_aff(&q, &a->sig[sel[i]]); if (c[i] < 0) g2_neg(&q, &q); g2_add(&acc, &acc, &q); }
+        }
+      }
+    } else {
+      uint64_t lam[64][4];
+      lagrange(lam, sel_ids, (int)t);
+      for (uint32_t i = 0; i < t; ++i) { g2_jac q, r; g2_from_aff(&q, &a->sig[sel[i]]); g2_mul(&r, &q, lam[i], 4); g2_add(&acc, &acc, &r); }
+    }
+    g2_aff aa; g2_to_aff(&aa, &acc);
+    g2_compress(a->out + 96 * j, &aa);
+    err[0] = err[1] = 0; a->st[j] = 0;
+  }
+  return NULL;
+}
+int bls_oracle_threshold_batch_rlc(size_t n_jobs, const uint32_t* share_off, const uint32_t* t, const uint8_t* sigs96,
+                                   const uint8_t* pks48, const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                                   const uint8_t* roots32, const uint8_t* dst, size_t dlen, uint8_t* out96, int32_t* status,
+                                   uint64_t* err, uint8_t* verdicts, uint64_t seed, int threads, int* batch_ok) {
+  bls_oracle_init();
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  const size_t n = n_jobs ? share_off[n_jobs] : 0;
+  g2_aff* H = (g2_aff*)malloc(sizeof(g2_aff) * (n_roots ? n_roots : 1));
+  g1_jac* kpk = (g1_jac*)malloc(sizeof(g1_jac) * (n ? n : 1));
+  g2_jac* ksig = (g2_jac*)malloc(sizeof(g2_jac) * (n ? n : 1));
+  g2_aff* sig = (g2_aff*)malloc(sizeof(g2_aff) * (n ? n : 1));
+  uint32_t* sr = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  fp12* f = (fp12*)malloc(sizeof(fp12) * (n_roots + 1));
+  if (!H || !kpk || !ksig || !sig || !sr || !f) { free(H); free(kpk); free(ksig); free(sig); free(sr); free(f); return -3; }
+  for (size_t j = 0; j < n_jobs; ++j) for (uint32_t i = share_off[j]; i < share_off[j + 1]; ++i) sr[i] = job_root[j];
+  pthread_t th[256];
+  hash_args ha[256]; rlc_args ra[256]; root_args ro[256]; sum2_args sa[256]; comb_args ca[256];
+  int nt = (size_t)threads < n_roots ? threads : (int)n_roots;
+  for (int i = 0; i < nt; ++i) { ha[i] = (hash_args){n_roots * i / nt, n_roots * (i + 1) / nt, roots32, dst, dlen, H}; pthread_create(&th[i], NULL, hash_worker, &ha[i]); }
+  for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+  int ns = (size_t)threads < n ? threads : (int)(n ? n : 1);
+  for (int i = 0; i < ns; ++i) { ra[i] = (rlc_args){n * i / ns, n * (i + 1) / ns, sigs96, pks48, seed, kpk, ksig, sig, verdicts}; pthread_create(&th[i], NULL, rlc_worker, &ra[i]); }
+  for (int i = 0; i < ns; ++i) pthread_join(th[i], NULL);
+  for (int i = 0; i < nt; ++i) { ro[i] = (root_args){n_roots * i / nt, n_roots * (i + 1) / nt, n, sr, kpk, H, f}; pthread_create(&th[i], NULL, root_worker, &ro[i]); }
+  for (int i = 0; i < ns; ++i) { sa[i] = (sum2_args){n * i / ns, n * (i + 1) / ns, ksig}; pthread_create(&th[nt + i < 256 ? nt + i : 255], NULL, sum2_worker, &sa[i]); }
+  for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+  for (int i = 0; i < ns; ++i) pthread_join(th[nt + i < 256 ? nt + i : 255], NULL);
+  g2_jac S; g2_set_inf(&S);
+  for (int i = 0; i < ns; ++i) g2_add(&S, &S, &sa[i].part);
+  fp12 acc = F12_ONE;
+  for (size_t r = 0; r < n_roots; ++r) f12_mul(&acc, &acc, &f[r]);
+  if (!g2_is_inf(&S)) {
+    g2_aff Sa; g2_to_aff(&Sa, &S);
+    g1_aff ng = G1_GEN; fp_neg(&ng.y, &ng.y);
+    fp12 fs; miller_loop(&fs, &ng, &Sa); f12_mul(&acc, &acc, &fs);
+  }
+  fp12 e; final_exp(&e, &acc);
+  const int ok = f12_is_one(&e);
+  if (batch_ok) *batch_ok = ok;
+  int rc = 0;
+  if (!ok) {       /* exact per-share verdicts (the per-share path), then the same selection */
+    rc = bls_oracle_threshold_batch(n_jobs, share_off, t, sigs96, pks48, ids, job_root, n_roots, roots32, dst, dlen, out96,
+                                    status, err, verdicts, 1, threads);
+  } else {
+    int nj = (size_t)threads < n_jobs ? threads : (int)(n_jobs ? n_jobs : 1);
+    for (int i = 0; i < nj; ++i) { ca[i] = (comb_args){n_jobs * i / nj, n_jobs * (i + 1) / nj, share_off, t, ids, sig, verdicts, out96, status, err}; pthread_create(&th[i], NULL, comb_worker, &ca[i]); }
+    for (int i = 0; i < nj; ++i) pthread_join(th[i], NULL);
+  }
+  free(H); free(kpk); free(ksig); free(sig); free(sr); free(f);
+  return rc;
 }
 
 /* self-test: the x-chain final exponentiation equals the cube of the textbook exponent */

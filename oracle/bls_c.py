@@ -35,6 +35,9 @@ def load():
         lib.bls_oracle_threshold_batch.argtypes = [ctypes.c_size_t, _u32p, _u32p, _u8p, _u8p, _u64p, _u32p,
                                                    ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, _i32p, _u64p,
                                                    _u8p, ctypes.c_int, ctypes.c_int]
+        lib.bls_oracle_threshold_batch_rlc.argtypes = [ctypes.c_size_t, _u32p, _u32p, _u8p, _u8p, _u64p, _u32p,
+                                                       ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, _i32p, _u64p,
+                                                       _u8p, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         lib.bls_oracle_init()
         _lib = lib
     return _lib
@@ -100,3 +103,33 @@ def threshold_batch(share_off, t, sigs96, pks48, ids, job_root, roots, threads, 
                                    st.ctypes.data_as(_i32p), err.ctypes.data_as(_u64p), ver.ctypes.data_as(_u8p),
                                    1 if verify_all else 0, int(threads))
     return out, st, err, ver
+
+
+def threshold_batch_rlc(share_off, t, sigs96, pks48, ids, job_root, roots, threads, dst=DST_POP, seed=0x5AFE57A4E):
+    """The RLC-batched CPU path (bls_oracle_threshold_batch_rlc): one multi-pairing and one final
+    exponentiation for the whole batch, per-share verification only if it fails.  Returns
+    (out96, status, err, verdicts, batch_ok)."""
+    import numpy as np
+    lib = load()
+    J = len(t)
+    off = np.ascontiguousarray(np.asarray(share_off, dtype=np.uint32))
+    tt = np.ascontiguousarray(np.asarray(t, dtype=np.uint32))
+    jr = np.ascontiguousarray(np.asarray(job_root, dtype=np.uint32))
+    idv = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64))
+    sg = np.frombuffer(sigs96, dtype=np.uint8)
+    pk = np.frombuffer(pks48, dtype=np.uint8)
+    rt = np.frombuffer(b"".join(roots), dtype=np.uint8)
+    out = np.zeros((J, 96), dtype=np.uint8)
+    st = np.zeros(J, dtype=np.int32)
+    err = np.zeros((J, 2), dtype=np.uint64)
+    ver = np.zeros(max(1, int(off[-1]) if J else 0), dtype=np.uint8)
+    ok = ctypes.c_int(0)
+    d, _keep = _b(dst)
+    rc = lib.bls_oracle_threshold_batch_rlc(J, off.ctypes.data_as(_u32p), tt.ctypes.data_as(_u32p), sg.ctypes.data_as(_u8p),
+                                            pk.ctypes.data_as(_u8p), idv.ctypes.data_as(_u64p), jr.ctypes.data_as(_u32p),
+                                            len(roots), rt.ctypes.data_as(_u8p), d, len(dst), out.ctypes.data_as(_u8p),
+                                            st.ctypes.data_as(_i32p), err.ctypes.data_as(_u64p), ver.ctypes.data_as(_u8p),
+                                            seed & (2**64 - 1), int(threads), ctypes.byref(ok))
+    if rc != 0:
+        raise RuntimeError("bls_oracle_threshold_batch_rlc: %d" % rc)
+    return out, st, err, ver, bool(ok.value)

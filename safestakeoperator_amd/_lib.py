@@ -21,6 +21,7 @@ SIGNATURES = {
     "ssb_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
     "ssb_destroy": (None, [_ctx]),
     "ssb_last_error": (ctypes.c_char_p, [_ctx]),
+    "ssb_check_pipeline_config": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "ssb_set_pipeline_depth": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_set_slot_streams": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_slot_stream": (ctypes.c_void_p, [_ctx, ctypes.c_int]),

@@ -495,8 +495,20 @@ void ssb_destroy(ssb_ctx* ctx) {
   delete ctx;
 }
 
+int ssb_check_pipeline_config(int depth, int streams) {
+  if (depth < 1 || depth > SSB_MAX_SLOTS || (streams != 1 && streams != 3)) return SSB_EINVAL;
+  // the HIP runtime reserves scratch per hardware queue for the largest kernel each queue ran;
+  // 8 slots x 3 streams ran out (HSA_STATUS_ERROR_OUT_OF_RESOURCES), 16 x 1 runs clean
+  if (depth * streams > SSB_MAX_SLOT_STREAMS) return SSB_EINVAL;
+  return SSB_OK;
+}
+
 int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
-  if (!ctx || depth < 1 || depth > SSB_MAX_SLOTS) return SSB_EINVAL;
+  if (!ctx) return SSB_EINVAL;
+  if (ssb_check_pipeline_config(depth, ctx->slot_streams) != SSB_OK) {
+    ctx->err = "pipeline depth x streams per slot outside the supported range (depth 1..16, depth x streams <= 16)";
+    return SSB_EINVAL;
+  }
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = ctx->nslots; i < depth; ++i) {
     if (init_slot(ctx->sl[i], ctx->slot_streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
@@ -509,7 +521,11 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
 }
 
 int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
-  if (!ctx || (streams != 1 && streams != 3)) return SSB_EINVAL;
+  if (!ctx) return SSB_EINVAL;
+  if (ssb_check_pipeline_config(ctx->nslots, streams) != SSB_OK) {
+    ctx->err = "streams per slot must be 1 or 3 and depth x streams <= 16 (lower the depth first)";
+    return SSB_EINVAL;
+  }
   if (streams == ctx->slot_streams) return SSB_OK;
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = 0; i < ctx->nslots; ++i) { sync_slot(ctx->sl[i]); free_slot(ctx->sl[i]); ctx->sl[i] = ssb_slot(); }

@@ -79,3 +79,33 @@ def test_threshold_batch_threads_agree():
             assert st[j] == c["expected_status"]
             if st[j] == 0:
                 assert out[j].tobytes().hex() == c["expected_sig"]
+
+
+def test_rlc_batch_path_matches_per_share():
+    """The RLC-batched CPU baseline (bls_oracle_threshold_batch_rlc) == the per-share path: on the
+    all-valid golden jobs the batch check passes and the combines agree (integer and 255-bit
+    Lagrange); on every golden job (invalid / undecodable / duplicate / zero-id shares) it fails and
+    the per-share verdicts take over."""
+    import json
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "threshold_cases.json")))["cases"]
+
+    def pack(cs):
+        roots, t, off, sigs, pks, ids, jr = [], [], [0], [], [], [], []
+        for c in cs:
+            r = bytes.fromhex(c["root"])
+            if r not in roots:
+                roots.append(r)
+            jr.append(roots.index(r)); t.append(c["t"])
+            sigs += [bytes.fromhex(s) for s in c["sigs"]]; pks += [bytes.fromhex(p) for p in c["pks"]]
+            ids += c["ids"]; off.append(len(sigs))
+        return off, t, b"".join(sigs), b"".join(pks), ids, jr, roots
+
+    good = [c for c in cases if all(c["share_verdicts"]) and c["expected_status"] == 0]
+    assert len(good) >= 3
+    for cs, want_ok in ((good, True), (cases, False)):
+        off, t, sg, pk, ids, jr, roots = pack(cs)
+        o1, s1, e1, v1 = bls_c.threshold_batch(off, t, sg, pk, ids, jr, roots, 4, verify_all=True)
+        o2, s2, e2, v2, ok = bls_c.threshold_batch_rlc(off, t, sg, pk, ids, jr, roots, 4)
+        assert ok == want_ok
+        assert (s1 == s2).all() and (e1 == e2).all() and (v1 == v2).all()
+        assert (o1[s1 == 0] == o2[s2 == 0]).all()
