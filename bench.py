@@ -288,7 +288,8 @@ def main():
         os.environ["SSB_TAILS"] = "1"
     # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 3)
     # + one for torch's own stream
-    set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "3") or 3))
+    set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "3") or 3)
+                  + int(os.environ.get("SSB_HASH_STREAMS", "0") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
 
     import numpy as np
     import torch

@@ -83,6 +83,16 @@ struct ssb_ctx {
   static constexpr int MAX_TAILS = 4;
   hipStream_t tails[MAX_TAILS] = {nullptr, nullptr, nullptr, nullptr};
   int ntails = 3;
+  // hash streams (SSB_HASH_STREAMS, default 0): with one stream per slot, hash_to_G2 of slot i's
+  // batch runs on hashs[i % nhash] beside the slot's decode / subgroup / MSM chain instead of in
+  // front of it (the hash depends on the roots only; the Miller loops wait for it)
+  static constexpr int MAX_HASH = 4;
+  hipStream_t hashs[MAX_HASH] = {nullptr, nullptr, nullptr, nullptr};
+  int nhash = 0;
+  // G1-side streams (SSB_G1_STREAMS, default 0): the per-root G1 sums of slot i's batch run on
+  // g1s[i % ng1] beside the slot's G2 MSM instead of after it
+  hipStream_t g1s[MAX_HASH] = {nullptr, nullptr, nullptr, nullptr};
+  int ng1 = 0;
   // decoded public keys (ssb_pk_cache_set): affine points + DEC_* flags, indexed by the caller
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0;
   // RLC key of each batch: fresh from getrandom() per call (default), or expanded from the caller's
@@ -353,12 +363,14 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   rlc_key key;
   if (int rc = draw_rlc_key(ctx, rlc_seed, key)) return rc;
   hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
+  if (ctx->cur->shared && ctx->nhash > 0) sh = ctx->hashs[(int)(ctx->cur - ctx->sl) % ctx->nhash];
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
   SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
   SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
   if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
   SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
   hipStream_t s1 = ctx->cur->side[1];
+  if (ctx->cur->shared && ctx->ng1 > 0) s1 = ctx->g1s[(int)(ctx->cur - ctx->sl) % ctx->ng1];
   const msm_plan& P = w.plan;
   if (n) {
     timed t(ctx, "k_decode");
@@ -465,6 +477,12 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   if (const char* e = getenv("SSB_TAILS")) ctx->ntails = std::max(1, std::min(ssb_ctx::MAX_TAILS, atoi(e)));
   for (int i = 1; i < ctx->ntails; ++i)
     if (hipStreamCreateWithFlags(&ctx->tails[i], hipStreamNonBlocking) != hipSuccess) { ctx->ntails = i; break; }
+  if (const char* e = getenv("SSB_HASH_STREAMS")) ctx->nhash = std::max(0, std::min(ssb_ctx::MAX_HASH, atoi(e)));
+  for (int i = 0; i < ctx->nhash; ++i)
+    if (hipStreamCreateWithFlags(&ctx->hashs[i], hipStreamNonBlocking) != hipSuccess) { ctx->nhash = i; break; }
+  if (const char* e = getenv("SSB_G1_STREAMS")) ctx->ng1 = std::max(0, std::min(ssb_ctx::MAX_HASH, atoi(e)));
+  for (int i = 0; i < ctx->ng1; ++i)
+    if (hipStreamCreateWithFlags(&ctx->g1s[i], hipStreamNonBlocking) != hipSuccess) { ctx->ng1 = i; break; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
@@ -490,6 +508,8 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->pkc_aff) hipFree(ctx->pkc_aff);
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
   for (int i = 1; i < ctx->ntails; ++i) if (ctx->tails[i]) { hipStreamSynchronize(ctx->tails[i]); hipStreamDestroy(ctx->tails[i]); }
+  for (int i = 0; i < ctx->nhash; ++i) if (ctx->hashs[i]) { hipStreamSynchronize(ctx->hashs[i]); hipStreamDestroy(ctx->hashs[i]); }
+  for (int i = 0; i < ctx->ng1; ++i) if (ctx->g1s[i]) { hipStreamSynchronize(ctx->g1s[i]); hipStreamDestroy(ctx->g1s[i]); }
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
