@@ -289,7 +289,7 @@ def main():
     # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 3)
     # + one for torch's own stream
     set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "3") or 3)
-                  + int(os.environ.get("SSB_HASH_STREAMS", "0") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
+                  + int(os.environ.get("SSB_HASH_STREAMS", "3") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
 
     import numpy as np
     import torch
@@ -444,15 +444,25 @@ def main():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
+        dbg = bool(os.environ.get("SSB_DEBUG_HOST"))
+        ev = []
         t0 = time.perf_counter()
         host_ms = []
         for i in range(args.steps):
             th = time.perf_counter()
+            if dbg:   # when the slot's stream reaches / finishes this batch
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(streams.get(i % S) or torch.cuda.ExternalStream(lib.ssb_slot_stream(eng.handle, i % S), device=dev))
             step(args.warmup + i, i % S)
+            if dbg:
+                e1.record(streams[i % S])
+                ev.append((e0, e1))
             host_ms.append((time.perf_counter() - th) * 1e3)
         torch.cuda.synchronize(dev)
-        if os.environ.get("SSB_DEBUG_HOST"):
+        if dbg:
             print("host ms per submit:", " ".join("%.2f" % x for x in host_ms), file=sys.stderr)
+            print("batch start/end ms:", " ".join("%.1f/%.1f" % (ev[0][0].elapsed_time(a), ev[0][0].elapsed_time(b))
+                                                   for a, b in ev), file=sys.stderr)
         if dist is not None:
             dist.barrier()
         return time.perf_counter() - t0

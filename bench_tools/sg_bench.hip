@@ -46,7 +46,7 @@ k_sg2(int n, const g2_aff* __restrict__ pts, uint32_t* __restrict__ out) {
 }
 
 int main() {
-  const int NMAX = 65536;
+  const int NMAX = 262144;
   // points: multiples of the hash of a fixed root (in G2) and raw isogeny images (not in G2)
   std::vector<g2_aff> h(NMAX);
   uint8_t m[32] = {0};
@@ -65,7 +65,7 @@ int main() {
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   printf("{");
   bool first = true;
-  for (int n : {16384, 65536}) {
+  for (int n : {16384, 65536, 131072, 262144}) {
     for (int v = 0; v < 4; ++v) {
       auto go = [&] {
         if (v == 0) hipLaunchKernelGGL(k_sg<0>, dim3(n / 64), dim3(64), 0, 0, n, d, o0);
@@ -87,6 +87,28 @@ int main() {
     int same = 0, ones = 0;
     for (int i = 0; i < n; ++i) { same += a[i] == b[i]; ones += a[i]; }
     printf(", \"n%d_agree\": %d, \"n%d_in_group\": %d", n, same, n, ones);
+  }
+  // cross-stream concurrency: K streams, each a chain of R launches of 16,384 points (one C2
+  // batch's subgroup checks); ideal = the time of one K*R*16384-point launch
+  {
+    const int n = 16384, R = 8;
+    hipStream_t ss[24];
+    for (int k = 0; k < 24; ++k) hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking);
+    for (int K : {1, 2, 4, 8, 12, 14, 16, 20}) {
+      float best = 1e9;
+      for (int rep = 0; rep < 3; ++rep) {
+        hipDeviceSynchronize();
+        hipEventRecord(e0, 0);
+        for (int k = 0; k < K; ++k) hipStreamWaitEvent(ss[k], e0, 0);
+        for (int r = 0; r < R; ++r)
+          for (int k = 0; k < K; ++k)
+            hipLaunchKernelGGL(k_sg2<1>, dim3(n / 64), dim3(64), 0, ss[k], n, d + (size_t)(k % 16) * n, ov + (size_t)(k % 16) * n);
+        for (int k = 0; k < K; ++k) { hipEvent_t e; hipEventCreate(&e); hipEventRecord(e, ss[k]); hipStreamWaitEvent(0, e, 0); }
+        hipEventRecord(e1, 0); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1); best = ms < best ? ms : best;
+      }
+      printf(", \"streams%d_ms\": %.3f, \"streams%d_ms_per_launch\": %.4f", K, best, K, best / (K * R));
+    }
   }
   printf("}\n");
   return 0;

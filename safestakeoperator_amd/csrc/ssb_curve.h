@@ -74,8 +74,9 @@ template <class F> SSB_INL void jac_dbl_inl(jac<F>& r, const jac<F>& p) {
 template <class F> SSB_FN void jac_dbl(jac<F>& r, const jac<F>& p) { jac_dbl_inl(r, p); }
 
 // madd-2007-bl: r = p + q, q affine.  Handles infinity and the doubling/opposite cases.
-// (_inl: inlined into the MSM bucket loops; jac_add_aff: out-of-line copy)
-template <class F> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+// (_inl: inlined into the MSM bucket loops; jac_add_aff: out-of-line copy; kNoCall: the rare
+// doubling case inlined too, for the call-free occupancy-2 kernels)
+template <class F, bool kNoCall = false> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   if (q.inf) { r = p; return; }
   if (jac_is_inf(p)) { jac_from_aff(r, q); return; }
   F Z1Z1, U2, S2, H, HH, I, J, rr, V, t;
@@ -85,8 +86,12 @@ template <class F> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, cons
   f_sub(H, U2, p.x);
   f_sub(rr, S2, p.y);
   if (f_is_zero(H)) {
-    if (f_is_zero(rr)) { jac<F> d; jac_from_aff(d, q); jac_dbl(r, d); }
-    else jac_set_inf(r);
+    if (f_is_zero(rr)) {
+      jac<F> d; jac_from_aff(d, q);
+      if (kNoCall) jac_dbl_inl(r, d); else jac_dbl(r, d);
+    } else {
+      jac_set_inf(r);
+    }
     return;
   }
   f_dbl(rr, rr);
@@ -242,6 +247,15 @@ template <class F> SSB_FN void jac_mul_x_abs_aff(jac<F>& r, const aff<F>& p) {
   }
   r = acc;
 }
+// no calls on the common path (the occupancy-2 subgroup kernel)
+template <class F> SSB_INL void jac_mul_x_abs_aff_inl(jac<F>& r, const aff<F>& p) {
+  jac<F> acc; jac_from_aff(acc, p);
+  for (int i = 62; i >= 0; --i) {
+    jac_dbl_inl(acc, acc);
+    if ((BLS_X_ABS >> i) & 1ull) jac_add_aff_inl<F, true>(acc, acc, p);
+  }
+  r = acc;
+}
 
 // ---- G2 endomorphism psi = twist^-1 o Frobenius o twist: (conj(x) cx, conj(y) cy) ----
 SSB_INL void g2_psi_aff(g2_aff& r, const g2_aff& p) {
@@ -258,6 +272,15 @@ SSB_INL void g2_psi_jac(g2_jac& r, const g2_jac& p) {
 }
 
 // G2 membership (sig_groupcheck): psi(P) == [x]P  (Scott 2021; == [r]P == O on BLS12-381)
+SSB_INL bool g2_in_subgroup_inl(const g2_aff& p) {
+  if (p.inf) return true;
+  g2_jac xp;
+  jac_mul_x_abs_aff_inl(xp, p);
+  jac_neg(xp, xp);  // x < 0
+  g2_aff ps;
+  g2_psi_aff(ps, p);
+  return jac_eq_aff(xp, ps);
+}
 SSB_FN bool g2_in_subgroup(const g2_aff& p) {
   if (p.inf) return true;
   g2_jac xp;
@@ -276,7 +299,7 @@ enum : uint32_t {
 };
 
 // blst_p2_uncompress semantics.  Returns DEC_* bits (0 on BLST_BAD_ENCODING / NOT_ON_CURVE).
-SSB_FN uint32_t g2_decompress(g2_aff& r, const uint8_t* in) {
+SSB_INL uint32_t g2_decompress_inl(g2_aff& r, const uint8_t* in) {
   const uint8_t b0 = in[0];
   r.inf = 0;
   if (!(b0 & 0x80)) return 0;
@@ -298,14 +321,15 @@ SSB_FN uint32_t g2_decompress(g2_aff& r, const uint8_t* in) {
   fp2 b = fp2_from_c(FP2_B2);
   fp2_add(y2, y2, b);
   fp2 y;
-  if (!fp2_sqrt(y, y2)) return 0;
+  if (!fp2_sqrt_inl(y, y2)) return 0;
   const bool want = (b0 & 0x20) != 0;
   if (fp2_lex_largest(y) != want) fp2_neg(y, y);
   r.x = x; r.y = y;
   return DEC_OK;
 }
+SSB_FN uint32_t g2_decompress(g2_aff& r, const uint8_t* in) { return g2_decompress_inl(r, in); }
 
-SSB_FN uint32_t g1_decompress(g1_aff& r, const uint8_t* in) {
+SSB_INL uint32_t g1_decompress_inl(g1_aff& r, const uint8_t* in) {
   const uint8_t b0 = in[0];
   r.inf = 0;
   if (!(b0 & 0x80)) return 0;
@@ -324,12 +348,13 @@ SSB_FN uint32_t g1_decompress(g1_aff& r, const uint8_t* in) {
   fp b = fp_from_c(FP_B1);
   fp_add(y2, y2, b);
   fp y;
-  if (!fp_sqrt(y, y2)) return 0;
+  if (!fp_sqrt_inl(y, y2)) return 0;
   const bool want = (b0 & 0x20) != 0;
   if (fp_lex_largest(y) != want) fp_neg(y, y);
   r.x = x; r.y = y;
   return DEC_OK;
 }
+SSB_FN uint32_t g1_decompress(g1_aff& r, const uint8_t* in) { return g1_decompress_inl(r, in); }
 
 // blst_p2_compress (Signature::serialize): x.c1 | x.c0 big-endian, flags in byte 0
 SSB_FN void g2_compress(uint8_t* out, const g2_aff& p) {

@@ -23,6 +23,14 @@
 #define SSB_WAVES_PER_EU 1
 #endif
 #define SSB_LB(n) __attribute__((amdgpu_flat_work_group_size(1, n), amdgpu_waves_per_eu(SSB_WAVES_PER_EU)))
+// Throughput kernels with every routine inlined: at most 256 registers per lane (VGPR + AGPR), so
+// two waves share each SIMD and hide each other's dependent-chain latency.  Measured on MI355X
+// (bench_tools/sg_bench.hip, G2 subgroup check over 262,144 points = 4 waves per SIMD):
+// 9.52 ms at one wave per SIMD, 7.10 ms at two.
+#ifndef SSB_LB2_WAVES
+#define SSB_LB2_WAVES 2
+#endif
+#define SSB_LB2(n) __attribute__((amdgpu_flat_work_group_size(1, n), amdgpu_waves_per_eu(SSB_LB2_WAVES)))
 #ifdef SSB_FN_INLINE  // experiment: every routine inlined (code size explodes; microbenchmarks only)
 #define SSB_FN __host__ __device__ __forceinline__
 #else
@@ -473,7 +481,9 @@ SSB_INL fp fp_pick8(const fp* t, int i) {
   for (int k = 1; k < 8; ++k) if (i == k) r = t[k];
   return r;
 }
-SSB_FN void fp_pow_sw(fp& r, const fp& a, const uint8_t* sch, int n) {
+// (_inl twins: bodies for the occupancy-2 per-share kernels, which must not call out of line --
+// a call's callee-saved registers and frame keep the kernel at one wave per SIMD)
+SSB_INL void fp_pow_sw_inl(fp& r, const fp& a, const uint8_t* sch, int n) {
   fp t[8], a2;
   t[0] = a;
   fp_sqr(a2, a);
@@ -486,6 +496,7 @@ SSB_FN void fp_pow_sw(fp& r, const fp& a, const uint8_t* sch, int n) {
   }
   r = acc;
 }
+SSB_FN void fp_pow_sw(fp& r, const fp& a, const uint8_t* sch, int n) { fp_pow_sw_inl(r, a, sch, n); }
 
 // Binary extended Euclid (variable time: inputs on this path are public).  For the Montgomery
 // form aR it returns (aR)^{-1} * R^3 / R = a^{-1} R.  inv(0) = 0.  About 4x fewer dependent
@@ -533,13 +544,14 @@ SSB_FN void fp_inv(fp& r, const fp& a) {
   mp_mont_mul<12>(r.l, t.l, P_R3, P_LIMBS, P_INV32);
 }
 // returns true iff a is a square; r = a^((p+1)/4) (a root when it is)
-SSB_FN bool fp_sqrt(fp& r, const fp& a) {
+SSB_INL bool fp_sqrt_inl(fp& r, const fp& a) {
   fp s, s2;
-  fp_pow_sw(s, a, EXPW_P_PLUS_1_DIV_4, EXPW_P_PLUS_1_DIV_4_N);
+  fp_pow_sw_inl(s, a, EXPW_P_PLUS_1_DIV_4, EXPW_P_PLUS_1_DIV_4_N);
   fp_sqr(s2, s);
   r = s;
   return fp_eq(s2, a);
 }
+SSB_FN bool fp_sqrt(fp& r, const fp& a) { return fp_sqrt_inl(r, a); }
 // ZCash sign: canonical(a) > (p-1)/2
 SSB_INL bool fp_lex_largest(const fp& a) {
   fp c; fp_from_mont(c, a);
@@ -655,12 +667,12 @@ SSB_FN void fp2_inv(fp2& r, const fp2& a) {
 }
 // Square root in Fp2 by the norm method (p = 3 mod 4).  Any root is returned; the caller fixes
 // the sign.  Returns false iff a is not a square.
-SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) {
+SSB_INL bool fp2_sqrt_inl(fp2& r, const fp2& a) {
   if (fp_is_zero(a.c1)) {
     fp s;
-    if (fp_sqrt(s, a.c0)) { r.c0 = s; r.c1 = fp_zero(); return true; }
+    if (fp_sqrt_inl(s, a.c0)) { r.c0 = s; r.c1 = fp_zero(); return true; }
     fp na; fp_neg(na, a.c0);
-    bool ok = fp_sqrt(s, na);
+    bool ok = fp_sqrt_inl(s, na);
     r.c0 = fp_zero(); r.c1 = s;
     return ok;
   }
@@ -668,11 +680,11 @@ SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) {
   fp_sqr(n, a.c0);
   fp_sqr(t, a.c1);
   fp_add(n, n, t);
-  if (!fp_sqrt(s, n)) return false;
+  if (!fp_sqrt_inl(s, n)) return false;
   fp c, half = fp_from_c(FP_HALF);
   fp_add(c, a.c0, s);
   fp_mul(c, c, half);                       // c = (a0 + s)/2  (nonzero since a1 != 0)
-  fp_pow_sw(t, c, EXPW_P_MINUS_3_DIV_4, EXPW_P_MINUS_3_DIV_4_N);  // t = c^((p-3)/4)
+  fp_pow_sw_inl(t, c, EXPW_P_MINUS_3_DIV_4, EXPW_P_MINUS_3_DIV_4_N);  // t = c^((p-3)/4)
   fp x, x2;
   fp_mul(x, c, t);                          // x^2 = c if c is a square, else -c
   fp_sqr(x2, x);
@@ -691,6 +703,7 @@ SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) {
   r = y;
   return fp2_eq(chk, a);
 }
+SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) { return fp2_sqrt_inl(r, a); }
 // ZCash sign for Fp2: c1 > (p-1)/2, or c0 > (p-1)/2 when c1 == 0
 SSB_INL bool fp2_lex_largest(const fp2& a) {
   if (!fp_is_zero(a.c1)) return fp_lex_largest(a.c1);

@@ -34,7 +34,7 @@ __global__ void SSB_LB(64) k_decode(int n, const uint8_t* __restrict__ sig96,
   if (pk48) pk_aff[s] = pk;
   flags[s] = fl;
 }
-__global__ void SSB_LB(64) k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
+__global__ void SSB_LB2(64) k_decode2(int n, const uint8_t* __restrict__ sig96, const uint8_t* __restrict__ pk48,
                                                 g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
                                                 uint32_t* __restrict__ sflags, uint32_t* __restrict__ pflags) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -56,7 +56,7 @@ __global__ void SSB_LB(64) k_decode2(int n, const uint8_t* __restrict__ sig96, c
 // decoded-public-key path (ssb_pk_cache_set): n lanes decode the signatures, the public keys are
 // gathered from the context's table of points decompressed once (lighthouse's PublicKey holds the
 // decompressed point too: the reference never decompresses a key per verification)
-__global__ void SSB_LB(64) k_decode_sig(int n, const uint8_t* __restrict__ sig96, g2_aff* __restrict__ sig_aff,
+__global__ void SSB_LB2(64) k_decode_sig(int n, const uint8_t* __restrict__ sig96, g2_aff* __restrict__ sig_aff,
                                                    uint32_t* __restrict__ sflags) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
@@ -75,7 +75,7 @@ __global__ void SSB_LB(256) k_pk_gather(int n, const uint32_t* __restrict__ pk_i
   if (i < n_cache) { pk_aff[s] = cache_aff[i]; pflags[s] = cache_flags[i]; }
   else pflags[s] = 0u;  // out-of-range index: the share cannot verify
 }
-__global__ void SSB_LB(64) k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
+__global__ void SSB_LB2(64) k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
                                                   uint32_t* __restrict__ pflags) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;

@@ -84,9 +84,11 @@ SSB_FN uint32_t unit_decode(g2_aff& sig, g1_aff& pk, const uint8_t* sig96, const
 
 // Split form used by the verify pipeline (independent per-share tasks, one thread each):
 //   decode_sig | decode_pk   then   subgroup | rlc_sig | rlc_pk
-SSB_FN uint32_t unit_decode_sig(g2_aff& sig, const uint8_t* sig96) { return g2_decompress(sig, sig96); }
-SSB_FN uint32_t unit_decode_pk(g1_aff& pk, const uint8_t* pk48) { return g1_decompress(pk, pk48); }
-SSB_FN uint32_t unit_subgroup(const g2_aff& sig) { return g2_in_subgroup(sig) ? DEC_IN_GROUP : 0u; }
+// Inlined whole (no out-of-line call on the common path): the per-share kernels built from these
+// run two waves per SIMD (SSB_LB2), which a call's frame and callee-saved registers prevent.
+SSB_INL uint32_t unit_decode_sig(g2_aff& sig, const uint8_t* sig96) { return g2_decompress_inl(sig, sig96); }
+SSB_INL uint32_t unit_decode_pk(g1_aff& pk, const uint8_t* pk48) { return g1_decompress_inl(pk, pk48); }
+SSB_INL uint32_t unit_subgroup(const g2_aff& sig) { return g2_in_subgroup_inl(sig) ? DEC_IN_GROUP : 0u; }
 // (k odd: the RLC scalars are rlc_scalar_odd)
 SSB_FN void unit_rlc_sig(g2_jac& r, const g2_aff& sig, uint64_t k) {
   const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};

@@ -83,12 +83,14 @@ struct ssb_ctx {
   static constexpr int MAX_TAILS = 4;
   hipStream_t tails[MAX_TAILS] = {nullptr, nullptr, nullptr, nullptr};
   int ntails = 3;
-  // hash streams (SSB_HASH_STREAMS, default 0): with one stream per slot, hash_to_G2 of slot i's
+  // hash streams (SSB_HASH_STREAMS, default 3): with one stream per slot, hash_to_G2 of slot i's
   // batch runs on hashs[i % nhash] beside the slot's decode / subgroup / MSM chain instead of in
-  // front of it (the hash depends on the roots only; the Miller loops wait for it)
-  static constexpr int MAX_HASH = 4;
-  hipStream_t hashs[MAX_HASH] = {nullptr, nullptr, nullptr, nullptr};
-  int nhash = 0;
+  // front of it (the hash depends on the roots only; the Miller loops wait for it).  Three keep
+  // up with 14 slots (5.4 ms of hash per 2.3 ms batch); measured C2 at 20 timed steps: 0 -> 5.85 M,
+  // 3 -> 6.33 M partial sigs/s; 2 fall behind (4.8 M).  Created with the first one-stream slot.
+  static constexpr int MAX_HASH = 8;
+  hipStream_t hashs[MAX_HASH] = {};
+  int nhash = 3;
   // G1-side streams (SSB_G1_STREAMS, default 0): the per-root G1 sums of slot i's batch run on
   // g1s[i % ng1] beside the slot's G2 MSM instead of after it
   hipStream_t g1s[MAX_HASH] = {nullptr, nullptr, nullptr, nullptr};
@@ -286,6 +288,9 @@ msm_plan plan_msm(size_t n, size_t n_roots) {
   const size_t g1n = n_roots ? n_roots : 1;
   p.g1_msm = g1_use_msm(n, n_roots);
   int c2 = msm_pick_c(n, 1, 3, 8), c1 = msm_pick_c(n, g1n, 2, 8);  // c <= 8: <= 4 buckets per window lane
+  // SSB_MSM_C2 / SSB_MSM_C1: force the window widths (experiments: latency vs work)
+  if (const char* e = getenv("SSB_MSM_C2")) c2 = std::max(3, std::min(8, atoi(e)));
+  if (const char* e = getenv("SSB_MSM_C1")) c1 = std::max(2, std::min(8, atoi(e)));
   auto keys = [&](int c, size_t g) { return (size_t)((64 + c - 1) / c) * g << c; };
   while (c1 > 2 && keys(c2, 1) + keys(c1, g1n) > MSM_KMAX) --c1;
   p.g2 = msm_cfg{(uint32_t)c2, (uint32_t)((64 + c2 - 1) / c2), 0u, 1u};
@@ -309,6 +314,7 @@ struct verify_ws {
   g2_jac* b2; g1_jac* b1; g1_jac* w1;                                              // MSM buckets / windows
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
   g2_jac* rsig; uint32_t* gst; uint8_t* gv0; uint8_t* gv1;                         // failed-batch group tests
+  g2_jac* w2; uint32_t* redo2; uint32_t* redo1;                                    // lane-group window kernels
   size_t npairs;
 };
 // Miller values of the pairs plus the levels of the 8-ary product tree
@@ -328,7 +334,9 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
          align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
          3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(n * sizeof(g2_jac)) +
-         align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots);
+         align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
+         align_up(MSM_WMAX * sizeof(g2_jac)) + align_up(MSM_WMAX * 4) +
+         align_up(((size_t)p.g1.ngroups * (p.g1.W + 1) + 1) * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
@@ -352,6 +360,8 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.rsig = c.take<g2_jac>(n);
   w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
   w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
+  w.w2 = c.take<g2_jac>(MSM_WMAX); w.redo2 = c.take<uint32_t>(MSM_WMAX);
+  w.redo1 = c.take<uint32_t>((size_t)w.plan.g1.ngroups * (w.plan.g1.W + 1) + 1);
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
@@ -405,7 +415,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
     timed t(ctx, "k_msm_g1", s1);
-    launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p);
+    launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p, w.redo1);
   } else {
     timed t(ctx, "k_sum_g1", s1);
     hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)n_roots), dim3(SEG_THREADS), 0, s1, (int)n_roots, w.rstart, w.rcnt, w.perm,
@@ -413,7 +423,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
   if (n) on_decoded();
-  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow); }
+  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w2, w.redo2); }
   SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
   { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f); }
