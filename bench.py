@@ -280,16 +280,17 @@ def main():
     for k in ("validators", "threshold", "operators", "roots", "pipeline"):
         if getattr(args, k) is None:
             setattr(args, k, preset[k])
-    # Hardware queues: on one MI355X, 17 queues ran at full speed, 19 lost a third of the throughput
-    # and 21 collapsed (the firmware time-slices queues beyond what it maps at once).  With N > 1
-    # the process group adds a stream of its own, so multi-GPU runs use one tail stream (the exact
-    # fallback's concurrency across slots is not exercised by all-valid batches).
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "SSB_TAILS" not in os.environ:
-        os.environ["SSB_TAILS"] = "1"
-    # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 3)
-    # + one for torch's own stream
-    set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "3") or 3)
-                  + int(os.environ.get("SSB_HASH_STREAMS", "3") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
+    # Hardware queues: every engine stream needs its own, and past about 22 the firmware time-slices
+    # them (measured C2, 20 steps: 14 slots + spec + 1 tail + 6 hash streams = 22 engine streams
+    # 7.19 M sigs/s; one more hash stream 6.0 M).  With N > 1 the process group adds a stream of
+    # its own, so multi-GPU runs keep one hash stream fewer.
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        os.environ.setdefault("SSB_TAILS", "1")
+        os.environ.setdefault("SSB_HASH_STREAMS", "5")
+    # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 1)
+    # + the hash streams (SSB_HASH_STREAMS, engine default 6) + one for torch's own stream
+    set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "1") or 1)
+                  + int(os.environ.get("SSB_HASH_STREAMS", "6") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
 
     import numpy as np
     import torch
@@ -518,7 +519,8 @@ def main():
                        "validators_per_gpu": V, "threshold": t, "operators": n, "roots": n_roots,
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
                        "batches_in_flight": S, "streams_per_slot": args.slot_streams,
-                       "tail_streams": int(os.environ.get("SSB_TAILS", "3") or 3)},
+                       "tail_streams": int(os.environ.get("SSB_TAILS", "1") or 1),
+                       "hash_streams": int(os.environ.get("SSB_HASH_STREAMS", "6") or 0)},
             "batch_latency_ms": round(latency_ms, 3),
             "public_keys": ("compressed per batch (ssb_threshold_aggregate_batch_dev)" if args.compressed_pk else
                             "decompressed once at registration (ssb_pk_cache_set + _cached_dev), as lighthouse's "

@@ -520,7 +520,7 @@ SSB_INL void fp_half_mod(uint32_t* x) {
     mp_shr1<12>(x);
   }
 }
-SSB_FN void fp_inv(fp& r, const fp& a) {
+SSB_FN void fp_inv_bgcd(fp& r, const fp& a) {
   uint32_t u[12], v[12], x1[12], x2[12];
   for (int i = 0; i < 12; ++i) { u[i] = a.l[i]; v[i] = P_LIMBS[i]; x1[i] = 0; x2[i] = 0; }
   x1[0] = 1;
@@ -542,6 +542,156 @@ SSB_FN void fp_inv(fp& r, const fp& a) {
   fp t;
   for (int i = 0; i < 12; ++i) t.l[i] = mp_eq<12>(u, one) ? x1[i] : x2[i];
   mp_mont_mul<12>(r.l, t.l, P_R3, P_LIMBS, P_INV32);
+}
+
+// ---- Bernstein-Yang "safegcd" inversion (variable time; every input on this path is public) ----
+// The binary Euclid above branches per bit, so the 64 lanes of a wave (distinct inputs) diverge:
+// measured on MI355X (bench_tools/inv_bench.hip) 734 us per inversion per wave -- one inversion
+// was ~0.75 ms of every latency-bound stage that ends in to-affine.  Here the work is batches of
+// 30 "divsteps" on the low 30 bits of (f, g) with branch-free selects, each batch folded into the
+// full-width values as one 2x2 matrix of int32 entries (|u| + |v| <= 2^30), applied with
+// v_mad_i64_i32 over 13 signed 30-bit limbs.  At most 1101 divsteps are needed for 381-bit inputs
+// ((49 d + 57) / 17), so 37 batches always suffice; a lane whose g reached 0 stops early.
+//   invariant: f = d x (mod p), g = e x (mod p); start f = p, g = x, d = 0, e = 1, delta = 1;
+//   end: g = 0, f = +-1, so x^-1 = +-d.
+struct s30 { int32_t v[13]; };
+constexpr uint32_t SG_M30 = 0x3fffffffu;
+struct sg_tables { int32_t pk[7][13]; };   // 2^j p, j = 0..6, as 13 x 30-bit limbs
+constexpr sg_tables make_sg_tables() {
+  sg_tables t{};
+  for (int j = 0; j < 7; ++j)
+    for (int l = 0; l < 13; ++l) {
+      uint32_t v = 0;
+      for (int b = 0; b < 30; ++b) {
+        const int bit = 30 * l + b - j;                       // bit of p feeding bit 30 l + b of 2^j p
+        if (bit >= 0 && bit < 384 && ((P_LIMBS[bit >> 5] >> (bit & 31)) & 1u)) v |= 1u << b;
+      }
+      t.pk[j][l] = (int32_t)v;
+    }
+  return t;
+}
+constexpr sg_tables SG_T = make_sg_tables();
+
+SSB_INL void s30_from_u32(s30& r, const uint32_t* l) {
+  uint64_t acc = 0;
+  int bits = 0, k = 0;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    if (bits < 30 && k < 12) { acc |= (uint64_t)l[k++] << bits; bits += 32; }
+    r.v[i] = (int32_t)(acc & SG_M30);
+    acc >>= 30; bits -= 30;
+  }
+}
+// a non-negative s30 value < 2^384 -> 12 x 32-bit limbs
+SSB_INL void s30_to_u32(uint32_t* l, const s30& a) {
+  uint64_t acc = 0;
+  int bits = 0, k = 0;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    acc |= (uint64_t)(uint32_t)a.v[i] << bits; bits += 30;
+    if (bits >= 32 && k < 12) { l[k++] = (uint32_t)acc; acc >>= 32; bits -= 32; }
+  }
+}
+// 30 divsteps on the low bits; returns the new delta and the transition matrix (scaled by 2^30)
+SSB_INL int32_t sg_divsteps30(int32_t delta, uint32_t f, uint32_t g, int32_t& u, int32_t& v, int32_t& q, int32_t& r) {
+  int32_t uu = 1, vv = 0, qq = 0, rr = 1;
+#pragma unroll
+  for (int i = 0; i < 30; ++i) {
+    const bool odd = (g & 1u) != 0;
+    const bool sw = odd && delta > 0;
+    // swap:  (f, g) <- (g, (g - f)/2),  (u, v) <- 2(q, r), (q, r) <- (q - u, r - v), delta <- 1 - delta
+    // odd:   g <- (g + f)/2,            (u, v) <- 2(u, v), (q, r) <- (q + u, r + v), delta <- 1 + delta
+    // even:  g <- g/2,                  (u, v) <- 2(u, v),                           delta <- 1 + delta
+    const uint32_t gs = sw ? g - f : (odd ? g + f : g);
+    const int32_t qs = sw ? qq - uu : (odd ? qq + uu : qq);
+    const int32_t rs = sw ? rr - vv : (odd ? rr + vv : rr);
+    const int32_t us = sw ? qq : uu, vs = sw ? rr : vv;
+    f = sw ? g : f;
+    delta = (sw ? -delta : delta) + 1;
+    g = gs >> 1;
+    uu = us * 2; vv = vs * 2; qq = qs; rr = rs;
+  }
+  u = uu; v = vv; q = qq; r = rr;
+  return delta;
+}
+// (f, g) <- (u f + v g, q f + r g) / 2^30  (exact)
+SSB_INL void sg_update_fg(s30& f, s30& g, int32_t u, int32_t v, int32_t q, int32_t r) {
+  int64_t cf = (int64_t)u * f.v[0] + (int64_t)v * g.v[0];
+  int64_t cg = (int64_t)q * f.v[0] + (int64_t)r * g.v[0];
+  cf >>= 30; cg >>= 30;
+#pragma unroll
+  for (int i = 1; i < 13; ++i) {
+    cf += (int64_t)u * f.v[i] + (int64_t)v * g.v[i];
+    cg += (int64_t)q * f.v[i] + (int64_t)r * g.v[i];
+    f.v[i - 1] = (int32_t)((uint32_t)cf & SG_M30);
+    g.v[i - 1] = (int32_t)((uint32_t)cg & SG_M30);
+    cf >>= 30; cg >>= 30;
+  }
+  f.v[12] = (int32_t)cf; g.v[12] = (int32_t)cg;
+}
+// (d, e) <- (u d + v e + md p, q d + r e + me p) / 2^30, md / me in [0, 2^30) chosen so the
+// divisions are exact (P_INV32 = -p^-1 mod 2^32).  |d'| <= max(|d|, |e|) + p.
+SSB_INL void sg_update_de(s30& d, s30& e, int32_t u, int32_t v, int32_t q, int32_t r) {
+  const uint32_t dl = (uint32_t)u * (uint32_t)d.v[0] + (uint32_t)v * (uint32_t)e.v[0];
+  const uint32_t el = (uint32_t)q * (uint32_t)d.v[0] + (uint32_t)r * (uint32_t)e.v[0];
+  const int32_t md = (int32_t)((dl * P_INV32) & SG_M30), me = (int32_t)((el * P_INV32) & SG_M30);
+  int64_t cd = (int64_t)u * d.v[0] + (int64_t)v * e.v[0] + (int64_t)md * SG_T.pk[0][0];
+  int64_t ce = (int64_t)q * d.v[0] + (int64_t)r * e.v[0] + (int64_t)me * SG_T.pk[0][0];
+  cd >>= 30; ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < 13; ++i) {
+    cd += (int64_t)u * d.v[i] + (int64_t)v * e.v[i] + (int64_t)md * SG_T.pk[0][i];
+    ce += (int64_t)q * d.v[i] + (int64_t)r * e.v[i] + (int64_t)me * SG_T.pk[0][i];
+    d.v[i - 1] = (int32_t)((uint32_t)cd & SG_M30);
+    e.v[i - 1] = (int32_t)((uint32_t)ce & SG_M30);
+    cd >>= 30; ce >>= 30;
+  }
+  d.v[12] = (int32_t)cd; e.v[12] = (int32_t)ce;
+}
+// r = a + s * b (s = +-1 or 0), limbs renormalised
+SSB_INL void s30_addmul(s30& r, const s30& a, const int32_t* b, int32_t s) {
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (int64_t)a.v[i] + (int64_t)s * b[i];
+    r.v[i] = (int32_t)((uint32_t)c & SG_M30);
+    c >>= 30;
+  }
+  r.v[12] = (int32_t)(c + (int64_t)a.v[12] + (int64_t)s * b[12]);
+}
+SSB_FN void fp_inv(fp& r, const fp& a) {
+  if (mp_is_zero<12>(a.l)) { r = fp_zero(); return; }      // inv(0) = 0, as blst
+  s30 f, g, d, e;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) { f.v[i] = SG_T.pk[0][i]; d.v[i] = 0; e.v[i] = 0; }
+  e.v[0] = 1;
+  s30_from_u32(g, a.l);
+  int32_t delta = 1;
+  for (int it = 0; it < 37; ++it) {
+    int32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 13; ++i) any |= g.v[i];
+    if (!any) break;
+    int32_t u, v, q, w;
+    delta = sg_divsteps30(delta, (uint32_t)f.v[0], (uint32_t)g.v[0], u, v, q, w);
+    sg_update_de(d, e, u, v, q, w);
+    sg_update_fg(f, g, u, v, q, w);
+  }
+  // x^-1 = d * f (f = +-1); |d| <= 37 p: shift into (0, 128 p) with +64 p, then reduce mod p
+  s30 zero;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) zero.v[i] = 0;
+  if (f.v[12] < 0) s30_addmul(d, zero, d.v, -1);
+  s30_addmul(d, d, SG_T.pk[6], 1);
+#pragma unroll
+  for (int j = 6; j >= 0; --j) {
+    s30 t;
+    s30_addmul(t, d, SG_T.pk[j], -1);
+    if (t.v[12] >= 0) d = t;
+  }
+  fp t;
+  s30_to_u32(t.l, d);
+  mp_mont_mul<12>(r.l, t.l, P_R3, P_LIMBS, P_INV32);        // (aR)^-1 -> a^-1 R
 }
 // returns true iff a is a square; r = a^((p+1)/4) (a root when it is)
 SSB_INL bool fp_sqrt_inl(fp& r, const fp& a) {

@@ -79,18 +79,22 @@ struct ssb_ctx {
   // every slot's.  spec: the speculative combines; tail: verdicts, exact fallback, exact combine.
   hipStream_t spec = nullptr, tail = nullptr;
   // tail streams: slot i uses tails[i % ntails] (tails[0] == tail).  More than one lets the exact
-  // fallbacks of failed batches on different slots run concurrently (SSB_TAILS, default 3; a caller must give the process enough hardware queues -- slots + 5 -- or streams share queues and serialise).
+  // fallbacks of failed batches on different slots run concurrently (SSB_TAILS, default 1: the
+  // hardware queues are worth more as hash streams; a caller must give the process enough hardware
+  // queues -- slots + 2 + tails + hash streams -- or streams share queues and serialise).
   static constexpr int MAX_TAILS = 4;
   hipStream_t tails[MAX_TAILS] = {nullptr, nullptr, nullptr, nullptr};
-  int ntails = 3;
-  // hash streams (SSB_HASH_STREAMS, default 3): with one stream per slot, hash_to_G2 of slot i's
+  int ntails = 1;
+  // hash streams (SSB_HASH_STREAMS, default 6): with one stream per slot, hash_to_G2 of slot i's
   // batch runs on hashs[i % nhash] beside the slot's decode / subgroup / MSM chain instead of in
-  // front of it (the hash depends on the roots only; the Miller loops wait for it).  Three keep
-  // up with 14 slots (5.4 ms of hash per 2.3 ms batch); measured C2 at 20 timed steps: 0 -> 5.85 M,
-  // 3 -> 6.33 M partial sigs/s; 2 fall behind (4.8 M).  Created with the first one-stream slot.
+  // front of it (the hash depends on the roots only; the Miller loops wait for it).  A hash is
+  // 5.4 ms of latency-bound kernels, so a burst of batches queues on this pool: measured C2 at the
+  // driver's 20 timed steps, 14 slots + spec + 1 tail + H hash streams: H = 0 5.85 M, 3 6.56 M,
+  // 5 6.85 M, 6 7.19 M partial sigs/s; H = 7 (23 engine streams) oversubscribes the hardware
+  // queues: 6.0 M.
   static constexpr int MAX_HASH = 8;
   hipStream_t hashs[MAX_HASH] = {};
-  int nhash = 3;
+  int nhash = 6;
   // G1-side streams (SSB_G1_STREAMS, default 0): the per-root G1 sums of slot i's batch run on
   // g1s[i % ng1] beside the slot's G2 MSM instead of after it
   hipStream_t g1s[MAX_HASH] = {nullptr, nullptr, nullptr, nullptr};

@@ -217,6 +217,32 @@ int main() {
       g2_aff a1, a2; jac_to_aff(a1, r1); jac_to_aff(a2, r2);
       uint8_t o1[96], o2[96]; g2_compress(o1, a1); g2_compress(o2, a2);
       printf("%s %s\n", hex(o1, 96).c_str(), hex(o2, 96).c_str());
+    } else if (cmd == "invtest") {  // invtest N -> "<ok> <n>": fp_inv (safegcd) == Fermat, a * a^-1 == 1
+      int n = 0; is >> n;
+      uint64_t z = 0x243F6A8885A308D3ull;
+      int ok = 0, cnt = 0;
+      for (int i = 0; i < n + 6; ++i) {
+        fp c;
+        for (int k = 0; k < 12; ++k) { z = z * 6364136223846793005ull + 1442695040888963407ull; c.l[k] = (uint32_t)(z >> 32); }
+        c.l[11] &= 0x1fffffffu;
+        if (!mp_gt<12>(P_LIMBS, c.l)) c.l[11] &= 0x0fffffffu;
+        if (i >= n) {                  // edge cases: 1, 2, p - 1, p - 2, 2^32, 2^380
+          for (int k = 0; k < 12; ++k) c.l[k] = 0;
+          if (i == n) c.l[0] = 1;
+          if (i == n + 1) c.l[0] = 2;
+          if (i == n + 2 || i == n + 3) { for (int k = 0; k < 12; ++k) c.l[k] = P_LIMBS[k]; c.l[0] -= (uint32_t)(i - n - 1); }
+          if (i == n + 4) c.l[1] = 1;
+          if (i == n + 5) c.l[11] = 1u << 28;
+        }
+        fp a; fp_to_mont(a, c);
+        fp x, y, one;
+        fp_inv(x, a); fp_inv_fermat(y, a); fp_mul(one, x, a);
+        ok += fp_eq(x, y) && fp_eq(one, fp_one());
+        ++cnt;
+      }
+      fp zi; fp_inv(zi, fp_zero());
+      ok += fp_is_zero(zi); ++cnt;
+      printf("%d %d\n", ok, cnt);
     } else if (cmd == "opcount") {  // opcount pk48 sig96 msg32 -> JSON of per-unit op counts
 #ifdef SSB_OPCOUNT
       std::string a, b, c; is >> a >> b >> c;

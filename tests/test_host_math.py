@@ -129,3 +129,10 @@ def test_accumulator_engine_reduction(host_exe):
     """la_fin (sum of scaled +-terms, one Barrett-style step) equals the modular sum, including the
     edge values 0 and p-1 and coefficients up to 300 per term."""
     assert _run(host_exe, ["lafin 20000"]) == ["0"]
+
+
+def test_safegcd_inversion(host_exe):
+    """fp_inv (Bernstein-Yang divsteps, ssb_field.h) against Fermat a^(p-2) on 20,000 pseudo-random
+    elements and the edge cases 1, 2, p-1, p-2, 2^32, 2^380; inv(0) = 0 (blst semantics)."""
+    ok, n = _run(host_exe, ["invtest 20000"])[0].split()
+    assert ok == n and int(n) == 20007
