@@ -47,7 +47,7 @@ MAD_PEAK_ISSUE = 256 * 4 * 16 * 2.4e9  # 16 lanes/clk/SIMD (wave64 mad = 4 cycle
 #   C4  configs[3]: 1,048,576 attestation shares over 8 GPUs -> 131,072 shares (32,768 x 4) per GPU
 #   C5  configs[4]: 1M validators x 13 shares (10-of-13) over 8 GPUs -> 131,072 validators per GPU
 CONFIGS = {
-    "C2": dict(validators=4096, threshold=3, operators=4, roots=64, pipeline=14),
+    "C2": dict(validators=4096, threshold=3, operators=4, roots=64, pipeline=20),
     "C3_3of4": dict(validators=65536, threshold=3, operators=4, roots=64, pipeline=3),
     "C3_5of7": dict(validators=65536, threshold=5, operators=7, roots=64, pipeline=3),
     "C4_per_gpu": dict(validators=32768, threshold=3, operators=4, roots=64, pipeline=4),
@@ -277,20 +277,22 @@ def main():
         args.config = "C4_global" if args.scaling == "strong" else "C2"
     strong = args.scaling == "strong"
     preset = CONFIGS[args.config]
+    explicit_pipeline = args.pipeline is not None
     for k in ("validators", "threshold", "operators", "roots", "pipeline"):
         if getattr(args, k) is None:
             setattr(args, k, preset[k])
-    # Hardware queues: every engine stream needs its own, and past about 22 the firmware time-slices
-    # them (measured C2, 20 steps: 14 slots + spec + 1 tail + 6 hash streams = 22 engine streams
-    # 7.19 M sigs/s; one more hash stream 6.0 M).  With N > 1 the process group adds a stream of
-    # its own, so multi-GPU runs keep one hash stream fewer.
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        os.environ.setdefault("SSB_TAILS", "1")
-        os.environ.setdefault("SSB_HASH_STREAMS", "5")
-    # slot streams + the speculative-combine stream + the tail streams (SSB_TAILS, engine default 1)
-    # + the hash streams (SSB_HASH_STREAMS, engine default 6) + one for torch's own stream
+    # Hardware queues: every ACTIVE engine stream needs its own, and past 20 the firmware
+    # time-slices them.  Measured C2 at the driver's 20 steps, one-stream slots, each batch wholly on
+    # its slot's stream (hash_to_G2, verdicts and combine too): 19 slots 7.18 M sigs/s (the 20th
+    # batch waits for a slot), 20 slots 9.33 M (every batch in flight at once), 21 slots 6.51 M,
+    # 20 slots + 2 hash streams 4.05 M.  With N > 1 the process group's all-gather runs on a stream
+    # of its own, so multi-GPU runs keep one slot fewer.
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not explicit_pipeline and args.pipeline >= 20:
+        args.pipeline = 19
+    # slot streams + the speculative-combine and tail streams (idle with one-stream slots, which run
+    # every stage on the slot's stream) + SSB_HASH_STREAMS (engine default 0) + one for torch
     set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "1") or 1)
-                  + int(os.environ.get("SSB_HASH_STREAMS", "6") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
+                  + int(os.environ.get("SSB_HASH_STREAMS", "0") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
 
     import numpy as np
     import torch
@@ -520,7 +522,8 @@ def main():
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
                        "batches_in_flight": S, "streams_per_slot": args.slot_streams,
                        "tail_streams": int(os.environ.get("SSB_TAILS", "1") or 1),
-                       "hash_streams": int(os.environ.get("SSB_HASH_STREAMS", "6") or 0)},
+                       "hash_streams": int(os.environ.get("SSB_HASH_STREAMS", "0") or 0),
+                       "post": os.environ.get("SSB_POST", "slot")},
             "batch_latency_ms": round(latency_ms, 3),
             "public_keys": ("compressed per batch (ssb_threshold_aggregate_batch_dev)" if args.compressed_pk else
                             "decompressed once at registration (ssb_pk_cache_set + _cached_dev), as lighthouse's "

@@ -86,15 +86,18 @@ typedef struct ssb_ctx ssb_ctx;
 int ssb_create(ssb_ctx** out, int device_ordinal);
 void ssb_destroy(ssb_ctx* ctx);
 const char* ssb_last_error(const ssb_ctx* ctx);
-/* Slots x streams-per-slot limit: the HIP runtime reserves scratch on every hardware queue for the
+/* Slots x streams-per-slot limits: the HIP runtime reserves scratch on every hardware queue for the
  * largest kernel that queue has run, and 8 slots x 3 streams exhausted it on an MI355X
- * (HSA_STATUS_ERROR_OUT_OF_RESOURCES) while 16 one-stream slots run clean. */
-#define SSB_MAX_SLOT_STREAMS 16
-/* SSB_OK if `depth` slots of `streams` streams are a supported configuration (depth 1..16,
- * streams 1 or 3, depth x streams <= SSB_MAX_SLOT_STREAMS), SSB_EINVAL otherwise.  No GPU needed;
- * ssb_set_pipeline_depth / ssb_set_slot_streams refuse what this refuses. */
+ * (HSA_STATUS_ERROR_OUT_OF_RESOURCES: the side streams run the large-scratch kernels) while
+ * one-stream slots run clean up to SSB_MAX_SLOT_STREAMS. */
+#define SSB_MAX_SLOT_STREAMS 24
+#define SSB_MAX_THREE_STREAM_SLOTS 5
+/* SSB_OK if `depth` slots of `streams` streams are a supported configuration (streams 1 or 3,
+ * depth x streams <= SSB_MAX_SLOT_STREAMS, three-stream slots at most SSB_MAX_THREE_STREAM_SLOTS),
+ * SSB_EINVAL otherwise.  No GPU needed; ssb_set_pipeline_depth / ssb_set_slot_streams refuse what
+ * this refuses. */
 int ssb_check_pipeline_config(int depth, int streams);
-/* Number of pipeline slots (1..16, default 1).  Each slot owns its streams and workspace; calls of
+/* Number of pipeline slots (1..24, default 1).  Each slot owns its streams and workspace; calls of
  * ssb_threshold_aggregate_batch_dev go to the slots round robin, so up to `depth` independent
  * batches are in flight and overlap on the device (e.g. the duties of consecutive slots).  Each
  * call's outputs are ready when the caller's `stream` reaches them. */
@@ -114,9 +117,11 @@ int ssb_set_rlc_deterministic(ssb_ctx* ctx, int on);
  * A *_dev call whose `stream` is a slot's main stream runs on THAT slot; any other stream gets the
  * next slot round robin. */
 void* ssb_slot_stream(ssb_ctx* ctx, int slot);
-/* Device-side kernel timing with hipEvents recorded on the engine's stream around each launch.
- * ssb_last_kernel_ms: the last launch of `kernel_name`.  ssb_kernel_timing(ctx, 1) clears and
- * starts accumulating every launch; ssb_kernel_time returns the total and the launch count. */
+/* Device-side kernel timing with hipEvents recorded on the engine's stream around each launch,
+ * only while timing is on (off by default: no events in the production path).
+ * ssb_kernel_timing(ctx, 1) clears and starts accumulating every launch (ssb_kernel_time returns
+ * the total and the launch count); ssb_kernel_timing(ctx, 2) records the last launch of each
+ * stage only (ssb_last_kernel_ms); ssb_kernel_timing(ctx, 0) stops. */
 int ssb_last_kernel_ms(const ssb_ctx* ctx, const char* kernel_name, float* ms);
 int ssb_kernel_timing(ssb_ctx* ctx, int on);
 int ssb_kernel_time(ssb_ctx* ctx, const char* kernel_name, float* total_ms, int* launches);

@@ -123,9 +123,12 @@ __global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict_
   }
   for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
 }
-// Small-integer Lagrange fast path (unit_lagrange_small): every selected share is a verified
+// Small-integer Lagrange fast path (unit_lagrange_small), for t <= FAST_T (larger thresholds take
+// the 255-bit path; the per-lane arrays stay small -- this kernel's private segment sets the
+// scratch the runtime reserves on every slot's hardware queue): every selected share is a verified
 // (hence order-r) point, so sum c_i sig_i with the integer c_i == lambda_i mod r is the reference's
 // combination.  fast[j] = 1 when the job was finished here; the 255-bit path skips those jobs.
+constexpr uint32_t FAST_T = 16;
 __global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                      const uint32_t* __restrict__ sel, const uint64_t* __restrict__ ids,
@@ -136,11 +139,11 @@ __global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
   uint32_t done = 0;
-  if (status[j] == SSB_DVF_OK) {
+  if (status[j] == SSB_DVF_OK && tt[j] <= FAST_T) {
     const uint32_t t = tt[j], b = off[j];
-    uint64_t x[SSB_MAX_T];
-    int64_t c[SSB_MAX_T];
-    const g2_aff* pts[SSB_MAX_T];
+    uint64_t x[FAST_T];
+    int64_t c[FAST_T];
+    const g2_aff* pts[FAST_T];
     for (uint32_t i = 0; i < t; ++i) { x[i] = ids[sel[b + i]]; pts[i] = &sig_aff[sel[b + i]]; }
     if (unit_lagrange_small(c, x, t)) {
       uint8_t o[96];

@@ -56,7 +56,7 @@ struct ssb_slot {
   void* ws = nullptr;
   size_t ws_bytes = 0;
 };
-constexpr int SSB_MAX_SLOTS = 16;
+constexpr int SSB_MAX_SLOTS = 24;
 
 struct ssb_ctx {
   int device = 0;
@@ -70,6 +70,7 @@ struct ssb_ctx {
   struct evpair { hipEvent_t a = nullptr, b = nullptr; bool used = false; };
   std::map<std::string, evpair> timers;               // last launch of each kernel
   bool accumulate = false;                             // ssb_kernel_timing(ctx, 1)
+  bool time_last = false;                              // ssb_kernel_timing(ctx, 2): last launch only
   std::map<std::string, std::vector<evpair>> history;  // every launch while accumulating
   std::vector<evpair> pool;
   g1_aff* negg1_pow = nullptr;                         // device: [2^s](-g1), s = 0..63 (G2 MSM pairs)
@@ -85,16 +86,16 @@ struct ssb_ctx {
   static constexpr int MAX_TAILS = 4;
   hipStream_t tails[MAX_TAILS] = {nullptr, nullptr, nullptr, nullptr};
   int ntails = 1;
-  // hash streams (SSB_HASH_STREAMS, default 6): with one stream per slot, hash_to_G2 of slot i's
+  // hash streams (SSB_HASH_STREAMS, default 0): with one stream per slot, hash_to_G2 of slot i's
   // batch runs on hashs[i % nhash] beside the slot's decode / subgroup / MSM chain instead of in
-  // front of it (the hash depends on the roots only; the Miller loops wait for it).  A hash is
-  // 5.4 ms of latency-bound kernels, so a burst of batches queues on this pool: measured C2 at the
-  // driver's 20 timed steps, 14 slots + spec + 1 tail + H hash streams: H = 0 5.85 M, 3 6.56 M,
-  // 5 6.85 M, 6 7.19 M partial sigs/s; H = 7 (23 engine streams) oversubscribes the hardware
-  // queues: 6.0 M.
+  // front of it (the hash depends on the roots only; the Miller loops wait for it).  They pay off
+  // when the slots are few (14 slots + spec + 1 tail at the driver's 20 steps: H = 0 5.85 M,
+  // 6 7.19 M partial sigs/s); the default configuration instead spends every hardware queue on a
+  // slot (20 slots, hash on the slot's stream: 9.33 M; 20 slots + 2 hash streams oversubscribe the
+  // queues: 4.05 M).
   static constexpr int MAX_HASH = 8;
   hipStream_t hashs[MAX_HASH] = {};
-  int nhash = 6;
+  int nhash = 0;
   // G1-side streams (SSB_G1_STREAMS, default 0): the per-root G1 sums of slot i's batch run on
   // g1s[i % ng1] beside the slot's G2 MSM instead of after it
   hipStream_t g1s[MAX_HASH] = {nullptr, nullptr, nullptr, nullptr};
@@ -198,13 +199,18 @@ void free_slot(ssb_slot& S) {
 
 // hipEvent pair around one kernel launch on the engine's stream (the stream the kernel runs on)
 struct timed {
-  ssb_ctx* ctx; ssb_ctx::evpair p; std::string name; hipStream_t st;
-  timed(ssb_ctx* c, const char* nm, hipStream_t s = nullptr) : ctx(c), name(nm), st(s ? s : c->cur->stream) {
+  ssb_ctx* ctx; ssb_ctx::evpair p; std::string name; hipStream_t st; bool on;
+  // events only while timing is on (ssb_kernel_timing): two event packets per stage and batch are
+  // not free on a queue that already carries a batch's ~40 kernels
+  timed(ssb_ctx* c, const char* nm, hipStream_t s = nullptr)
+      : ctx(c), name(nm), st(s ? s : c->cur->stream), on(c->accumulate || c->time_last) {
+    if (!on) return;
     if (!ctx->pool.empty()) { p = ctx->pool.back(); ctx->pool.pop_back(); }
     else { hipEventCreate(&p.a); hipEventCreate(&p.b); }
     hipEventRecord(p.a, st);
   }
   ~timed() {
+    if (!on) return;
     hipEventRecord(p.b, st);
     p.used = true;
     if (ctx->accumulate) { ctx->history[name].push_back(p); return; }
@@ -286,6 +292,17 @@ bool fallback_per_share() {
 bool fallback_on_tail() {
   const char* e = getenv("SSB_FB_STREAM");
   return !(e && !strcmp(e, "slot"));
+}
+// One-stream slots run their whole batch on the slot's stream (SSB_POST=slot, the default): the
+// verdicts, the exact fallback (no-ops when the batch passed) and ONE combine from the verdicts
+// follow the final exponentiation in order, instead of a speculative combine on the shared spec
+// stream plus the exact path on a shared tail stream.  Every hardware queue then carries one slot
+// (measured C2 at the driver's 20 steps: a shared tail stream finishes the batches one at a time,
+// ~0.7 ms apart, once the pairing chains of all slots end together).  SSB_POST=tail keeps the
+// shared streams (the three-stream latency configuration always does).
+bool post_on_slot(const ssb_slot* s) {
+  static const bool slot = [] { const char* e = getenv("SSB_POST"); return !(e && !strcmp(e, "tail")); }();
+  return s->shared && slot;
 }
 msm_plan plan_msm(size_t n, size_t n_roots) {
   msm_plan p;
@@ -446,7 +463,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   // have the largest private segments, and the runtime reserves scratch per hardware queue for the
   // largest kernel the queue has run (on every slot stream, 12 slots ran out of resources).
   // SSB_FB_STREAM=slot puts them on the slot's own stream (few slots only).
-  const bool fb_tail = fallback_on_tail();
+  const bool fb_tail = fallback_on_tail() && !post_on_slot(ctx->cur);
   hipStream_t fbs = fb_tail ? tail : st;
   if (fb_tail && tail != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
@@ -531,16 +548,17 @@ void ssb_destroy(ssb_ctx* ctx) {
 
 int ssb_check_pipeline_config(int depth, int streams) {
   if (depth < 1 || depth > SSB_MAX_SLOTS || (streams != 1 && streams != 3)) return SSB_EINVAL;
-  // the HIP runtime reserves scratch per hardware queue for the largest kernel each queue ran;
-  // 8 slots x 3 streams ran out (HSA_STATUS_ERROR_OUT_OF_RESOURCES), 16 x 1 runs clean
-  if (depth * streams > SSB_MAX_SLOT_STREAMS) return SSB_EINVAL;
+  // the HIP runtime reserves scratch per hardware queue for the largest kernel each queue ran:
+  // 8 slots x 3 streams ran out (HSA_STATUS_ERROR_OUT_OF_RESOURCES -- the side streams run the
+  // large-scratch kernels); one-stream slots run clean up to SSB_MAX_SLOT_STREAMS
+  if (depth * streams > SSB_MAX_SLOT_STREAMS || (streams == 3 && depth > SSB_MAX_THREE_STREAM_SLOTS)) return SSB_EINVAL;
   return SSB_OK;
 }
 
 int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
   if (!ctx) return SSB_EINVAL;
   if (ssb_check_pipeline_config(depth, ctx->slot_streams) != SSB_OK) {
-    ctx->err = "pipeline depth x streams per slot outside the supported range (depth 1..16, depth x streams <= 16)";
+    ctx->err = "pipeline depth x streams per slot outside the supported range (one-stream slots: depth 1..24; three-stream slots: depth 1..5)";
     return SSB_EINVAL;
   }
   SSB_HIP(hipSetDevice(ctx->device));
@@ -557,7 +575,7 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
 int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
   if (!ctx) return SSB_EINVAL;
   if (ssb_check_pipeline_config(ctx->nslots, streams) != SSB_OK) {
-    ctx->err = "streams per slot must be 1 or 3 and depth x streams <= 16 (lower the depth first)";
+    ctx->err = "streams per slot must be 1 or 3, and three-stream slots at most 5 (lower the depth first)";
     return SSB_EINVAL;
   }
   if (streams == ctx->slot_streams) return SSB_OK;
@@ -599,7 +617,8 @@ int ssb_kernel_timing(ssb_ctx* ctx, int on) {
   for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
   for (auto& kv : ctx->history) for (auto& p : kv.second) ctx->pool.push_back(p);
   ctx->history.clear();
-  ctx->accumulate = on != 0;
+  ctx->accumulate = on == 1;
+  ctx->time_last = on == 2;
   return SSB_OK;
 }
 
@@ -788,7 +807,8 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
                 align_up(4 * n * sizeof(g2_jac)) + align_up(n_jobs * 4);
   if ((rc = ensure_ws(ctx, need))) return rc;
   hipStream_t user = (hipStream_t)stream;
-  hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = slot_tail(ctx);
+  const bool on_slot = post_on_slot(ctx->cur);
+  hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = on_slot ? st : slot_tail(ctx);
   // order the engine's streams after the caller's stream, and the caller's stream after them
   hipEvent_t e_user;
   SSB_HIP(hipEventCreateWithFlags(&e_user, hipEventDisableTiming));
@@ -814,16 +834,19 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
-  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict, spec, tl))) return rc;
-  if (!n) spec();
-  // exact path, only if the RLC batch failed (every kernel is a no-op when w.ok == 1)
-  SSB_HIP(hipStreamWaitEvent(tl, ctx->cur->ev_comb, 0));
+  if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict,
+                       [&] { if (!on_slot) spec(); }, tl))) return rc;
+  if (!n && !on_slot) spec();
+  // exact path: on the shared tail stream only if the RLC batch failed (every kernel a no-op when
+  // w.ok == 1, the speculative combine stands); on the slot's stream always (no speculative pass)
+  const uint32_t* gate = on_slot ? nullptr : (const uint32_t*)w.ok;
+  if (!on_slot) SSB_HIP(hipStreamWaitEvent(tl, ctx->cur->ev_comb, 0));
   st = tl;
-  hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids, (const uint8_t*)verdict, w.flags, (const uint32_t*)w.ok, sel, out_status, out_err);
-  hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)w.ok, fast, out_sig96);
-  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)w.ok, (const uint32_t*)fast, lam);
-  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)w.ok, (const uint32_t*)fast, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)w.ok, (const uint32_t*)fast, out_sig96, 4);
+  { timed tm(ctx, "k_select", st); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids, (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err); }
+  { timed tm(ctx, "k_combine_fast", st); hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, gate, fast, out_sig96); }
+  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, gate, (const uint32_t*)fast, lam);
+  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate, (const uint32_t*)fast, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate, (const uint32_t*)fast, out_sig96, 4);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
   ctx->cur->out_pending = true;

@@ -162,8 +162,10 @@ class Engine:
         self._check(self._lib.ssb_last_kernel_ms(self._h, name.encode(), ctypes.byref(ms)), "ssb_last_kernel_ms")
         return float(ms.value)
 
-    def kernel_timing(self, on: bool):
-        self._check(self._lib.ssb_kernel_timing(self._h, 1 if on else 0), "ssb_kernel_timing")
+    def kernel_timing(self, on, last_only: bool = False):
+        """Start (accumulate every launch, or with last_only the last launch of each stage for
+        last_kernel_ms) or stop the engine's event timing; off by default."""
+        self._check(self._lib.ssb_kernel_timing(self._h, (2 if last_only else 1) if on else 0), "ssb_kernel_timing")
 
     def kernel_time(self, name: str):
         """(total ms, launches) accumulated since kernel_timing(True)."""

@@ -83,6 +83,32 @@ def test_c2_full_batch_matches_c_oracle(engine, rate):
     assert rate == 0 or wl["n_bad"] > 100
 
 
+@pytest.mark.parametrize("rate", [0.0, 0.01], ids=["valid", "invalid_1pct"])
+def test_c2_one_stream_slots_match_c_oracle(engine, rate):
+    """The throughput configuration bench.py runs: one-stream slots, every stage of a batch on its
+    slot's stream (SSB_POST=slot: verdicts, the exact fallback -- group tests when the batch fails --
+    and one combine from the verdicts, no speculative pass), several slots in turn.  Every verdict,
+    status and combined signature == the C oracle on the same bytes."""
+    lib = engine._lib
+    assert lib.ssb_set_slot_streams(engine.handle, 1) == 0, lib.ssb_last_error(engine.handle)
+    assert lib.ssb_set_pipeline_depth(engine.handle, 4) == 0, lib.ssb_last_error(engine.handle)
+    try:
+        V, t, n, R = 4096, 3, 4, 64
+        wl = bench.make_workload(engine, V, t, n, R, rank=2, invalid_rate=rate)
+        runs = [_agg(engine, wl, V, t, n) for _ in range(3)]          # three consecutive slots
+        o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
+        for out, st, err, ver in runs:
+            assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
+            assert (st == o_st).all() and (err == o_err).all()
+            ok = st == 0
+            assert (out[ok] == o_out[ok]).all()
+            _check_against_truth(wl, V, t, n, out, st, err, ver)
+        assert rate == 0 or wl["n_bad"] > 100
+    finally:
+        lib.ssb_set_pipeline_depth(engine.handle, 1)
+        lib.ssb_set_slot_streams(engine.handle, 3)
+
+
 def _verify_cached_dev(engine, cache_pk48, pk_index, sigs96, root_idx, roots, seed=None):
     import torch
     lib = engine._lib
