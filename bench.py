@@ -448,6 +448,13 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
         dbg = bool(os.environ.get("SSB_DEBUG_HOST"))
+        # SSB_DEBUG_GATE: hold every slot's stream until all steps are enqueued (profiling aid: a
+        # kernel trace then shows the device timeline, not the tracer's per-launch host overhead)
+        gate = torch.zeros((1,), dtype=torch.int32, device=dev) if os.environ.get("SSB_DEBUG_GATE") else None
+        if gate is not None:
+            torch.cuda.synchronize(dev)
+            for k in range(S):
+                lib.ssb_debug_hold(ctypes.c_void_p(lib.ssb_slot_stream(eng.handle, k)), ctypes.c_void_p(gate.data_ptr()), 3000000)
         ev = []
         t0 = time.perf_counter()
         host_ms = []
@@ -461,6 +468,8 @@ def main():
                 e1.record(streams[i % S])
                 ev.append((e0, e1))
             host_ms.append((time.perf_counter() - th) * 1e3)
+        if gate is not None:
+            gate.fill_(1)
         torch.cuda.synchronize(dev)
         if dbg:
             print("host ms per submit:", " ".join("%.2f" % x for x in host_ms), file=sys.stderr)

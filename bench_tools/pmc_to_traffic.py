@@ -7,7 +7,7 @@ import json
 import sys
 
 GROUPS = {
-    "k_decode": ["k_decode2"],
+    "k_decode": ["k_decode_sig", "k_pk_gather"],
     "k_subgroup": ["k_subgroup"],
     "k_msm_g2": ["void k_msm_bucket<ssb::fp2>", "void k_msm_window<ssb::fp2>"],
     "k_msm_g1": ["void k_msm_bucket<ssb::fp>", "void k_msm_window_seq<ssb::fp>", "k_msm_horner"],

@@ -117,6 +117,11 @@ int ssb_set_rlc_deterministic(ssb_ctx* ctx, int on);
  * A *_dev call whose `stream` is a slot's main stream runs on THAT slot; any other stream gets the
  * next slot round robin. */
 void* ssb_slot_stream(ssb_ctx* ctx, int slot);
+/* Profiling aid: enqueue on `stream` a one-wave kernel that waits until the device word *flag is
+ * non-zero (or about max_us microseconds have passed), so batches enqueued behind it on several
+ * streams start together -- a kernel-trace of a pipelined run then shows the device timeline
+ * rather than the profiler's per-launch host overhead.  Not used by the product path. */
+int ssb_debug_hold(void* stream, const uint32_t* flag, uint32_t max_us);
 /* Device-side kernel timing with hipEvents recorded on the engine's stream around each launch,
  * only while timing is on (off by default: no events in the production path).
  * ssb_kernel_timing(ctx, 1) clears and starts accumulating every launch (ssb_kernel_time returns

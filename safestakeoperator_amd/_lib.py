@@ -25,6 +25,7 @@ SIGNATURES = {
     "ssb_set_pipeline_depth": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_set_slot_streams": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_slot_stream": (ctypes.c_void_p, [_ctx, ctypes.c_int]),
+    "ssb_debug_hold": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "ssb_set_rlc_deterministic": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_last_kernel_ms": (ctypes.c_int, [_ctx, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float)]),
     "ssb_kernel_timing": (ctypes.c_int, [_ctx, ctypes.c_int]),

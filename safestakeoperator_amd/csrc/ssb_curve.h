@@ -74,9 +74,8 @@ template <class F> SSB_INL void jac_dbl_inl(jac<F>& r, const jac<F>& p) {
 template <class F> SSB_FN void jac_dbl(jac<F>& r, const jac<F>& p) { jac_dbl_inl(r, p); }
 
 // madd-2007-bl: r = p + q, q affine.  Handles infinity and the doubling/opposite cases.
-// (_inl: inlined into the MSM bucket loops; jac_add_aff: out-of-line copy; kNoCall: the rare
-// doubling case inlined too, for the call-free occupancy-2 kernels)
-template <class F, bool kNoCall = false> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+// (_inl: inlined into the MSM bucket loops; jac_add_aff: out-of-line copy)
+template <class F> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   if (q.inf) { r = p; return; }
   if (jac_is_inf(p)) { jac_from_aff(r, q); return; }
   F Z1Z1, U2, S2, H, HH, I, J, rr, V, t;
@@ -86,12 +85,8 @@ template <class F, bool kNoCall = false> SSB_INL void jac_add_aff_inl(jac<F>& r,
   f_sub(H, U2, p.x);
   f_sub(rr, S2, p.y);
   if (f_is_zero(H)) {
-    if (f_is_zero(rr)) {
-      jac<F> d; jac_from_aff(d, q);
-      if (kNoCall) jac_dbl_inl(r, d); else jac_dbl(r, d);
-    } else {
-      jac_set_inf(r);
-    }
+    if (f_is_zero(rr)) { jac<F> d; jac_from_aff(d, q); jac_dbl(r, d); }
+    else jac_set_inf(r);
     return;
   }
   f_dbl(rr, rr);
@@ -247,15 +242,6 @@ template <class F> SSB_FN void jac_mul_x_abs_aff(jac<F>& r, const aff<F>& p) {
   }
   r = acc;
 }
-// no calls on the common path (the occupancy-2 subgroup kernel)
-template <class F> SSB_INL void jac_mul_x_abs_aff_inl(jac<F>& r, const aff<F>& p) {
-  jac<F> acc; jac_from_aff(acc, p);
-  for (int i = 62; i >= 0; --i) {
-    jac_dbl_inl(acc, acc);
-    if ((BLS_X_ABS >> i) & 1ull) jac_add_aff_inl<F, true>(acc, acc, p);
-  }
-  r = acc;
-}
 
 // ---- G2 endomorphism psi = twist^-1 o Frobenius o twist: (conj(x) cx, conj(y) cy) ----
 SSB_INL void g2_psi_aff(g2_aff& r, const g2_aff& p) {
@@ -272,14 +258,42 @@ SSB_INL void g2_psi_jac(g2_jac& r, const g2_jac& p) {
 }
 
 // G2 membership (sig_groupcheck): psi(P) == [x]P  (Scott 2021; == [r]P == O on BLS12-381)
+// Mixed addition for the membership test's [|x|]P chain, ordered so few temporaries are live (the
+// occupancy-2 subgroup kernel spills 54 registers with it, 146 with jac_add_aff_inl).  Returns
+// false on the exceptional case acc == +-P: then [k -+ 1]P = O for the chain's current prefix k,
+// 1 <= k -+ 1 < r, so P cannot have order r -- the answer is "not in G2" without the doubling.
+SSB_INL bool g2_add_aff_sg(g2_jac& r, const g2_jac& p, const g2_aff& q) {
+  if (jac_is_inf(p)) { jac_from_aff(r, q); return true; }
+  fp2 Z1Z1, H, rr, HH, z3, t;
+  fp2_sqr(Z1Z1, p.z);
+  fp2_mul(H, q.x, Z1Z1); fp2_sub(H, H, p.x);                        // U2 - X1
+  fp2_mul(t, q.y, p.z); fp2_mul(t, t, Z1Z1); fp2_sub(rr, t, p.y);   // S2 - Y1
+  if (fp2_is_zero(H)) return false;
+  fp2_dbl(rr, rr);
+  fp2_sqr(HH, H);
+  fp2_add(z3, p.z, H); fp2_sqr(z3, z3); fp2_sub(z3, z3, Z1Z1); fp2_sub(z3, z3, HH);
+  fp2 I, J, V;
+  fp2_dbl(I, HH); fp2_dbl(I, I);
+  fp2_mul(J, H, I);
+  fp2_mul(V, p.x, I);
+  fp2 x3, y3;
+  fp2_sqr(x3, rr); fp2_sub(x3, x3, J); fp2_dbl(t, V); fp2_sub(x3, x3, t);
+  fp2_sub(t, V, x3); fp2_mul(y3, rr, t); fp2_mul(t, p.y, J); fp2_dbl(t, t); fp2_sub(y3, y3, t);
+  r.x = x3; r.y = y3; r.z = z3;
+  return true;
+}
+// call-free membership test (the occupancy-2 subgroup kernel); same answers as g2_in_subgroup
 SSB_INL bool g2_in_subgroup_inl(const g2_aff& p) {
   if (p.inf) return true;
-  g2_jac xp;
-  jac_mul_x_abs_aff_inl(xp, p);
-  jac_neg(xp, xp);  // x < 0
+  g2_jac acc; jac_from_aff(acc, p);
+  for (int i = 62; i >= 0; --i) {
+    jac_dbl_inl(acc, acc);
+    if (((BLS_X_ABS >> i) & 1ull) && !g2_add_aff_sg(acc, acc, p)) return false;
+  }
+  jac_neg(acc, acc);  // x < 0
   g2_aff ps;
   g2_psi_aff(ps, p);
-  return jac_eq_aff(xp, ps);
+  return jac_eq_aff(acc, ps);
 }
 SSB_FN bool g2_in_subgroup(const g2_aff& p) {
   if (p.inf) return true;

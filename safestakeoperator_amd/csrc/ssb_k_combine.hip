@@ -155,6 +155,15 @@ __global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict
   fast[j] = done;
 }
 
+// profiling aid (ssb_debug_hold): one wave polls *flag until it is non-zero or max_polls polls of
+// ~2 us have passed (the exit every run reaches), so work queued behind it on the stream starts
+// together once the host has enqueued everything
+__global__ void k_hold(const uint32_t* flag, uint32_t max_polls) {
+  for (uint32_t i = 0; i < max_polls; ++i) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+    __builtin_amdgcn_s_sleep(127);
+  }
+}
 __global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) b[i] = a[i];

@@ -122,15 +122,15 @@ __global__ void SSB_LB(256) k_order_scatter(uint32_t K, uint32_t K2, const uint3
 }
 
 // ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
+// (block bodies take their block index and LDS explicitly, so one launch can run the G2 and the
+// G1 side's blocks side by side: k_msm_bucket2 / k_msm_window2 below)
 template <class F>
-__global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
-                                                   const uint32_t* __restrict__ start,
-                                                   const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ ent,
-                                                   const uint32_t* __restrict__ flags, const aff<F>* __restrict__ pts,
-                                                   jac<F>* __restrict__ bsum) {
-  __shared__ jac<F> sh[64];
+SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
+                              const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                              const uint32_t* __restrict__ ent, const uint32_t* __restrict__ flags,
+                              const aff<F>* __restrict__ pts, jac<F>* __restrict__ bsum) {
   const int lane = threadIdx.x, J = 1 << lj, j = lane & (J - 1);
-  const uint32_t ob = blockIdx.x * (64u >> lj) + (uint32_t)(lane >> lj);
+  const uint32_t ob = bid * (64u >> lj) + (uint32_t)(lane >> lj);
   const uint32_t key = ob < nb ? order[base + ob] : 0u, b = key - base;
   jac<F> acc;
   jac_set_inf(acc);
@@ -157,6 +157,15 @@ __global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, cons
   }
   if (j == 0 && ob < nb) bsum[b] = acc;
 }
+template <class F>
+__global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
+                                                   const uint32_t* __restrict__ start,
+                                                   const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ ent,
+                                                   const uint32_t* __restrict__ flags, const aff<F>* __restrict__ pts,
+                                                   jac<F>* __restrict__ bsum) {
+  __shared__ jac<F> sh[64];
+  msm_bucket_block<F>(blockIdx.x, sh, nb, base, lj, order, start, cnt, ent, flags, pts, bsum);
+}
 
 // ---- window sums  sum_d d * B_d  (one workgroup per (group, window)) ----
 // G1: out_jac[gw] (Jacobian, for the Horner combine).  G2: the window is affine pair gw of the
@@ -165,22 +174,21 @@ __global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, cons
 // only the windows it flagged -- an exceptional addition, e.g. an empty bucket -- are recomputed
 // here; the others just take lane_sum[w] to the outputs)
 template <class F>
-__global__ void SSB_LB(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
-                                                   aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
-                                                   const g1_aff* __restrict__ negg1_pow, const uint32_t* __restrict__ redo,
-                                                   const jac<F>* __restrict__ lane_sum) {
-  __shared__ jac<F> sh[64];
+SSB_INL void msm_window_block(uint32_t bid, jac<F>* sh, int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
+                              aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
+                              const g1_aff* __restrict__ negg1_pow, const uint32_t* __restrict__ redo,
+                              const jac<F>* __restrict__ lane_sum) {
   const int t = threadIdx.x, B = 1 << c, L = B < 64 ? B : 64, m = B / L;
-  const jac<F>* bk = bsum + (size_t)blockIdx.x * B;
-  if (redo && !redo[blockIdx.x]) {
+  const jac<F>* bk = bsum + (size_t)bid * B;
+  if (redo && !redo[bid]) {
     if (t == 0) {
-      const jac<F> U = lane_sum[blockIdx.x];
-      if (out_jac) out_jac[blockIdx.x] = U;
+      const jac<F> U = lane_sum[bid];
+      if (out_jac) out_jac[bid] = U;
       if (out_q) {
         aff<F> a;
         jac_to_aff(a, U);
-        out_q[blockIdx.x] = a;
-        out_p[blockIdx.x] = negg1_pow[c * blockIdx.x];
+        out_q[bid] = a;
+        out_p[bid] = negg1_pow[c * bid];
       }
     }
     return;
@@ -210,16 +218,24 @@ __global__ void SSB_LB(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, 
     __syncthreads();
   }
   if (t == 0) {
-    if (out_jac) out_jac[blockIdx.x] = U;
+    if (out_jac) out_jac[bid] = U;
     if (out_q) {
       aff<F> a;
       jac_to_aff(a, U);
-      out_q[blockIdx.x] = a;
-      out_p[blockIdx.x] = negg1_pow[c * blockIdx.x];
+      out_q[bid] = a;
+      out_p[bid] = negg1_pow[c * bid];
     }
   }
 }
 
+template <class F>
+__global__ void SSB_LB(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
+                                                   aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
+                                                   const g1_aff* __restrict__ negg1_pow, const uint32_t* __restrict__ redo,
+                                                   const jac<F>* __restrict__ lane_sum) {
+  __shared__ jac<F> sh[64];
+  msm_window_block<F>(blockIdx.x, sh, c, bsum, out_jac, out_q, out_p, negg1_pow, redo, lane_sum);
+}
 
 // ---- window sums and the G1 Horner as LANE-GROUP programs (ssb_lane_progs.h) ----
 // These stages are chains of point additions on a handful of workgroups -- latency, not
@@ -365,9 +381,9 @@ __global__ void __launch_bounds__(NT) k_msm_horner_lane(int ngroups, int c, int 
 // ---- window sums for narrow windows (2^c <= 16 buckets): one lane per (group, window), the
 // sequential running sum  R += B_d, U += R  for d = 2^c - 1 .. 1  (2 (2^c - 1) additions) ----
 template <class F>
-__global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
-                                                       jac<F>* __restrict__ out_jac) {
-  const uint32_t gw = blockIdx.x * blockDim.x + threadIdx.x;
+SSB_INL void msm_window_seq_block(uint32_t bid, uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
+                                  jac<F>* __restrict__ out_jac) {
+  const uint32_t gw = bid * blockDim.x + threadIdx.x;
   if (gw >= ngw) return;
   const int B = 1 << c;
   const jac<F>* bk = bsum + (size_t)gw * B;
@@ -380,6 +396,37 @@ __global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* _
     jac_add(U, U, R);
   }
   out_jac[gw] = U;
+}
+template <class F>
+__global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
+                                                       jac<F>* __restrict__ out_jac) {
+  msm_window_seq_block<F>(blockIdx.x, ngw, c, bsum, out_jac);
+}
+
+// ---- the G2 and G1 sides in one launch (one-stream slots: the two MSMs overlap on the device
+// instead of running back to back on the slot's stream; blocks [0, nblk2) are G2's) ----
+struct msm_bucket_args {
+  uint32_t nb, base; int lj; const uint32_t* order; const uint32_t* start; const uint32_t* cnt; const uint32_t* ent;
+};
+__global__ void SSB_LB(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
+                                         const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig,
+                                         const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1) {
+  __shared__ g2_jac sh[64];
+  if (blockIdx.x < nblk2)
+    msm_bucket_block<fp2>(blockIdx.x, sh, a2.nb, a2.base, a2.lj, a2.order, a2.start, a2.cnt, a2.ent, flags, sig, b2);
+  else
+    msm_bucket_block<fp>(blockIdx.x - nblk2, reinterpret_cast<g1_jac*>(sh), a1.nb, a1.base, a1.lj, a1.order, a1.start,
+                         a1.cnt, a1.ent, flags, pk, b1);
+}
+__global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* __restrict__ b2, g2_aff* __restrict__ pair_q,
+                                         g1_aff* __restrict__ pair_p, const g1_aff* __restrict__ negg1_pow,
+                                         uint32_t ngw1, int c1, const g1_jac* __restrict__ b1, g1_jac* __restrict__ w1) {
+  __shared__ g2_jac sh[64];
+  if (blockIdx.x < nblk2)
+    msm_window_block<fp2>(blockIdx.x, sh, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
+                          (const g2_jac*)nullptr);
+  else
+    msm_window_seq_block<fp>(blockIdx.x - nblk2, ngw1, c1, b1, w1);
 }
 
 // ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
@@ -509,6 +556,23 @@ void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
     hipLaunchKernelGGL(k_msm_horner, dim3((c.ngroups + 63) / 64), dim3(64), 0, st, (int)c.ngroups, (int)c.c, (int)c.W,
                        (const g1_jac*)wsum, root_sum, (const uint32_t*)nullptr);
   }
+}
+
+bool msm_fused_ok(const msm_cfg& c1) { return msm_lane_mask() == 0 && c1.c <= 4; }
+
+void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int lj1, const uint32_t* order,
+              const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
+              const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
+              g1_jac* wsum1, g1_aff* root_sum) {
+  const uint32_t nb2 = c2.ngroups * c2.W << c2.c, nb1 = c1.ngroups * c1.W << c1.c;
+  const uint32_t nblk2 = (nb2 + (64u >> lj2) - 1) / (64u >> lj2), nblk1 = (nb1 + (64u >> lj1) - 1) / (64u >> lj1);
+  const msm_bucket_args a2{nb2, c2.base, lj2, order, start, cnt, ent}, a1{nb1, c1.base, lj1, order, start, cnt, ent};
+  hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1), dim3(64), 0, st, nblk2, a2, a1, flags, sig, pk, b2, b1);
+  const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W;
+  hipLaunchKernelGGL(k_msm_window2, dim3(nw2 + (nw1 + 63) / 64), dim3(64), 0, st, nw2, (int)c2.c, (const g2_jac*)b2,
+                     pair_q, pair_p, negg1_pow, nw1, (int)c1.c, (const g1_jac*)b1, wsum1);
+  hipLaunchKernelGGL(k_msm_horner, dim3((c1.ngroups + 63) / 64), dim3(64), 0, st, (int)c1.ngroups, (int)c1.c, (int)c1.W,
+                     (const g1_jac*)wsum1, root_sum, (const uint32_t*)nullptr);
 }
 
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc) {

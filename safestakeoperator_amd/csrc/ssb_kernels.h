@@ -95,6 +95,7 @@ __global__ void k_combine_fast(int n_jobs, const uint32_t* __restrict__ off, con
                                const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ fast,
                                uint8_t* __restrict__ out96);
 __global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b);
+__global__ void k_hold(const uint32_t* flag, uint32_t max_polls);
 
 }  // namespace k
 
@@ -126,6 +127,14 @@ void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
             const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum, uint32_t* redo);
 // gflags[s] = DEC_IN_GROUP when signature s (decodable, not infinity) passes psi(P) == [x]P
 // subgroup checks: single-lane (default) or SSB_SUBGROUP=lane (8-lane groups + exact redo of exceptional shares)
+// msm_g2 + msm_g1 as three launches on one stream (bucket sums of both sides, window sums of both
+// sides, the G1 Horner): the two MSMs overlap on the device.  Only without lane-group window
+// kernels and with G1 windows of <= 16 buckets (msm_fused_ok).
+bool msm_fused_ok(const msm_cfg& c1);
+void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int lj1, const uint32_t* order,
+              const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
+              const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
+              g1_jac* wsum1, g1_aff* root_sum);
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups
 // (ssb_k_bisect.hip); no-op when *ok.  Workspace: cnt/start/cursor n_roots words, perm n words,

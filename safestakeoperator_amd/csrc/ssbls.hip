@@ -432,7 +432,16 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));
   // G1 sums (per root) on side[1] -- then the caller's speculative combine, off the critical path --
-  // G2 MSM on the main stream
+  // G2 MSM on the main stream.  One-stream slots: both MSMs in the same three launches (they
+  // overlap on the device instead of running back to back on the slot's stream).
+  const bool fused = ctx->cur->shared && s1 == st && P.g1_msm && launch::msm_fused_ok(P.g1);
+  if (fused) {
+    if (n) on_decoded();
+    timed t(ctx, "k_msm_g2");
+    launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
+                     w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p);
+    SSB_HIP(hipEventRecord(ctx->cur->ev_r1, st));
+  } else {
   SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
     timed t(ctx, "k_msm_g1", s1);
@@ -445,6 +454,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
   if (n) on_decoded();
   { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w2, w.redo2); }
+  }
   SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
   { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f); }
@@ -593,6 +603,12 @@ int ssb_set_rlc_deterministic(ssb_ctx* ctx, int on) {
   if (!ctx) return SSB_EINVAL;
   ctx->rlc_deterministic = on != 0;
   return SSB_OK;
+}
+
+int ssb_debug_hold(void* stream, const uint32_t* flag, uint32_t max_us) {
+  if (!flag) return SSB_EINVAL;
+  hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, max_us / 2 + 1);
+  return hipGetLastError() == hipSuccess ? SSB_OK : SSB_EHIP;
 }
 
 void* ssb_slot_stream(ssb_ctx* ctx, int slot) {
