@@ -1,0 +1,199 @@
+// ssb_blocks.h -- workgroup bodies of the kernels that the one-stream slot path also runs FUSED:
+// a fused launch gives each body its own range of blocks (block index and LDS passed explicitly),
+// so independent stages of a batch -- the G2 and G1 MSMs, the hash_to_G2 stages beside the
+// per-share kernels -- overlap on the device although the slot has a single stream
+// (ssb_k_fused.hip).  The stand-alone kernels (ssb_k_msm.hip, ssb_k_hash.hip) wrap the same bodies.
+#pragma once
+#include "ssb_kernels.h"
+#include "ssb_lane_ops.h"
+
+namespace ssb {
+namespace k {
+
+// ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
+// (block bodies take their block index and LDS explicitly, so one launch can run the G2 and the
+// G1 side's blocks side by side: k_msm_bucket2 / k_msm_window2 below)
+template <class F>
+SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
+                              const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                              const uint32_t* __restrict__ ent, const uint32_t* __restrict__ flags,
+                              const aff<F>* __restrict__ pts, jac<F>* __restrict__ bsum) {
+  const int lane = threadIdx.x, J = 1 << lj, j = lane & (J - 1);
+  const uint32_t ob = bid * (64u >> lj) + (uint32_t)(lane >> lj);
+  const uint32_t key = ob < nb ? order[base + ob] : 0u, b = key - base;
+  jac<F> acc;
+  jac_set_inf(acc);
+  if (ob < nb) {
+    const uint32_t s = start[key], e = s + cnt[key];
+    // software pipelined: the next entry's point is in flight while this one is added
+    uint32_t x = s + j, fl = 0;
+    aff<F> q;
+    if (x < e) { const uint32_t i = ent[x]; fl = flags[i]; q = pts[i]; }
+    while (x < e) {
+      const uint32_t xn = x + J;
+      uint32_t fn = 0;
+      aff<F> qn;
+      if (xn < e) { const uint32_t i = ent[xn]; fn = flags[i]; qn = pts[i]; }
+      if (fl & FLAG_CANDIDATE) jac_add_aff_inl(acc, acc, q);
+      q = qn; fl = fn; x = xn;
+    }
+  }
+  for (int h = J >> 1; h >= 1; h >>= 1) {
+    sh[lane] = acc;
+    __syncthreads();
+    if (j < h) { jac<F> o = sh[lane + h]; jac_add(acc, acc, o); }
+    __syncthreads();
+  }
+  if (j == 0 && ob < nb) bsum[b] = acc;
+}
+// ---- window sums  sum_d d * B_d  (one workgroup per (group, window)) ----
+// G1: out_jac[gw] (Jacobian, for the Horner combine).  G2: the window is affine pair gw of the
+// multi-pairing: out_q[gw] = W_gw, out_p[gw] = [2^(c gw)](-g1) from negg1_pow.
+// (redo != nullptr: the lane-group kernel below already summed the window into lane_sum, and
+// only the windows it flagged -- an exceptional addition, e.g. an empty bucket -- are recomputed
+// here; the others just take lane_sum[w] to the outputs)
+template <class F>
+SSB_INL void msm_window_block(uint32_t bid, jac<F>* sh, int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
+                              aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
+                              const g1_aff* __restrict__ negg1_pow, const uint32_t* __restrict__ redo,
+                              const jac<F>* __restrict__ lane_sum) {
+  const int t = threadIdx.x, B = 1 << c, L = B < 64 ? B : 64, m = B / L;
+  const jac<F>* bk = bsum + (size_t)bid * B;
+  if (redo && !redo[bid]) {
+    if (t == 0) {
+      const jac<F> U = lane_sum[bid];
+      if (out_jac) out_jac[bid] = U;
+      if (out_q) {
+        aff<F> a;
+        jac_to_aff(a, U);
+        out_q[bid] = a;
+        out_p[bid] = negg1_pow[c * bid];
+      }
+    }
+    return;
+  }
+  jac<F> S, U;
+  jac_set_inf(S);
+  jac_set_inf(U);
+  if (t < L) {
+    for (int e = m - 1; e >= 1; --e) { jac<F> o = bk[t * m + e]; jac_add(S, S, o); jac_add(U, U, S); }
+    jac<F> o = bk[t * m]; jac_add(S, S, o);
+  }
+  // suffix scan over the lanes: S_t <- sum_{t' >= t} S_t'
+  for (int off = 1; off < L; off <<= 1) {
+    sh[t] = S;
+    __syncthreads();
+    if (t + off < L) { jac<F> o = sh[t + off]; jac_add(S, S, o); }
+    __syncthreads();
+  }
+  if (t >= 1 && t < L) {
+    for (int q = m; q > 1; q >>= 1) jac_dbl(S, S);
+    jac_add(U, U, S);
+  }
+  for (int h = L >> 1; h >= 1; h >>= 1) {
+    sh[t] = U;
+    __syncthreads();
+    if (t < h) { jac<F> o = sh[t + h]; jac_add(U, U, o); }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (out_jac) out_jac[bid] = U;
+    if (out_q) {
+      aff<F> a;
+      jac_to_aff(a, U);
+      out_q[bid] = a;
+      out_p[bid] = negg1_pow[c * bid];
+    }
+  }
+}
+
+// ---- window sums for narrow windows (2^c <= 16 buckets): one lane per (group, window), the
+// sequential running sum  R += B_d, U += R  for d = 2^c - 1 .. 1  (2 (2^c - 1) additions) ----
+template <class F>
+SSB_INL void msm_window_seq_block(uint32_t bid, uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
+                                  jac<F>* __restrict__ out_jac) {
+  const uint32_t gw = bid * blockDim.x + threadIdx.x;
+  if (gw >= ngw) return;
+  const int B = 1 << c;
+  const jac<F>* bk = bsum + (size_t)gw * B;
+  jac<F> R, U;
+  jac_set_inf(R);
+  jac_set_inf(U);
+  for (int d = B - 1; d >= 1; --d) {
+    jac<F> o = bk[d];
+    jac_add(R, R, o);
+    jac_add(U, U, R);
+  }
+  out_jac[gw] = U;
+}
+// 2: simplified SWU, one lane per (root, u_j, candidate x1 / x2): both square roots run at once
+// instead of one after the other; then the 3-isogeny.  Lanes 4i+2j+c, 16 roots per block.
+struct h2c_cand { fp2 x, y; uint32_t ok; };
+constexpr size_t H2C_MAP_LDS = 64 * sizeof(h2c_cand);
+SSB_INL void h2c_map_block(uint32_t bid, h2c_cand* cs, int n, const fp2* __restrict__ u, g2_aff* __restrict__ q) {
+  const int t = bid * 64 + threadIdx.x;
+  const int i = t >> 2, j = (t >> 1) & 1, c = t & 1;
+  const bool act = i < n;
+  fp2 uu = act ? u[2 * i + j] : fp2_one();
+  fp2 x, y;
+  const bool ok = sswu_candidate(x, y, uu, c);
+  cs[threadIdx.x].x = x; cs[threadIdx.x].y = y; cs[threadIdx.x].ok = ok ? 1u : 0u;
+  __syncthreads();
+  if (act && c == 0) {
+    const h2c_cand o = cs[threadIdx.x + 1];
+    g2_aff r;
+    sswu_finish(r, uu, ok ? x : o.x, ok ? y : o.y);
+    q[2 * i + j] = r;
+  }
+}
+
+// 3: q0 + q1 and the cofactor clearing as lane-group programs (8 lanes per root, 8 roots per block)
+constexpr int H2C_S0 = lane::G2_ADD_SCRATCH > lane::G2_MADD_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G2_MADD_SCRATCH;
+constexpr int H2C_GS = H2C_S0 + 6 + 4 + 6 + 30;
+constexpr size_t H2C_CLEAR_LDS = (lane::LP_NCODE_CONST + 8 * H2C_GS) * sizeof(fp) + 8 * sizeof(uint32_t);
+SSB_INL void h2c_clear_block(uint32_t bid, fp* lds, int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
+                             uint32_t* __restrict__ exc_out) {
+  using namespace ssb::lane;
+  uint32_t* flg = (uint32_t*)(lds + LP_NCODE_CONST + 8 * H2C_GS);
+  const int gi = threadIdx.x / 8, role = threadIdx.x % 8;
+  const int i = bid * 8 + gi;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + gi * H2C_GS, 0, 0, 0, (lu32*)&flg[gi], role};
+  lp_init_consts(g);
+  const bool act = i < n;
+  const int P = H2C_S0, Q1 = P + 6, R = Q1 + 4, W = R + 6;
+  {
+    g2_aff a0, a1;
+    if (act) { a0 = q[2 * i]; a1 = q[2 * i + 1]; } else { a0.x = fp2_zero(); a0.y = fp2_one(); a1 = a0; a1.x = fp2_one(); }
+    if (role < 4) { g.s[P + role] = ((const fp*)&a0)[role]; g.s[Q1 + role] = ((const fp*)&a1)[role]; }
+    if (role == 4) g.s[P + 4] = fp_one();
+    if (role == 5) g.s[P + 5] = fp_zero();
+  }
+  __syncthreads();
+  uint32_t exc = 0;
+  g2_madd(g, P, Q1, P, exc);      // q0 + q1 (q0, q1 never infinity: iso3_map of the SWU points)
+  g2_clear_cofactor(g, P, R, W, exc);
+  if (act) {
+    if (role < 6) ((fp*)&hj[i])[role] = g.s[R + role];
+    if (role == 0) exc_out[i] = exc;
+  }
+}
+
+// 4: affine output; a root whose lane-group stage met an exceptional addition (or every root,
+// with exact_all: the test knob SSB_H2C_EXACT) is redone exactly, hj[i] serving as its temporary
+SSB_INL void h2c_affine_block(uint32_t bid, int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
+                              const uint32_t* __restrict__ exc, int exact_all, g2_aff* __restrict__ out) {
+  const int i = bid * 64 + threadIdx.x;
+  if (i >= n) return;
+  g2_jac s;
+  if (exc[i] || exact_all) {
+    h2c_clear_exact(s, q[2 * i], q[2 * i + 1], &hj[i]);
+  } else {
+    s = hj[i];
+  }
+  g2_aff a;
+  jac_to_aff(a, s);
+  out[i] = a;
+}
+
+}  // namespace k
+}  // namespace ssb

@@ -2,7 +2,7 @@
 // Launched from ssbls.hip (declarations in ssb_kernels.h); one TU per kernel family so the
 // library compiles in parallel.
 #include "ssb_kernels.h"
-#include "ssb_lane_ops.h"
+#include "ssb_blocks.h"
 
 namespace ssb {
 namespace k {
@@ -23,73 +23,23 @@ __global__ void SSB_LB(64) k_h2c_u(int n, const uint8_t* __restrict__ roots, con
   u[2 * i + 1] = u1;
 }
 
-// 2: simplified SWU, one lane per (root, u_j, candidate x1 / x2): both square roots run at once
-// instead of one after the other; then the 3-isogeny.  Lanes 4i+2j+c, 16 roots per block.
+// 2: simplified SWU (h2c_map_block, ssb_blocks.h), 16 roots per block
 __global__ void SSB_LB(64) k_h2c_map(int n, const fp2* __restrict__ u, g2_aff* __restrict__ q) {
-  struct cand_t { fp2 x, y; uint32_t ok; };
-  __shared__ cand_t cs[64];
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i = t >> 2, j = (t >> 1) & 1, c = t & 1;
-  const bool act = i < n;
-  fp2 uu = act ? u[2 * i + j] : fp2_one();
-  fp2 x, y;
-  const bool ok = sswu_candidate(x, y, uu, c);
-  cs[threadIdx.x].x = x; cs[threadIdx.x].y = y; cs[threadIdx.x].ok = ok ? 1u : 0u;
-  __syncthreads();
-  if (act && c == 0) {
-    const cand_t o = cs[threadIdx.x + 1];
-    g2_aff r;
-    sswu_finish(r, uu, ok ? x : o.x, ok ? y : o.y);
-    q[2 * i + j] = r;
-  }
+  __shared__ h2c_cand cs[64];
+  h2c_map_block(blockIdx.x, cs, n, u, q);
 }
 
-// 3: q0 + q1 and the cofactor clearing as lane-group programs (8 lanes per root)
-constexpr int H2C_S0 = lane::G2_ADD_SCRATCH > lane::G2_MADD_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G2_MADD_SCRATCH;
-constexpr int H2C_GS = H2C_S0 + 6 + 4 + 6 + 30;
+// 3: q0 + q1 and the cofactor clearing (h2c_clear_block, ssb_blocks.h)
 __global__ void SSB_LB(64) k_h2c_clear(int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
                                                   uint32_t* __restrict__ exc_out) {
-  using namespace ssb::lane;
-  __shared__ fp lds[LP_NCODE_CONST + 8 * H2C_GS];
-  __shared__ uint32_t flg[8];
-  const int gi = threadIdx.x / 8, role = threadIdx.x % 8;
-  const int i = blockIdx.x * 8 + gi;
-  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + gi * H2C_GS, 0, 0, 0, (lu32*)&flg[gi], role};
-  lp_init_consts(g);
-  const bool act = i < n;
-  const int P = H2C_S0, Q1 = P + 6, R = Q1 + 4, W = R + 6;
-  {
-    g2_aff a0, a1;
-    if (act) { a0 = q[2 * i]; a1 = q[2 * i + 1]; } else { a0.x = fp2_zero(); a0.y = fp2_one(); a1 = a0; a1.x = fp2_one(); }
-    if (role < 4) { g.s[P + role] = ((const fp*)&a0)[role]; g.s[Q1 + role] = ((const fp*)&a1)[role]; }
-    if (role == 4) g.s[P + 4] = fp_one();
-    if (role == 5) g.s[P + 5] = fp_zero();
-  }
-  __syncthreads();
-  uint32_t exc = 0;
-  g2_madd(g, P, Q1, P, exc);      // q0 + q1 (q0, q1 never infinity: iso3_map of the SWU points)
-  g2_clear_cofactor(g, P, R, W, exc);
-  if (act) {
-    if (role < 6) ((fp*)&hj[i])[role] = g.s[R + role];
-    if (role == 0) exc_out[i] = exc;
-  }
+  __shared__ fp lds[H2C_CLEAR_LDS / sizeof(fp) + 1];
+  h2c_clear_block(blockIdx.x, lds, n, q, hj, exc_out);
 }
 
-// 4: affine output; a root whose lane-group stage met an exceptional addition (or every root,
-// with exact_all: the test knob SSB_H2C_EXACT) is redone exactly, hj[i] serving as its temporary
+// 4: affine output (h2c_affine_block, ssb_blocks.h)
 __global__ void SSB_LB(64) k_h2c_affine(int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
                                                    const uint32_t* __restrict__ exc, int exact_all, g2_aff* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2_jac s;
-  if (exc[i] || exact_all) {
-    h2c_clear_exact(s, q[2 * i], q[2 * i + 1], &hj[i]);
-  } else {
-    s = hj[i];
-  }
-  g2_aff a;
-  jac_to_aff(a, s);
-  out[i] = a;
+  h2c_affine_block(blockIdx.x, n, q, hj, exc, exact_all, out);
 }
 
 __global__ void SSB_LB(64) k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
@@ -136,20 +86,31 @@ __global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* _
 
 namespace launch {
 size_t hash_ws_bytes(size_t n) { return n * (2 * sizeof(fp2) + 2 * sizeof(g2_aff) + sizeof(g2_jac) + 4) + 1024; }
-void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws, const uint8_t* lens) {
-  if (n <= 0) return;
+h2c_ws carve_h2c(void* ws, size_t n) {
   char* p = (char*)ws;
   auto take = [&](size_t b) { char* r = p; p += (b + 255) & ~(size_t)255; return r; };
-  fp2* u = (fp2*)take(2 * n * sizeof(fp2));
-  g2_aff* q = (g2_aff*)take(2 * n * sizeof(g2_aff));
-  g2_jac* hj = (g2_jac*)take(n * sizeof(g2_jac));
-  uint32_t* exc = (uint32_t*)take(n * 4);
-  hipLaunchKernelGGL(k::k_h2c_u, dim3((n + 63) / 64), dim3(64), 0, st, n, roots, lens, dst, u);
-  hipLaunchKernelGGL(k::k_h2c_map, dim3((4 * n + 63) / 64), dim3(64), 0, st, n, u, q);
-  hipLaunchKernelGGL(k::k_h2c_clear, dim3((n + 7) / 8), dim3(64), 0, st, n, q, hj, exc);
+  h2c_ws w;
+  w.u = (fp2*)take(2 * n * sizeof(fp2));
+  w.q = (g2_aff*)take(2 * n * sizeof(g2_aff));
+  w.hj = (g2_jac*)take(n * sizeof(g2_jac));
+  w.exc = (uint32_t*)take(n * 4);
+  return w;
+}
+int h2c_exact_all() {
   const char* ex = getenv("SSB_H2C_EXACT");
-  const int exact_all = (ex && atoi(ex) != 0) ? 1 : 0;
-  hipLaunchKernelGGL(k::k_h2c_affine, dim3((n + 63) / 64), dim3(64), 0, st, n, q, hj, exc, exact_all, out);
+  return (ex && atoi(ex) != 0) ? 1 : 0;
+}
+void h2c_u(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, const h2c_ws& w, const uint8_t* lens) {
+  hipLaunchKernelGGL(k::k_h2c_u, dim3((n + 63) / 64), dim3(64), 0, st, n, roots, lens, dst, w.u);
+}
+void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws, const uint8_t* lens) {
+  if (n <= 0) return;
+  const h2c_ws w = carve_h2c(ws, (size_t)n);
+  h2c_u(st, n, roots, dst, w, lens);
+  hipLaunchKernelGGL(k::k_h2c_map, dim3((4 * n + 63) / 64), dim3(64), 0, st, n, (const fp2*)w.u, w.q);
+  hipLaunchKernelGGL(k::k_h2c_clear, dim3((n + 7) / 8), dim3(64), 0, st, n, (const g2_aff*)w.q, w.hj, w.exc);
+  hipLaunchKernelGGL(k::k_h2c_affine, dim3((n + 63) / 64), dim3(64), 0, st, n, (const g2_aff*)w.q, w.hj,
+                     (const uint32_t*)w.exc, h2c_exact_all(), out);
 }
 }  // namespace launch
 }  // namespace ssb

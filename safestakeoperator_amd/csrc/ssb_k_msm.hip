@@ -19,6 +19,7 @@
 // Every addition is the complete Jacobian formula of ssb_curve.h (infinity, doubling and opposite
 // inputs handled), so the sums are exact for any inputs.
 #include "ssb_kernels.h"
+#include "ssb_blocks.h"
 #include "ssb_lane_ops.h"
 
 namespace ssb {
@@ -121,42 +122,7 @@ __global__ void SSB_LB(256) k_order_scatter(uint32_t K, uint32_t K2, const uint3
   order[atomicAdd(&bins[(key >= K2 ? 256u : 0u) + 255u - c], 1u)] = key;
 }
 
-// ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
-// (block bodies take their block index and LDS explicitly, so one launch can run the G2 and the
-// G1 side's blocks side by side: k_msm_bucket2 / k_msm_window2 below)
-template <class F>
-SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
-                              const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
-                              const uint32_t* __restrict__ ent, const uint32_t* __restrict__ flags,
-                              const aff<F>* __restrict__ pts, jac<F>* __restrict__ bsum) {
-  const int lane = threadIdx.x, J = 1 << lj, j = lane & (J - 1);
-  const uint32_t ob = bid * (64u >> lj) + (uint32_t)(lane >> lj);
-  const uint32_t key = ob < nb ? order[base + ob] : 0u, b = key - base;
-  jac<F> acc;
-  jac_set_inf(acc);
-  if (ob < nb) {
-    const uint32_t s = start[key], e = s + cnt[key];
-    // software pipelined: the next entry's point is in flight while this one is added
-    uint32_t x = s + j, fl = 0;
-    aff<F> q;
-    if (x < e) { const uint32_t i = ent[x]; fl = flags[i]; q = pts[i]; }
-    while (x < e) {
-      const uint32_t xn = x + J;
-      uint32_t fn = 0;
-      aff<F> qn;
-      if (xn < e) { const uint32_t i = ent[xn]; fn = flags[i]; qn = pts[i]; }
-      if (fl & FLAG_CANDIDATE) jac_add_aff_inl(acc, acc, q);
-      q = qn; fl = fn; x = xn;
-    }
-  }
-  for (int h = J >> 1; h >= 1; h >>= 1) {
-    sh[lane] = acc;
-    __syncthreads();
-    if (j < h) { jac<F> o = sh[lane + h]; jac_add(acc, acc, o); }
-    __syncthreads();
-  }
-  if (j == 0 && ob < nb) bsum[b] = acc;
-}
+// ---- bucket sums (msm_bucket_block, ssb_blocks.h) ----
 template <class F>
 __global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
                                                    const uint32_t* __restrict__ start,
@@ -167,67 +133,7 @@ __global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, cons
   msm_bucket_block<F>(blockIdx.x, sh, nb, base, lj, order, start, cnt, ent, flags, pts, bsum);
 }
 
-// ---- window sums  sum_d d * B_d  (one workgroup per (group, window)) ----
-// G1: out_jac[gw] (Jacobian, for the Horner combine).  G2: the window is affine pair gw of the
-// multi-pairing: out_q[gw] = W_gw, out_p[gw] = [2^(c gw)](-g1) from negg1_pow.
-// (redo != nullptr: the lane-group kernel below already summed the window into lane_sum, and
-// only the windows it flagged -- an exceptional addition, e.g. an empty bucket -- are recomputed
-// here; the others just take lane_sum[w] to the outputs)
-template <class F>
-SSB_INL void msm_window_block(uint32_t bid, jac<F>* sh, int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
-                              aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
-                              const g1_aff* __restrict__ negg1_pow, const uint32_t* __restrict__ redo,
-                              const jac<F>* __restrict__ lane_sum) {
-  const int t = threadIdx.x, B = 1 << c, L = B < 64 ? B : 64, m = B / L;
-  const jac<F>* bk = bsum + (size_t)bid * B;
-  if (redo && !redo[bid]) {
-    if (t == 0) {
-      const jac<F> U = lane_sum[bid];
-      if (out_jac) out_jac[bid] = U;
-      if (out_q) {
-        aff<F> a;
-        jac_to_aff(a, U);
-        out_q[bid] = a;
-        out_p[bid] = negg1_pow[c * bid];
-      }
-    }
-    return;
-  }
-  jac<F> S, U;
-  jac_set_inf(S);
-  jac_set_inf(U);
-  if (t < L) {
-    for (int e = m - 1; e >= 1; --e) { jac<F> o = bk[t * m + e]; jac_add(S, S, o); jac_add(U, U, S); }
-    jac<F> o = bk[t * m]; jac_add(S, S, o);
-  }
-  // suffix scan over the lanes: S_t <- sum_{t' >= t} S_t'
-  for (int off = 1; off < L; off <<= 1) {
-    sh[t] = S;
-    __syncthreads();
-    if (t + off < L) { jac<F> o = sh[t + off]; jac_add(S, S, o); }
-    __syncthreads();
-  }
-  if (t >= 1 && t < L) {
-    for (int q = m; q > 1; q >>= 1) jac_dbl(S, S);
-    jac_add(U, U, S);
-  }
-  for (int h = L >> 1; h >= 1; h >>= 1) {
-    sh[t] = U;
-    __syncthreads();
-    if (t < h) { jac<F> o = sh[t + h]; jac_add(U, U, o); }
-    __syncthreads();
-  }
-  if (t == 0) {
-    if (out_jac) out_jac[bid] = U;
-    if (out_q) {
-      aff<F> a;
-      jac_to_aff(a, U);
-      out_q[bid] = a;
-      out_p[bid] = negg1_pow[c * bid];
-    }
-  }
-}
-
+// ---- window sums (msm_window_block, ssb_blocks.h) ----
 template <class F>
 __global__ void SSB_LB(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ out_jac,
                                                    aff<F>* __restrict__ out_q, g1_aff* __restrict__ out_p,
@@ -378,25 +284,7 @@ __global__ void __launch_bounds__(NT) k_msm_horner_lane(int ngroups, int c, int 
   }
 }
 
-// ---- window sums for narrow windows (2^c <= 16 buckets): one lane per (group, window), the
-// sequential running sum  R += B_d, U += R  for d = 2^c - 1 .. 1  (2 (2^c - 1) additions) ----
-template <class F>
-SSB_INL void msm_window_seq_block(uint32_t bid, uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
-                                  jac<F>* __restrict__ out_jac) {
-  const uint32_t gw = bid * blockDim.x + threadIdx.x;
-  if (gw >= ngw) return;
-  const int B = 1 << c;
-  const jac<F>* bk = bsum + (size_t)gw * B;
-  jac<F> R, U;
-  jac_set_inf(R);
-  jac_set_inf(U);
-  for (int d = B - 1; d >= 1; --d) {
-    jac<F> o = bk[d];
-    jac_add(R, R, o);
-    jac_add(U, U, R);
-  }
-  out_jac[gw] = U;
-}
+// ---- narrow-window sums (msm_window_seq_block, ssb_blocks.h) ----
 template <class F>
 __global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
                                                        jac<F>* __restrict__ out_jac) {
@@ -408,25 +296,41 @@ __global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* _
 struct msm_bucket_args {
   uint32_t nb, base; int lj; const uint32_t* order; const uint32_t* start; const uint32_t* cnt; const uint32_t* ent;
 };
-__global__ void SSB_LB(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
+// hash_to_G2 stages riding along (nblk of their own; 0 = none): the SWU map beside the subgroup
+// checks, the cofactor clearing beside the bucket sums, the affine output beside the window sums
+struct h2c_fuse { int n; const fp2* u; g2_aff* q; g2_jac* hj; uint32_t* exc; int exact_all; g2_aff* out; };
+constexpr size_t BUCKET2_LDS = 64 * sizeof(g2_jac) > H2C_CLEAR_LDS ? 64 * sizeof(g2_jac) : H2C_CLEAR_LDS;
+__global__ void SSB_LB(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, uint32_t nblk1, msm_bucket_args a1,
                                          const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig,
-                                         const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1) {
-  __shared__ g2_jac sh[64];
-  if (blockIdx.x < nblk2)
-    msm_bucket_block<fp2>(blockIdx.x, sh, a2.nb, a2.base, a2.lj, a2.order, a2.start, a2.cnt, a2.ent, flags, sig, b2);
-  else
-    msm_bucket_block<fp>(blockIdx.x - nblk2, reinterpret_cast<g1_jac*>(sh), a1.nb, a1.base, a1.lj, a1.order, a1.start,
-                         a1.cnt, a1.ent, flags, pk, b1);
+                                         const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1,
+                                         h2c_fuse h) {
+  __shared__ __attribute__((aligned(16))) char lds[BUCKET2_LDS];
+  uint32_t bid = blockIdx.x;
+  if (bid < nblk2) {
+    msm_bucket_block<fp2>(bid, (g2_jac*)lds, a2.nb, a2.base, a2.lj, a2.order, a2.start, a2.cnt, a2.ent, flags, sig, b2);
+    return;
+  }
+  bid -= nblk2;
+  if (bid < nblk1) {
+    msm_bucket_block<fp>(bid, (g1_jac*)lds, a1.nb, a1.base, a1.lj, a1.order, a1.start, a1.cnt, a1.ent, flags, pk, b1);
+    return;
+  }
+  h2c_clear_block(bid - nblk1, (fp*)lds, h.n, h.q, h.hj, h.exc);
 }
 __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* __restrict__ b2, g2_aff* __restrict__ pair_q,
                                          g1_aff* __restrict__ pair_p, const g1_aff* __restrict__ negg1_pow,
-                                         uint32_t ngw1, int c1, const g1_jac* __restrict__ b1, g1_jac* __restrict__ w1) {
+                                         uint32_t nblk1, uint32_t ngw1, int c1, const g1_jac* __restrict__ b1,
+                                         g1_jac* __restrict__ w1, h2c_fuse h) {
   __shared__ g2_jac sh[64];
-  if (blockIdx.x < nblk2)
-    msm_window_block<fp2>(blockIdx.x, sh, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
+  uint32_t bid = blockIdx.x;
+  if (bid < nblk2) {
+    msm_window_block<fp2>(bid, sh, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
                           (const g2_jac*)nullptr);
-  else
-    msm_window_seq_block<fp>(blockIdx.x - nblk2, ngw1, c1, b1, w1);
+    return;
+  }
+  bid -= nblk2;
+  if (bid < nblk1) { msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1); return; }
+  h2c_affine_block(bid - nblk1, h.n, h.q, h.hj, h.exc, h.exact_all, h.out);
 }
 
 // ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
@@ -474,6 +378,17 @@ __global__ void SSB_LB2(64) k_subgroup_fix(int n, const uint32_t* __restrict__ s
                                           const uint32_t* __restrict__ exc, uint32_t* __restrict__ gflags) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n || !exc[s]) return;
+  const uint32_t sf = sflags[s];
+  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+}
+
+// subgroup checks (blocks [0, nbs)) with the hash's SWU map riding along (the remaining blocks)
+__global__ void SSB_LB2(64) k_subgroup_map(int n, uint32_t nbs, const uint32_t* __restrict__ sflags,
+                                           const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags, h2c_fuse h) {
+  __shared__ h2c_cand cs[64];
+  if (blockIdx.x >= nbs) { h2c_map_block(blockIdx.x - nbs, cs, h.n, h.u, h.q); return; }
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
   const uint32_t sf = sflags[s];
   gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
 }
@@ -560,19 +475,34 @@ void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
 
 bool msm_fused_ok(const msm_cfg& c1) { return msm_lane_mask() == 0 && c1.c <= 4; }
 
+h2c_fuse fuse_of(const h2c_ws* hw, int n_roots, g2_aff* out) {
+  h2c_fuse h{0, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+  if (hw && n_roots > 0) h = h2c_fuse{n_roots, hw->u, hw->q, hw->hj, hw->exc, h2c_exact_all(), out};
+  return h;
+}
+
 void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int lj1, const uint32_t* order,
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
-              g1_jac* wsum1, g1_aff* root_sum) {
+              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw, int n_roots, g2_aff* H) {
+  const h2c_fuse h = fuse_of(hw, n_roots, H);
   const uint32_t nb2 = c2.ngroups * c2.W << c2.c, nb1 = c1.ngroups * c1.W << c1.c;
   const uint32_t nblk2 = (nb2 + (64u >> lj2) - 1) / (64u >> lj2), nblk1 = (nb1 + (64u >> lj1) - 1) / (64u >> lj1);
+  const uint32_t nbc = h.n ? (uint32_t)(h.n + 7) / 8 : 0u, nba = h.n ? (uint32_t)(h.n + 63) / 64 : 0u;
   const msm_bucket_args a2{nb2, c2.base, lj2, order, start, cnt, ent}, a1{nb1, c1.base, lj1, order, start, cnt, ent};
-  hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1), dim3(64), 0, st, nblk2, a2, a1, flags, sig, pk, b2, b1);
-  const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W;
-  hipLaunchKernelGGL(k_msm_window2, dim3(nw2 + (nw1 + 63) / 64), dim3(64), 0, st, nw2, (int)c2.c, (const g2_jac*)b2,
-                     pair_q, pair_p, negg1_pow, nw1, (int)c1.c, (const g1_jac*)b1, wsum1);
+  hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1 + nbc), dim3(64), 0, st, nblk2, a2, nblk1, a1, flags, sig, pk, b2, b1, h);
+  const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W, nbw1 = (nw1 + 63) / 64;
+  hipLaunchKernelGGL(k_msm_window2, dim3(nw2 + nbw1 + nba), dim3(64), 0, st, nw2, (int)c2.c, (const g2_jac*)b2,
+                     pair_q, pair_p, negg1_pow, nbw1, nw1, (int)c1.c, (const g1_jac*)b1, wsum1, h);
   hipLaunchKernelGGL(k_msm_horner, dim3((c1.ngroups + 63) / 64), dim3(64), 0, st, (int)c1.ngroups, (int)c1.c, (int)c1.W,
                      (const g1_jac*)wsum1, root_sum, (const uint32_t*)nullptr);
+}
+
+void subgroup_map(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, const h2c_ws* hw,
+                  int n_roots) {
+  const h2c_fuse h = fuse_of(hw, n_roots, nullptr);
+  const uint32_t nbs = (uint32_t)(n + 63) / 64, nbm = h.n ? (uint32_t)(4 * h.n + 63) / 64 : 0u;
+  if (nbs + nbm) hipLaunchKernelGGL(k_subgroup_map, dim3(nbs + nbm), dim3(64), 0, st, n, nbs, sflags, sig, gflags, h);
 }
 
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc) {

@@ -108,6 +108,11 @@ namespace launch {
 void lane_subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // staged hash_to_G2 of n roots into out (ssb_k_hash.hip); ws: hash_ws_bytes(n) device bytes
 size_t hash_ws_bytes(size_t n);
+// the staged hash's workspace (u, the SWU points q, the cleared Jacobian points hj, exc flags)
+struct h2c_ws { fp2* u; g2_aff* q; g2_jac* hj; uint32_t* exc; };
+h2c_ws carve_h2c(void* ws, size_t n);
+int h2c_exact_all();
+void h2c_u(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, const h2c_ws& w, const uint8_t* lens = nullptr);
 // (lens: per-message lengths <= 32, or nullptr for 32-byte roots)
 void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst, g2_aff* out, void* ws,
                 const uint8_t* lens = nullptr);
@@ -129,12 +134,17 @@ void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, con
 // subgroup checks: single-lane (default) or SSB_SUBGROUP=lane (8-lane groups + exact redo of exceptional shares)
 // msm_g2 + msm_g1 as three launches on one stream (bucket sums of both sides, window sums of both
 // sides, the G1 Horner): the two MSMs overlap on the device.  Only without lane-group window
-// kernels and with G1 windows of <= 16 buckets (msm_fused_ok).
+// kernels and with G1 windows of <= 16 buckets (msm_fused_ok).  With hw (the staged hash's
+// workspace, after h2c_u and subgroup_map's SWU map), the cofactor clearing rides along the
+// bucket sums and the affine output H[0..n_roots) along the window sums.
 bool msm_fused_ok(const msm_cfg& c1);
 void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int lj1, const uint32_t* order,
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
-              g1_jac* wsum1, g1_aff* root_sum);
+              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw = nullptr, int n_roots = 0, g2_aff* H = nullptr);
+// the subgroup checks with (hw != nullptr) the hash's SWU map of n_roots roots in the same launch
+void subgroup_map(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, const h2c_ws* hw,
+                  int n_roots);
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups
 // (ssb_k_bisect.hip); no-op when *ok.  Workspace: cnt/start/cursor n_roots words, perm n words,

@@ -395,14 +395,26 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   if (int rc = draw_rlc_key(ctx, rlc_seed, key)) return rc;
   hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
   if (ctx->cur->shared && ctx->nhash > 0) sh = ctx->hashs[(int)(ctx->cur - ctx->sl) % ctx->nhash];
-  // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
-  SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
-  SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
-  if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
-  SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
   hipStream_t s1 = ctx->cur->side[1];
   if (ctx->cur->shared && ctx->ng1 > 0) s1 = ctx->g1s[(int)(ctx->cur - ctx->sl) % ctx->ng1];
   const msm_plan& P = w.plan;
+  // One-stream slots: the G2 and G1 MSMs share launches (msm_both), and the hash_to_G2 stages ride
+  // along the batch's own kernels -- the SWU map beside the subgroup checks, the cofactor clearing
+  // beside the bucket sums, the affine output beside the window sums -- instead of standing in
+  // front of the decode on the slot's stream (their few latency-bound waves fill no device).
+  const bool fused = ctx->cur->shared && s1 == st && P.g1_msm && launch::msm_fused_ok(P.g1);
+  const char* sgp = getenv("SSB_SUBGROUP");
+  const bool fuse_hash = fused && sh == st && n && n_roots && !(sgp && sgp[0] == 'l');
+  const launch::h2c_ws hw = launch::carve_h2c(w.hws, n_roots);
+  // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
+  SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
+  SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
+  if (fuse_hash) {
+    launch::h2c_u(st, (int)n_roots, d_roots, dst, hw);
+  } else {
+    if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
+    SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
+  }
   if (n) {
     timed t(ctx, "k_decode");
     if (d_pk_index) {
@@ -426,7 +438,8 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, key, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent, w.order); }
   if (n) {
-    { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags, w.gexc); }
+    if (fuse_hash) { timed t(ctx, "k_subgroup"); launch::subgroup_map(st, (int)n, w.sflags, w.sig_aff, w.gflags, &hw, (int)n_roots); }
+    else { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags, w.gexc); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, d_share_root,
                        (uint32_t)n_roots, w.flags);
   }
@@ -434,13 +447,14 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   // G1 sums (per root) on side[1] -- then the caller's speculative combine, off the critical path --
   // G2 MSM on the main stream.  One-stream slots: both MSMs in the same three launches (they
   // overlap on the device instead of running back to back on the slot's stream).
-  const bool fused = ctx->cur->shared && s1 == st && P.g1_msm && launch::msm_fused_ok(P.g1);
   if (fused) {
     if (n) on_decoded();
     timed t(ctx, "k_msm_g2");
     launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
-                     w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p);
+                     w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p, fuse_hash ? &hw : nullptr,
+                     (int)n_roots, w.H);
     SSB_HIP(hipEventRecord(ctx->cur->ev_r1, st));
+    if (fuse_hash) SSB_HIP(hipEventRecord(ctx->cur->ev_hash, st));
   } else {
   SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
