@@ -19,7 +19,8 @@ CSRC = os.path.join(HERE, "csrc")
 VARIANT = os.environ.get("SSB_VARIANT", "")
 LIB = os.path.join(HERE, "libssbls%s.so" % ("_" + VARIANT if VARIANT else ""))
 SOURCES = ["ssbls.hip", "ssb_k_lane.hip", "ssb_k_verify.hip", "ssb_k_pair.hip", "ssb_k_hash.hip",
-           "ssb_k_combine.hip", "ssb_k_msm.hip", "ssb_k_bisect.hip", "ssb_k_wire.hip", "ssb_k_dkg.hip"]
+           "ssb_k_combine.hip", "ssb_k_msm.hip", "ssb_k_bisect.hip", "ssb_k_wire.hip", "ssb_k_dkg.hip",
+           "ssb_k_fused.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SSB_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]

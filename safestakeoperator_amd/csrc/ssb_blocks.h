@@ -10,6 +10,35 @@
 namespace ssb {
 namespace k {
 
+SSB_INL bool share_decodable(uint32_t sf, uint32_t pf) {
+  return (sf & DEC_OK) && !(sf & DEC_INF) && (pf & DEC_OK) && !(pf & DEC_INF);
+}
+
+template <bool SCATTER>
+SSB_INL void msm_entries(int i, uint64_t k, uint32_t g, const msm_cfg& c, uint32_t* __restrict__ cnt,
+                         uint32_t* __restrict__ ent) {
+  const uint64_t mask = (1ull << c.c) - 1ull;
+  for (uint32_t w = 0; w < c.W; ++w) {
+    const uint32_t d = (uint32_t)((k >> (c.c * w)) & mask);
+    if (!d) continue;
+    const uint32_t key = c.base + ((g * c.W + w) << c.c) + d;
+    if (SCATTER) ent[atomicAdd(&cnt[key], 1u)] = (uint32_t)i;
+    else atomicAdd(&cnt[key], 1u);
+  }
+}
+
+// one share's entries of both MSMs (the count pass, or with SCATTER the scatter pass of the sort);
+// a share whose root index is out of range has none (it cannot enter the batch)
+template <bool SCATTER>
+SSB_INL void msm_sort_lane(int i, const rlc_key& key, const uint32_t* __restrict__ share_root, const msm_cfg& c2,
+                           const msm_cfg& c1, uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
+  const uint32_t g = share_root[i];
+  if (g >= c1.ngroups) return;
+  const uint64_t k = rlc_scalar_odd(key, (uint64_t)i);
+  msm_entries<SCATTER>(i, k, 0u, c2, cnt, ent);
+  msm_entries<SCATTER>(i, k, g, c1, cnt, ent);
+}
+
 // ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
 // (block bodies take their block index and LDS explicitly, so one launch can run the G2 and the
 // G1 side's blocks side by side: k_msm_bucket2 / k_msm_window2 below)

@@ -1,0 +1,140 @@
+// ssb_k_fused.hip -- kernels (gfx950) of the one-stream slot path that carry independent stages of
+// a batch in one launch (ssb_blocks.h): the counting sort of the MSM entries rides along the
+// decode and the subgroup checks instead of standing between them as ten small launches.
+// Launched from ssbls.hip (declarations in ssb_kernels.h).
+#include "ssb_kernels.h"
+#include "ssb_blocks.h"
+
+namespace ssb {
+namespace k {
+
+// blocks [0, nz): zero the sort's counts (and the order bins); then one lane per root: the hash's
+// expand_message_xmd + the two field elements (k_h2c_u)
+__global__ void SSB_LB(64) k_prep_fused(uint32_t nz, uint32_t K, uint32_t* __restrict__ cnt, int n_roots,
+                                        const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
+  if (blockIdx.x < nz) {
+    for (uint32_t x = blockIdx.x * 64 * 16 + threadIdx.x; x < (blockIdx.x + 1) * 64 * 16 && x < K; x += 64) cnt[x] = 0u;
+    return;
+  }
+  const int i = (blockIdx.x - nz) * 64 + threadIdx.x;
+  if (i >= n_roots) return;
+  uint8_t m[32];
+  for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
+  fp2 u0, u1;
+  h2c_field(u0, u1, m, dst.b, dst.len, 32);
+  u[2 * i] = u0;
+  u[2 * i + 1] = u1;
+}
+
+// blocks [0, nbd): signature decode; [nbd, 2 nbd): public keys (gathered from the cache, or
+// decoded); [2 nbd, 3 nbd): the sort's count pass
+template <bool CACHED>
+__global__ void SSB_LB2(64) k_decode_count(int n, uint32_t nbd, const uint8_t* __restrict__ sig96,
+                                           const uint8_t* __restrict__ pk48, const uint32_t* __restrict__ pk_index,
+                                           uint32_t n_cache, const g1_aff* __restrict__ cache_aff,
+                                           const uint32_t* __restrict__ cache_flags, g2_aff* __restrict__ sig_aff,
+                                           g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ sflags,
+                                           uint32_t* __restrict__ pflags, rlc_key key, const uint32_t* __restrict__ share_root,
+                                           msm_cfg c2, msm_cfg c1, uint32_t* __restrict__ cnt) {
+  const uint32_t part = blockIdx.x / nbd;
+  const int s = (blockIdx.x - part * nbd) * 64 + threadIdx.x;
+  if (s >= n) return;
+  if (part == 0) {
+    uint8_t b[96];
+    for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
+    g2_aff sig;
+    sflags[s] = unit_decode_sig(sig, b);
+    sig_aff[s] = sig;
+  } else if (part == 1) {
+    if (CACHED) {
+      const uint32_t i = pk_index[s];
+      if (i < n_cache) { pk_aff[s] = cache_aff[i]; pflags[s] = cache_flags[i]; }
+      else pflags[s] = 0u;   // out-of-range index: the share cannot verify
+    } else {
+      uint8_t b[48];
+      for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
+      g1_aff pk;
+      pflags[s] = unit_decode_pk(pk, b);
+      pk_aff[s] = pk;
+    }
+  } else {
+    msm_sort_lane<false>(s, key, share_root, c2, c1, cnt, (uint32_t*)nullptr);
+  }
+}
+
+// One workgroup: start[] = cur[] = exclusive scan of cnt[0..K), then the bucket order (within each
+// MSM's key range, by count, largest first -- the k_order_* kernels' order)
+constexpr int SS_T = 1024;
+__global__ void __launch_bounds__(SS_T) k_sort_scan(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
+                                                    uint32_t* __restrict__ order) {
+  __shared__ uint32_t sh[SS_T];
+  __shared__ uint32_t bins[512];
+  const int t = threadIdx.x;
+  const uint32_t per = (K + SS_T - 1) / SS_T, k0 = t * per, k1 = k0 + per < K ? k0 + per : K;
+  if (t < 512) bins[t] = 0u;
+  uint32_t sum = 0;
+  for (uint32_t k = k0; k < k1; ++k) sum += cnt[k];
+  sh[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < SS_T; off <<= 1) {
+    const uint32_t o = t >= off ? sh[t - off] : 0u;
+    __syncthreads();
+    sh[t] += o;
+    __syncthreads();
+  }
+  uint32_t run = sh[t] - sum;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t c = cnt[k];
+    start[k] = run; cur[k] = run; run += c;
+    atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of the 512 bins (threads 0..511), then scatter the keys
+  const uint32_t v = t < 512 ? bins[t] : 0u;
+  sh[t] = v;
+  __syncthreads();
+  for (int off = 1; off < 512; off <<= 1) {
+    const uint32_t o = (t < 512 && t >= off) ? sh[t - off] : 0u;
+    __syncthreads();
+    if (t < 512) sh[t] += o;
+    __syncthreads();
+  }
+  if (t < 512) bins[t] = sh[t] - v;
+  __syncthreads();
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t c = cnt[k];
+    order[atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u)] = k;
+  }
+}
+
+}  // namespace k
+
+namespace launch {
+using namespace ssb::k;
+
+void prep_fused(hipStream_t st, const fused_sort& fs, int n_roots, const uint8_t* roots, const dst_arg& dst, const h2c_ws& hw) {
+  const uint32_t nz = (fs.K + 64 * 16 - 1) / (64 * 16), nu = (uint32_t)(n_roots + 63) / 64;
+  hipLaunchKernelGGL(k_prep_fused, dim3(nz + nu), dim3(64), 0, st, nz, fs.K, fs.cnt, n_roots, roots, dst, hw.u);
+}
+
+void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
+                  uint32_t n_cache, const g1_aff* cache_aff, const uint32_t* cache_flags, g2_aff* sig_aff, g1_aff* pk_aff,
+                  uint32_t* sflags, uint32_t* pflags, const fused_sort& fs) {
+  if (n <= 0) return;
+  const uint32_t nbd = (uint32_t)(n + 63) / 64;
+  if (pk_index)
+    hipLaunchKernelGGL(k_decode_count<true>, dim3(3 * nbd), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
+                       cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt);
+  else
+    hipLaunchKernelGGL(k_decode_count<false>, dim3(3 * nbd), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
+                       cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt);
+}
+
+void sort_scan(hipStream_t st, const fused_sort& fs) {
+  hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(SS_T), 0, st, fs.K, fs.c1.base, (const uint32_t*)fs.cnt, fs.start, fs.cur,
+                     fs.order);
+}
+
+}  // namespace launch
+}  // namespace ssb

@@ -25,23 +25,6 @@
 namespace ssb {
 namespace k {
 
-SSB_INL bool share_decodable(uint32_t sf, uint32_t pf) {
-  return (sf & DEC_OK) && !(sf & DEC_INF) && (pf & DEC_OK) && !(pf & DEC_INF);
-}
-
-template <bool SCATTER>
-SSB_INL void msm_entries(int i, uint64_t k, uint32_t g, const msm_cfg& c, uint32_t* __restrict__ cnt,
-                         uint32_t* __restrict__ ent) {
-  const uint64_t mask = (1ull << c.c) - 1ull;
-  for (uint32_t w = 0; w < c.W; ++w) {
-    const uint32_t d = (uint32_t)((k >> (c.c * w)) & mask);
-    if (!d) continue;
-    const uint32_t key = c.base + ((g * c.W + w) << c.c) + d;
-    if (SCATTER) ent[atomicAdd(&cnt[key], 1u)] = (uint32_t)i;
-    else atomicAdd(&cnt[key], 1u);
-  }
-}
-
 // cnt[key] += 1 per (share, window) entry (SCATTER: ent[cursor[key]++] = share)
 template <bool SCATTER>
 __global__ void SSB_LB(256) k_msm_sort(int n, rlc_key key, const uint32_t* __restrict__ sflags,
@@ -50,11 +33,7 @@ __global__ void SSB_LB(256) k_msm_sort(int n, rlc_key key, const uint32_t* __res
                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !share_decodable(sflags[i], pflags[i])) return;
-  const uint32_t g = share_root[i];
-  if (g >= c1.ngroups) return;  // out-of-range root index: the share cannot enter the batch
-  const uint64_t k = rlc_scalar_odd(key, (uint64_t)i);
-  msm_entries<SCATTER>(i, k, 0u, c2, cnt, ent);
-  msm_entries<SCATTER>(i, k, g, c1, cnt, ent);
+  msm_sort_lane<SCATTER>(i, key, share_root, c2, c1, cnt, ent);
 }
 // ---- exclusive scan of the bucket counts: 1024 per block, block totals, offsets ----
 constexpr int SCAN_T = 256, SCAN_PER = 4, SCAN_BLOCK = SCAN_T * SCAN_PER;
@@ -382,15 +361,32 @@ __global__ void SSB_LB2(64) k_subgroup_fix(int n, const uint32_t* __restrict__ s
   gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
 }
 
-// subgroup checks (blocks [0, nbs)) with the hash's SWU map riding along (the remaining blocks)
+// subgroup checks (blocks [0, nbs)) with the hash's SWU map riding along (the next nbm blocks)
+// and, for the fused sort (sc.ent != nullptr), the counting sort's scatter (the remaining blocks);
+// a subgroup lane also writes the share's combined flags (k_flags) when sc.flags is given
+struct sort_scatter { int n; rlc_key key; const uint32_t* share_root; msm_cfg c2, c1; uint32_t* cur; uint32_t* ent;
+                      const uint32_t* pflags; uint32_t n_roots; uint32_t* flags; };
 __global__ void SSB_LB2(64) k_subgroup_map(int n, uint32_t nbs, const uint32_t* __restrict__ sflags,
-                                           const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags, h2c_fuse h) {
+                                           const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags, h2c_fuse h,
+                                           uint32_t nbm, sort_scatter sc) {
   __shared__ h2c_cand cs[64];
-  if (blockIdx.x >= nbs) { h2c_map_block(blockIdx.x - nbs, cs, h.n, h.u, h.q); return; }
+  if (blockIdx.x >= nbs) {
+    const uint32_t b = blockIdx.x - nbs;
+    if (b < nbm) { h2c_map_block(b, cs, h.n, h.u, h.q); return; }
+    const int i = (b - nbm) * 64 + threadIdx.x;
+    if (i < sc.n) msm_sort_lane<true>(i, sc.key, sc.share_root, sc.c2, sc.c1, sc.cur, sc.ent);
+    return;
+  }
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const uint32_t sf = sflags[s];
-  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+  const uint32_t gf = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+  gflags[s] = gf;
+  if (sc.flags) {
+    uint32_t f = combine_flags(sf, sc.pflags[s], gf);
+    if (sc.share_root[s] >= sc.n_roots) f &= ~FLAG_CANDIDATE;
+    sc.flags[s] = f;
+  }
 }
 
 }  // namespace k
@@ -499,10 +495,17 @@ void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int
 }
 
 void subgroup_map(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, const h2c_ws* hw,
-                  int n_roots) {
+                  int n_roots, const fused_sort* fs) {
   const h2c_fuse h = fuse_of(hw, n_roots, nullptr);
   const uint32_t nbs = (uint32_t)(n + 63) / 64, nbm = h.n ? (uint32_t)(4 * h.n + 63) / 64 : 0u;
-  if (nbs + nbm) hipLaunchKernelGGL(k_subgroup_map, dim3(nbs + nbm), dim3(64), 0, st, n, nbs, sflags, sig, gflags, h);
+  sort_scatter sc{0, rlc_key{}, nullptr, msm_cfg{}, msm_cfg{}, nullptr, nullptr, nullptr, 0u, nullptr};
+  uint32_t nsc = 0;
+  if (fs) {
+    sc = sort_scatter{n, fs->key, fs->share_root, fs->c2, fs->c1, fs->cur, fs->ent, fs->pflags, fs->n_roots, fs->flags};
+    nsc = (uint32_t)(n + 63) / 64;
+  }
+  if (nbs + nbm + nsc)
+    hipLaunchKernelGGL(k_subgroup_map, dim3(nbs + nbm + nsc), dim3(64), 0, st, n, nbs, sflags, sig, gflags, h, nbm, sc);
 }
 
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc) {

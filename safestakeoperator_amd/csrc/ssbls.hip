@@ -406,16 +406,26 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   const char* sgp = getenv("SSB_SUBGROUP");
   const bool fuse_hash = fused && sh == st && n && n_roots && !(sgp && sgp[0] == 'l');
   const launch::h2c_ws hw = launch::carve_h2c(w.hws, n_roots);
+  // ... and the MSM entries' counting sort rides along the decode and the subgroup checks
+  const bool fuse_sort = fuse_hash && P.K <= launch::FUSED_SORT_KMAX;
+  const launch::fused_sort fs{key, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.ent, w.order,
+                              w.pflags, (uint32_t)n_roots, w.flags};
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
   SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
   SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
-  if (fuse_hash) {
+  if (fuse_sort) {
+    launch::prep_fused(st, fs, (int)n_roots, d_roots, dst, hw);
+  } else if (fuse_hash) {
     launch::h2c_u(st, (int)n_roots, d_roots, dst, hw);
   } else {
     if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
     SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
   }
-  if (n) {
+  if (fuse_sort) {
+    timed t(ctx, "k_decode");
+    launch::decode_count(st, (int)n, d_sig, d_pk, d_pk_index, (uint32_t)ctx->pkc_n, (const g1_aff*)ctx->pkc_aff,
+                         (const uint32_t*)ctx->pkc_flags, w.sig_aff, w.pk_aff, w.sflags, w.pflags, fs);
+  } else if (n) {
     timed t(ctx, "k_decode");
     if (d_pk_index) {
       hipLaunchKernelGGL(k_decode_sig, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, w.sig_aff, w.sflags);
@@ -436,12 +446,18 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     hipLaunchKernelGGL(k_root_scan, dim3(1), dim3(64), 0, s1, (int)n_roots, w.rcnt, w.rstart, w.rcur);
     if (n) hipLaunchKernelGGL(k_root_scatter, dim3(nblk(n, 256)), dim3(256), 0, s1, (int)n, (int)n_roots, d_share_root, w.rcur, w.perm);
   }
+  if (fuse_sort) {
+    { timed t(ctx, "k_msm_sort"); launch::sort_scan(st, fs); }
+    timed t(ctx, "k_subgroup");
+    launch::subgroup_map(st, (int)n, w.sflags, w.sig_aff, w.gflags, &hw, (int)n_roots, &fs);   // + flags, scatter
+  } else {
   { timed t(ctx, "k_msm_sort"); launch::msm_sort(st, (int)n, key, w.sflags, w.pflags, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.sbsum, w.ent, w.order); }
   if (n) {
     if (fuse_hash) { timed t(ctx, "k_subgroup"); launch::subgroup_map(st, (int)n, w.sflags, w.sig_aff, w.gflags, &hw, (int)n_roots); }
     else { timed t(ctx, "k_subgroup"); launch::subgroup(st, (int)n, w.sflags, w.sig_aff, w.gflags, w.gexc); }
     hipLaunchKernelGGL(k_flags, dim3(nblk(n, 256)), dim3(256), 0, st, (int)n, w.sflags, w.pflags, w.gflags, d_share_root,
                        (uint32_t)n_roots, w.flags);
+  }
   }
   SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));
   // G1 sums (per root) on side[1] -- then the caller's speculative combine, off the critical path --
