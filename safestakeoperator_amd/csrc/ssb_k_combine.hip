@@ -13,13 +13,10 @@ namespace k {
 SSB_INL bool job_ok(uint32_t b, uint32_t e, uint32_t t, uint32_t n_shares) {
   return t >= 1 && t <= SSB_MAX_T && b <= e && e <= n_shares;
 }
-__global__ void k_select(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
-                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
-                         const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
-                         uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_jobs) return;
-  if (skip_if_ok && *skip_if_ok) return;
+SSB_INL void select_job(int j, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                        const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
+                        const uint32_t* __restrict__ flags, uint32_t* __restrict__ sel, int32_t* __restrict__ status,
+                        uint64_t* __restrict__ err) {
   const uint32_t b = off[j], e = off[j + 1], t = tt[j];
   if (!job_ok(b, e, t, n_shares)) { status[j] = SSB_DVF_INVALID_JOB; err[2 * j] = t; err[2 * j + 1] = e - b; return; }
   const uint32_t n = e - b;
@@ -40,6 +37,15 @@ __global__ void k_select(int n_jobs, uint32_t n_shares, const uint32_t* __restri
   if (cnt < t) { status[j] = SSB_DVF_INSUFFICIENT_VALID_SIGNATURES; err[2 * j] = cnt; err[2 * j + 1] = t; return; }
   status[j] = SSB_DVF_OK; err[2 * j] = 0; err[2 * j + 1] = 0;
 }
+__global__ void k_select(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
+                         const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
+                         uint32_t* __restrict__ sel, int32_t* __restrict__ status, uint64_t* __restrict__ err) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  select_job(j, n_shares, off, tt, ids, verdict, flags, sel, status, err);
+}
 __global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ flags,
                              uint32_t* __restrict__ sel, uint32_t* __restrict__ tt, int32_t* __restrict__ status,
                              uint64_t* __restrict__ err) {
@@ -54,6 +60,13 @@ __global__ void k_select_all(int n_jobs, const uint32_t* __restrict__ off, const
   }
   status[j] = st; err[2 * j] = 0; err[2 * j + 1] = 0;
 }
+SSB_INL void lagrange_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                          const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel, fr* __restrict__ lam) {
+  const uint32_t b = off[j], t = tt[j];
+  uint64_t x[SSB_MAX_T];
+  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
+  unit_lagrange(lam + b, x, t);
+}
 __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                            const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
                            const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
@@ -62,10 +75,7 @@ __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const u
   if (j >= n_jobs || status[j] != SSB_DVF_OK) return;
   if (skip_if_ok && *skip_if_ok) return;
   if (fast && fast[j]) return;
-  const uint32_t b = off[j], t = tt[j];
-  uint64_t x[SSB_MAX_T];
-  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
-  unit_lagrange(lam + b, x, t);
+  lagrange_job(j, off, tt, ids, sel, lam);
 }
 __global__ void SSB_LB(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
@@ -129,6 +139,23 @@ __global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict_
 // (hence order-r) point, so sum c_i sig_i with the integer c_i == lambda_i mod r is the reference's
 // combination.  fast[j] = 1 when the job was finished here; the 255-bit path skips those jobs.
 constexpr uint32_t FAST_T = 16;
+// fast[j] = 1 when the job was finished here
+SSB_INL uint32_t combine_fast_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                                  const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                                  const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
+                                  uint8_t* __restrict__ out96) {
+  if (status[j] != SSB_DVF_OK || tt[j] > FAST_T) return 0u;
+  const uint32_t t = tt[j], b = off[j];
+  uint64_t x[FAST_T];
+  int64_t c[FAST_T];
+  const g2_aff* pts[FAST_T];
+  for (uint32_t i = 0; i < t; ++i) { x[i] = ids[sel[b + i]]; pts[i] = &sig_aff[sel[b + i]]; }
+  if (!unit_lagrange_small(c, x, t)) return 0u;
+  uint8_t o[96];
+  unit_combine_small(o, pts, c, t);
+  for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
+  return 1u;
+}
 __global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                      const uint32_t* __restrict__ sel, const uint64_t* __restrict__ ids,
@@ -138,26 +165,25 @@ __global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
-  uint32_t done = 0;
-  if (status[j] == SSB_DVF_OK && tt[j] <= FAST_T) {
-    const uint32_t t = tt[j], b = off[j];
-    uint64_t x[FAST_T];
-    int64_t c[FAST_T];
-    const g2_aff* pts[FAST_T];
-    for (uint32_t i = 0; i < t; ++i) { x[i] = ids[sel[b + i]]; pts[i] = &sig_aff[sel[b + i]]; }
-    if (unit_lagrange_small(c, x, t)) {
-      uint8_t o[96];
-      unit_combine_small(o, pts, c, t);
-      for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
-      done = 1;
-    }
-  }
-  fast[j] = done;
+  fast[j] = combine_fast_job(j, off, tt, status, sel, ids, sig_aff, out96);
+}
+// k_select + k_combine_fast + k_lagrange of one job in one thread (one launch instead of three)
+__global__ void SSB_LB(64) k_select_combine(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off,
+                                            const uint32_t* __restrict__ tt, const uint64_t* __restrict__ ids,
+                                            const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ flags,
+                                            const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ sel,
+                                            int32_t* __restrict__ status, uint64_t* __restrict__ err,
+                                            const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ fast,
+                                            uint8_t* __restrict__ out96, fr* __restrict__ lam) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  if (skip_if_ok && *skip_if_ok) return;
+  select_job(j, n_shares, off, tt, ids, verdict, flags, sel, status, err);
+  const uint32_t f = combine_fast_job(j, off, tt, status, sel, ids, sig_aff, out96);
+  fast[j] = f;
+  if (!f && status[j] == SSB_DVF_OK) lagrange_job(j, off, tt, ids, sel, lam);
 }
 
-// profiling aid (ssb_debug_hold): one wave polls *flag until it is non-zero or max_polls polls of
-// ~2 us have passed (the exit every run reaches), so work queued behind it on the stream starts
-// together once the host has enqueued everything
 __global__ void k_hold(const uint32_t* flag, uint32_t max_polls) {
   for (uint32_t i = 0; i < max_polls; ++i) {
     if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;

@@ -89,6 +89,13 @@ __global__ void k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
                                                     const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride);
+__global__ void k_select_combine(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off,
+                                 const uint32_t* __restrict__ tt, const uint64_t* __restrict__ ids,
+                                 const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ flags,
+                                 const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ sel,
+                                 int32_t* __restrict__ status, uint64_t* __restrict__ err,
+                                 const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ fast,
+                                 uint8_t* __restrict__ out96, fr* __restrict__ lam);
 __global__ void k_combine_fast(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
@@ -174,7 +181,8 @@ int fallback_levels(size_t n);
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
-                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict);
+                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict,
+                     bool with_verdicts = false);
 // wire-format records bincode(bls::Signature) -> 96-byte compressed signatures (ssb_k_wire.hip)
 constexpr size_t WIRE_SIG_BYTES = 202;
 void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status);

@@ -52,6 +52,7 @@ struct ssb_slot {
   hipEvent_t ev_sdec = nullptr, ev_r2 = nullptr, ev_r1 = nullptr, ev_user = nullptr, ev_fin = nullptr;
   bool out_pending = false;         // ev_out marks the end of the last _dev batch on this slot
   bool shared = false;              // side[] alias `stream` (one stream per slot)
+  bool out_on_stream = false;       // the last batch's ev_out was recorded on `stream` itself
   // workspace arena (grown on demand, never shrunk)
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -130,7 +131,7 @@ struct carve {
 // after the end of the slot's previous batch (whose last kernels run on the context streams).
 int ensure_ws(ssb_ctx* ctx, size_t bytes) {
   ssb_slot* S = ctx->cur;
-  if (S->out_pending) {
+  if (S->out_pending && !S->out_on_stream) {   // (a same-stream wait would only add a queue packet)
     if (hipStreamWaitEvent(S->stream, S->ev_out, 0) != hipSuccess) { ctx->err = "hipStreamWaitEvent failed"; return SSB_EHIP; }
   }
   if (bytes <= ctx->cur->ws_bytes) return SSB_OK;
@@ -411,15 +412,19 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   const launch::fused_sort fs{key, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.ent, w.order,
                               w.pflags, (uint32_t)n_roots, w.flags};
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
-  SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
-  SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
+  // (events only between distinct streams: on one stream the order is given, and every record or
+  // wait is one more packet in the slot's queue)
+  if (sh != st) {
+    SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
+    SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
+  }
   if (fuse_sort) {
     launch::prep_fused(st, fs, (int)n_roots, d_roots, dst, hw);
   } else if (fuse_hash) {
     launch::h2c_u(st, (int)n_roots, d_roots, dst, hw);
   } else {
     if (n_roots) { timed t(ctx, "k_hash_to_g2", sh); launch::hash_to_g2(sh, (int)n_roots, d_roots, dst, w.H, w.hws); }
-    SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
+    if (sh != st) SSB_HIP(hipEventRecord(ctx->cur->ev_hash, sh));
   }
   if (fuse_sort) {
     timed t(ctx, "k_decode");
@@ -435,9 +440,11 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
       hipLaunchKernelGGL(k_decode2, dim3(nblk(2 * n, 64)), dim3(64), 0, st, (int)n, d_sig, d_pk, w.sig_aff, w.pk_aff, w.sflags, w.pflags);
     }
   }
-  SSB_HIP(hipEventRecord(ctx->cur->ev_sdec, st));
   // side[1]: per-share G1 products and the root segments, beside the subgroup checks
-  SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_sdec, 0));
+  if (s1 != st) {
+    SSB_HIP(hipEventRecord(ctx->cur->ev_sdec, st));
+    SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_sdec, 0));
+  }
   if (!P.g1_msm) {
     timed t(ctx, "k_rlc_pk", s1);
     if (n) hipLaunchKernelGGL(k_rlc_pk, dim3(nblk(n, 64)), dim3(64), 0, s1, (int)n, key, w.sflags, w.pflags, w.pk_aff, w.rpk);
@@ -459,7 +466,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
                        (uint32_t)n_roots, w.flags);
   }
   }
-  SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));
+  if (s1 != st || !post_on_slot(ctx->cur)) SSB_HIP(hipEventRecord(ctx->cur->ev_dec, st));   // s1 / the spec stream
   // G1 sums (per root) on side[1] -- then the caller's speculative combine, off the critical path --
   // G2 MSM on the main stream.  One-stream slots: both MSMs in the same three launches (they
   // overlap on the device instead of running back to back on the slot's stream).
@@ -469,10 +476,8 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
                      w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p, fuse_hash ? &hw : nullptr,
                      (int)n_roots, w.H);
-    SSB_HIP(hipEventRecord(ctx->cur->ev_r1, st));
-    if (fuse_hash) SSB_HIP(hipEventRecord(ctx->cur->ev_hash, st));
   } else {
-  SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
+  if (s1 != st) SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
     timed t(ctx, "k_msm_g1", s1);
     launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p, w.redo1);
@@ -481,12 +486,12 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)n_roots), dim3(SEG_THREADS), 0, s1, (int)n_roots, w.rstart, w.rcnt, w.perm,
                        w.flags, w.rpk, (const g2_jac*)nullptr, w.pair_p, (g2_aff*)nullptr);
   }
-  SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
+  if (s1 != st) SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
   if (n) on_decoded();
   { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w2, w.redo2); }
   }
-  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
-  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
+  if (!fused && s1 != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
+  if (!fuse_hash && sh != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
   { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f); }
   {
     timed t(ctx, "k_final");
@@ -511,13 +516,14 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   if (n) {
     timed t(ctx, "k_fallback_verify", fbs);
-    hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, fbs, (int)n, w.ok, w.flags, d_verdict);
-    if (fallback_per_share())
+    if (fallback_per_share()) {
+      hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, fbs, (int)n, w.ok, w.flags, d_verdict);
       hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, fbs, (int)n, w.ok, w.flags,
                          d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
-    else
+    } else {   // the fast verdicts ride along the fallback's first launch
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff,
-                              w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict);
+                              w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict, true);
+    }
   }
   if (!fb_tail && tail != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
@@ -856,10 +862,10 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   const bool on_slot = post_on_slot(ctx->cur);
   hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = on_slot ? st : slot_tail(ctx);
   // order the engine's streams after the caller's stream, and the caller's stream after them
-  hipEvent_t e_user;
-  SSB_HIP(hipEventCreateWithFlags(&e_user, hipEventDisableTiming));
-  SSB_HIP(hipEventRecord(e_user, user));
-  SSB_HIP(hipStreamWaitEvent(st, e_user, 0));
+  if (user != st) {
+    SSB_HIP(hipEventRecord(ctx->cur->ev_user, user));
+    SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_user, 0));
+  }
   carve c{(char*)ctx->cur->ws};
   verify_ws w = carve_verify(c, n, n_roots);
   uint32_t* share_job = c.take<uint32_t>(n);
@@ -873,9 +879,10 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
   auto spec = [&] {
     hipStreamWaitEvent(sc, ctx->cur->ev_dec, 0);
-    { timed tm(ctx, "k_select", sc); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, (uint32_t)n, share_off, t, ids, (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err); }
-    { timed tm(ctx, "k_combine_fast", sc); hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, (const uint32_t*)nullptr, fast, out_sig96); }
-    { timed tm(ctx, "k_lagrange", sc); hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, ids, sel, out_status, (const uint32_t*)nullptr, (const uint32_t*)fast, lam); }
+    { timed tm(ctx, "k_combine_fast", sc);   // select + small-integer combine + Lagrange, one launch
+      hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, (uint32_t)n, share_off, t, ids,
+                         (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err, w.sig_aff, fast,
+                         out_sig96, lam); }
     if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4); }
     hipEventRecord(ctx->cur->ev_comb, sc);
@@ -888,16 +895,21 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   const uint32_t* gate = on_slot ? nullptr : (const uint32_t*)w.ok;
   if (!on_slot) SSB_HIP(hipStreamWaitEvent(tl, ctx->cur->ev_comb, 0));
   st = tl;
-  { timed tm(ctx, "k_select", st); hipLaunchKernelGGL(k_select, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids, (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err); }
-  { timed tm(ctx, "k_combine_fast", st); hipLaunchKernelGGL(k_combine_fast, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, sel, ids, w.sig_aff, gate, fast, out_sig96); }
-  hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, ids, sel, out_status, gate, (const uint32_t*)fast, lam);
+  if (on_slot) {
+    timed tm(ctx, "k_combine_fast", st);
+    hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids,
+                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam);
+  } else {
+    hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids,
+                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam);
+  }
   if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate, (const uint32_t*)fast, term);
   hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate, (const uint32_t*)fast, out_sig96, 4);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
   ctx->cur->out_pending = true;
-  SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
-  hipEventDestroy(e_user);
+  ctx->cur->out_on_stream = st == ctx->cur->stream;
+  if (user != st) SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
   return SSB_OK;
 }
 
@@ -917,17 +929,20 @@ int verify_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint32_t* pk_i
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   if ((rc = ensure_ws(ctx, verify_ws_bytes(n, n_roots)))) return rc;
   hipStream_t user = (hipStream_t)stream, st = ctx->cur->stream;
-  SSB_HIP(hipEventRecord(ctx->cur->ev_user, user));
-  SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_user, 0));
+  if (user != st) {
+    SSB_HIP(hipEventRecord(ctx->cur->ev_user, user));
+    SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_user, 0));
+  }
   carve c{(char*)ctx->cur->ws};
   verify_ws w = carve_verify(c, n, n_roots);
   // root indices >= n_roots: those shares are skipped by the sums and get verdict 0
-  hipStream_t tl = slot_tail(ctx);
+  hipStream_t tl = post_on_slot(ctx->cur) ? st : slot_tail(ctx);
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, root_idx, roots32, d, rlc_seed, verdicts, [] {},
                        tl))) return rc;
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, tl));
   ctx->cur->out_pending = true;
-  SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
+  ctx->cur->out_on_stream = tl == ctx->cur->stream;
+  if (user != tl) SSB_HIP(hipStreamWaitEvent(user, ctx->cur->ev_out, 0));
   return SSB_OK;
 }
 
