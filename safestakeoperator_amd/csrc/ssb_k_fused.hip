@@ -64,15 +64,16 @@ __global__ void SSB_LB2(64) k_decode_count(int n, uint32_t nbd, const uint8_t* _
 
 // One workgroup: start[] = cur[] = exclusive scan of cnt[0..K), then the bucket order (within each
 // MSM's key range, by count, largest first -- the k_order_* kernels' order)
-constexpr int SS_T = 1024;
+constexpr int SS_T = 256;   // 4 waves: a 16-wave workgroup waits long for a free CU under load
 __global__ void __launch_bounds__(SS_T) k_sort_scan(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
                                                     uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
                                                     uint32_t* __restrict__ order) {
   __shared__ uint32_t sh[SS_T];
   __shared__ uint32_t bins[512];
+  static_assert(2 * SS_T == 512, "two order bins per thread");
   const int t = threadIdx.x;
   const uint32_t per = (K + SS_T - 1) / SS_T, k0 = t * per, k1 = k0 + per < K ? k0 + per : K;
-  if (t < 512) bins[t] = 0u;
+  bins[2 * t] = 0u; bins[2 * t + 1] = 0u;
   uint32_t sum = 0;
   for (uint32_t k = k0; k < k1; ++k) sum += cnt[k];
   sh[t] = sum;
@@ -90,17 +91,18 @@ __global__ void __launch_bounds__(SS_T) k_sort_scan(uint32_t K, uint32_t K2, con
     atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u);
   }
   __syncthreads();
-  // exclusive scan of the 512 bins (threads 0..511), then scatter the keys
-  const uint32_t v = t < 512 ? bins[t] : 0u;
-  sh[t] = v;
+  // exclusive scan of the 512 bins, two per thread, then scatter the keys
+  const uint32_t v0 = bins[2 * t], v1 = bins[2 * t + 1];
+  sh[t] = v0 + v1;
   __syncthreads();
-  for (int off = 1; off < 512; off <<= 1) {
-    const uint32_t o = (t < 512 && t >= off) ? sh[t - off] : 0u;
+  for (int off = 1; off < SS_T; off <<= 1) {
+    const uint32_t o = t >= off ? sh[t - off] : 0u;
     __syncthreads();
-    if (t < 512) sh[t] += o;
+    sh[t] += o;
     __syncthreads();
   }
-  if (t < 512) bins[t] = sh[t] - v;
+  const uint32_t base = sh[t] - v0 - v1;
+  bins[2 * t] = base; bins[2 * t + 1] = base + v0;
   __syncthreads();
   for (uint32_t k = k0; k < k1; ++k) {
     const uint32_t c = cnt[k];

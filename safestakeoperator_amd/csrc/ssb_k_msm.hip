@@ -278,45 +278,37 @@ struct msm_bucket_args {
 // hash_to_G2 stages riding along (nblk of their own; 0 = none): the SWU map beside the subgroup
 // checks, the cofactor clearing beside the bucket sums, the affine output beside the window sums
 struct h2c_fuse { int n; const fp2* u; g2_aff* q; g2_jac* hj; uint32_t* exc; int exact_all; g2_aff* out; };
-constexpr size_t BUCKET2_LDS = 64 * sizeof(g2_jac) > H2C_CLEAR_LDS ? 64 * sizeof(g2_jac) : H2C_CLEAR_LDS;
-__global__ void SSB_LB(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, uint32_t nblk1, msm_bucket_args a1,
+__global__ void SSB_LB(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
                                          const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig,
-                                         const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1,
-                                         h2c_fuse h) {
-  __shared__ __attribute__((aligned(16))) char lds[BUCKET2_LDS];
-  uint32_t bid = blockIdx.x;
-  if (bid < nblk2) {
-    msm_bucket_block<fp2>(bid, (g2_jac*)lds, a2.nb, a2.base, a2.lj, a2.order, a2.start, a2.cnt, a2.ent, flags, sig, b2);
-    return;
-  }
-  bid -= nblk2;
-  if (bid < nblk1) {
-    msm_bucket_block<fp>(bid, (g1_jac*)lds, a1.nb, a1.base, a1.lj, a1.order, a1.start, a1.cnt, a1.ent, flags, pk, b1);
-    return;
-  }
-  h2c_clear_block(bid - nblk1, (fp*)lds, h.n, h.q, h.hj, h.exc);
+                                         const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1) {
+  __shared__ g2_jac sh[64];
+  if (blockIdx.x < nblk2)
+    msm_bucket_block<fp2>(blockIdx.x, sh, a2.nb, a2.base, a2.lj, a2.order, a2.start, a2.cnt, a2.ent, flags, sig, b2);
+  else
+    msm_bucket_block<fp>(blockIdx.x - nblk2, (g1_jac*)sh, a1.nb, a1.base, a1.lj, a1.order, a1.start, a1.cnt, a1.ent, flags,
+                         pk, b1);
 }
+// (the cofactor clearing's lane programs need 32 KB of LDS per block: they ride with the window
+// sums, a launch of few blocks, not with the bucket sums, whose many blocks the LDS would thin out)
+constexpr size_t WINDOW2_LDS = 64 * sizeof(g2_jac) > H2C_CLEAR_LDS ? 64 * sizeof(g2_jac) : H2C_CLEAR_LDS;
 __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* __restrict__ b2, g2_aff* __restrict__ pair_q,
                                          g1_aff* __restrict__ pair_p, const g1_aff* __restrict__ negg1_pow,
                                          uint32_t nblk1, uint32_t ngw1, int c1, const g1_jac* __restrict__ b1,
                                          g1_jac* __restrict__ w1, h2c_fuse h) {
-  __shared__ g2_jac sh[64];
+  __shared__ __attribute__((aligned(16))) char lds[WINDOW2_LDS];
   uint32_t bid = blockIdx.x;
   if (bid < nblk2) {
-    msm_window_block<fp2>(bid, sh, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
+    msm_window_block<fp2>(bid, (g2_jac*)lds, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
                           (const g2_jac*)nullptr);
     return;
   }
   bid -= nblk2;
   if (bid < nblk1) { msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1); return; }
-  h2c_affine_block(bid - nblk1, h.n, h.q, h.hj, h.exc, h.exact_all, h.out);
+  h2c_clear_block(bid - nblk1, (fp*)lds, h.n, h.q, h.hj, h.exc);
 }
 
 // ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
-__global__ void SSB_LB(64) k_msm_horner(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
-                                                   g1_aff* __restrict__ out, const uint32_t* __restrict__ redo) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngroups || (redo && !redo[g])) return;
+SSB_INL void msm_horner_lane(int g, int c, int W, const g1_jac* __restrict__ wsum, g1_aff* __restrict__ out) {
   const g1_jac* ws = wsum + (size_t)g * W;
   g1_jac acc = ws[W - 1];
   for (int w = W - 2; w >= 0; --w) {
@@ -328,6 +320,20 @@ __global__ void SSB_LB(64) k_msm_horner(int ngroups, int c, int W, const g1_jac*
   g1_aff a;
   jac_to_aff(a, acc);
   out[g] = a;
+}
+__global__ void SSB_LB(64) k_msm_horner(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
+                                                   g1_aff* __restrict__ out, const uint32_t* __restrict__ redo) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups || (redo && !redo[g])) return;
+  msm_horner_lane(g, c, W, wsum, out);
+}
+
+// the G1 Horner (blocks [0, nbh)) with the hash's affine output riding along
+__global__ void SSB_LB(64) k_msm_horner2(uint32_t nbh, int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
+                                        g1_aff* __restrict__ out, h2c_fuse h) {
+  if (blockIdx.x >= nbh) { h2c_affine_block(blockIdx.x - nbh, h.n, h.q, h.hj, h.exc, h.exact_all, h.out); return; }
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < ngroups) msm_horner_lane(g, c, W, wsum, out);
 }
 
 // per-share G1 RLC product (the G1 side when the roots' groups are small: 64 doublings per share
@@ -486,12 +492,13 @@ void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int
   const uint32_t nblk2 = (nb2 + (64u >> lj2) - 1) / (64u >> lj2), nblk1 = (nb1 + (64u >> lj1) - 1) / (64u >> lj1);
   const uint32_t nbc = h.n ? (uint32_t)(h.n + 7) / 8 : 0u, nba = h.n ? (uint32_t)(h.n + 63) / 64 : 0u;
   const msm_bucket_args a2{nb2, c2.base, lj2, order, start, cnt, ent}, a1{nb1, c1.base, lj1, order, start, cnt, ent};
-  hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1 + nbc), dim3(64), 0, st, nblk2, a2, nblk1, a1, flags, sig, pk, b2, b1, h);
+  hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1), dim3(64), 0, st, nblk2, a2, a1, flags, sig, pk, b2, b1);
   const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W, nbw1 = (nw1 + 63) / 64;
-  hipLaunchKernelGGL(k_msm_window2, dim3(nw2 + nbw1 + nba), dim3(64), 0, st, nw2, (int)c2.c, (const g2_jac*)b2,
+  hipLaunchKernelGGL(k_msm_window2, dim3(nw2 + nbw1 + nbc), dim3(64), 0, st, nw2, (int)c2.c, (const g2_jac*)b2,
                      pair_q, pair_p, negg1_pow, nbw1, nw1, (int)c1.c, (const g1_jac*)b1, wsum1, h);
-  hipLaunchKernelGGL(k_msm_horner, dim3((c1.ngroups + 63) / 64), dim3(64), 0, st, (int)c1.ngroups, (int)c1.c, (int)c1.W,
-                     (const g1_jac*)wsum1, root_sum, (const uint32_t*)nullptr);
+  const uint32_t nbh = (c1.ngroups + 63) / 64;
+  hipLaunchKernelGGL(k_msm_horner2, dim3(nbh + nba), dim3(64), 0, st, nbh, (int)c1.ngroups, (int)c1.c, (int)c1.W,
+                     (const g1_jac*)wsum1, root_sum, h);
 }
 
 void subgroup_map(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, const h2c_ws* hw,
