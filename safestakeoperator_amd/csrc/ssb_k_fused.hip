@@ -10,8 +10,9 @@ namespace k {
 
 // blocks [0, nz): zero the sort's counts (and the order bins); then one lane per root: the hash's
 // expand_message_xmd + the two field elements (k_h2c_u)
-__global__ void SSB_LB(64) k_prep_fused(uint32_t nz, uint32_t K, uint32_t* __restrict__ cnt, int n_roots,
-                                        const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
+__global__ void SSB_LB(64) k_prep_fused(uint32_t nz, uint32_t K, uint32_t* __restrict__ cnt, uint32_t* __restrict__ tickets,
+                                        int n_roots, const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
+  if (blockIdx.x == 0 && threadIdx.x < 4) tickets[threadIdx.x] = 0u;
   if (blockIdx.x < nz) {
     for (uint32_t x = blockIdx.x * 64 * 16 + threadIdx.x; x < (blockIdx.x + 1) * 64 * 16 && x < K; x += 64) cnt[x] = 0u;
     return;
@@ -26,6 +27,52 @@ __global__ void SSB_LB(64) k_prep_fused(uint32_t nz, uint32_t K, uint32_t* __res
   u[2 * i + 1] = u1;
 }
 
+// One wave: start[] = cur[] = exclusive scan of cnt[0..K), then the bucket order (within each MSM's
+// key range, by count, largest first -- the k_order_* kernels' order).  sh: 64 + 512 words of LDS.
+SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
+                            uint32_t* __restrict__ cur, uint32_t* __restrict__ order, uint32_t* sh) {
+  uint32_t* bins = sh + 64;
+  const int t = threadIdx.x;
+  const uint32_t per = (K + 63) / 64, k0 = t * per, k1 = k0 + per < K ? k0 + per : K;
+  for (int b = t; b < 512; b += 64) bins[b] = 0u;
+  uint32_t sum = 0;
+  for (uint32_t k = k0; k < k1; ++k) sum += cnt[k];
+  sh[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = t >= off ? sh[t - off] : 0u;
+    __syncthreads();
+    sh[t] += o;
+    __syncthreads();
+  }
+  uint32_t run = sh[t] - sum;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t c = cnt[k];
+    start[k] = run; cur[k] = run; run += c;
+    atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of the 512 bins, eight per lane
+  uint32_t v[8], tot = 0;
+  for (int q = 0; q < 8; ++q) { v[q] = bins[8 * t + q]; tot += v[q]; }
+  __syncthreads();
+  sh[t] = tot;
+  __syncthreads();
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = t >= off ? sh[t - off] : 0u;
+    __syncthreads();
+    sh[t] += o;
+    __syncthreads();
+  }
+  uint32_t base = sh[t] - tot;
+  for (int q = 0; q < 8; ++q) { bins[8 * t + q] = base; base += v[q]; }
+  __syncthreads();
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t c = cnt[k];
+    order[atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u)] = k;
+  }
+}
+
 // blocks [0, nbd): signature decode; [nbd, 2 nbd): public keys (gathered from the cache, or
 // decoded); [2 nbd, 3 nbd): the sort's count pass
 template <bool CACHED>
@@ -35,9 +82,27 @@ __global__ void SSB_LB2(64) k_decode_count(int n, uint32_t nbd, const uint8_t* _
                                            const uint32_t* __restrict__ cache_flags, g2_aff* __restrict__ sig_aff,
                                            g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ sflags,
                                            uint32_t* __restrict__ pflags, rlc_key key, const uint32_t* __restrict__ share_root,
-                                           msm_cfg c2, msm_cfg c1, uint32_t* __restrict__ cnt) {
+                                           msm_cfg c2, msm_cfg c1, uint32_t* __restrict__ cnt, uint32_t K,
+                                           uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
+                                           uint32_t* __restrict__ order, uint32_t* __restrict__ tickets) {
   const uint32_t part = blockIdx.x / nbd;
   const int s = (blockIdx.x - part * nbd) * 64 + threadIdx.x;
+  if (part == 2) {   // count pass; the last count block to finish runs the scans
+    __shared__ uint32_t sh[64 + 512];
+    __shared__ uint32_t last;
+    if (s < n) msm_sort_lane<false>(s, key, share_root, c2, c1, cnt, (uint32_t*)nullptr);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      last = atomicAdd(&tickets[0], 1u) == nbd - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (last) {
+      __threadfence();
+      sort_scan_wave(K, c1.base, cnt, start, cur, order, sh);
+    }
+    return;
+  }
   if (s >= n) return;
   if (part == 0) {
     uint8_t b[96];
@@ -57,56 +122,6 @@ __global__ void SSB_LB2(64) k_decode_count(int n, uint32_t nbd, const uint8_t* _
       pflags[s] = unit_decode_pk(pk, b);
       pk_aff[s] = pk;
     }
-  } else {
-    msm_sort_lane<false>(s, key, share_root, c2, c1, cnt, (uint32_t*)nullptr);
-  }
-}
-
-// One workgroup: start[] = cur[] = exclusive scan of cnt[0..K), then the bucket order (within each
-// MSM's key range, by count, largest first -- the k_order_* kernels' order)
-constexpr int SS_T = 256;   // 4 waves: a 16-wave workgroup waits long for a free CU under load
-__global__ void __launch_bounds__(SS_T) k_sort_scan(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt,
-                                                    uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
-                                                    uint32_t* __restrict__ order) {
-  __shared__ uint32_t sh[SS_T];
-  __shared__ uint32_t bins[512];
-  static_assert(2 * SS_T == 512, "two order bins per thread");
-  const int t = threadIdx.x;
-  const uint32_t per = (K + SS_T - 1) / SS_T, k0 = t * per, k1 = k0 + per < K ? k0 + per : K;
-  bins[2 * t] = 0u; bins[2 * t + 1] = 0u;
-  uint32_t sum = 0;
-  for (uint32_t k = k0; k < k1; ++k) sum += cnt[k];
-  sh[t] = sum;
-  __syncthreads();
-  for (int off = 1; off < SS_T; off <<= 1) {
-    const uint32_t o = t >= off ? sh[t - off] : 0u;
-    __syncthreads();
-    sh[t] += o;
-    __syncthreads();
-  }
-  uint32_t run = sh[t] - sum;
-  for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t c = cnt[k];
-    start[k] = run; cur[k] = run; run += c;
-    atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u);
-  }
-  __syncthreads();
-  // exclusive scan of the 512 bins, two per thread, then scatter the keys
-  const uint32_t v0 = bins[2 * t], v1 = bins[2 * t + 1];
-  sh[t] = v0 + v1;
-  __syncthreads();
-  for (int off = 1; off < SS_T; off <<= 1) {
-    const uint32_t o = t >= off ? sh[t - off] : 0u;
-    __syncthreads();
-    sh[t] += o;
-    __syncthreads();
-  }
-  const uint32_t base = sh[t] - v0 - v1;
-  bins[2 * t] = base; bins[2 * t + 1] = base + v0;
-  __syncthreads();
-  for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t c = cnt[k];
-    order[atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u)] = k;
   }
 }
 
@@ -117,7 +132,7 @@ using namespace ssb::k;
 
 void prep_fused(hipStream_t st, const fused_sort& fs, int n_roots, const uint8_t* roots, const dst_arg& dst, const h2c_ws& hw) {
   const uint32_t nz = (fs.K + 64 * 16 - 1) / (64 * 16), nu = (uint32_t)(n_roots + 63) / 64;
-  hipLaunchKernelGGL(k_prep_fused, dim3(nz + nu), dim3(64), 0, st, nz, fs.K, fs.cnt, n_roots, roots, dst, hw.u);
+  hipLaunchKernelGGL(k_prep_fused, dim3(nz + nu), dim3(64), 0, st, nz, fs.K, fs.cnt, fs.tickets, n_roots, roots, dst, hw.u);
 }
 
 void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
@@ -127,16 +142,14 @@ void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk
   const uint32_t nbd = (uint32_t)(n + 63) / 64;
   if (pk_index)
     hipLaunchKernelGGL(k_decode_count<true>, dim3(3 * nbd), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
-                       cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt);
+                       cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt,
+                       fs.K, fs.start, fs.cur, fs.order, fs.tickets);
   else
     hipLaunchKernelGGL(k_decode_count<false>, dim3(3 * nbd), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
-                       cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt);
+                       cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt,
+                       fs.K, fs.start, fs.cur, fs.order, fs.tickets);
 }
 
-void sort_scan(hipStream_t st, const fused_sort& fs) {
-  hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(SS_T), 0, st, fs.K, fs.c1.base, (const uint32_t*)fs.cnt, fs.start, fs.cur,
-                     fs.order);
-}
 
 }  // namespace launch
 }  // namespace ssb

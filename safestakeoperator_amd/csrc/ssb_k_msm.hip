@@ -291,23 +291,9 @@ __global__ void SSB_LB(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm
 // (the cofactor clearing's lane programs need 32 KB of LDS per block: they ride with the window
 // sums, a launch of few blocks, not with the bucket sums, whose many blocks the LDS would thin out)
 constexpr size_t WINDOW2_LDS = 64 * sizeof(g2_jac) > H2C_CLEAR_LDS ? 64 * sizeof(g2_jac) : H2C_CLEAR_LDS;
-__global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* __restrict__ b2, g2_aff* __restrict__ pair_q,
-                                         g1_aff* __restrict__ pair_p, const g1_aff* __restrict__ negg1_pow,
-                                         uint32_t nblk1, uint32_t ngw1, int c1, const g1_jac* __restrict__ b1,
-                                         g1_jac* __restrict__ w1, h2c_fuse h) {
-  __shared__ __attribute__((aligned(16))) char lds[WINDOW2_LDS];
-  uint32_t bid = blockIdx.x;
-  if (bid < nblk2) {
-    msm_window_block<fp2>(bid, (g2_jac*)lds, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
-                          (const g2_jac*)nullptr);
-    return;
-  }
-  bid -= nblk2;
-  if (bid < nblk1) { msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1); return; }
-  h2c_clear_block(bid - nblk1, (fp*)lds, h.n, h.q, h.hj, h.exc);
-}
-
-// ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
+// With tickets (the fused one-stream path), the last G1-window block to finish also runs the G1
+// Horner of every root, and the last clearing block the affine output of every root: both ride in
+// this launch behind the G2 window sums instead of following in a launch of their own.
 SSB_INL void msm_horner_lane(int g, int c, int W, const g1_jac* __restrict__ wsum, g1_aff* __restrict__ out) {
   const g1_jac* ws = wsum + (size_t)g * W;
   g1_jac acc = ws[W - 1];
@@ -321,6 +307,45 @@ SSB_INL void msm_horner_lane(int g, int c, int W, const g1_jac* __restrict__ wsu
   jac_to_aff(a, acc);
   out[g] = a;
 }
+struct window2_tail { uint32_t* tickets; int ngroups1, W1; g1_aff* root_sum; };
+SSB_INL bool last_block(uint32_t* ticket, uint32_t nblocks, uint32_t* flag_lds) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    *flag_lds = atomicAdd(ticket, 1u) == nblocks - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  const bool last = *flag_lds != 0;
+  if (last) __threadfence();
+  return last;
+}
+__global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* __restrict__ b2, g2_aff* __restrict__ pair_q,
+                                         g1_aff* __restrict__ pair_p, const g1_aff* __restrict__ negg1_pow,
+                                         uint32_t nblk1, uint32_t ngw1, int c1, const g1_jac* __restrict__ b1,
+                                         g1_jac* __restrict__ w1, h2c_fuse h, window2_tail tl) {
+  __shared__ __attribute__((aligned(16))) char lds[WINDOW2_LDS];
+  __shared__ uint32_t last;
+  uint32_t bid = blockIdx.x;
+  if (bid < nblk2) {
+    msm_window_block<fp2>(bid, (g2_jac*)lds, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
+                          (const g2_jac*)nullptr);
+    return;
+  }
+  bid -= nblk2;
+  if (bid < nblk1) {
+    if (!tl.tickets) { msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1); return; }
+    if (bid * 64 + threadIdx.x < ngw1) msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1);
+    if (last_block(&tl.tickets[1], nblk1, &last))
+      for (int g = threadIdx.x; g < tl.ngroups1; g += 64) msm_horner_lane(g, c1, tl.W1, w1, tl.root_sum);
+    return;
+  }
+  bid -= nblk1;
+  h2c_clear_block(bid, (fp*)lds, h.n, h.q, h.hj, h.exc);
+  if (tl.tickets && last_block(&tl.tickets[2], (uint32_t)(h.n + 7) / 8, &last))
+    for (uint32_t b = 0; b * 64 < (uint32_t)h.n; ++b) h2c_affine_block(b, h.n, h.q, h.hj, h.exc, h.exact_all, h.out);
+}
+
+// ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
 __global__ void SSB_LB(64) k_msm_horner(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
                                                    g1_aff* __restrict__ out, const uint32_t* __restrict__ redo) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -486,7 +511,7 @@ h2c_fuse fuse_of(const h2c_ws* hw, int n_roots, g2_aff* out) {
 void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int lj1, const uint32_t* order,
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
-              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw, int n_roots, g2_aff* H) {
+              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw, int n_roots, g2_aff* H, uint32_t* tickets) {
   const h2c_fuse h = fuse_of(hw, n_roots, H);
   const uint32_t nb2 = c2.ngroups * c2.W << c2.c, nb1 = c1.ngroups * c1.W << c1.c;
   const uint32_t nblk2 = (nb2 + (64u >> lj2) - 1) / (64u >> lj2), nblk1 = (nb1 + (64u >> lj1) - 1) / (64u >> lj1);
@@ -494,8 +519,10 @@ void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int
   const msm_bucket_args a2{nb2, c2.base, lj2, order, start, cnt, ent}, a1{nb1, c1.base, lj1, order, start, cnt, ent};
   hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1), dim3(64), 0, st, nblk2, a2, a1, flags, sig, pk, b2, b1);
   const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W, nbw1 = (nw1 + 63) / 64;
+  const window2_tail tl{tickets, (int)c1.ngroups, (int)c1.W, root_sum};
   hipLaunchKernelGGL(k_msm_window2, dim3(nw2 + nbw1 + nbc), dim3(64), 0, st, nw2, (int)c2.c, (const g2_jac*)b2,
-                     pair_q, pair_p, negg1_pow, nbw1, nw1, (int)c1.c, (const g1_jac*)b1, wsum1, h);
+                     pair_q, pair_p, negg1_pow, nbw1, nw1, (int)c1.c, (const g1_jac*)b1, wsum1, h, tl);
+  if (tickets) return;   // the Horner and the affine H ran in the window launch's last blocks
   const uint32_t nbh = (c1.ngroups + 63) / 64;
   hipLaunchKernelGGL(k_msm_horner2, dim3(nbh + nba), dim3(64), 0, st, nbh, (int)c1.ngroups, (int)c1.c, (int)c1.W,
                      (const g1_jac*)wsum1, root_sum, h);

@@ -148,10 +148,13 @@ bool msm_fused_ok(const msm_cfg& c1);
 void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int lj1, const uint32_t* order,
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
-              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw = nullptr, int n_roots = 0, g2_aff* H = nullptr);
-// The counting sort of the MSM entries in three launches that ride along the batch's kernels
+              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw = nullptr, int n_roots = 0, g2_aff* H = nullptr,
+              uint32_t* tickets = nullptr);
+// (with tickets: the G1 Horner and the affine H(root) run in the window launch's last G1-window /
+// last clearing block instead of a launch of their own)
+// The counting sort of the MSM entries in two launches that ride along the batch's kernels
 // (one-stream slots, K <= FUSED_SORT_KMAX keys): the count pass beside the decode
-// (decode_count), the scans and the bucket order in one workgroup (sort_scan), the scatter beside
+// (decode_count, whose last count block also runs the scans and the bucket order), the scatter beside
 // the subgroup checks (subgroup_map).  Every share with an in-range root gets entries (the decode
 // flags are not known yet); the bucket sums skip the non-candidates, as they do for the others.
 constexpr uint32_t FUSED_SORT_KMAX = 65536;
@@ -159,6 +162,7 @@ struct fused_sort {
   rlc_key key; const uint32_t* share_root; msm_cfg c2, c1; uint32_t K;
   uint32_t* cnt; uint32_t* start; uint32_t* cur; uint32_t* ent; uint32_t* order;
   const uint32_t* pflags; uint32_t n_roots; uint32_t* flags;
+  uint32_t* tickets;   // 4 words, zeroed by prep_fused: [0] count blocks done, [1] G1 windows, [2] clears
 };
 // the subgroup checks with (hw != nullptr) the hash's SWU map of n_roots roots and (fs != nullptr)
 // the sort's scatter in the same launch; with fs the lanes also write the combined share flags
@@ -166,12 +170,12 @@ void subgroup_map(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* s
                   int n_roots, const fused_sort* fs = nullptr);
 // zero the sort's counts + the hash's first stage (expand_message_xmd) of n_roots roots
 void prep_fused(hipStream_t st, const fused_sort& fs, int n_roots, const uint8_t* roots, const dst_arg& dst, const h2c_ws& hw);
-// decode (signatures; public keys decoded or gathered from the cache) + the sort's count pass
+// decode (signatures; public keys decoded or gathered from the cache) + the sort's count pass; the
+// last count block to finish scans the counts (start, cursor) and orders the buckets
 void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
                   uint32_t n_cache, const g1_aff* cache_aff, const uint32_t* cache_flags, g2_aff* sig_aff, g1_aff* pk_aff,
                   uint32_t* sflags, uint32_t* pflags, const fused_sort& fs);
-// start / cursor (exclusive scan of the counts) and the bucket order, one workgroup
-void sort_scan(hipStream_t st, const fused_sort& fs);
+// (the exclusive scan of the counts and the bucket order run in decode_count's last count block)
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups
 // (ssb_k_bisect.hip); no-op when *ok.  Workspace: cnt/start/cursor n_roots words, perm n words,

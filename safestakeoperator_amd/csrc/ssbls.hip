@@ -330,6 +330,7 @@ struct verify_ws {
   g1_aff* pair_p;     // pair P points: root sums, then [2^(c w)](-g1)
   g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags; uint32_t* gexc;
   fp12* f; uint32_t* ok;
+  uint32_t* tickets;   // fused launches: completion tickets of the blocks (zeroed per batch by k_prep_fused)
   char* hws;          // staged hash_to_G2 workspace
   uint32_t* cnt; uint32_t* start; uint32_t* cur; uint32_t* sbsum; uint32_t* ent;   // MSM counting sort
   uint32_t* order;                                                                 // buckets by count
@@ -369,7 +370,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
   w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
   w.gflags = c.take<uint32_t>(n); w.gexc = c.take<uint32_t>(n);
-  w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1);
+  w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1); w.tickets = c.take<uint32_t>(4);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   w.cnt = c.take<uint32_t>(w.plan.K); w.start = c.take<uint32_t>(w.plan.K); w.cur = c.take<uint32_t>(w.plan.K);
   w.sbsum = c.take<uint32_t>(1024); w.ent = c.take<uint32_t>(w.plan.n_ent); w.order = c.take<uint32_t>(w.plan.K);
@@ -410,7 +411,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   // ... and the MSM entries' counting sort rides along the decode and the subgroup checks
   const bool fuse_sort = fuse_hash && P.K <= launch::FUSED_SORT_KMAX;
   const launch::fused_sort fs{key, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.ent, w.order,
-                              w.pflags, (uint32_t)n_roots, w.flags};
+                              w.pflags, (uint32_t)n_roots, w.flags, w.tickets};
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
   // (events only between distinct streams: on one stream the order is given, and every record or
   // wait is one more packet in the slot's queue)
@@ -453,8 +454,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     hipLaunchKernelGGL(k_root_scan, dim3(1), dim3(64), 0, s1, (int)n_roots, w.rcnt, w.rstart, w.rcur);
     if (n) hipLaunchKernelGGL(k_root_scatter, dim3(nblk(n, 256)), dim3(256), 0, s1, (int)n, (int)n_roots, d_share_root, w.rcur, w.perm);
   }
-  if (fuse_sort) {
-    { timed t(ctx, "k_msm_sort"); launch::sort_scan(st, fs); }
+  if (fuse_sort) {   // (the scans ran in the decode launch's last count block)
     timed t(ctx, "k_subgroup");
     launch::subgroup_map(st, (int)n, w.sflags, w.sig_aff, w.gflags, &hw, (int)n_roots, &fs);   // + flags, scatter
   } else {
@@ -475,7 +475,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     timed t(ctx, "k_msm_g2");
     launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
                      w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p, fuse_hash ? &hw : nullptr,
-                     (int)n_roots, w.H);
+                     (int)n_roots, w.H, fuse_sort ? w.tickets : nullptr);
   } else {
   if (s1 != st) SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
