@@ -277,7 +277,6 @@ def main():
         args.config = "C4_global" if args.scaling == "strong" else "C2"
     strong = args.scaling == "strong"
     preset = CONFIGS[args.config]
-    explicit_pipeline = args.pipeline is not None
     for k in ("validators", "threshold", "operators", "roots", "pipeline"):
         if getattr(args, k) is None:
             setattr(args, k, preset[k])
@@ -285,10 +284,9 @@ def main():
     # time-slices them.  Measured C2 at the driver's 20 steps, one-stream slots, each batch wholly on
     # its slot's stream (hash_to_G2, verdicts and combine too): 19 slots 7.18 M sigs/s (the 20th
     # batch waits for a slot), 20 slots 9.33 M (every batch in flight at once), 21 slots 6.51 M,
-    # 20 slots + 2 hash streams 4.05 M.  With N > 1 the process group's all-gather runs on a stream
-    # of its own, so multi-GPU runs keep one slot fewer.
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not explicit_pipeline and args.pipeline >= 20:
-        args.pipeline = 19
+    # 20 slots + 2 hash streams 4.05 M.  With N > 1 the all-gather runs on RCCL's stream: it is
+    # issued once per pipeline round (exchange_group), after the round's batches, so that stream is
+    # not active beside the 20 slot queues.
     # slot streams + the speculative-combine and tail streams (idle with one-stream slots, which run
     # every stage on the slot's stream) + SSB_HASH_STREAMS (engine default 0) + one for torch
     set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "1") or 1)
@@ -392,27 +390,53 @@ def main():
                 o["ver"].data_ptr(), ctypes.c_void_p(s.cuda_stream))
             if rc != 0:
                 raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
-            if dist is not None:
-                # RCCL all-gather over xGMI, the one exchange step, asynchronous: RCCL's stream waits
-                # for this batch, the slot's stream does not wait for RCCL (only its next reuse does)
-                if strong:
-                    _, works = exchange_var(o["ver"].to(cdev), o["out"].to(cdev), o["st"].to(cdev), o["err"].to(cdev),
-                                            sizes=sizes, async_op=True)
-                else:
-                    _, works = exchange(o["ver"].to(cdev), o["out"].to(cdev), o["st"].to(cdev), async_op=True)
-                pending[k] = [w for w in works if w is not None]
+        group.append(k)
+        if len(group) >= S:
+            exchange_group()
+
+    group = []      # slots whose results are not exchanged yet
+
+    def exchange_group():
+        """RCCL all-gather over xGMI of the results of the batches since the last exchange, ONE
+        collective for the group (fewer, larger collectives: with one hardware queue per slot, an
+        all-gather per batch would keep RCCL's stream active beside the 20 slot queues, and past 20
+        active queues the firmware time-slices them).  Asynchronous: RCCL's stream waits for the
+        group's batches, no slot stream waits for RCCL -- only a slot's next batch, which rewrites
+        its output buffers, waits for the all-gather that reads them."""
+        if dist is None or not group:
+            group.clear()
+            return
+        s = streams[group[-1]]
+        with torch.cuda.stream(s):
+            for k in group[:-1]:
+                ev = torch.cuda.Event()
+                ev.record(streams[k])
+                s.wait_event(ev)
+            cat = lambda key: torch.cat([outs[k][key] for k in group]).to(cdev)
+            g = len(group)
+            if strong:
+                _, works = exchange_var(cat("ver"), cat("out"), cat("st"), cat("err"),
+                                        sizes=[(a * g, b * g) for a, b in sizes], async_op=True)
+            else:
+                _, works = exchange(cat("ver"), cat("out"), cat("st"), async_op=True)
+        works = [w for w in works if w is not None]
+        for k in group:
+            pending[k] = works
+        group.clear()
 
     # phase 1: single-batch latency and per-kernel times (depth 1, no overlap between batches)
     # (latency configuration: 3 streams per slot, hash_to_G2 and the G1 side beside the main chain)
     if lib.ssb_set_pipeline_depth(eng.handle, 1) != 0 or lib.ssb_set_slot_streams(eng.handle, 3) != 0:
         raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
     step(0, 0)
+    exchange_group()
     torch.cuda.synchronize(dev)
     eng.kernel_timing(True)
     lat = []
     for i in range(3):
         t0 = time.perf_counter()
         step(1 + i, 0)
+        exchange_group()
         torch.cuda.synchronize(dev)
         lat.append(time.perf_counter() - t0)
     kt = {k: eng.kernel_time(k) for k in ["k_hash_to_g2", "k_decode", "k_subgroup", "k_msm_sort", "k_msm_g2",
@@ -434,6 +458,7 @@ def main():
         the master signature"""
         for i in range(max(args.warmup, S)):
             step(i, i % S)
+        exchange_group()
         torch.cuda.synchronize(dev)
         ok_st = ok_comb = True
         for o in outs:
@@ -468,6 +493,7 @@ def main():
                 e1.record(streams[i % S])
                 ev.append((e0, e1))
             host_ms.append((time.perf_counter() - th) * 1e3)
+        exchange_group()
         if gate is not None:
             gate.fill_(1)
         torch.cuda.synchronize(dev)
