@@ -262,6 +262,7 @@ def main():
     ap.add_argument("--slot-streams", type=int, default=1, choices=(1, 3),
                     help="streams per slot (1: batch in order on one queue; 3: hash / G1 side overlapped)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-buffers", action="store_true", help="skip the PCIe-inclusive host-buffer run")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, the measured path) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--compressed-pk", action="store_true",
@@ -369,6 +370,24 @@ def main():
     d_pkidx = torch.arange(0, N, dtype=torch.int32, device=dev)
     use_cache = [not args.compressed_pk]
 
+    # host-buffer variant (reported beside the headline, never the value): the batch's inputs come
+    # from pinned host memory and its results go back to it, copied on the slot's stream around the
+    # engine call (PCIe inclusive)
+    use_host = [False]
+    host_io = {}
+
+    def host_bufs(k):
+        if k not in host_io:
+            pin = lambda t: t.cpu().pin_memory()
+            host_io[k] = dict(h_sig=pin(d_sig), h_ids=pin(d_ids), h_jr=pin(d_jr), h_roots=pin(d_roots),
+                              d_sig=torch.empty_like(d_sig), d_ids=torch.empty_like(d_ids), d_jr=torch.empty_like(d_jr),
+                              d_roots=torch.empty_like(d_roots),
+                              h_out=torch.empty((V, 96), dtype=torch.uint8).pin_memory(),
+                              h_st=torch.empty((V,), dtype=torch.int32).pin_memory(),
+                              h_err=torch.empty((V, 2), dtype=torch.int64).pin_memory(),
+                              h_ver=torch.empty((N,), dtype=torch.uint8).pin_memory())
+        return host_io[k]
+
     def step(i, k):
         """batch i on pipeline slot k (engine slot k, output buffers k); the caller's stream is the
         slot's own main stream (ssb_slot_stream), so the bench adds no hardware queue"""
@@ -378,18 +397,30 @@ def main():
         s = streams[k]
         fn = lib.ssb_threshold_aggregate_batch_cached_dev if use_cache[0] else lib.ssb_threshold_aggregate_batch_dev
         pk_arg = d_pkidx if use_cache[0] else d_pk
+        src = dict(d_sig=d_sig, d_ids=d_ids, d_jr=d_jr, d_roots=d_roots)
         with torch.cuda.stream(s):
             # the slot's output buffers are rewritten by this batch: order it after the all-gather
             # of the slot's previous batch (a stream wait, the host does not block)
             for w in pending.pop(k, []):
                 w.wait()
+            if use_host[0]:
+                hb = host_bufs(k)
+                for key in ("d_sig", "d_ids", "d_jr", "d_roots"):
+                    hb[key].copy_(hb["h" + key[1:]], non_blocking=True)
+                src = hb
             rc = fn(
-                eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(), pk_arg.data_ptr(), d_ids.data_ptr(),
-                d_jr.data_ptr(), n_roots, d_roots.data_ptr(), ctypes.cast(dst_arr, _lib._u8p), len(DST),
+                eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), src["d_sig"].data_ptr(), pk_arg.data_ptr(),
+                src["d_ids"].data_ptr(), src["d_jr"].data_ptr(), n_roots, src["d_roots"].data_ptr(),
+                ctypes.cast(dst_arr, _lib._u8p), len(DST),
                 (seed_base + i) & (2 ** 64 - 1), o["out"].data_ptr(), o["st"].data_ptr(), o["err"].data_ptr(),
                 o["ver"].data_ptr(), ctypes.c_void_p(s.cuda_stream))
             if rc != 0:
                 raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
+            if use_host[0]:
+                hb["h_out"].copy_(o["out"], non_blocking=True)
+                hb["h_st"].copy_(o["st"], non_blocking=True)
+                hb["h_err"].copy_(o["err"], non_blocking=True)
+                hb["h_ver"].copy_(o["ver"], non_blocking=True)
         group.append(k)
         if len(group) >= S:
             exchange_group()
@@ -512,6 +543,12 @@ def main():
     use_cache[0] = not args.compressed_pk
     ok_head = warm_and_check()
     elapsed = timed_run()
+    elapsed_host = None
+    if world == 1 and not args.no_host_buffers:
+        use_host[0] = True
+        warm_and_check()
+        elapsed_host = timed_run()
+        use_host[0] = False
     ok_st = ok_comb = ok_head and ok_other
     if dist is not None:
         tt = torch.tensor([elapsed, elapsed_other], dtype=torch.float64, device=cdev)
@@ -566,6 +603,9 @@ def main():
             ("value_pk_cached" if args.compressed_pk else "value_compressed_pk"):
                 round(V_glob * n * args.steps / elapsed_other, 1),
             "combined_sigs_per_s": round(combined, 1),
+            "value_host_buffers": (round(V_glob * n * args.steps / elapsed_host, 1) if elapsed_host else None),
+            "host_buffers": "inputs H2D from pinned host memory and results D2H on the slot's stream around each "
+                            "batch (PCIe inclusive; the headline's inputs are resident in HBM)",
             "results_ok": ok_all,
             "invalid_shares_per_batch": wl["n_bad"],
             "roofline": {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),
@@ -584,6 +624,9 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    torch.cuda.synchronize(dev)
+    host_io.clear()      # pinned host buffers released before the engine and the runtime go away
+    streams.clear()
     eng.close()
 
 

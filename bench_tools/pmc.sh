@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=${1:-pmc}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 -u bench.py --steps 2 --warmup 1 --pipeline 1 --slot-streams 3 --no-cpu-baseline"
+CMD="python3 -u bench.py --steps 2 --warmup 1 --pipeline 1 --slot-streams 3 --no-cpu-baseline --no-host-buffers"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS"; do
   i=$((i+1))
