@@ -224,5 +224,68 @@ SSB_INL void h2c_affine_block(uint32_t bid, int n, const g2_aff* __restrict__ q,
   out[i] = a;
 }
 
+// ---- per-job bodies of the a-1 scan and the combine (ssb_k_combine.hip; the one-stream path also
+// runs them speculatively beside the window sums) ----
+// A job the engine cannot run -- t == 0, t > SSB_MAX_T, share_off[j + 1] < share_off[j] or past the
+// batch's n_shares (only the *_dev entry points can pass one: the host wrapper refuses them) --
+// gets SSB_DVF_INVALID_JOB and is never selected, so no later kernel indexes its fixed t-arrays or
+// its share range.  (k_share_map clamps the ranges the same way.)
+SSB_INL bool job_ok(uint32_t b, uint32_t e, uint32_t t, uint32_t n_shares) {
+  return t >= 1 && t <= SSB_MAX_T && b <= e && e <= n_shares;
+}
+SSB_INL void select_job(int j, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                        const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
+                        const uint32_t* __restrict__ flags, uint32_t* __restrict__ sel, int32_t* __restrict__ status,
+                        uint64_t* __restrict__ err) {
+  const uint32_t b = off[j], e = off[j + 1], t = tt[j];
+  if (!job_ok(b, e, t, n_shares)) { status[j] = SSB_DVF_INVALID_JOB; err[2 * j] = t; err[2 * j + 1] = e - b; return; }
+  const uint32_t n = e - b;
+  if (n < t) { status[j] = SSB_DVF_INSUFFICIENT_SIGNATURES; err[2 * j] = n; err[2 * j + 1] = t; return; }
+  uint32_t cnt = 0;
+  for (uint32_t s = b; s < e; ++s) {
+    const uint64_t id = ids[s];
+    if (id == 0) { status[j] = SSB_DVF_INVALID_OPERATOR_ID; err[2 * j] = 0; err[2 * j + 1] = 0; return; }
+    bool dup = false;
+    for (uint32_t k = 0; k < cnt; ++k) dup = dup || (ids[sel[b + k]] == id);
+    if (dup) continue;
+    if (verdict ? (verdict[s] != 0) : ((flags[s] & FLAG_CANDIDATE) != 0)) {
+      sel[b + cnt] = s;
+      ++cnt;
+      if (cnt >= t) break;
+    }
+  }
+  if (cnt < t) { status[j] = SSB_DVF_INSUFFICIENT_VALID_SIGNATURES; err[2 * j] = cnt; err[2 * j + 1] = t; return; }
+  status[j] = SSB_DVF_OK; err[2 * j] = 0; err[2 * j + 1] = 0;
+}
+SSB_INL void lagrange_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                          const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel, fr* __restrict__ lam) {
+  const uint32_t b = off[j], t = tt[j];
+  uint64_t x[SSB_MAX_T];
+  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
+  unit_lagrange(lam + b, x, t);
+}
+// Small-integer Lagrange fast path (unit_lagrange_small), for t <= FAST_T (larger thresholds take
+// the 255-bit path; the per-lane arrays stay small -- this kernel's private segment sets the
+// scratch the runtime reserves on every slot's hardware queue): every selected share is a verified
+// (hence order-r) point, so sum c_i sig_i with the integer c_i == lambda_i mod r is the reference's
+// combination.  fast[j] = 1 when the job was finished here; the 255-bit path skips those jobs.
+constexpr uint32_t FAST_T = 16;
+// fast[j] = 1 when the job was finished here
+SSB_INL uint32_t combine_fast_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                                  const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                                  const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
+                                  uint8_t* __restrict__ out96) {
+  if (status[j] != SSB_DVF_OK || tt[j] > FAST_T) return 0u;
+  const uint32_t t = tt[j], b = off[j];
+  uint64_t x[FAST_T];
+  int64_t c[FAST_T];
+  const g2_aff* pts[FAST_T];
+  for (uint32_t i = 0; i < t; ++i) { x[i] = ids[sel[b + i]]; pts[i] = &sig_aff[sel[b + i]]; }
+  if (!unit_lagrange_small(c, x, t)) return 0u;
+  uint8_t o[96];
+  unit_combine_small(o, pts, c, t);
+  for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
+  return 1u;
+}
 }  // namespace k
 }  // namespace ssb

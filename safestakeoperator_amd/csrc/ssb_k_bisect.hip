@@ -55,22 +55,13 @@ __global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, in
   for (int s = t; s < n; s += PREP_THREADS)
     if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
 }
-// blocks [0, nbv): the verdicts of a passing batch and of non-candidates (k_verdict_fast; the
-// candidates of a failed batch are left to the levels below); then threads [0, n): rsig[s] = k_s
-// sig_s, [n, 2n): rpk[s] = k_s pk_s (candidates only, failed batch only)
-__global__ void SSB_LB(64) k_fb_rlc(int n, uint32_t nbv, rlc_key key, const uint32_t* __restrict__ ok,
+// threads [0, n): rsig[s] = k_s sig_s;  [n, 2n): rpk[s] = k_s pk_s  (candidates only)
+__global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restrict__ ok,
                                    const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig_aff,
                                    const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
-                                   g1_jac* __restrict__ rpk, uint8_t* __restrict__ verdict) {
-  if (blockIdx.x < nbv) {
-    const int s = blockIdx.x * 64 + threadIdx.x;
-    if (s >= n) return;
-    const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
-    if (*ok || !cand) verdict[s] = cand ? 1 : 0;
-    return;
-  }
+                                   g1_jac* __restrict__ rpk) {
   if (*ok) return;
-  const int g = (blockIdx.x - nbv) * blockDim.x + threadIdx.x;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
   // binary double-and-add (no window table): the private segment stays small -- every tail queue
   // reserves scratch for the largest kernel it has run, and this one is launched on every batch
   if (g < n) {
@@ -239,21 +230,15 @@ int fallback_levels(size_t n) {
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
-                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict, bool with_verdicts) {
+                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict) {
   using namespace ssb::k;
-  if (n <= 0) return;
+  if (n <= 0 || n_roots <= 0) return;
   auto nb = [](size_t x, unsigned b) { return (unsigned)((x + b - 1) / b); };
-  const unsigned nbv = with_verdicts ? nb((size_t)n, 64) : 0u;
-  if (n_roots <= 0) {
-    if (nbv) hipLaunchKernelGGL(k_fb_rlc, dim3(nbv), dim3(64), 0, st, n, nbv, key, ok, flags, sig, pk, rsig, rpk, verdict);
-    return;
-  }
   const int L = fallback_levels((size_t)n);
   const int lb = fallback_log2_branch();
   hipLaunchKernelGGL(k_fb_prep, dim3(1), dim3(PREP_THREADS), 0, st, n, n_roots, L, lb, ok, share_root, cnt, start, cursor,
                      gst, perm);
-  hipLaunchKernelGGL(k_fb_rlc, dim3(nbv + nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, nbv, key, ok, flags, sig, pk, rsig, rpk,
-                     verdict);
+  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, key, ok, flags, sig, pk, rsig, rpk);
   for (int l = 0; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;

@@ -2,6 +2,7 @@
 // Launched from ssbls.hip (declarations in ssb_kernels.h); one TU per kernel family so the
 // library compiles in parallel.
 #include "ssb_kernels.h"
+#include "ssb_blocks.h"
 #include "ssb_lane_ops.h"
 
 namespace ssb {
@@ -14,13 +15,21 @@ constexpr int ML_SLOTS = ML_S0 + 18 + 6;
 // one Miller loop per pair (P[p], Q[p]), one workgroup each: the roots' (S_r, H(root r)) and the
 // G2 MSM windows' ([2^(c w)](-g1), W_w)
 __global__ void SSB_LB(64) k_miller_pairs(int npairs, const g1_aff* __restrict__ Pa,
-                                                     const g2_aff* __restrict__ Qa, fp12* __restrict__ f) {
+                                                     const g2_aff* __restrict__ Qa, fp12* __restrict__ f, spec_jobs sj) {
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + ML_SLOTS];
   __shared__ uint32_t flg;
   const int p = blockIdx.x, lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
-  if (p >= npairs) return;
+  if (p >= npairs) {   // the speculative a-1 scan + combine, 64 jobs per block (candidate flags as verdicts)
+    const int j = (p - npairs) * 64 + lane_;
+    if (j >= sj.n_jobs) return;
+    select_job(j, sj.n_shares, sj.off, sj.tt, sj.ids, (const uint8_t*)nullptr, sj.flags, sj.sel, sj.status, sj.err);
+    const uint32_t fj = combine_fast_job(j, sj.off, sj.tt, sj.status, sj.sel, sj.ids, sj.sig_aff, sj.out96);
+    sj.fast[j] = fj;
+    if (!fj && sj.status[j] == SSB_DVF_OK) lagrange_job(j, sj.off, sj.tt, sj.ids, sj.sel, sj.lam);
+    return;
+  }
   const g1_aff P = Pa[p];
   const g2_aff Q = Qa[p];
   if (P.inf || Q.inf) {  // e(O, Q) = e(P, O) = 1  (uniform per workgroup)
@@ -58,7 +67,7 @@ __global__ void SSB_LB(64) k_fallback_lane(int n, const uint32_t* __restrict__ o
   lp_init_consts(g);
   const int F1 = FB_S0, B = F1 + 18, F2 = B + 6, TMP = F2 + 18;
   for (int s = blockIdx.x; s < n; s += gridDim.x) {
-    if (!(flags[s] & FLAG_CANDIDATE)) continue;  // uniform per workgroup; verdict written by k_verdict_fast
+    if (!(flags[s] & FLAG_CANDIDATE)) continue;  // uniform per workgroup; verdict written by k_final_lane
     const g1_aff pk = pk_aff[s];
     const g2_aff h = H[share_root[s]], sg = sig_aff[s];
     const g1_aff ng = g1_neg_generator();
@@ -104,7 +113,10 @@ __global__ void SSB_LB(64) k_fp12_prod8(int n, const fp12* __restrict__ in, fp12
 
 // product of the n values, then ONE final exponentiation -> batch verdict
 constexpr int FE_S0 = lane::FP12_MUL_SCRATCH;
-__global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok) {
+// (with verdict != nullptr it also writes the verdicts of a passing batch and of the non-candidates
+// -- the candidates of a failed batch are left to the exact fallback)
+__global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok, int nv,
+                                        const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdict) {
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + FE_S0 + 12 + 12 + 84];
   __shared__ uint32_t flg;
@@ -126,6 +138,14 @@ __global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint
       one = one && (k == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v));
     }
     *ok = one ? 1u : 0u;
+    flg = one ? 1u : 0u;
+  }
+  if (!verdict) return;
+  __syncthreads();
+  const bool pass = flg != 0;
+  for (int s = threadIdx.x; s < nv; s += 64) {
+    const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
+    if (pass || !cand) verdict[s] = cand ? 1 : 0;
   }
 }
 

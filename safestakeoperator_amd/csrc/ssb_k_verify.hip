@@ -94,15 +94,6 @@ __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32
   if (share_root[s] >= n_roots) f &= ~FLAG_CANDIDATE;  // no H(root): the share cannot verify
   flags[s] = f;
 }
-// Verdicts when the RLC batch check passed (every candidate is valid) and for non-candidates; the
-// candidates of a failed batch are left to k_fallback_lane (ssb_k_pair.hip).
-__global__ void k_verdict_fast(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
-                               uint8_t* __restrict__ verdict) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  const bool cand = (flags[s] & FLAG_CANDIDATE) != 0;
-  if (*ok || !cand) verdict[s] = cand ? 1 : 0;
-}
 
 // ---- per-root RLC sums: counting sort of the shares by root, then one block per (root, group) ----
 __global__ void k_root_hist(int n, int n_roots, const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt) {

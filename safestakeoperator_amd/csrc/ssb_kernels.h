@@ -10,6 +10,14 @@ namespace ssb {
 // DST passed by value to the hashing kernels
 struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
 
+// The a-1 scan + combine of a batch's jobs, run speculatively from the candidate flags (the
+// one-stream path runs it beside the Miller loops; the exact pass on the verdicts follows only if
+// the batch check failed)
+struct spec_jobs {
+  int n_jobs; uint32_t n_shares; const uint32_t* off; const uint32_t* tt; const uint64_t* ids; const uint32_t* flags;
+  uint32_t* sel; int32_t* status; uint64_t* err; const g2_aff* sig_aff; uint32_t* fast; uint8_t* out96; fr* lam;
+};
+
 // One bucket MSM of the RLC sums (ssb_k_msm.hip): c-bit windows, W = ceil(64 / c) of them,
 // `ngroups` independent sums; bucket key = base + ((group * W + window) << c) + digit.
 struct msm_cfg { uint32_t c, W, base, ngroups; };
@@ -49,16 +57,17 @@ __global__ void k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __r
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
                         const uint32_t* __restrict__ gflags, const uint32_t* __restrict__ share_root, uint32_t n_roots,
                         uint32_t* __restrict__ flags);
-__global__ void k_verdict_fast(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
-                               uint8_t* __restrict__ verdict);
+
 __global__ void k_fallback_lane(int n, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ flags,
                                 const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ H,
                                 const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
                                 uint8_t* __restrict__ verdict);
+// (blocks [npairs, ..): the speculative a-1 scan + combine of sj's jobs, 64 per block)
 __global__ void k_miller_pairs(int npairs, const g1_aff* __restrict__ P, const g2_aff* __restrict__ Q,
-                               fp12* __restrict__ f);
+                               fp12* __restrict__ f, spec_jobs sj);
 __global__ void k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out);
-__global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok);
+__global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok, int nv,
+                             const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdict);
 __global__ void k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
                                              const g2_aff* __restrict__ H, uint8_t* __restrict__ out96);
 __global__ void k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48);
@@ -185,8 +194,7 @@ int fallback_levels(size_t n);
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
-                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict,
-                     bool with_verdicts = false);
+                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict);
 // wire-format records bincode(bls::Signature) -> 96-byte compressed signatures (ssb_k_wire.hip)
 constexpr size_t WIRE_SIG_BYTES = 202;
 void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status);

@@ -392,7 +392,8 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
 template <class F>
 int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
                const uint32_t* d_pk_index, const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t rlc_seed,
-               uint8_t* d_verdict, F on_decoded, hipStream_t tail) {
+               uint8_t* d_verdict, F on_decoded, hipStream_t tail, const spec_jobs* sj = nullptr,
+               bool* spec_done = nullptr) {
   rlc_key key;
   if (int rc = draw_rlc_key(ctx, rlc_seed, key)) return rc;
   hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
@@ -492,7 +493,16 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   if (!fused && s1 != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   if (!fuse_hash && sh != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
-  { timed t(ctx, "k_miller"); hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f); }
+  {
+    // one-stream slots: the speculative combine rides along the Miller loops (a few latency-bound
+    // blocks), so a passing batch's tail is only no-op launches
+    spec_jobs sjv{};
+    unsigned nbsp = 0;
+    if (sj && sj->n_jobs > 0 && st == ctx->cur->stream) { sjv = *sj; nbsp = (unsigned)((sj->n_jobs + 63) / 64); }
+    if (spec_done) *spec_done = nbsp > 0;
+    timed t(ctx, "k_miller");
+    hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs + nbsp), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f, sjv);
+  }
   {
     timed t(ctx, "k_final");
     int np = (int)w.npairs;
@@ -502,7 +512,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
       hipLaunchKernelGGL(k_fp12_prod8, dim3((unsigned)nparts), dim3(64), 0, st, np, cur, cur + np);
       cur += np; np = nparts;
     }
-    hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok);
+    hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok, (int)n, (const uint32_t*)w.flags, d_verdict);
   }
   // verdicts (+ the exact fallback when the batch failed) on the slot's tail stream: its kernels
   // have the largest private segments, and the runtime reserves scratch per hardware queue for the
@@ -516,14 +526,13 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   if (n) {
     timed t(ctx, "k_fallback_verify", fbs);
-    if (fallback_per_share()) {
-      hipLaunchKernelGGL(k_verdict_fast, dim3(nblk(n, 256)), dim3(256), 0, fbs, (int)n, w.ok, w.flags, d_verdict);
+    // (the fast verdicts -- a passing batch, non-candidates -- were written by k_final_lane)
+    if (fallback_per_share())
       hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, fbs, (int)n, w.ok, w.flags,
                          d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
-    } else {   // the fast verdicts ride along the fallback's first launch
+    else
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff,
-                              w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict, true);
-    }
+                              w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict);
   }
   if (!fb_tail && tail != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
@@ -887,12 +896,17 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
+  // one-stream slots: the speculative pass rides in the window-sum launch (msm_both), no stream
+  const spec_jobs sj{(int)n_jobs, (uint32_t)n, share_off, t, ids, w.flags, sel, out_status, out_err, w.sig_aff, fast,
+                     out_sig96, lam};
+  bool spec_in_window = false;
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict,
-                       [&] { if (!on_slot) spec(); }, tl))) return rc;
+                       [&] { if (!on_slot) spec(); }, tl, on_slot ? &sj : nullptr, &spec_in_window))) return rc;
   if (!n && !on_slot) spec();
-  // exact path: on the shared tail stream only if the RLC batch failed (every kernel a no-op when
-  // w.ok == 1, the speculative combine stands); on the slot's stream always (no speculative pass)
-  const uint32_t* gate = on_slot ? nullptr : (const uint32_t*)w.ok;
+  // exact path: only if the RLC batch failed (every kernel a no-op when w.ok == 1, the speculative
+  // combine stands) -- on the shared tail stream, or on the slot's stream; one-stream slots whose
+  // window launch could not carry the speculative pass run the exact pass always
+  const uint32_t* gate = (on_slot && !spec_in_window) ? nullptr : (const uint32_t*)w.ok;
   if (!on_slot) SSB_HIP(hipStreamWaitEvent(tl, ctx->cur->ev_comb, 0));
   st = tl;
   if (on_slot) {
@@ -903,8 +917,11 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids,
                        (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam);
   }
-  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate, (const uint32_t*)fast, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate, (const uint32_t*)fast, out_sig96, 4);
+  // (after a speculative pass in the window launch the general combine of the jobs the small-
+  // integer path did not finish still follows here, on whichever selection stands)
+  const uint32_t* gate2 = spec_in_window ? nullptr : gate;
+  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate2, (const uint32_t*)fast, out_sig96, 4);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
   ctx->cur->out_pending = true;
