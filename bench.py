@@ -48,10 +48,12 @@ MAD_PEAK_ISSUE = 256 * 4 * 16 * 2.4e9  # 16 lanes/clk/SIMD (wave64 mad = 4 cycle
 #   C5  configs[4]: 1M validators x 13 shares (10-of-13) over 8 GPUs -> 131,072 validators per GPU
 CONFIGS = {
     "C2": dict(validators=4096, threshold=3, operators=4, roots=64, pipeline=20),
-    "C3_3of4": dict(validators=65536, threshold=3, operators=4, roots=64, pipeline=3),
-    "C3_5of7": dict(validators=65536, threshold=5, operators=7, roots=64, pipeline=3),
+    # C3 / C5 name a final verify: the step also verifies every combined signature against the
+    # validator's master key (batched across validators by RLC, ssb_verify_batch_cached_dev)
+    "C3_3of4": dict(validators=65536, threshold=3, operators=4, roots=64, pipeline=3, final_verify=True),
+    "C3_5of7": dict(validators=65536, threshold=5, operators=7, roots=64, pipeline=3, final_verify=True),
     "C4_per_gpu": dict(validators=32768, threshold=3, operators=4, roots=64, pipeline=4),
-    "C5_per_gpu": dict(validators=131072, threshold=10, operators=13, roots=64, pipeline=2),
+    "C5_per_gpu": dict(validators=131072, threshold=10, operators=13, roots=64, pipeline=2, final_verify=True),
     # ONE global batch of 1,048,576 shares split over the ranks (--scaling strong)
     "C4_global": dict(validators=262144, threshold=3, operators=4, roots=64, pipeline=2),
 }
@@ -261,6 +263,10 @@ def main():
     ap.add_argument("--pipeline", type=int, default=None, help="independent batches in flight (engine pipeline slots)")
     ap.add_argument("--slot-streams", type=int, default=1, choices=(1, 3),
                     help="streams per slot (1: batch in order on one queue; 3: hash / G1 side overlapped)")
+    ap.add_argument("--final-verify", dest="final_verify", action="store_true", default=None,
+                    help="each step also verifies the combined signatures against the master keys (a-8); "
+                         "default on for the C3 / C5 configs, which name it")
+    ap.add_argument("--no-final-verify", dest="final_verify", action="store_false")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-buffers", action="store_true", help="skip the PCIe-inclusive host-buffer run")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -281,6 +287,8 @@ def main():
     for k in ("validators", "threshold", "operators", "roots", "pipeline"):
         if getattr(args, k) is None:
             setattr(args, k, preset[k])
+    if args.final_verify is None:
+        args.final_verify = bool(preset.get("final_verify", False))
     # Hardware queues: every ACTIVE engine stream needs its own, and past 20 the firmware
     # time-slices them.  Measured C2 at the driver's 20 steps, one-stream slots, each batch wholly on
     # its slot's stream (hash_to_G2, verdicts and combine too): 19 slots 7.18 M sigs/s (the 20th
@@ -354,7 +362,8 @@ def main():
     d_roots = dt8(b"".join(wl["roots"]))
     S = max(1, args.pipeline)
     outs = [dict(out=torch.empty((V, 96), dtype=torch.uint8, device=dev), st=torch.empty((V,), dtype=torch.int32, device=dev),
-                 err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev))
+                 err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev),
+                 fv=torch.empty((V,), dtype=torch.uint8, device=dev))
             for _ in range(S)]
     dst_arr = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
     lib = eng._lib
@@ -363,11 +372,15 @@ def main():
     streams = {}
     pending = {}    # slot -> in-flight all-gather handles reading that slot's output buffers
 
-    # validator registration (outside the timed region): every operator key decompressed once
-    pk_host = np.frombuffer(wl["pks"], dtype=np.uint8)
-    if lib.ssb_pk_cache_set(eng.handle, N, pk_host.ctypes.data_as(_lib._u8p)) != 0:
+    # validator registration (outside the timed region): every operator key decompressed once, and
+    # with the final verify the validators' master keys after them (table rows N .. N+V-1)
+    mpks = b"".join(eng.sk_to_pk_batch(wl["master"])) if args.final_verify else b""
+    pk_host = np.frombuffer(wl["pks"] + mpks, dtype=np.uint8)
+    if lib.ssb_pk_cache_set(eng.handle, N + (V if args.final_verify else 0), pk_host.ctypes.data_as(_lib._u8p)) != 0:
         raise RuntimeError("ssb_pk_cache_set: %s" % lib.ssb_last_error(eng.handle))
     d_pkidx = torch.arange(0, N, dtype=torch.int32, device=dev)
+    d_midx = torch.arange(N, N + V, dtype=torch.int32, device=dev)
+    d_mpk = dt8(mpks) if args.final_verify else None
     use_cache = [not args.compressed_pk]
 
     # host-buffer variant (reported beside the headline, never the value): the batch's inputs come
@@ -416,11 +429,23 @@ def main():
                 o["ver"].data_ptr(), ctypes.c_void_p(s.cuda_stream))
             if rc != 0:
                 raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
+            if args.final_verify:
+                # a-8: every combined signature against its validator's master key, same slot and
+                # stream, after the combine (a job that did not combine holds zero bytes: verdict 0)
+                vfn = lib.ssb_verify_batch_cached_dev if use_cache[0] else lib.ssb_verify_batch_dev
+                mk = d_midx if use_cache[0] else d_mpk
+                rc = vfn(eng.handle, V, mk.data_ptr(), o["out"].data_ptr(), src["d_jr"].data_ptr(), n_roots,
+                         src["d_roots"].data_ptr(), ctypes.cast(dst_arr, _lib._u8p), len(DST),
+                         (seed_base + i + (1 << 32)) & (2 ** 64 - 1), o["fv"].data_ptr(), ctypes.c_void_p(s.cuda_stream))
+                if rc != 0:
+                    raise RuntimeError("ssb_verify_batch_cached_dev: %s" % lib.ssb_last_error(eng.handle))
             if use_host[0]:
                 hb["h_out"].copy_(o["out"], non_blocking=True)
                 hb["h_st"].copy_(o["st"], non_blocking=True)
                 hb["h_err"].copy_(o["err"], non_blocking=True)
                 hb["h_ver"].copy_(o["ver"], non_blocking=True)
+                if args.final_verify:
+                    hb.setdefault("h_fv", torch.empty((V,), dtype=torch.uint8).pin_memory()).copy_(o["fv"], non_blocking=True)
         group.append(k)
         if len(group) >= S:
             exchange_group()
@@ -497,6 +522,8 @@ def main():
             ok_st = ok_st and bool(((st_host == 0) == job_ok).all()) and bool((o["ver"].cpu().numpy() == valid).all())
             out_host = o["out"].cpu().numpy()
             ok_comb = ok_comb and all(out_host[v].tobytes() == msig[v] for v in range(min(64, V)) if job_ok[v])
+            if args.final_verify:
+                ok_comb = ok_comb and bool(((o["fv"].cpu().numpy() == 1) == job_ok).all())
         return ok_st and ok_comb
 
     def timed_run():
@@ -573,6 +600,8 @@ def main():
         achieved = km[dom] / (avg[dom] * 1e-3) / 1e12 if avg[dom] > 0 else 0.0
         peak = MAD_PEAK_MEASURED / 1e12
         step_mads = sum(km.values())
+        if args.final_verify:   # + the combined-signature verify: V shares, no combine
+            step_mads += sum(v for k, v in kernel_mads(mads, V, 1, 1, n_roots).items() if k != "k_combine_fast")
         rec = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -589,7 +618,7 @@ def main():
             "config": {"workload": ("%s: %d validators x %d shares (%d-of-%d), %d roots, ONE batch split over %d GPU(s); "
                                     "verify + combine" % (args.config, V_glob, n, t, n, n_roots, world)) if strong else
                                    ("%s: %d validators x %d shares (%d-of-%d), %d roots per GPU; verify + combine"
-                                    % (args.config, V, n, t, n, n_roots)),
+                                    % (args.config, V, n, t, n, n_roots)) + (" + final verify" if args.final_verify else ""),
                        "validators_per_gpu": V, "threshold": t, "operators": n, "roots": n_roots,
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
                        "batches_in_flight": S, "streams_per_slot": args.slot_streams,
@@ -603,6 +632,9 @@ def main():
             ("value_pk_cached" if args.compressed_pk else "value_compressed_pk"):
                 round(V_glob * n * args.steps / elapsed_other, 1),
             "combined_sigs_per_s": round(combined, 1),
+            "final_verify": ("every step verifies its %d combined signatures against the master keys "
+                             "(ssb_verify_batch_cached_dev, RLC batch); combined_sigs_per_s counts verified ones" % V
+                             if args.final_verify else None),
             "value_host_buffers": (round(V_glob * n * args.steps / elapsed_host, 1) if elapsed_host else None),
             "host_buffers": "inputs H2D from pinned host memory and results D2H on the slot's stream around each "
                             "batch (PCIe inclusive; the headline's inputs are resident in HBM)",
