@@ -508,10 +508,19 @@ def main():
         raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
     streams.clear()
     msig = eng.sign_batch(wl["master"][:64], wl["job_root"][:64], wl["roots"])
+    primed = []
 
     def warm_and_check():
         """warmup, then correctness of every slot's last batch: every share valid, every combine ==
         the master signature"""
+        if os.environ.get("SSB_PRIME", "1") != "0" and not primed:
+            # first use of each slot's queue one at a time (untimed): 20 queues acquiring their
+            # scratch at once intermittently failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES
+            for k in range(S):
+                step(k, k)
+                exchange_group()
+                torch.cuda.synchronize(dev)
+            primed.append(1)
         for i in range(max(args.warmup, S)):
             step(i, i % S)
         exchange_group()

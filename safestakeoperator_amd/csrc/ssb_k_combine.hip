@@ -130,10 +130,32 @@ __global__ void k_hold(const uint32_t* flag, uint32_t max_polls) {
     __builtin_amdgcn_s_sleep(127);
   }
 }
+// Scratch primer: a private array as large as the largest private segment of the slot kernels
+// (runtime-indexed, so it lives in scratch), over a full-device grid.  Run once per new queue,
+// one queue at a time (launch::prime_queue): the queue acquires its scratch while the others are
+// idle.  Twenty queues acquiring scratch at once on their first batches intermittently failed with
+// HSA_STATUS_ERROR_OUT_OF_RESOURCES (about 1 run in 10 at 20 slots); primed one by one, 0 in 14.
+constexpr int PRIME_WORDS = 640;   // 2560 B per lane >= k_msm_window2's 2080 B (the largest)
+__global__ void SSB_LB(64) k_scratch_prime(uint32_t* __restrict__ out, uint32_t seed) {
+  uint32_t buf[PRIME_WORDS];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int i = 0; i < PRIME_WORDS; ++i) buf[(i * 37u + t) % PRIME_WORDS] = (uint32_t)i ^ seed;
+  if (seed == 0xffffffffu) out[t & 63u] = buf[(t * 13u) % PRIME_WORDS];   // never taken: keeps buf
+}
 __global__ void k_copy_u8(int n, const uint8_t* __restrict__ a, uint8_t* __restrict__ b) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) b[i] = a[i];
 }
 
 }  // namespace k
+
+namespace launch {
+int prime_queue(hipStream_t st) {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  hipLaunchKernelGGL(k::k_scratch_prime, dim3((unsigned)(ncu * 32)), dim3(64), 0, st, (uint32_t*)nullptr, 0u);
+  if (hipGetLastError() != hipSuccess) return -1;
+  return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+}
+}  // namespace launch
 }  // namespace ssb

@@ -195,6 +195,9 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
                      uint8_t* gv0, uint8_t* gv1, uint8_t* verdict);
+// first use of a new queue: acquire its scratch for the largest slot kernel while the other queues
+// are idle (ssb_k_combine.hip); synchronous, 0 on success
+int prime_queue(hipStream_t st);
 // wire-format records bincode(bls::Signature) -> 96-byte compressed signatures (ssb_k_wire.hip)
 constexpr size_t WIRE_SIG_BYTES = 202;
 void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status);

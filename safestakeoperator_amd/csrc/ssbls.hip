@@ -183,6 +183,11 @@ int init_slot(ssb_slot& S, int streams) {
   }
   for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user, &S.ev_fin})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
+  // each new queue acquires its scratch now, alone (slots are created one after the other)
+  if (!getenv("SSB_NO_PRIME")) {
+    if (launch::prime_queue(S.stream)) return SSB_EHIP;
+    if (!S.shared) for (hipStream_t sd : S.side) if (launch::prime_queue(sd)) return SSB_EHIP;
+  }
   return SSB_OK;
 }
 void sync_slot(ssb_slot& S) {

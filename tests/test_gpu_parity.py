@@ -441,3 +441,55 @@ def test_dleq_verify_golden(engine):
     proofs = [tuple(bytes.fromhex(c[k]) for k in ("x1", "y1", "x2", "y2", "c", "r")) for c in d["cases"]]
     assert engine.dleq_verify_batch(proofs) == [c["expect"] for c in d["cases"]]
     assert engine.dleq_verify_batch(proofs * 200) == [c["expect"] for c in d["cases"]] * 200
+
+
+def _golden_batch(cases, reps):
+    roots, t, offs, sigs, pks, ids, jr = [], [], [0], [], [], [], []
+    for _ in range(reps):
+        for c in cases:
+            r = bytes.fromhex(c["root"])
+            if r not in roots:
+                roots.append(r)
+            jr.append(roots.index(r))
+            t.append(c["t"])
+            sigs += [bytes.fromhex(s) for s in c["sigs"]]
+            pks += [bytes.fromhex(p) for p in c["pks"]]
+            ids += c["ids"]
+            offs.append(len(sigs))
+    return roots, t, offs, sigs, pks, ids, jr
+
+
+@pytest.mark.parametrize("subset", ["all", "valid"])
+def test_golden_cases_one_stream_fused(engine, subset):
+    """The fixture jobs replicated into a batch large enough for the fused one-stream path (per-root
+    G1 bucket MSM, the counting sort riding along the decode and the subgroup checks, the hash
+    stages along the batch's kernels) on one-stream slots -- the configuration bench.py times.
+    'all' holds the non-subgroup, infinity, bad-encoding and wrong-root shares (the batch check
+    fails into the exact fallback); 'valid' only passing jobs (the batch check passes).  Every
+    status, combined signature and share verdict == the fixture, on two consecutive slots."""
+    cases = _load("threshold_cases.json")["cases"]
+    if subset == "valid":
+        cases = [c for c in cases if all(c["share_verdicts"]) and c["expected_status"] == 0]
+    reps = 1
+    while True:
+        roots, t, offs, sigs, pks, ids, jr = _golden_batch(cases, reps)
+        if len(sigs) >= 128 * len(roots) + 64:
+            break
+        reps += 1
+    lib = engine._lib
+    assert lib.ssb_set_slot_streams(engine.handle, 1) == 0, lib.ssb_last_error(engine.handle)
+    assert lib.ssb_set_pipeline_depth(engine.handle, 2) == 0, lib.ssb_last_error(engine.handle)
+    try:
+        for _ in range(2):
+            out, st, err, ver = engine.threshold_aggregate_batch_raw(t, offs, b"".join(sigs), b"".join(pks), ids, jr, roots)
+            for k in range(len(t)):
+                c = cases[k % len(cases)]
+                assert int(st[k]) == c["expected_status"], c["name"]
+                if c["expected_status"] == 0:
+                    assert out[k].tobytes().hex() == c["expected_sig"], c["name"]
+                elif c["expected_status"] in (2, 4):
+                    assert [int(err[k, 0]), int(err[k, 1])] == c["expected_payload"], c["name"]
+                assert [bool(v) for v in ver[offs[k]:offs[k + 1]]] == c["share_verdicts"], c["name"]
+    finally:
+        lib.ssb_set_pipeline_depth(engine.handle, 1)
+        lib.ssb_set_slot_streams(engine.handle, 3)
