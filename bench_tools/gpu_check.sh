@@ -11,7 +11,7 @@ if [ "$MODE" != "notests" ]; then
   tail -3 $OUT/tests.log
 fi
 echo "[gpu_check] bench"
-timeout -k 10 300 python -u bench.py --steps $STEPS --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+timeout -k 10 300 python -u bench.py --steps $STEPS --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 echo "[gpu_check] rocprof"
 GPU_MAX_HW_QUEUES=20 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
