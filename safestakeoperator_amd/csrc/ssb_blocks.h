@@ -54,23 +54,19 @@ SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t ba
   jac_set_inf(acc);
   if (ob < nb) {
     const uint32_t s = start[key], e = s + cnt[key];
-    // software pipelined: the next entry's point is in flight while this one is added
-    uint32_t x = s + j, fl = 0;
-    aff<F> q;
-    if (x < e) { const uint32_t i = ent[x]; fl = flags[i]; q = pts[i]; }
-    while (x < e) {
-      const uint32_t xn = x + J;
-      uint32_t fn = 0;
-      aff<F> qn;
-      if (xn < e) { const uint32_t i = ent[xn]; fn = flags[i]; qn = pts[i]; }
-      if (fl & FLAG_CANDIDATE) jac_add_aff_inl(acc, acc, q);
-      q = qn; fl = fn; x = xn;
+    // one point live: with the tree's addition inlined too, the body fits 256 registers and the
+    // bucket launch runs two waves per SIMD, which hide each other's latency (round 2: the former
+    // software-pipelined loop, two points live, held 256 VGPRs + 165 AGPRs = one wave per SIMD;
+    // C2 at 20 steps 11.2 -> 12.1 M partial sigs/s)
+    for (uint32_t x = s + j; x < e; x += J) {
+      const uint32_t i = ent[x];
+      if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pts[i]; jac_add_aff_inl(acc, acc, q); }
     }
   }
   for (int h = J >> 1; h >= 1; h >>= 1) {
     sh[lane] = acc;
     __syncthreads();
-    if (j < h) { jac<F> o = sh[lane + h]; jac_add(acc, acc, o); }
+    if (j < h) { jac<F> o = sh[lane + h]; jac_add_inl(acc, acc, o); }
     __syncthreads();
   }
   if (j == 0 && ob < nb) bsum[b] = acc;

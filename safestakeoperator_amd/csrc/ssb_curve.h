@@ -103,7 +103,7 @@ template <class F> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, cons
 template <class F> SSB_FN void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) { jac_add_aff_inl(r, p, q); }
 
 // add-2007-bl: general Jacobian addition with the special cases.
-template <class F> SSB_FN void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
+template <class F> SSB_INL void jac_add_inl(jac<F>& r, const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) { r = q; return; }
   if (jac_is_inf(q)) { r = p; return; }
   F Z1Z1, Z2Z2, U1, U2, S1, S2, H, I, J, rr, V, t;
@@ -116,7 +116,7 @@ template <class F> SSB_FN void jac_add(jac<F>& r, const jac<F>& p, const jac<F>&
   f_sub(H, U2, U1);
   f_sub(rr, S2, S1);
   if (f_is_zero(H)) {
-    if (f_is_zero(rr)) jac_dbl(r, p); else jac_set_inf(r);
+    if (f_is_zero(rr)) jac_dbl_inl(r, p); else jac_set_inf(r);
     return;
   }
   f_dbl(rr, rr);
@@ -129,6 +129,7 @@ template <class F> SSB_FN void jac_add(jac<F>& r, const jac<F>& p, const jac<F>&
   f_add(z3, p.z, q.z); f_sqr(z3, z3); f_sub(z3, z3, Z1Z1); f_sub(z3, z3, Z2Z2); f_mul(z3, z3, H);
   r.x = x3; r.y = y3; r.z = z3;
 }
+template <class F> SSB_FN void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) { jac_add_inl(r, p, q); }
 
 template <class F> SSB_FN void jac_to_aff(aff<F>& r, const jac<F>& p) {
   if (jac_is_inf(p)) { f_set_zero(r.x); f_set_zero(r.y); r.inf = 1; return; }

@@ -75,8 +75,11 @@ SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, const uint32_t* __restrict_
 
 // blocks [0, nbd): signature decode; [nbd, 2 nbd): public keys (gathered from the cache, or
 // decoded); [2 nbd, 3 nbd): the sort's count pass
+#ifndef SSB_DC_WAVES   // experiment knob: waves per SIMD the decode launch is built for
+#define SSB_DC_WAVES 2
+#endif
 template <bool CACHED>
-__global__ void SSB_LB2(64) k_decode_count(int n, uint32_t nbd, const uint8_t* __restrict__ sig96,
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_DC_WAVES))) k_decode_count(int n, uint32_t nbd, const uint8_t* __restrict__ sig96,
                                            const uint8_t* __restrict__ pk48, const uint32_t* __restrict__ pk_index,
                                            uint32_t n_cache, const g1_aff* __restrict__ cache_aff,
                                            const uint32_t* __restrict__ cache_flags, g2_aff* __restrict__ sig_aff,

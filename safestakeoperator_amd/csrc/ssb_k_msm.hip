@@ -103,7 +103,7 @@ __global__ void SSB_LB(256) k_order_scatter(uint32_t K, uint32_t K2, const uint3
 
 // ---- bucket sums (msm_bucket_block, ssb_blocks.h) ----
 template <class F>
-__global__ void SSB_LB(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
+__global__ void SSB_LB2(64) k_msm_bucket(uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
                                                    const uint32_t* __restrict__ start,
                                                    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ flags, const aff<F>* __restrict__ pts,
@@ -278,7 +278,7 @@ struct msm_bucket_args {
 // hash_to_G2 stages riding along (nblk of their own; 0 = none): the SWU map beside the subgroup
 // checks, the cofactor clearing beside the bucket sums, the affine output beside the window sums
 struct h2c_fuse { int n; const fp2* u; g2_aff* q; g2_jac* hj; uint32_t* exc; int exact_all; g2_aff* out; };
-__global__ void SSB_LB(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
+__global__ void SSB_LB2(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
                                          const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig,
                                          const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1) {
   __shared__ g2_jac sh[64];
