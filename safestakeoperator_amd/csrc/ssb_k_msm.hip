@@ -278,7 +278,13 @@ struct msm_bucket_args {
 // hash_to_G2 stages riding along (nblk of their own; 0 = none): the SWU map beside the subgroup
 // checks, the cofactor clearing beside the bucket sums, the affine output beside the window sums
 struct h2c_fuse { int n; const fp2* u; g2_aff* q; g2_jac* hj; uint32_t* exc; int exact_all; g2_aff* out; };
-__global__ void SSB_LB2(64) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
+#ifndef SSB_B2_WAVES   // experiment knob: waves per SIMD of the fused bucket launch
+#define SSB_B2_WAVES 2
+#endif
+#ifndef SSB_SG_WAVES   // experiment knob: waves per SIMD of the subgroup-check launch
+#define SSB_SG_WAVES 2
+#endif
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_B2_WAVES))) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
                                          const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig,
                                          const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1) {
   __shared__ g2_jac sh[64];
@@ -397,7 +403,7 @@ __global__ void SSB_LB2(64) k_subgroup_fix(int n, const uint32_t* __restrict__ s
 // a subgroup lane also writes the share's combined flags (k_flags) when sc.flags is given
 struct sort_scatter { int n; rlc_key key; const uint32_t* share_root; msm_cfg c2, c1; uint32_t* cur; uint32_t* ent;
                       const uint32_t* pflags; uint32_t n_roots; uint32_t* flags; };
-__global__ void SSB_LB2(64) k_subgroup_map(int n, uint32_t nbs, const uint32_t* __restrict__ sflags,
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_SG_WAVES))) k_subgroup_map(int n, uint32_t nbs, const uint32_t* __restrict__ sflags,
                                            const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags, h2c_fuse h,
                                            uint32_t nbm, sort_scatter sc) {
   __shared__ h2c_cand cs[64];
