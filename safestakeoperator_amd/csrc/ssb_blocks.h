@@ -44,7 +44,7 @@ SSB_INL void msm_sort_lane(int i, const rlc_key& key, const uint32_t* __restrict
 // G1 side's blocks side by side: k_msm_bucket2 / k_msm_window2 below)
 template <class F>
 SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
-                              const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                              const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
                               const uint32_t* __restrict__ ent, const uint32_t* __restrict__ flags,
                               const aff<F>* __restrict__ pts, jac<F>* __restrict__ bsum) {
   const int lane = threadIdx.x, J = 1 << lj, j = lane & (J - 1);
@@ -53,7 +53,9 @@ SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t ba
   jac<F> acc;
   jac_set_inf(acc);
   if (ob < nb) {
-    const uint32_t s = start[key], e = s + cnt[key];
+    // end[key]: the scatter's cursor, start + count after the scatter (the counts themselves are
+    // zeroed by the scan for the slot's next batch)
+    const uint32_t s = start[key], e = end[key];
     // one point live: with the tree's addition inlined too, the body fits 256 registers and the
     // bucket launch runs two waves per SIMD, which hide each other's latency (round 2: the former
     // software-pipelined loop, two points live, held 256 VGPRs + 165 AGPRs = one wave per SIMD;

@@ -29,7 +29,7 @@ __global__ void SSB_LB(64) k_prep_fused(uint32_t nz, uint32_t K, uint32_t* __res
 
 // One wave: start[] = cur[] = exclusive scan of cnt[0..K), then the bucket order (within each MSM's
 // key range, by count, largest first -- the k_order_* kernels' order).  sh: 64 + 512 words of LDS.
-SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
+SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, uint32_t* __restrict__ cnt, uint32_t* __restrict__ start,
                             uint32_t* __restrict__ cur, uint32_t* __restrict__ order, uint32_t* sh) {
   uint32_t* bins = sh + 64;
   const int t = threadIdx.x;
@@ -70,6 +70,7 @@ SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, const uint32_t* __restrict_
   for (uint32_t k = k0; k < k1; ++k) {
     const uint32_t c = cnt[k];
     order[atomicAdd(&bins[(k >= K2 ? 256u : 0u) + 255u - (c < 255u ? c : 255u)], 1u)] = k;
+    cnt[k] = 0u;   // dead from here (the buckets read the cursors): clean for the slot's next batch
   }
 }
 
@@ -78,6 +79,8 @@ SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, const uint32_t* __restrict_
 #ifndef SSB_DC_WAVES   // experiment knob: waves per SIMD the decode launch is built for
 #define SSB_DC_WAVES 2
 #endif
+// (blocks [3 nbd, 3 nbd + nbu): the hash's first stage, one lane per root, when the slot's counts
+// and tickets are already clean -- then no prep launch stands in front of the decode)
 template <bool CACHED>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_DC_WAVES))) k_decode_count(int n, uint32_t nbd, const uint8_t* __restrict__ sig96,
                                            const uint8_t* __restrict__ pk48, const uint32_t* __restrict__ pk_index,
@@ -87,8 +90,21 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
                                            uint32_t* __restrict__ pflags, rlc_key key, const uint32_t* __restrict__ share_root,
                                            msm_cfg c2, msm_cfg c1, uint32_t* __restrict__ cnt, uint32_t K,
                                            uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
-                                           uint32_t* __restrict__ order, uint32_t* __restrict__ tickets) {
+                                           uint32_t* __restrict__ order, uint32_t* __restrict__ tickets,
+                                           int n_roots, const uint8_t* __restrict__ roots, dst_arg dst,
+                                           fp2* __restrict__ u) {
   const uint32_t part = blockIdx.x / nbd;
+  if (part >= 3) {
+    const int i = (int)(blockIdx.x - 3 * nbd) * 64 + threadIdx.x;
+    if (i >= n_roots) return;
+    uint8_t m[32];
+    for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
+    fp2 u0, u1;
+    h2c_field(u0, u1, m, dst.b, dst.len, 32);
+    u[2 * i] = u0;
+    u[2 * i + 1] = u1;
+    return;
+  }
   const int s = (blockIdx.x - part * nbd) * 64 + threadIdx.x;
   if (part == 2) {   // count pass; the last count block to finish runs the scans
     __shared__ uint32_t sh[64 + 512];
@@ -103,6 +119,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
     if (last) {
       __threadfence();
       sort_scan_wave(K, c1.base, cnt, start, cur, order, sh);
+      if (threadIdx.x == 0) tickets[0] = 0u;   // every count block has passed: clean for the next batch
     }
     return;
   }
@@ -140,17 +157,22 @@ void prep_fused(hipStream_t st, const fused_sort& fs, int n_roots, const uint8_t
 
 void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
                   uint32_t n_cache, const g1_aff* cache_aff, const uint32_t* cache_flags, g2_aff* sig_aff, g1_aff* pk_aff,
-                  uint32_t* sflags, uint32_t* pflags, const fused_sort& fs) {
+                  uint32_t* sflags, uint32_t* pflags, const fused_sort& fs, int n_roots, const uint8_t* roots,
+                  const dst_arg* dst, const h2c_ws* hw) {
   if (n <= 0) return;
   const uint32_t nbd = (uint32_t)(n + 63) / 64;
+  const bool u = dst && hw && n_roots > 0;
+  const uint32_t nbu = u ? (uint32_t)(n_roots + 63) / 64 : 0u;
+  const dst_arg d = u ? *dst : dst_arg{};
+  fp2* uo = u ? hw->u : nullptr;
   if (pk_index)
-    hipLaunchKernelGGL(k_decode_count<true>, dim3(3 * nbd), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
+    hipLaunchKernelGGL(k_decode_count<true>, dim3(3 * nbd + nbu), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
                        cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt,
-                       fs.K, fs.start, fs.cur, fs.order, fs.tickets);
+                       fs.K, fs.start, fs.cur, fs.order, fs.tickets, u ? n_roots : 0, roots, d, uo);
   else
-    hipLaunchKernelGGL(k_decode_count<false>, dim3(3 * nbd), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
+    hipLaunchKernelGGL(k_decode_count<false>, dim3(3 * nbd + nbu), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
                        cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt,
-                       fs.K, fs.start, fs.cur, fs.order, fs.tickets);
+                       fs.K, fs.start, fs.cur, fs.order, fs.tickets, u ? n_roots : 0, roots, d, uo);
 }
 
 

@@ -341,14 +341,18 @@ __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* _
   if (bid < nblk1) {
     if (!tl.tickets) { msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1); return; }
     if (bid * 64 + threadIdx.x < ngw1) msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1);
-    if (last_block(&tl.tickets[1], nblk1, &last))
+    if (last_block(&tl.tickets[1], nblk1, &last)) {
       for (int g = threadIdx.x; g < tl.ngroups1; g += 64) msm_horner_lane(g, c1, tl.W1, w1, tl.root_sum);
+      if (threadIdx.x == 0) tl.tickets[1] = 0u;   // clean for the slot's next batch
+    }
     return;
   }
   bid -= nblk1;
   h2c_clear_block(bid, (fp*)lds, h.n, h.q, h.hj, h.exc);
-  if (tl.tickets && last_block(&tl.tickets[2], (uint32_t)(h.n + 7) / 8, &last))
+  if (tl.tickets && last_block(&tl.tickets[2], (uint32_t)(h.n + 7) / 8, &last)) {
     for (uint32_t b = 0; b * 64 < (uint32_t)h.n; ++b) h2c_affine_block(b, h.n, h.q, h.hj, h.exc, h.exact_all, h.out);
+    if (threadIdx.x == 0) tl.tickets[2] = 0u;
+  }
 }
 
 // ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----

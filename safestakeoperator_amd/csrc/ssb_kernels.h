@@ -181,9 +181,12 @@ void subgroup_map(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* s
 void prep_fused(hipStream_t st, const fused_sort& fs, int n_roots, const uint8_t* roots, const dst_arg& dst, const h2c_ws& hw);
 // decode (signatures; public keys decoded or gathered from the cache) + the sort's count pass; the
 // last count block to finish scans the counts (start, cursor) and orders the buckets
+// (with dst and hw: the hash's first stage of n_roots roots rides along -- the slot's counts and
+// tickets were left clean by its previous batch, so no prep launch runs in front)
 void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
                   uint32_t n_cache, const g1_aff* cache_aff, const uint32_t* cache_flags, g2_aff* sig_aff, g1_aff* pk_aff,
-                  uint32_t* sflags, uint32_t* pflags, const fused_sort& fs);
+                  uint32_t* sflags, uint32_t* pflags, const fused_sort& fs, int n_roots = 0, const uint8_t* roots = nullptr,
+                  const dst_arg* dst = nullptr, const h2c_ws* hw = nullptr);
 // (the exclusive scan of the counts and the bucket order run in decode_count's last count block)
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups

@@ -56,6 +56,12 @@ struct ssb_slot {
   // workspace arena (grown on demand, never shrunk)
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  // the fused one-stream path leaves the sort counts [0, clean_K) at clean_cnt and the tickets at
+  // clean_tickets zeroed for the slot's next batch (its scan and its last blocks reset them); any
+  // other use of the workspace clears this, and the next batch zeroes them in a prep launch
+  uint32_t* clean_cnt = nullptr;
+  uint32_t* clean_tickets = nullptr;
+  uint32_t clean_K = 0;
 };
 constexpr int SSB_MAX_SLOTS = 24;
 
@@ -129,12 +135,14 @@ struct carve {
 
 // Every entry point takes the slot's workspace through here: the slot's main stream is ordered
 // after the end of the slot's previous batch (whose last kernels run on the context streams).
-int ensure_ws(ssb_ctx* ctx, size_t bytes) {
+int ensure_ws(ssb_ctx* ctx, size_t bytes, bool verify_layout = false) {
   ssb_slot* S = ctx->cur;
   if (S->out_pending && !S->out_on_stream) {   // (a same-stream wait would only add a queue packet)
     if (hipStreamWaitEvent(S->stream, S->ev_out, 0) != hipSuccess) { ctx->err = "hipStreamWaitEvent failed"; return SSB_EHIP; }
   }
+  if (!verify_layout) S->clean_cnt = nullptr;   // another layout overwrites the counts (see run_verify)
   if (bytes <= ctx->cur->ws_bytes) return SSB_OK;
+  S->clean_cnt = nullptr;
   if (S->out_pending) hipEventSynchronize(S->ev_out);
   if (ctx->cur->ws) { hipStreamSynchronize(ctx->cur->stream); hipFree(ctx->cur->ws); ctx->cur->ws = nullptr; ctx->cur->ws_bytes = 0; }
   size_t want = bytes + bytes / 4;
@@ -425,8 +433,19 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     SSB_HIP(hipEventRecord(ctx->cur->ev_in, st));
     SSB_HIP(hipStreamWaitEvent(sh, ctx->cur->ev_in, 0));
   }
-  if (fuse_sort) {
+  // counts and tickets left clean by the slot's previous batch (same workspace layout): no prep
+  // launch -- the hash's first stage rides along the decode instead.  A small launch in front of
+  // the decode waited for a free wave slot behind the other slots' decode waves (~1.5 ms on the
+  // last batches of the driver's run, profiles/r02_gate_timeline.txt)
+  const bool clean = fuse_sort && n && ctx->cur->clean_cnt == w.cnt && ctx->cur->clean_tickets == w.tickets &&
+                     ctx->cur->clean_K >= P.K && !getenv("SSB_ALWAYS_PREP");
+  // this batch's counts / tickets are clean at its end only on the fused path (its scan and last
+  // blocks reset them); any other path writes the workspace without leaving them clean
+  if (fuse_sort) { ctx->cur->clean_cnt = w.cnt; ctx->cur->clean_tickets = w.tickets; ctx->cur->clean_K = P.K; }
+  else ctx->cur->clean_cnt = nullptr;
+  if (fuse_sort && !clean) {
     launch::prep_fused(st, fs, (int)n_roots, d_roots, dst, hw);
+  } else if (fuse_sort) {
   } else if (fuse_hash) {
     launch::h2c_u(st, (int)n_roots, d_roots, dst, hw);
   } else {
@@ -436,7 +455,8 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   if (fuse_sort) {
     timed t(ctx, "k_decode");
     launch::decode_count(st, (int)n, d_sig, d_pk, d_pk_index, (uint32_t)ctx->pkc_n, (const g1_aff*)ctx->pkc_aff,
-                         (const uint32_t*)ctx->pkc_flags, w.sig_aff, w.pk_aff, w.sflags, w.pflags, fs);
+                         (const uint32_t*)ctx->pkc_flags, w.sig_aff, w.pk_aff, w.sflags, w.pflags, fs, (int)n_roots,
+                         d_roots, clean ? &dst : nullptr, clean ? &hw : nullptr);
   } else if (n) {
     timed t(ctx, "k_decode");
     if (d_pk_index) {
@@ -479,14 +499,14 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   if (fused) {
     if (n) on_decoded();
     timed t(ctx, "k_msm_g2");
-    launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
+    launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cur, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
                      w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p, fuse_hash ? &hw : nullptr,
                      (int)n_roots, w.H, fuse_sort ? w.tickets : nullptr);
   } else {
   if (s1 != st) SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
     timed t(ctx, "k_msm_g1", s1);
-    launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cnt, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p, w.redo1);
+    launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cur, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p, w.redo1);
   } else {
     timed t(ctx, "k_sum_g1", s1);
     hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)n_roots), dim3(SEG_THREADS), 0, s1, (int)n_roots, w.rstart, w.rcnt, w.perm,
@@ -494,7 +514,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   if (s1 != st) SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
   if (n) on_decoded();
-  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cnt, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w2, w.redo2); }
+  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cur, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w2, w.redo2); }
   }
   if (!fused && s1 != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   if (!fuse_hash && sh != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
@@ -834,7 +854,7 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   size_t io = align_up(n * 48) + align_up(n * 96) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n);
   if ((rc = ensure_io(ctx, io))) return rc;
-  if ((rc = ensure_ws(ctx, verify_ws_bytes(n, n_roots)))) return rc;
+  if ((rc = ensure_ws(ctx, verify_ws_bytes(n, n_roots), true))) return rc;
   carve ci{(char*)ctx->io};
   uint8_t* d_pk = ci.take<uint8_t>(n * 48); uint8_t* d_sig = ci.take<uint8_t>(n * 96);
   uint32_t* d_root = ci.take<uint32_t>(n); uint8_t* d_roots = ci.take<uint8_t>(n_roots * 32); uint8_t* d_v = ci.take<uint8_t>(n);
@@ -871,7 +891,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   const size_t n = n_shares;
   size_t need = verify_ws_bytes(n, n_roots) + align_up(n * 4) * 3 + align_up(n) + align_up(n * sizeof(fr)) +
                 align_up(4 * n * sizeof(g2_jac)) + align_up(n_jobs * 4);
-  if ((rc = ensure_ws(ctx, need))) return rc;
+  if ((rc = ensure_ws(ctx, need, true))) return rc;
   hipStream_t user = (hipStream_t)stream;
   const bool on_slot = post_on_slot(ctx->cur);
   hipStream_t st = ctx->cur->stream, sc = ctx->spec, tl = on_slot ? st : slot_tail(ctx);
@@ -949,7 +969,7 @@ int verify_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint32_t* pk_i
   SSB_HIP(hipSetDevice(ctx->device));
   pick_slot(ctx, stream);
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
-  if ((rc = ensure_ws(ctx, verify_ws_bytes(n, n_roots)))) return rc;
+  if ((rc = ensure_ws(ctx, verify_ws_bytes(n, n_roots), true))) return rc;
   hipStream_t user = (hipStream_t)stream, st = ctx->cur->stream;
   if (user != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_user, user));

@@ -466,7 +466,10 @@ def test_golden_cases_one_stream_fused(engine, subset):
     stages along the batch's kernels) on one-stream slots -- the configuration bench.py times.
     'all' holds the non-subgroup, infinity, bad-encoding and wrong-root shares (the batch check
     fails into the exact fallback); 'valid' only passing jobs (the batch check passes).  Every
-    status, combined signature and share verdict == the fixture, on two consecutive slots."""
+    status, combined signature and share verdict == the fixture, five batches on two slots: a
+    reused slot starts from the counts and tickets its previous batch left zeroed (no prep
+    launch), and a hash_to_G2 call on a slot in between (another workspace layout) must send that
+    slot's next batch back through the prep launch."""
     cases = _load("threshold_cases.json")["cases"]
     if subset == "valid":
         cases = [c for c in cases if all(c["share_verdicts"]) and c["expected_status"] == 0]
@@ -479,8 +482,12 @@ def test_golden_cases_one_stream_fused(engine, subset):
     lib = engine._lib
     assert lib.ssb_set_slot_streams(engine.handle, 1) == 0, lib.ssb_last_error(engine.handle)
     assert lib.ssb_set_pipeline_depth(engine.handle, 2) == 0, lib.ssb_last_error(engine.handle)
+    hc = _load("hash_to_g2.json")["cases"][:2]
     try:
-        for _ in range(2):
+        for it in range(5):
+            if it == 3:   # another entry point carves the next slot's workspace differently
+                got = engine.hash_to_g2([bytes.fromhex(c["msg"]) for c in hc])
+                assert [o.hex() for o in got] == [c["out192"] for c in hc]
             out, st, err, ver = engine.threshold_aggregate_batch_raw(t, offs, b"".join(sigs), b"".join(pks), ids, jr, roots)
             for k in range(len(t)):
                 c = cases[k % len(cases)]
