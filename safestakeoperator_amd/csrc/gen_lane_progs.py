@@ -471,6 +471,9 @@ def programs():
     define("FP12_MUL", 12, 12, 64, lambda: flat12(f12_mul(sym_fp12(A), sym_fp12(B))))
     define("FP12_SQR", 12, 0, 64, lambda: flat12(f12_sqr(sym_fp12(A))))
     define("FP12_CYC_SQR", 12, 0, 64, lambda: flat12(f12_cyc_sqr(sym_fp12(A))))
+    # two cyclotomic squarings in one program: the second squaring's operands are formed from the
+    # first one's products directly (accumulator forms), so the first output stage disappears
+    define("FP12_CYC_SQR2", 12, 0, 64, lambda: flat12(f12_cyc_sqr(f12_cyc_sqr(sym_fp12(A)))))
     define("FP12_CONJ", 12, 0, 64, lambda: flat12(f12_conj(sym_fp12(A))))
     for n in (1, 2, 3):
         define("FP12_FROB%d" % n, 12, 0, 64, lambda n=n: flat12(f12_frob(sym_fp12(A), n)))

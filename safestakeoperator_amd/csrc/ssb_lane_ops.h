@@ -203,18 +203,27 @@ SSB_INL void st12(lfp* s, const fp12& f) {
 }
 template <class GR> SSB_INL void f12_mul(GR& g, int a, int b, int d) { g.a = a; g.b = b; g.d = d; lp_fp12_mul(g); }
 template <class GR> SSB_INL void f12_cyc_sqr(GR& g, int a, int d) { g.a = a; g.d = d; lp_fp12_cyc_sqr(g); }
+template <class GR> SSB_INL void f12_cyc_sqr2(GR& g, int a, int d) { g.a = a; g.d = d; lp_fp12_cyc_sqr2(g); }
 template <class GR> SSB_INL void f12_conj(GR& g, int a, int d) { g.a = a; g.d = d; lp_fp12_conj(g); }
 template <class GR> SSB_INL void f12_frob(GR& g, int n, int a, int d) {
   g.a = a; g.d = d;
   if (n == 1) lp_fp12_frob1(g); else if (n == 2) lp_fp12_frob2(g); else lp_fp12_frob3(g);
 }
 
-// r = f^x (x = -0xd201000000010000), f cyclotomic; r != f
+// r = f^x (x = -0xd201000000010000), f cyclotomic; r != f.  The runs of squarings between the
+// multiplications (1, 2, 3, 9, 32, 16) go two at a time through lp_fp12_cyc_sqr2 (three program
+// stages instead of four: the first squaring's output stage is folded into the second's operands)
 template <class GR> SSB_INL void f12_cyc_exp_x(GR& g, int r, int f) {
   lg_copy<64>(g, f, r, 12);
+  int run = 0;
   for (int i = 62; i >= 0; --i) {
-    f12_cyc_sqr(g, r, r);
-    if ((BLS_X_ABS >> i) & 1ull) f12_mul(g, r, f, r);
+    ++run;
+    const bool bit = ((BLS_X_ABS >> i) & 1ull) != 0;
+    if (bit || i == 0) {
+      for (; run >= 2; run -= 2) f12_cyc_sqr2(g, r, r);
+      if (run) { f12_cyc_sqr(g, r, r); run = 0; }
+      if (bit) f12_mul(g, r, f, r);
+    }
   }
   f12_conj(g, r, r);
 }
