@@ -329,6 +329,73 @@ SSB_INL void mp_mont_mul_fips4(uint32_t* r, const uint32_t* a, const uint32_t* b
   for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
 }
 
+// r = (a*b + c*d) / 2^(32N) mod m: the FIPS product with BOTH products summed into each column
+// before the column's reduction MACs -- one Montgomery reduction for a sum of two products (lazy
+// reduction).  Inputs a, b, c < m and d <= m: a*b + c*d < 2 m^2 < m 2^(32N), so the result is < 2m
+// before the final conditional subtraction; a column holds at most 3N products, (acc, top) 96 bits.
+// The columns are generated by template recursion (a plain unrolled loop of this size is not
+// unrolled by the compiler, and the limb arrays then go to scratch).
+template <int N, int K>
+struct mont2_col {
+  SSB_INL static void run(uint32_t* m, uint32_t* t, uint64_t& acc, uint32_t& top, const uint32_t* a, const uint32_t* b,
+                          const uint32_t* c, const uint32_t* d, const uint32_t* mod, uint32_t minv) {
+    constexpr int jlo = K - (N - 1) > 0 ? K - (N - 1) : 0;
+    constexpr int jhi = K < N - 1 ? K : N - 1;
+    constexpr int mhi = K - 1 < N - 1 ? K - 1 : N - 1;
+#pragma unroll
+    for (int j = jlo; j <= jhi; j += 4) {
+      const int left = jhi - j + 1;
+      if (left >= 4) SSB_MAC4(SSB_V, SSB_V, acc, top, a[j], b[K - j], a[j + 1], b[K - j - 1], a[j + 2], b[K - j - 2], a[j + 3], b[K - j - 3]);
+      else if (left >= 2) { SSB_MAC2(SSB_V, SSB_V, acc, top, a[j], b[K - j], a[j + 1], b[K - j - 1]); if (left == 3) SSB_MAC(acc, top, a[j + 2], b[K - j - 2]); }
+      else SSB_MAC(acc, top, a[j], b[K - j]);
+    }
+#pragma unroll
+    for (int j = jlo; j <= jhi; j += 4) {
+      const int left = jhi - j + 1;
+      if (left >= 4) SSB_MAC4(SSB_V, SSB_V, acc, top, c[j], d[K - j], c[j + 1], d[K - j - 1], c[j + 2], d[K - j - 2], c[j + 3], d[K - j - 3]);
+      else if (left >= 2) { SSB_MAC2(SSB_V, SSB_V, acc, top, c[j], d[K - j], c[j + 1], d[K - j - 1]); if (left == 3) SSB_MAC(acc, top, c[j + 2], d[K - j - 2]); }
+      else SSB_MAC(acc, top, c[j], d[K - j]);
+    }
+#pragma unroll
+    for (int j = jlo; j <= mhi; j += 4) {
+      const int left = mhi - j + 1;
+      if (left >= 4) SSB_MAC4(SSB_V, SSB_S, acc, top, m[j], mod[K - j], m[j + 1], mod[K - j - 1], m[j + 2], mod[K - j - 2], m[j + 3], mod[K - j - 3]);
+      else if (left >= 2) { SSB_MAC2(SSB_V, SSB_S, acc, top, m[j], mod[K - j], m[j + 1], mod[K - j - 1]); if (left == 3) SSB_MACS(acc, top, m[j + 2], mod[K - j - 2]); }
+      else SSB_MACS(acc, top, m[j], mod[K - j]);
+    }
+    if (K < N) {
+      m[K < N ? K : 0] = (uint32_t)acc * minv;
+      SSB_MACS(acc, top, m[K < N ? K : 0], mod[0]);  // low word becomes 0
+    } else {
+      t[K >= N ? K - N : 0] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+    mont2_col<N, K + 1>::run(m, t, acc, top, a, b, c, d, mod, minv);
+  }
+};
+template <int N>
+struct mont2_col<N, 2 * N - 1> {
+  SSB_INL static void run(uint32_t*, uint32_t*, uint64_t&, uint32_t&, const uint32_t*, const uint32_t*, const uint32_t*,
+                          const uint32_t*, const uint32_t*, uint32_t) {}
+};
+template <int N>
+SSB_INL void mp_mont_mul2_fips4(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* c,
+                                const uint32_t* d, const uint32_t* mod, uint32_t minv) {
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+  uint32_t top = 0;
+  mont2_col<N, 0>::run(m, t, acc, top, a, b, c, d, mod, minv);
+  t[N - 1] = (uint32_t)acc;
+  uint32_t s2[N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s2[i] = subb(t[i], mod[i], br, br);
+  const bool keep = br != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = keep ? t[i] : s2[i];
+}
+
 // FIPS, two accumulators interleaved inside each asm chunk (halves the dependent chain).
 template <int N>
 SSB_INL void mp_mont_mul_fips4x2(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* mod,
@@ -777,16 +844,20 @@ SSB_INL void fp2_sub(fp2& r, const fp2& a, const fp2& b) { fp_sub(r.c0, a.c0, b.
 SSB_INL void fp2_dbl(fp2& r, const fp2& a) { fp_dbl(r.c0, a.c0); fp_dbl(r.c1, a.c1); }
 SSB_INL void fp2_neg(fp2& r, const fp2& a) { fp_neg(r.c0, a.c0); fp_neg(r.c1, a.c1); }
 SSB_INL void fp2_conj(fp2& r, const fp2& a) { r.c0 = a.c0; fp_neg(r.c1, a.c1); }
+// Schoolbook with lazy reduction: c0 = a0 b0 + a1 (p - b1), c1 = a0 b1 + a1 b0, each ONE Montgomery
+// reduction of a sum of two products (mp_mont_mul2_fips4): four products and two reductions, no
+// modular additions, instead of Karatsuba's three Montgomery products and five modular additions.
+// (Counted as three products, the algorithmic unit of the op counter.)
 SSB_INL void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
-  fp t0, t1, s0, s1, t2;
-  fp_mul(t0, a.c0, b.c0);
-  fp_mul(t1, a.c1, b.c1);
-  fp_add(s0, a.c0, a.c1);
-  fp_add(s1, b.c0, b.c1);
-  fp_mul(t2, s0, s1);
-  fp_sub(r.c0, t0, t1);
-  fp_sub(t2, t2, t0);
-  fp_sub(r.c1, t2, t1);
+  SSB_CNT(fp_mul); SSB_CNT(fp_mul); SSB_CNT(fp_mul);
+  fp nb1, c0, c1;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) nb1.l[i] = subb(P_LIMBS[i], b.c1.l[i], br, br);   // p - b1 in (0, p]
+  mp_mont_mul2_fips4<12>(c0.l, a.c0.l, b.c0.l, a.c1.l, nb1.l, P_LIMBS, P_INV32);
+  mp_mont_mul2_fips4<12>(c1.l, a.c0.l, b.c1.l, a.c1.l, b.c0.l, P_LIMBS, P_INV32);
+  r.c0 = c0;
+  r.c1 = c1;
 }
 SSB_INL void fp2_sqr(fp2& r, const fp2& a) {
   fp s, d, m;
