@@ -859,10 +859,19 @@ SSB_INL void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   r.c0 = c0;
   r.c1 = c1;
 }
+// (a0 + a1)(a0 - a1) with both factors left unreduced (< 2p): the Montgomery product accepts them
+// (4p^2 < p 2^384, the result is < 2p before its final subtraction), which saves the two modular
+// corrections of the sum and the difference
 SSB_INL void fp2_sqr(fp2& r, const fp2& a) {
   fp s, d, m;
-  fp_add(s, a.c0, a.c1);
-  fp_sub(d, a.c0, a.c1);
+  uint32_t c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) s.l[i] = addc(a.c0.l[i], a.c1.l[i], c, c);          // a0 + a1 < 2p
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d.l[i] = subb(P_LIMBS[i], a.c1.l[i], br, br);      // p - a1 in (0, p]
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d.l[i] = addc(d.l[i], a.c0.l[i], c, c);             // a0 - a1 + p < 2p
   fp_mul(m, a.c0, a.c1);
   fp_mul(r.c0, s, d);
   fp_dbl(r.c1, m);
