@@ -334,7 +334,7 @@ def main():
     V, t, n, n_roots = args.validators, args.threshold, args.operators, args.roots
     V_glob = V * (1 if strong else world)             # validators of the whole job (all ranks)
     eng = Engine(local)
-    from safestakeoperator_amd.shard import exchange, exchange_var, shard_jobs, shard_sizes
+    from safestakeoperator_amd.shard import BatchExchange, shard_jobs, shard_sizes
     sizes = None
     if strong:
         # this rank's contiguous, share-balanced slice of the ONE global batch (seed of rank 0, so the
@@ -383,23 +383,18 @@ def main():
     d_mpk = dt8(mpks) if args.final_verify else None
     use_cache = [not args.compressed_pk]
 
-    # host-buffer variant (reported beside the headline, never the value): the batch's inputs come
-    # from pinned host memory and its results go back to it, copied on the slot's stream around the
-    # engine call (PCIe inclusive)
+    # host-buffer variant (reported beside the headline, never the value): every batch's inputs
+    # start in ordinary host memory and its results end there, PCIe inclusive -- through the
+    # library's asynchronous host entry point (ssb_threshold_aggregate_batch[_cached]_submit /
+    # ssb_batch_wait): one host memcpy into the slot's pinned, device-mapped staging buffer, the
+    # kernels read it and write their outputs in place over PCIe, the outputs are delivered when the
+    # batch is waited for; up to S batches in flight
     use_host = [False]
-    host_io = {}
-
-    def host_bufs(k):
-        if k not in host_io:
-            pin = lambda t: t.cpu().pin_memory()
-            host_io[k] = dict(h_sig=pin(d_sig), h_ids=pin(d_ids), h_jr=pin(d_jr), h_roots=pin(d_roots),
-                              d_sig=torch.empty_like(d_sig), d_ids=torch.empty_like(d_ids), d_jr=torch.empty_like(d_jr),
-                              d_roots=torch.empty_like(d_roots),
-                              h_out=torch.empty((V, 96), dtype=torch.uint8).pin_memory(),
-                              h_st=torch.empty((V,), dtype=torch.int32).pin_memory(),
-                              h_err=torch.empty((V, 2), dtype=torch.int64).pin_memory(),
-                              h_ver=torch.empty((N,), dtype=torch.uint8).pin_memory())
-        return host_io[k]
+    host_io = {}                                   # slot -> the PendingBatch last submitted on it
+    h_in = dict(off=np.arange(0, N + 1, n, dtype=np.uint32), t=np.full(V, t, dtype=np.uint32),
+                sig=np.frombuffer(wl["sigs"], dtype=np.uint8), pk=np.frombuffer(wl["pks"], dtype=np.uint8),
+                pkidx=np.arange(0, N, dtype=np.uint32), ids=np.asarray(wl["ids"], dtype=np.uint64),
+                jr=np.asarray(wl["job_root"], dtype=np.uint32), roots=np.frombuffer(b"".join(wl["roots"]), dtype=np.uint8))
 
     def step(i, k):
         """batch i on pipeline slot k (engine slot k, output buffers k); the caller's stream is the
@@ -411,16 +406,16 @@ def main():
         fn = lib.ssb_threshold_aggregate_batch_cached_dev if use_cache[0] else lib.ssb_threshold_aggregate_batch_dev
         pk_arg = d_pkidx if use_cache[0] else d_pk
         src = dict(d_sig=d_sig, d_ids=d_ids, d_jr=d_jr, d_roots=d_roots)
+        if use_host[0]:   # (world == 1 only; the library picks slot k round robin like the _dev calls)
+            host_io[k] = eng.submit_batch_raw(h_in["t"], h_in["off"], h_in["sig"], h_in["pk"], h_in["ids"], h_in["jr"],
+                                              h_in["roots"], seed=(seed_base + i) & (2 ** 64 - 1),
+                                              pk_index=h_in["pkidx"] if use_cache[0] else None)
+            return
         with torch.cuda.stream(s):
             # the slot's output buffers are rewritten by this batch: order it after the all-gather
             # of the slot's previous batch (a stream wait, the host does not block)
             for w in pending.pop(k, []):
                 w.wait()
-            if use_host[0]:
-                hb = host_bufs(k)
-                for key in ("d_sig", "d_ids", "d_jr", "d_roots"):
-                    hb[key].copy_(hb["h" + key[1:]], non_blocking=True)
-                src = hb
             rc = fn(
                 eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), src["d_sig"].data_ptr(), pk_arg.data_ptr(),
                 src["d_ids"].data_ptr(), src["d_jr"].data_ptr(), n_roots, src["d_roots"].data_ptr(),
@@ -439,26 +434,22 @@ def main():
                          (seed_base + i + (1 << 32)) & (2 ** 64 - 1), o["fv"].data_ptr(), ctypes.c_void_p(s.cuda_stream))
                 if rc != 0:
                     raise RuntimeError("ssb_verify_batch_cached_dev: %s" % lib.ssb_last_error(eng.handle))
-            if use_host[0]:
-                hb["h_out"].copy_(o["out"], non_blocking=True)
-                hb["h_st"].copy_(o["st"], non_blocking=True)
-                hb["h_err"].copy_(o["err"], non_blocking=True)
-                hb["h_ver"].copy_(o["ver"], non_blocking=True)
-                if args.final_verify:
-                    hb.setdefault("h_fv", torch.empty((V,), dtype=torch.uint8).pin_memory()).copy_(o["fv"], non_blocking=True)
         group.append(k)
         if len(group) >= S:
             exchange_group()
 
     group = []      # slots whose results are not exchanged yet
+    xchg = BatchExchange(strong, sizes=sizes, device=cdev) if dist is not None else None
 
     def exchange_group():
         """RCCL all-gather over xGMI of the results of the batches since the last exchange, ONE
-        collective for the group (fewer, larger collectives: with one hardware queue per slot, an
-        all-gather per batch would keep RCCL's stream active beside the 20 slot queues, and past 20
-        active queues the firmware time-slices them).  Asynchronous: RCCL's stream waits for the
-        group's batches, no slot stream waits for RCCL -- only a slot's next batch, which rewrites
-        its output buffers, waits for the all-gather that reads them."""
+        collective per array for the group (fewer, larger collectives: with one hardware queue per
+        slot, an all-gather per batch would keep RCCL's stream active beside the 20 slot queues, and
+        past 20 active queues the firmware time-slices them).  Asynchronous: RCCL's stream waits
+        for the group's batches, no slot stream waits for RCCL -- only a slot's next batch, which
+        rewrites its output buffers, waits for the all-gather that reads them.  Weak scaling:
+        every rank's own batch (shard.exchange); strong: this rank's shard of the one global
+        batch, reassembled per batch in the global order (shard.exchange_var)."""
         if dist is None or not group:
             group.clear()
             return
@@ -468,14 +459,7 @@ def main():
                 ev = torch.cuda.Event()
                 ev.record(streams[k])
                 s.wait_event(ev)
-            cat = lambda key: torch.cat([outs[k][key] for k in group]).to(cdev)
-            g = len(group)
-            if strong:
-                _, works = exchange_var(cat("ver"), cat("out"), cat("st"), cat("err"),
-                                        sizes=[(a * g, b * g) for a, b in sizes], async_op=True)
-            else:
-                _, works = exchange(cat("ver"), cat("out"), cat("st"), async_op=True)
-        works = [w for w in works if w is not None]
+            works = xchg.flush([outs[k] for k in group])
         for k in group:
             pending[k] = works
         group.clear()
@@ -507,12 +491,30 @@ def main():
     if lib.ssb_set_slot_streams(eng.handle, args.slot_streams) != 0 or lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
         raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
     streams.clear()
-    msig = eng.sign_batch(wl["master"][:64], wl["job_root"][:64], wl["roots"])
+    # the master key's signature of every validator: every combined signature must equal it
+    # (tests/test_generic_threshold.rs:35), checked for every slot's batch, untimed
+    msig = eng.sign_batch(wl["master"], wl["job_root"], wl["roots"])
+    msig_arr = np.frombuffer(b"".join(msig), dtype=np.uint8).reshape(V, 96)
     primed = []
 
+    def check_slots(host=False):
+        """every slot's last batch: statuses, every share verdict and every combined signature (all
+        V validators) == the workload's truth; with host=True the copies in the pinned host buffers"""
+        ok = True
+        for k, o in enumerate(outs):
+            if host:
+                out_host, st_host, _, ver_host = host_io[k].wait()
+            else:
+                st_host, ver_host, out_host = o["st"].cpu().numpy(), o["ver"].cpu().numpy(), o["out"].cpu().numpy()
+            ok = ok and bool(((st_host == 0) == job_ok).all()) and bool((ver_host == valid).all())
+            ok = ok and bool((out_host[job_ok] == msig_arr[job_ok]).all())
+            if args.final_verify and not host:
+                fv = o["fv"].cpu().numpy()
+                ok = ok and bool(((fv == 1) == job_ok).all())
+        return ok
+
     def warm_and_check():
-        """warmup, then correctness of every slot's last batch: every share valid, every combine ==
-        the master signature"""
+        """warmup, then correctness of every slot's last batch"""
         if os.environ.get("SSB_PRIME", "1") != "0" and not primed:
             # first use of each slot's queue one at a time (untimed): 20 queues acquiring their
             # scratch at once intermittently failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES
@@ -525,15 +527,7 @@ def main():
             step(i, i % S)
         exchange_group()
         torch.cuda.synchronize(dev)
-        ok_st = ok_comb = True
-        for o in outs:
-            st_host = o["st"].cpu().numpy()
-            ok_st = ok_st and bool(((st_host == 0) == job_ok).all()) and bool((o["ver"].cpu().numpy() == valid).all())
-            out_host = o["out"].cpu().numpy()
-            ok_comb = ok_comb and all(out_host[v].tobytes() == msig[v] for v in range(min(64, V)) if job_ok[v])
-            if args.final_verify:
-                ok_comb = ok_comb and bool(((o["fv"].cpu().numpy() == 1) == job_ok).all())
-        return ok_st and ok_comb
+        return check_slots(host=use_host[0])
 
     def timed_run():
         if dist is not None:
@@ -563,6 +557,9 @@ def main():
         exchange_group()
         if gate is not None:
             gate.fill_(1)
+        if use_host[0]:
+            for pb in host_io.values():   # every batch's outputs delivered to host memory
+                pb.wait()
         torch.cuda.synchronize(dev)
         if dbg:
             print("host ms per submit:", " ".join("%.2f" % x for x in host_ms), file=sys.stderr)
@@ -573,19 +570,28 @@ def main():
         return time.perf_counter() - t0
 
     # the other public-key variant first (reported beside the headline), then the headline
+    # (after each timed run, untimed: the batches the timed steps produced -- the last one on every
+    # slot -- are checked like the warm-up ones, and for N > 1 the last exchange's gathered results)
     use_cache[0] = args.compressed_pk
     ok_other = warm_and_check()
     elapsed_other = timed_run()
+    ok_other = ok_other and check_slots()
     use_cache[0] = not args.compressed_pk
     ok_head = warm_and_check()
     elapsed = timed_run()
+    ok_timed = check_slots()
+    ok_x = True
+    if xchg is not None:
+        ok_x, _ = xchg.check_last()
     elapsed_host = None
-    if world == 1 and not args.no_host_buffers:
+    ok_host = True
+    if world == 1 and not args.no_host_buffers and not args.final_verify:
         use_host[0] = True
-        warm_and_check()
+        ok_host = warm_and_check()
         elapsed_host = timed_run()
+        ok_host = ok_host and check_slots(host=True)
         use_host[0] = False
-    ok_st = ok_comb = ok_head and ok_other
+    ok_st = ok_comb = ok_head and ok_other and ok_timed and ok_x and ok_host
     if dist is not None:
         tt = torch.tensor([elapsed, elapsed_other], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -645,9 +651,15 @@ def main():
                              "(ssb_verify_batch_cached_dev, RLC batch); combined_sigs_per_s counts verified ones" % V
                              if args.final_verify else None),
             "value_host_buffers": (round(V_glob * n * args.steps / elapsed_host, 1) if elapsed_host else None),
-            "host_buffers": "inputs H2D from pinned host memory and results D2H on the slot's stream around each "
-                            "batch (PCIe inclusive; the headline's inputs are resident in HBM)",
+            "host_buffers": "every batch's inputs start in, and its results end in, ordinary host memory: "
+                            "ssb_threshold_aggregate_batch%s_submit copies them into the slot's pinned device-mapped "
+                            "staging buffer, the kernels read / write it in place over PCIe, ssb_batch_wait delivers "
+                            "the outputs; timed from the first submit to the last delivery (the headline's inputs are "
+                            "resident in HBM)" % ("_cached" if not args.compressed_pk else ""),
             "results_ok": ok_all,
+            "results_checked": "every slot's last warm-up AND last timed batch: all %d statuses, %d share verdicts and "
+                               "combined signatures (== the master key's signature)%s" % (
+                                   V, N, "; the last exchange's gathered results == local" if world > 1 else ""),
             "invalid_shares_per_batch": wl["n_bad"],
             "roofline": {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),
                          "peak": round(peak, 2), "unit": "TMAD/s", "frac": round(achieved / peak, 5),
@@ -666,7 +678,7 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     torch.cuda.synchronize(dev)
-    host_io.clear()      # pinned host buffers released before the engine and the runtime go away
+    host_io.clear()
     streams.clear()
     eng.close()
 

@@ -21,6 +21,9 @@
  *                                     blst_p1_mult(h, s) == CommittedPoly::eval(party)
  *                                     (src/math/polynomial.rs:68-81), batched
  *   ssb_dleq_verify_batch          <- DKG::dleq_verify (src/crypto/dkg.rs:674-692), batched
+ *   ssb_pk_validate_batch          <- bls::PublicKey::deserialize (key_validate) + serialize, as
+ *                                     the reference deserializes operator / validator keys
+ *                                     (src/validation/operator_committee_definitions.rs:47-56)
  *   ssb_decode_wire_sigs           <- bincode::deserialize::<Signature>(&data) on a received
  *                                     partial signature (src/validation/operator.rs:108; the
  *                                     records are written by bincode::serialize(&sig),
@@ -42,9 +45,12 @@
  *     share index); `rlc_seed` is only XORed into that key.  The key never leaves the library, so a
  *     sender cannot craft shares whose errors cancel in the combination (see
  *     ssb_set_rlc_deterministic for the one exception).
- *   - Host-pointer functions copy inputs to the device and results back; they are synchronous.
- *     The *_dev variants take DEVICE pointers and a hipStream_t (as void*), enqueue everything
- *     on that stream and return without synchronising.
+ *   - Host-pointer functions copy inputs to the device and results back; they are synchronous
+ *     (ssb_threshold_aggregate_batch_submit / ssb_batch_wait is the asynchronous form).
+ *     The *_dev variants take DEVICE pointers -- or device-mapped pinned host memory
+ *     (hipHostMalloc(.., hipHostMallocMapped)), which the kernels then read and write in place
+ *     over PCIe -- and a hipStream_t (as void*), enqueue everything on that stream and return
+ *     without synchronising.
  *   - Return value of every function: SSB_OK or a negative SSB_E* code (ssb_last_error() has
  *     the message).  No C++ exception crosses this ABI.  A context must not be used by two
  *     threads at once (one context per thread, or an external mutex).
@@ -203,6 +209,31 @@ int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* s
                                   uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
                                   uint64_t* out_err, uint8_t* share_verdicts);
 
+/* Asynchronous form of ssb_threshold_aggregate_batch (same arguments and checks, plus `ticket`):
+ * the inputs are copied into the next pipeline slot's pinned, device-mapped staging buffer (a host
+ * memcpy; the caller's input buffers are free again on return), the batch is enqueued on that slot
+ * with its kernels reading the staging buffer in place over PCIe and writing their outputs there
+ * (zero-copy: no copy kernels, no copy queues), and the call returns.  ssb_batch_wait(ctx, ticket)
+ * blocks until the batch is done and copies its outputs to out_sig96 / out_status / out_err /
+ * share_verdicts, which the caller keeps valid until then.  A slot's previous host batch is
+ * delivered the same way before the slot is reused, so with ssb_set_pipeline_depth(S) up to S
+ * batches are in flight.  ssb_threshold_aggregate_batch = submit + wait. */
+int ssb_threshold_aggregate_batch_submit(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off,
+                                         const uint32_t* t, const uint8_t* sig96, const uint8_t* pk48,
+                                         const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                                         const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                         uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
+                                         uint64_t* out_err, uint8_t* share_verdicts, uint64_t* ticket);
+/* Same with public keys as indices into the ssb_pk_cache_set table (ssb_threshold_aggregate_batch_cached_dev). */
+int ssb_threshold_aggregate_batch_cached_submit(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off,
+                                                const uint32_t* t, const uint8_t* sig96, const uint32_t* pk_index,
+                                                const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                                                const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                                uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
+                                                uint64_t* out_err, uint8_t* share_verdicts, uint64_t* ticket);
+/* Wait for a submitted batch and deliver its outputs (SSB_OK at once if already delivered). */
+int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket);
+
 /* Same, all array arguments are device pointers; `stream` is a hipStream_t (NULL = default).
  * The caller owns the job shapes: share_off must be non-decreasing with share_off[n_jobs] ==
  * n_shares and 1 <= t[j] <= SSB_MAX_T; a job that breaks this (the library cannot check device
@@ -244,6 +275,13 @@ int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t
 
 /* SecretKey::public_key: out_pk48[i] = compress(sk_i * g1). */
 int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* out_pk48);
+
+/* bls::PublicKey::deserialize + PublicKey::serialize (lighthouse; blst key_validate), batched: out_valid[i]
+ * = 1 iff pk48[i] decodes (ZCash flags, x < p, on the curve), is not infinity and lies in G1; then
+ * out_pk48[i] is its recompression (equal to the input for a canonical encoding), else zeros.  The
+ * keys every other entry point takes are expected to have passed this (registration time; pinned
+ * by the keys the reference's own sources deserialize, tests/golden/reference_kats.json). */
+int ssb_pk_validate_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint8_t* out_valid, uint8_t* out_pk48);
 
 /* lagrange_coeffs for one id set: out 32-byte little-endian scalars (blst_scalar.b layout). */
 int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* out32);

@@ -1325,3 +1325,51 @@ int bls_oracle_selftest(void) {
   if (!g1_is_inf(&z)) return 2;
   return 0;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* public keys (G1): the reference's own known answers pin these                               */
+/* ------------------------------------------------------------------------------------------ */
+static void g1_compress(uint8_t* out, const g1_aff* a) {  /* blst_p1_affine_compress (ZCash flags) */
+  if (a->inf) { memset(out, 0, 48); out[0] = 0xc0; return; }
+  uint64_t l[6];
+  fp_from_mont(l, &a->x); limbs_to_be48(out, l);
+  out[0] |= 0x80;
+  if (fp_is_lex_largest(&a->y)) out[0] |= 0x20;
+}
+
+/* bls::SecretKey::deserialize(32-byte big-endian) -> public_key().serialize(): 0 < sk < r
+   (blst_sk_check), pk = [sk] g1 compressed.  Returns 1, or 0 for an invalid key.  Pinned by the
+   reference's KAT src/deposit/mod.rs:75-77. */
+int bls_oracle_sk_to_pk(const uint8_t* sk32be, uint8_t* out48) {
+  bls_oracle_init();
+  uint64_t k[4];
+  for (int i = 0; i < 4; ++i) {
+    uint64_t v = 0;
+    for (int b = 0; b < 8; ++b) v = (v << 8) | sk32be[8 * (3 - i) + b];
+    k[i] = v;
+  }
+  int lt = 0, nz = (k[0] | k[1] | k[2] | k[3]) != 0;
+  for (int i = 3; i >= 0; --i) if (k[i] != RL[i]) { lt = k[i] < RL[i]; break; }
+  if (!lt || !nz) return 0;
+  g1_jac g, p; g1_from_aff(&g, &G1_GEN);
+  g1_mul(&p, &g, k, 4);
+  g1_aff a; g1_to_aff(&a, &p);
+  g1_compress(out48, &a);
+  return 1;
+}
+
+/* bls::PublicKey::deserialize (lighthouse -> blst key_validate): a 48-byte compressed G1 point
+   that decodes, is not infinity and lies in G1 ([r]P == O).  Returns 1 and writes the point's
+   recompression (== the input for a canonical encoding), or 0. */
+int bls_oracle_pk_validate(const uint8_t* pk48, uint8_t* out48) {
+  bls_oracle_init();
+  g1_aff a;
+  memset(out48, 0, 48);
+  if (!g1_decompress(&a, pk48) || a.inf) return 0;
+  g1_jac p, z; g1_from_aff(&p, &a);
+  uint64_t r[4]; memcpy(r, RL, 32);
+  g1_mul(&z, &p, r, 4);
+  if (!g1_is_inf(&z)) return 0;
+  g1_compress(out48, &a);
+  return 1;
+}

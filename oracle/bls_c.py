@@ -38,6 +38,8 @@ def load():
         lib.bls_oracle_threshold_batch_rlc.argtypes = [ctypes.c_size_t, _u32p, _u32p, _u8p, _u8p, _u64p, _u32p,
                                                        ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, _i32p, _u64p,
                                                        _u8p, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        lib.bls_oracle_sk_to_pk.argtypes = [_u8p, _u8p]
+        lib.bls_oracle_pk_validate.argtypes = [_u8p, _u8p]
         lib.bls_oracle_init()
         _lib = lib
     return _lib
@@ -133,3 +135,21 @@ def threshold_batch_rlc(share_off, t, sigs96, pks48, ids, job_root, roots, threa
     if rc != 0:
         raise RuntimeError("bls_oracle_threshold_batch_rlc: %d" % rc)
     return out, st, err, ver, bool(ok.value)
+
+
+def sk_to_pk(sk32be):
+    """bls::SecretKey::deserialize(32 B big-endian) -> public_key().serialize() (48 B), or None
+    for a key outside (0, r)."""
+    lib = load()
+    out = (ctypes.c_uint8 * 48)()
+    s, _a = _b(sk32be)
+    return bytes(out) if lib.bls_oracle_sk_to_pk(s, ctypes.cast(out, _u8p)) else None
+
+
+def pk_validate(pk48):
+    """bls::PublicKey::deserialize: (valid, recompressed 48 B)."""
+    lib = load()
+    out = (ctypes.c_uint8 * 48)()
+    p, _a = _b(pk48)
+    ok = bool(lib.bls_oracle_pk_validate(p, ctypes.cast(out, _u8p)))
+    return ok, bytes(out)

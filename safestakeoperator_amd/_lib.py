@@ -40,6 +40,13 @@ SIGNATURES = {
                                                          ctypes.c_void_p, _sz, ctypes.c_void_p, _u8p, _sz,
                                                          ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_threshold_aggregate_batch_submit": (ctypes.c_int, [_ctx, _sz, _u32p, _u32p, _u8p, _u8p, _u64p, _u32p, _sz,
+                                                            _u8p, _u8p, _sz, ctypes.c_uint64, _u8p, _i32p, _u64p, _u8p,
+                                                            ctypes.POINTER(ctypes.c_uint64)]),
+    "ssb_threshold_aggregate_batch_cached_submit": (ctypes.c_int, [_ctx, _sz, _u32p, _u32p, _u8p, _u32p, _u64p, _u32p,
+                                                                   _sz, _u8p, _u8p, _sz, ctypes.c_uint64, _u8p, _i32p,
+                                                                   _u64p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),
+    "ssb_batch_wait": (ctypes.c_int, [_ctx, ctypes.c_uint64]),
     "ssb_pk_cache_set": (ctypes.c_int, [_ctx, _sz, _u8p]),
     "ssb_verify_batch_dev": (ctypes.c_int, [_ctx, _sz, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz,
                                             ctypes.c_void_p, _u8p, _sz, ctypes.c_uint64, ctypes.c_void_p,
@@ -55,6 +62,7 @@ SIGNATURES = {
     "ssb_unsafe_aggregate_batch": (ctypes.c_int, [_ctx, _sz, _u32p, _u8p, _u64p, _u8p, _i32p]),
     "ssb_sign_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u32p, _sz, _u8p, _u8p, _sz, _u8p]),
     "ssb_sk_to_pk_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p]),
+    "ssb_pk_validate_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _u8p]),
     "ssb_lagrange_coeffs": (ctypes.c_int, [_ctx, _sz, _u64p, _u8p]),
     "ssb_feldman_verify_batch": (ctypes.c_int, [_ctx, _sz, _sz, _u8p, _u64p, _u8p, _u8p, _u8p]),
     "ssb_dleq_verify_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p, _u8p, _u8p]),
@@ -79,11 +87,16 @@ def load():
         return _LIB
     # One HIP runtime per process: PyTorch (device memory, streams, RCCL for the callers) ships its
     # own libamdhip64; load it first so libssbls.so binds to the same runtime.  (With the library
-    # loaded first, a later torch.cuda init in the same process finds "No HIP GPUs".)
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # loaded first, a later torch.cuda init in the same process finds "No HIP GPUs".)  A C-ABI-only
+    # caller that never uses torch sets SSB_NO_TORCH=1 and skips the import; a broken torch install
+    # is logged, not fatal -- the library itself does not need torch.
+    if os.environ.get("SSB_NO_TORCH", "") not in ("1", "true"):
+        try:
+            import torch  # noqa: F401
+        except Exception as e:  # ImportError, or OSError / RuntimeError from a broken ROCm install
+            import logging
+            logging.getLogger(__name__).warning("torch not loaded before libssbls.so (%s); a later torch.cuda "
+                                                "init in this process may not see the GPU", e)
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libssbls.so is not built (run `python -m safestakeoperator_amd.build`); "
                            "there is no CPU fallback")

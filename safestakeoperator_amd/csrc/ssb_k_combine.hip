@@ -40,7 +40,7 @@ __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const u
   if (fast && fast[j]) return;
   lagrange_job(j, off, tt, ids, sel, lam);
 }
-__global__ void SSB_LB(64) k_combine_terms(int n, const uint32_t* __restrict__ share_job,
+__global__ void SSB_LB(64) k_combine_terms(int n, uint32_t n_jobs, const uint32_t* __restrict__ share_job,
                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                                       const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                                       const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
@@ -50,6 +50,7 @@ __global__ void SSB_LB(64) k_combine_terms(int n, const uint32_t* __restrict__ s
   if (s >= n) return;
   if (skip_if_ok && *skip_if_ok) return;
   const uint32_t j = share_job[s];
+  if (j >= n_jobs) return;   // outside every well-formed job (k_share_map's sentinel)
   if (fast && fast[j]) return;
   const uint32_t k = (uint32_t)s - off[j];
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
@@ -60,7 +61,7 @@ __global__ void SSB_LB(64) k_combine_terms(int n, const uint32_t* __restrict__ s
 }
 // verified candidates only: four lanes per share, one base-u digit each (unit_combine_term_gls);
 // term[4 s + q]
-__global__ void SSB_LB(64) k_combine_terms_gls(int n, const uint32_t* __restrict__ share_job,
+__global__ void SSB_LB(64) k_combine_terms_gls(int n, uint32_t n_jobs, const uint32_t* __restrict__ share_job,
                                               const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                               const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                               const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
@@ -71,6 +72,7 @@ __global__ void SSB_LB(64) k_combine_terms_gls(int n, const uint32_t* __restrict
   if (skip_if_ok && *skip_if_ok) return;
   const int s = g >> 2, q = g & 3;
   const uint32_t j = share_job[s];
+  if (j >= n_jobs) return;   // outside every well-formed job (k_share_map's sentinel)
   if (fast && fast[j]) return;
   const uint32_t k = (uint32_t)s - off[j];
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;

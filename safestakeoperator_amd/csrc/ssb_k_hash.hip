@@ -74,6 +74,30 @@ __global__ void SSB_LB(64) k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le,
   g1_compress(o, a);
   for (int b = 0; b < 48; ++b) out48[48 * (size_t)i + b] = o[b];
 }
+// bls::PublicKey::deserialize + serialize (lighthouse -> blst key_validate): decode, not infinity,
+// in G1 ([r]P == O, registration-time work, the plain windowed multiplication); valid[i] = 1 and the
+// recompression in out48, else valid[i] = 0 and zeros.  Pinned by the keys the reference's own
+// sources deserialize (tests/golden/reference_kats.json).
+__global__ void SSB_LB(64) k_pk_validate(int n, const uint8_t* __restrict__ pk48, uint8_t* __restrict__ valid,
+                                         uint8_t* __restrict__ out48) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t b[48];
+  for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)i + k];
+  g1_aff a;
+  const uint32_t f = unit_decode_pk(a, b);
+  bool ok = (f & DEC_OK) && !(f & DEC_INF);
+  if (ok) {
+    g1_jac z;
+    jac_mul_w4(z, a, R_LIMBS, 8);
+    ok = f_is_zero(z.z);
+  }
+  uint8_t o[48];
+  if (ok) g1_compress(o, a);
+  else for (int k = 0; k < 48; ++k) o[k] = 0;
+  valid[i] = ok ? 1 : 0;
+  for (int k = 0; k < 48; ++k) out48[48 * (size_t)i + k] = o[k];
+}
 __global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* __restrict__ out192) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

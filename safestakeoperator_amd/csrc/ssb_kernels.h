@@ -38,8 +38,9 @@ __global__ void k_sum_seg(int n_roots, const uint32_t* __restrict__ start, const
                           const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ rsig, g1_aff* __restrict__ s1,
                           g2_aff* __restrict__ s2);
 
-__global__ void k_share_map(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ job_root,
-                            uint32_t* __restrict__ share_job, uint32_t* __restrict__ share_root);
+__global__ void k_share_map(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                            const uint32_t* __restrict__ job_root, uint32_t* __restrict__ share_job,
+                            uint32_t* __restrict__ share_root);
 __global__ void k_decode(int n, const uint8_t* __restrict__ sig96,
                                                const uint8_t* __restrict__ pk48, int group_check,
                                                g2_aff* __restrict__ sig_aff, g1_aff* __restrict__ pk_aff,
@@ -72,6 +73,8 @@ __global__ void k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t
                                              const g2_aff* __restrict__ H, uint8_t* __restrict__ out96);
 __global__ void k_sk_to_pk(int n, const uint8_t* __restrict__ sk32le, uint8_t* __restrict__ out48);
 __global__ void k_serialize_g2(int n, const g2_aff* __restrict__ pts, uint8_t* __restrict__ out192);
+__global__ void k_pk_validate(int n, const uint8_t* __restrict__ pk48, uint8_t* __restrict__ valid,
+                              uint8_t* __restrict__ out48);
 __global__ void k_select(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                          const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
                          const uint32_t* __restrict__ flags, const uint32_t* __restrict__ skip_if_ok,
@@ -83,13 +86,13 @@ __global__ void k_lagrange(int n_jobs, const uint32_t* __restrict__ off, const u
                            const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
                            const int32_t* __restrict__ status, const uint32_t* __restrict__ skip_if_ok,
                            const uint32_t* __restrict__ fast, fr* __restrict__ lam);
-__global__ void k_combine_terms(int n, const uint32_t* __restrict__ share_job,
+__global__ void k_combine_terms(int n, uint32_t n_jobs, const uint32_t* __restrict__ share_job,
                                                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                                       const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                                       const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
                                                       const uint32_t* __restrict__ skip_if_ok, const uint32_t* __restrict__ fast,
                                                       g2_jac* __restrict__ term);
-__global__ void k_combine_terms_gls(int n, const uint32_t* __restrict__ share_job, const uint32_t* __restrict__ off,
+__global__ void k_combine_terms_gls(int n, uint32_t n_jobs, const uint32_t* __restrict__ share_job, const uint32_t* __restrict__ off,
                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                     const uint32_t* __restrict__ sel, const fr* __restrict__ lam,
                                     const g2_aff* __restrict__ sig_aff, const uint32_t* __restrict__ skip_if_ok,

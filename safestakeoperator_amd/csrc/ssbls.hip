@@ -62,6 +62,18 @@ struct ssb_slot {
   uint32_t* clean_cnt = nullptr;
   uint32_t* clean_tickets = nullptr;
   uint32_t clean_K = 0;
+  // host-buffer batches (ssb_threshold_aggregate_batch_submit): a pinned, device-mapped staging
+  // buffer the kernels read their inputs from and write their outputs to in place, over PCIe
+  // (zero-copy: no copy kernel, no copy queue); the outputs of the pending batch are copied to the
+  // caller's pointers when it is waited for (or when the slot is reused)
+  uint8_t* hst = nullptr;
+  size_t hst_bytes = 0;
+  hipEvent_t ev_host = nullptr;
+  uint64_t host_ticket = 0;         // the batch whose outputs are still in the staging buffer (0: none)
+  struct {
+    uint8_t* sig; int32_t* st; uint64_t* err; uint8_t* ver;
+    size_t nj, n, o_sig, o_st, o_err, o_ver;
+  } ho = {};
 };
 constexpr int SSB_MAX_SLOTS = 24;
 
@@ -112,6 +124,7 @@ struct ssb_ctx {
   // RLC key of each batch: fresh from getrandom() per call (default), or expanded from the caller's
   // seed (ssb_set_rlc_deterministic: reproducible runs / tests only)
   bool rlc_deterministic = false;
+  uint64_t ticket_gen = 0;          // host-buffer batch tickets: (generation << 8) | slot
 };
 
 namespace {
@@ -189,7 +202,8 @@ int init_slot(ssb_slot& S, int streams) {
     if (S.shared) S.side[i] = S.stream;
     else if (hipStreamCreateWithFlags(&S.side[i], hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
   }
-  for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user, &S.ev_fin})
+  for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user, &S.ev_fin,
+                        &S.ev_host})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
   // each new queue acquires its scratch now, alone (slots are created one after the other)
   if (!getenv("SSB_NO_PRIME")) {
@@ -198,15 +212,32 @@ int init_slot(ssb_slot& S, int streams) {
   }
   return SSB_OK;
 }
+// the pending host-buffer batch of the slot: wait for it, copy its outputs to the caller's pointers
+hipError_t deliver_host(ssb_slot& S) {
+  if (!S.host_ticket) return hipSuccess;
+  S.host_ticket = 0;
+  const hipError_t e = hipEventSynchronize(S.ev_host);
+  if (e != hipSuccess) return e;
+  const auto& h = S.ho;
+  memcpy(h.sig, S.hst + h.o_sig, h.nj * 96);
+  memcpy(h.st, S.hst + h.o_st, h.nj * 4);
+  memcpy(h.err, S.hst + h.o_err, h.nj * 16);
+  if (h.ver && h.n) memcpy(h.ver, S.hst + h.o_ver, h.n);
+  return hipSuccess;
+}
 void sync_slot(ssb_slot& S) {
+  deliver_host(S);
   if (S.stream) hipStreamSynchronize(S.stream);
   if (!S.shared) for (hipStream_t sd : S.side) if (sd) hipStreamSynchronize(sd);
   if (S.out_pending) hipEventSynchronize(S.ev_out);
 }
 void free_slot(ssb_slot& S) {
+  deliver_host(S);
   if (S.ws) hipFree(S.ws);
+  if (S.hst) hipHostFree(S.hst);
   if (!S.shared) for (hipStream_t sd : S.side) if (sd) hipStreamDestroy(sd);
-  for (hipEvent_t e : {S.ev_in, S.ev_hash, S.ev_dec, S.ev_comb, S.ev_out, S.ev_sdec, S.ev_r2, S.ev_r1, S.ev_user, S.ev_fin})
+  for (hipEvent_t e : {S.ev_in, S.ev_hash, S.ev_dec, S.ev_comb, S.ev_out, S.ev_sdec, S.ev_r2, S.ev_r1, S.ev_user, S.ev_fin,
+                       S.ev_host})
     if (e) hipEventDestroy(e);
   if (S.stream) hipStreamDestroy(S.stream);
 }
@@ -909,7 +940,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
-  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, job_root, share_job, share_root);
+  if (n) hipLaunchKernelGGL(k_share_map, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root);
   // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
   auto spec = [&] {
     hipStreamWaitEvent(sc, ctx->cur->ev_dec, 0);
@@ -917,7 +948,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
       hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, (uint32_t)n, share_off, t, ids,
                          (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err, w.sig_aff, fast,
                          out_sig96, lam); }
-    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
+    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
@@ -945,7 +976,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   // (after a speculative pass in the window launch the general combine of the jobs the small-
   // integer path did not finish still follows here, on whichever selection stands)
   const uint32_t* gate2 = spec_in_window ? nullptr : gate;
-  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term);
+  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term);
   hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate2, (const uint32_t*)fast, out_sig96, 4);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
@@ -1055,14 +1086,17 @@ int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
   return SSB_OK;
 }
 
-int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint32_t* t,
-                                  const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids, const uint32_t* job_root,
-                                  size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
-                                  uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status, uint64_t* out_err,
-                                  uint8_t* share_verdicts) {
+}  // extern "C"
+namespace {
+// the body of the two submit entry points: public keys compressed (pk48) or cache indices (pk_index)
+int submit_impl(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint32_t* t, const uint8_t* sig96,
+                const uint8_t* pk48, const uint32_t* pk_index, const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
+                int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, uint64_t* ticket) {
   if (!ctx) return SSB_EINVAL;
+  if (ticket) *ticket = 0;
   if (n_jobs == 0) return SSB_OK;
-  if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0) {
+  if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0 || !ticket) {
     ctx->err = "null pointer or no roots"; return SSB_EINVAL;
   }
   if (share_off[0] != 0) { ctx->err = "share_off[0] must be 0"; return SSB_EINVAL; }
@@ -1072,36 +1106,97 @@ int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* s
     if (job_root[j] >= n_roots) { ctx->err = "job_root out of range"; return SSB_EINVAL; }
   }
   const size_t n = share_off[n_jobs];
-  if (n && (!sig96 || !pk48 || !ids)) { ctx->err = "null share arrays"; return SSB_EINVAL; }
+  if (n && (!sig96 || !(pk48 || pk_index) || !ids)) { ctx->err = "null share arrays"; return SSB_EINVAL; }
+  if (pk_index && !ctx->pkc_aff) { ctx->err = "no public-key cache (ssb_pk_cache_set)"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
-  size_t io = align_up(n * 96) + align_up(n * 48) + align_up(n * 8) + align_up((n_jobs + 1) * 4) + align_up(n_jobs * 4) * 2 +
-              align_up(n_roots * 32) + align_up(n_jobs * 96) + align_up(n_jobs * 4) + align_up(n_jobs * 16) + align_up(n);
-  int rc;
-  if ((rc = ensure_io(ctx, io))) return rc;
-  carve ci{(char*)ctx->io};
-  uint8_t* d_sig = ci.take<uint8_t>(n * 96); uint8_t* d_pk = ci.take<uint8_t>(n * 48); uint64_t* d_ids = ci.take<uint64_t>(n);
-  uint32_t* d_off = ci.take<uint32_t>(n_jobs + 1); uint32_t* d_t = ci.take<uint32_t>(n_jobs); uint32_t* d_jr = ci.take<uint32_t>(n_jobs);
-  uint8_t* d_roots = ci.take<uint8_t>(n_roots * 32); uint8_t* d_out = ci.take<uint8_t>(n_jobs * 96);
-  int32_t* d_st = ci.take<int32_t>(n_jobs); uint64_t* d_err = ci.take<uint64_t>(n_jobs * 2); uint8_t* d_v = ci.take<uint8_t>(n);
-  hipStream_t st = ctx->cur->stream;
-  if (n) {
-    SSB_HIP(hipMemcpyAsync(d_sig, sig96, n * 96, hipMemcpyHostToDevice, st));
-    SSB_HIP(hipMemcpyAsync(d_pk, pk48, n * 48, hipMemcpyHostToDevice, st));
-    SSB_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, st));
+  // the next slot round robin; its previous host batch is delivered before its staging is reused
+  const int k = ctx->next;
+  ssb_slot& S = ctx->sl[k];
+  SSB_HIP(deliver_host(S));
+  size_t o = 0;
+  auto at = [&](size_t bytes) { const size_t r = o; o += align_up(bytes); return r; };
+  const size_t i_sig = at(n * 96), i_pk = at(pk_index ? n * 4 : n * 48), i_ids = at(n * 8), i_off = at((n_jobs + 1) * 4), i_t = at(n_jobs * 4),
+               i_jr = at(n_jobs * 4), i_roots = at(n_roots * 32), o_sig = at(n_jobs * 96), o_st = at(n_jobs * 4),
+               o_err = at(n_jobs * 16), o_ver = at(n ? n : 1);
+  if (o > S.hst_bytes) {
+    if (S.hst) { hipHostFree(S.hst); S.hst = nullptr; S.hst_bytes = 0; }
+    const size_t want = o + o / 4;
+    if (hipHostMalloc((void**)&S.hst, want, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess) {
+      S.hst = nullptr; ctx->err = "hipHostMalloc staging failed"; return SSB_ENOMEM;
+    }
+    S.hst_bytes = want;
   }
-  SSB_HIP(hipMemcpyAsync(d_off, share_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, st));
-  SSB_HIP(hipMemcpyAsync(d_t, t, n_jobs * 4, hipMemcpyHostToDevice, st));
-  SSB_HIP(hipMemcpyAsync(d_jr, job_root, n_jobs * 4, hipMemcpyHostToDevice, st));
-  SSB_HIP(hipMemcpyAsync(d_roots, roots32, n_roots * 32, hipMemcpyHostToDevice, st));
-  if ((rc = ssb_threshold_aggregate_batch_dev(ctx, n_jobs, n, d_off, d_t, d_sig, d_pk, d_ids, d_jr, n_roots, d_roots, dst,
-                                              dst_len, rlc_seed, d_out, d_st, d_err, d_v, st)))
-    return rc;
-  SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipMemcpyAsync(out_err, d_err, n_jobs * 16, hipMemcpyDeviceToHost, st));
-  if (share_verdicts && n) SSB_HIP(hipMemcpyAsync(share_verdicts, d_v, n, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  uint8_t* h = S.hst;
+  if (n) {
+    memcpy(h + i_sig, sig96, n * 96);
+    if (pk_index) memcpy(h + i_pk, pk_index, n * 4); else memcpy(h + i_pk, pk48, n * 48);
+    memcpy(h + i_ids, ids, n * 8);
+  }
+  memcpy(h + i_off, share_off, (n_jobs + 1) * 4);
+  memcpy(h + i_t, t, n_jobs * 4);
+  memcpy(h + i_jr, job_root, n_jobs * 4);
+  memcpy(h + i_roots, roots32, n_roots * 32);
+  uint8_t* d = nullptr;
+  SSB_HIP(hipHostGetDevicePointer((void**)&d, S.hst, 0));
+  int rc = aggregate_dev(ctx, n_jobs, n, (const uint32_t*)(d + i_off), (const uint32_t*)(d + i_t), d + i_sig,
+                         pk_index ? nullptr : d + i_pk, pk_index ? (const uint32_t*)(d + i_pk) : nullptr,
+                         (const uint64_t*)(d + i_ids), (const uint32_t*)(d + i_jr), n_roots, d + i_roots, dst, dst_len,
+                         rlc_seed, d + o_sig, (int32_t*)(d + o_st), (uint64_t*)(d + o_err), d + o_ver, (void*)S.stream);
+  if (rc) return rc;
+  SSB_HIP(hipEventRecord(S.ev_host, S.stream));
+  S.ho.sig = out_sig96; S.ho.st = out_status; S.ho.err = out_err; S.ho.ver = share_verdicts;
+  S.ho.nj = n_jobs; S.ho.n = n; S.ho.o_sig = o_sig; S.ho.o_st = o_st; S.ho.o_err = o_err; S.ho.o_ver = o_ver;
+  S.host_ticket = (++ctx->ticket_gen << 8) | (uint64_t)k;
+  *ticket = S.host_ticket;
   return SSB_OK;
+}
+}  // namespace
+extern "C" {
+
+int ssb_threshold_aggregate_batch_submit(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint32_t* t,
+                                         const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids,
+                                         const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
+                                         const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
+                                         int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts,
+                                         uint64_t* ticket) {
+  if (ctx && n_jobs && share_off && share_off[n_jobs] && !pk48) { ctx->err = "null pk48"; return SSB_EINVAL; }
+  return submit_impl(ctx, n_jobs, share_off, t, sig96, pk48, nullptr, ids, job_root, n_roots, roots32, dst, dst_len,
+                     rlc_seed, out_sig96, out_status, out_err, share_verdicts, ticket);
+}
+
+int ssb_threshold_aggregate_batch_cached_submit(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint32_t* t,
+                                                const uint8_t* sig96, const uint32_t* pk_index, const uint64_t* ids,
+                                                const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
+                                                const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
+                                                int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts,
+                                                uint64_t* ticket) {
+  if (ctx && n_jobs && share_off && share_off[n_jobs] && !pk_index) { ctx->err = "null pk_index"; return SSB_EINVAL; }
+  return submit_impl(ctx, n_jobs, share_off, t, sig96, nullptr, pk_index, ids, job_root, n_roots, roots32, dst, dst_len,
+                     rlc_seed, out_sig96, out_status, out_err, share_verdicts, ticket);
+}
+
+int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket) {
+  if (!ctx) return SSB_EINVAL;
+  if (ticket == 0) return SSB_OK;
+  const int k = (int)(ticket & 0xff);
+  if (k >= ctx->nslots || (ticket >> 8) > ctx->ticket_gen) { ctx->err = "unknown ticket"; return SSB_EINVAL; }
+  ssb_slot& S = ctx->sl[k];
+  if (S.host_ticket != ticket) return SSB_OK;   // already delivered (its slot was reused, or waited before)
+  SSB_HIP(deliver_host(S));
+  return SSB_OK;
+}
+
+int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint32_t* t,
+                                  const uint8_t* sig96, const uint8_t* pk48, const uint64_t* ids, const uint32_t* job_root,
+                                  size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                  uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status, uint64_t* out_err,
+                                  uint8_t* share_verdicts) {
+  uint64_t ticket = 0;
+  const int rc = ssb_threshold_aggregate_batch_submit(ctx, n_jobs, share_off, t, sig96, pk48, ids, job_root, n_roots, roots32,
+                                                      dst, dst_len, rlc_seed, out_sig96, out_status, out_err, share_verdicts,
+                                                      &ticket);
+  if (rc) return rc;
+  return ssb_batch_wait(ctx, ticket);
 }
 
 int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint8_t* sig96,
@@ -1136,12 +1231,12 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
     SSB_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, st));
   }
   SSB_HIP(hipMemcpyAsync(d_off, share_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_share_map, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, d_off, (const uint32_t*)nullptr, share_job, (uint32_t*)nullptr);
+  if (n) hipLaunchKernelGGL(k_share_map, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, d_off, (const uint32_t*)nullptr, (const uint32_t*)nullptr, share_job, (uint32_t*)nullptr);
   if (n) hipLaunchKernelGGL(k_decode, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sig, (const uint8_t*)nullptr, 0, sig_aff, (g1_aff*)nullptr, flags);
   hipLaunchKernelGGL(k_select_all, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, flags, sel, tt, d_st, err);
   // unsafe_aggregate does not subgroup-check its inputs (blst.rs:77-84): always the exact 255-bit path
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, (const uint32_t*)nullptr, (const uint32_t*)nullptr, lam);
-  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, (const uint32_t*)nullptr, term);
+  if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, (const uint32_t*)nullptr, term);
   hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out, 1);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
@@ -1191,6 +1286,25 @@ int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* o
   SSB_HIP(hipMemcpyAsync(d_sk, sk32le, n * 32, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_sk_to_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sk, d_out);
   SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(out_pk48, d_out, n * 48, hipMemcpyDeviceToHost, st));
+  SSB_HIP(hipStreamSynchronize(st));
+  return SSB_OK;
+}
+
+int ssb_pk_validate_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint8_t* out_valid, uint8_t* out_pk48) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!pk48 || !out_valid || !out_pk48 || n > (size_t)INT32_MAX) { ctx->err = "null pointer or n too large"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = ensure_ws(ctx, 2 * align_up(n * 48) + align_up(n)))) return rc;
+  carve c{(char*)ctx->cur->ws};
+  uint8_t* d_in = c.take<uint8_t>(n * 48); uint8_t* d_out = c.take<uint8_t>(n * 48); uint8_t* d_v = c.take<uint8_t>(n);
+  hipStream_t st = ctx->cur->stream;
+  SSB_HIP(hipMemcpyAsync(d_in, pk48, n * 48, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_pk_validate, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const uint8_t*)d_in, d_v, d_out);
+  SSB_HIP(hipGetLastError());
+  SSB_HIP(hipMemcpyAsync(out_valid, d_v, n, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_pk48, d_out, n * 48, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipStreamSynchronize(st));
   return SSB_OK;

@@ -93,40 +93,50 @@ def shard_sizes(share_off: Sequence[int], world: int) -> List[Tuple[int, int]]:
 
 
 def exchange_var(verdicts_u8: torch.Tensor, sigs96: torch.Tensor, status: torch.Tensor, err: torch.Tensor,
-                 group=None, sizes: Sequence[Tuple[int, int]] = None, async_op: bool = False):
+                 group=None, sizes: Sequence[Tuple[int, int]] = None, async_op: bool = False, batches: int = 1):
     """All-gather results whose sizes differ per rank (a strong-scaling split of one batch): every
     array padded to the largest rank's size, gathered, then trimmed and concatenated in rank order.
-    `sizes` = every rank's (shares, jobs) (shard_sizes); gathered first when not given.  Returns
-    the GLOBAL (verdicts[N], sigs[J, 96], status[J], err[J, 2]) on every rank; with async_op the
-    padded gathers are left in flight and a finish() closure (trim + concatenate, call after the
-    handles' wait()) is returned with the handles."""
+    `sizes` = every rank's (shares, jobs) of ONE batch (shard_sizes); gathered first when not given.
+    Returns the GLOBAL (verdicts[N], sigs[J, 96], status[J], err[J, 2]) on every rank; with async_op
+    the padded gathers are left in flight and a finish() closure (trim + concatenate, call after the
+    handles' wait()) is returned with the handles.
+    batches > 1: the local arrays are that many same-shape batches of this rank's shard back to back
+    (one collective for a group of pipelined batches); the result is then a list of `batches` global
+    tuples, batch b reassembled from every rank's b-th slice."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     dev = verdicts_u8.device
+    B = max(1, int(batches))
+    n_loc, j_loc = int(verdicts_u8.numel()) // B, int(status.numel()) // B
     if sizes is None:
-        n_loc, j_loc = int(verdicts_u8.numel()), int(status.numel())
         g, _ = _all_gather(torch.tensor([n_loc, j_loc], dtype=torch.int64, device=dev), world, group, False)
         sizes = [tuple(x) for x in g.cpu().tolist()]
     n_max = max(max(s[0] for s in sizes), 1)
     j_max = max(max(s[1] for s in sizes), 1)
+    nb_max = (n_max + 7) // 8
 
-    def padded(x, m):
-        p = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=dev)
-        p[:x.shape[0]] = x
-        return p
+    def padded(x, m):   # (B * rows, ...) -> (B * m, ...), each batch's rows padded to m
+        x = x.reshape((B, -1) + tuple(x.shape[1:]))
+        p = torch.zeros((B, m) + tuple(x.shape[2:]), dtype=x.dtype, device=dev)
+        p[:, :x.shape[1]] = x
+        return p.reshape((B * m,) + tuple(x.shape[2:]))
 
+    bits_loc = torch.cat([pack_bits(verdicts_u8[b * n_loc:(b + 1) * n_loc]) for b in range(B)]) if B > 1 else pack_bits(verdicts_u8)
     gathered, works = [], []
-    for x, m in ((pack_bits(verdicts_u8), (n_max + 7) // 8), (sigs96, j_max), (status, j_max), (err, j_max)):
+    for x, m in ((bits_loc, nb_max), (sigs96, j_max), (status, j_max), (err, j_max)):
         g, w = _all_gather(padded(x, m), world, group, async_op)
-        gathered.append(g)
+        gathered.append(g.view((world, B, m) + tuple(g.shape[2:])))
         works.append(w)
     bits, sg, st, er = gathered
 
+    def one(b):
+        ver = torch.cat([unpack_bits(bits[r, b], sizes[r][0]) for r in range(world)])
+        return (ver, torch.cat([sg[r, b, :sizes[r][1]] for r in range(world)]),
+                torch.cat([st[r, b, :sizes[r][1]] for r in range(world)]),
+                torch.cat([er[r, b, :sizes[r][1]] for r in range(world)]))
+
     def finish():
-        ver = torch.cat([unpack_bits(bits[r], sizes[r][0]) for r in range(world)])
-        return (ver, torch.cat([sg[r, :sizes[r][1]] for r in range(world)]),
-                torch.cat([st[r, :sizes[r][1]] for r in range(world)]),
-                torch.cat([er[r, :sizes[r][1]] for r in range(world)]))
+        return [one(b) for b in range(B)] if B > 1 else one(0)
     return (finish, works) if async_op else finish()
 
 
@@ -144,3 +154,72 @@ def run_sharded(batch_fn, share_off: Sequence[int], per_share: Dict[str, Sequenc
     jobs = {k: v[j0:j1] for k, v in per_job.items()}
     ver, sg, st, er = batch_fn(lb["share_off"], shares, jobs)
     return exchange_var(ver, sg, st, er, group=group, sizes=shard_sizes(share_off, world))
+
+
+class BatchExchange:
+    """The per-group exchange step of a pipelined run (bench.py): the results of the batches
+    submitted since the last exchange -- one per pipeline slot -- are all-gathered in ONE
+    collective per array (fewer, larger collectives), asynchronously; the caller makes each
+    slot's next batch wait for the handles (`works`) before it rewrites that slot's outputs.
+
+      weak:   every rank runs its own batch of the same shape (`exchange`);
+      strong: every rank runs its shard of ONE global batch (`exchange_var` with `sizes` = the
+              per-batch (shares, jobs) of every rank, `batches` = the group size), reassembled
+              into the global order per batch.
+
+    `check_last()` (untimed) verifies the last group's gathered results against this rank's local
+    outputs at this rank's position, and returns the gathered / reassembled results for further
+    checks.  `outs[k]` holds the slot's tensors "ver", "out", "st", "err"."""
+
+    def __init__(self, strong: bool, sizes: Sequence[Tuple[int, int]] = None, group=None, device=None):
+        self.strong, self.sizes, self.group, self.device = strong, sizes, group, device
+        self.last = None     # (local output dicts, gathered or finish closure, works)
+
+    def flush(self, outs: Sequence[Dict[str, torch.Tensor]]):
+        dev = self.device
+        cat = lambda key: torch.cat([o[key] for o in outs]).to(dev) if dev is not None else torch.cat([o[key] for o in outs])
+        if self.strong:
+            res, works = exchange_var(cat("ver"), cat("out"), cat("st"), cat("err"), group=self.group, sizes=self.sizes,
+                                      async_op=True, batches=len(outs))
+        else:
+            res, works = exchange(cat("ver"), cat("out"), cat("st"), group=self.group, async_op=True)
+        works = [w for w in works if w is not None]
+        self.last = (list(outs), res, works)
+        return works
+
+    def check_last(self):
+        """(ok, results): ok iff every batch of the last group came back from the collective equal
+        to this rank's local outputs (weak: the gathered row of this rank; strong: the slice of the
+        reassembled global batch at this rank's offsets)."""
+        import torch.distributed as dist
+        if self.last is None:
+            return True, None
+        outs, res, works = self.last
+        for w in works:
+            w.wait()
+        rank = dist.get_rank(self.group)
+        ok = True
+        if self.strong:
+            glob = res()
+            if not isinstance(glob, list):
+                glob = [glob]
+            s0 = sum(s[0] for s in self.sizes[:rank])
+            j0 = sum(s[1] for s in self.sizes[:rank])
+            for o, (ver, sg, st, er) in zip(outs, glob):
+                n, j = o["ver"].numel(), o["st"].numel()
+                ok = ok and torch.equal(ver[s0:s0 + n].cpu(), o["ver"].cpu()) and torch.equal(sg[j0:j0 + j].cpu(), o["out"].cpu())
+                ok = ok and torch.equal(st[j0:j0 + j].cpu(), o["st"].cpu()) and torch.equal(er[j0:j0 + j].cpu(), o["err"].cpu())
+            return ok, glob
+        bits, sg, st = res
+        B = len(outs)
+        n, j = outs[0]["ver"].numel(), outs[0]["st"].numel()
+        world = bits.shape[0]
+        per_batch = []
+        all_ver = [unpack_bits(bits[r], B * n) for r in range(world)]
+        for b, o in enumerate(outs):
+            ok = ok and torch.equal(all_ver[rank][b * n:(b + 1) * n].cpu(), o["ver"].cpu())
+            ok = ok and torch.equal(sg[rank][b * j:(b + 1) * j].cpu(), o["out"].cpu())
+            ok = ok and torch.equal(st[rank][b * j:(b + 1) * j].cpu(), o["st"].cpu())
+            per_batch.append([(all_ver[r][b * n:(b + 1) * n], sg[r][b * j:(b + 1) * j], st[r][b * j:(b + 1) * j])
+                              for r in range(world)])
+        return ok, per_batch

@@ -295,6 +295,21 @@ class Engine:
                                                  out.ctypes.data_as(_lib._u8p)), "ssb_sk_to_pk_batch")
         return [out[48 * i:48 * (i + 1)].tobytes() for i in range(n)]
 
+    def pk_validate_batch(self, pks: Sequence[bytes]) -> List[Optional[bytes]]:
+        """bls::PublicKey::deserialize + serialize per key: the recompressed key, or None for a key
+        that does not decode, is infinity or lies outside G1 (ssb_pk_validate_batch)."""
+        n = len(pks)
+        if n == 0:
+            return []
+        if any(len(p) != 48 for p in pks):
+            raise ValueError("public keys are 48 bytes")
+        inp = np.frombuffer(b"".join(pks), dtype=np.uint8)
+        ok = np.zeros(n, dtype=np.uint8)
+        out = np.zeros(48 * n, dtype=np.uint8)
+        self._check(self._lib.ssb_pk_validate_batch(self._h, n, inp.ctypes.data_as(_lib._u8p), ok.ctypes.data_as(_lib._u8p),
+                                                    out.ctypes.data_as(_lib._u8p)), "ssb_pk_validate_batch")
+        return [out[48 * i:48 * (i + 1)].tobytes() if ok[i] else None for i in range(n)]
+
     def lagrange_coeffs(self, ids: Sequence[int]) -> List[int]:
         t = len(ids)
         if t == 0:
@@ -331,6 +346,41 @@ class Engine:
             "ssb_threshold_aggregate_batch")
         return out[:J], st[:J], err[:J], ver[:N]
 
+    def submit_batch_raw(self, t, share_off, sigs, pks, ids, job_root, roots, seed: Optional[int] = None,
+                         dst: bytes = DST, pk_index=None) -> "PendingBatch":
+        """Asynchronous packed form (ssb_threshold_aggregate_batch_submit): the inputs are staged and
+        the batch enqueued on the next pipeline slot; PendingBatch.wait() returns (out_sig96[J,96],
+        status[J], err[J,2], share_verdicts[N]).  Inputs may be numpy arrays (uint32 offsets / t /
+        job roots, uint64 ids, uint8 signatures / keys / roots) or Python sequences / bytes."""
+        J = len(t)
+        off = np.ascontiguousarray(np.asarray(share_off, dtype=np.uint32))
+        N = int(off[-1]) if J else 0
+        tt = np.ascontiguousarray(np.asarray(t, dtype=np.uint32))
+        sg = np.frombuffer(sigs, dtype=np.uint8) if isinstance(sigs, (bytes, bytearray)) else np.ascontiguousarray(sigs)
+        if pk_index is not None:
+            pk = np.ascontiguousarray(np.asarray(pk_index, dtype=np.uint32))
+        else:
+            pk = np.frombuffer(pks, dtype=np.uint8) if isinstance(pks, (bytes, bytearray)) else np.ascontiguousarray(pks)
+        idv = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64)) if N else np.zeros(1, np.uint64)
+        jr = np.ascontiguousarray(np.asarray(job_root, dtype=np.uint32))
+        rt = (np.frombuffer(b"".join(roots), dtype=np.uint8) if not isinstance(roots, np.ndarray)
+              else np.ascontiguousarray(roots))
+        n_roots = len(roots) if not isinstance(roots, np.ndarray) else rt.size // 32
+        pb = PendingBatch(self, J, N)
+        d, dp = _lib.buf(dst)
+        tk = ctypes.c_uint64(0)
+        fn = (self._lib.ssb_threshold_aggregate_batch_cached_submit if pk_index is not None
+              else self._lib.ssb_threshold_aggregate_batch_submit)
+        pkp = pk.ctypes.data_as(_lib._u32p) if pk_index is not None else pk.ctypes.data_as(_lib._u8p)
+        self._check(fn(
+            self._h, J, off.ctypes.data_as(_lib._u32p), tt.ctypes.data_as(_lib._u32p), sg.ctypes.data_as(_lib._u8p),
+            pkp, idv.ctypes.data_as(_lib._u64p), jr.ctypes.data_as(_lib._u32p), n_roots,
+            rt.ctypes.data_as(_lib._u8p), dp, len(dst), _rlc_seed(seed), pb.out.ctypes.data_as(_lib._u8p),
+            pb.st.ctypes.data_as(_lib._i32p), pb.err.ctypes.data_as(_lib._u64p), pb.ver.ctypes.data_as(_lib._u8p),
+            ctypes.byref(tk)), "ssb_threshold_aggregate_batch_submit")
+        pb.ticket = tk.value
+        return pb
+
     def unsafe_aggregate_batch_raw(self, share_off: Sequence[int], sigs: bytes, ids: Sequence[int]):
         J = len(share_off) - 1
         off = np.ascontiguousarray(np.asarray(share_off, dtype=np.uint32))
@@ -346,6 +396,22 @@ class Engine:
 
 
 _DEFAULT_ENGINE: Optional[Engine] = None
+
+
+class PendingBatch:
+    """A submitted host-buffer batch (Engine.submit_batch_raw): its output arrays stay alive here
+    until the library has delivered into them."""
+
+    def __init__(self, engine: Engine, J: int, N: int):
+        self.engine, self.J, self.N, self.ticket = engine, J, N, 0
+        self.out = np.zeros((max(J, 1), 96), dtype=np.uint8)
+        self.st = np.zeros(max(J, 1), dtype=np.int32)
+        self.err = np.zeros((max(J, 1), 2), dtype=np.uint64)
+        self.ver = np.zeros(max(N, 1), dtype=np.uint8)
+
+    def wait(self):
+        self.engine._check(self.engine._lib.ssb_batch_wait(self.engine._h, self.ticket), "ssb_batch_wait")
+        return self.out[:self.J], self.st[:self.J], self.err[:self.J], self.ver[:self.N]
 
 
 def default_engine() -> Engine:

@@ -36,3 +36,61 @@ def test_pipeline_config_guard():
     assert not ok(8, 3) and not ok(6, 3) and not ok(25, 1) and not ok(0, 1) and not ok(4, 2)
     # a null context is refused before any HIP call
     assert lib.ssb_set_pipeline_depth(None, 4) == -1 and lib.ssb_set_slot_streams(None, 3) == -1
+
+
+def _capi_input(cases):
+    roots = []
+    for c in cases:
+        if c["root"] not in roots:
+            roots.append(c["root"])
+    lines = ["%d %d" % (len(cases), len(roots))] + roots
+    for c in cases:
+        lines.append("%d %d %d" % (c["t"], len(c["sigs"]), roots.index(c["root"])))
+        lines += ["%s %s %d" % (s, p, i) for s, p, i in zip(c["sigs"], c["pks"], c["ids"])]
+    return "\n".join(lines) + "\n"
+
+
+def test_plain_c_caller_builds_and_rejects_bad_input():
+    """tests/native/capi_golden.c: gcc against include/ssbls.h alone, linked to libssbls.so; on a
+    malformed input it stops before touching the device."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "native"))
+    from build_capi import build_capi
+    build(verbose=False)
+    exe = build_capi()
+    r = subprocess.run([exe], input="0 0\n", capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "bad header" in r.stderr
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_plain_c_caller_golden_cases():
+    """The drop-in boundary from plain C (no Python in the call path): every golden threshold case
+    in one ssb_threshold_aggregate_batch call, statuses / error fields / combined signatures / share
+    verdicts == tests/golden/threshold_cases.json, and ssb_verify_batch's verdicts == the same."""
+    import json
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "native"))
+    from build_capi import BIN, build_capi
+    exe = BIN if os.path.exists(BIN) else build_capi()
+    with open(os.path.join(os.path.dirname(__file__), "golden", "threshold_cases.json")) as f:
+        cases = json.load(f)["cases"]
+    r = subprocess.run([exe], input=_capi_input(cases), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout.split("\n")
+    want_ver = ""
+    for j, c in enumerate(cases):
+        f = out[j].split()
+        assert f[0] == "job" and int(f[1]) == j
+        assert int(f[2]) == c["expected_status"], c["name"]
+        if c["expected_status"] == 0:
+            assert f[5] == c["expected_sig"] == c["master_sig"], c["name"]
+        elif c["expected_status"] in (2, 4):
+            assert [int(f[3]), int(f[4])] == c["expected_payload"], c["name"]
+        want_ver += "".join("1" if v else "0" for v in c["share_verdicts"])
+    assert out[len(cases)] == "verdicts " + want_ver
+    assert out[len(cases) + 1] == "verify " + want_ver

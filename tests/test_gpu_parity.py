@@ -500,3 +500,99 @@ def test_golden_cases_one_stream_fused(engine, subset):
     finally:
         lib.ssb_set_pipeline_depth(engine.handle, 1)
         lib.ssb_set_slot_streams(engine.handle, 3)
+
+
+def _dev_aggregate(engine, n_shares, offs, tt, sigs, pks, ids, jr, roots):
+    """ssb_threshold_aggregate_batch_dev on raw (possibly malformed) job arrays; host copies back."""
+    import ctypes
+    import torch
+    from safestakeoperator_amd import _lib
+    lib, dev = engine._lib, torch.device("cuda", 0)
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    J = len(tt)
+    d_off = torch.tensor(offs, dtype=torch.int32, device=dev)
+    d_t = torch.tensor(tt, dtype=torch.int32, device=dev)
+    d_sig, d_pk, d_roots = u8(b"".join(sigs)), u8(b"".join(pks)), u8(b"".join(roots))
+    d_ids = torch.tensor(ids, dtype=torch.int64, device=dev)
+    d_jr = torch.tensor(jr, dtype=torch.int32, device=dev)
+    out = torch.zeros((J, 96), dtype=torch.uint8, device=dev)
+    st = torch.full((J,), -7, dtype=torch.int32, device=dev)
+    err = torch.zeros((J, 2), dtype=torch.int64, device=dev)
+    ver = torch.zeros((n_shares,), dtype=torch.uint8, device=dev)
+    dst = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
+    rc = lib.ssb_threshold_aggregate_batch_dev(engine.handle, J, n_shares, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(),
+                                               d_pk.data_ptr(), d_ids.data_ptr(), d_jr.data_ptr(), len(roots),
+                                               d_roots.data_ptr(), ctypes.cast(dst, _lib._u8p), len(DST), 5,
+                                               out.data_ptr(), st.data_ptr(), err.data_ptr(), ver.data_ptr(), None)
+    assert rc == 0, lib.ssb_last_error(engine.handle)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), st.cpu().numpy(), ver.cpu().numpy()
+
+
+def test_dev_malformed_job_shapes(engine):
+    """_dev contract: malformed jobs -- t = 0, a decreasing range, share_off[0] > 0,
+    share_off[n_jobs] < n_shares -- get SSB_DVF_INVALID_JOB, shares outside every well-formed range
+    never enter a job (k_share_map's sentinel, even over a workspace a previous batch left filled),
+    and every well-formed job still combines to its master signature."""
+    V, t, n = 64, 3, 4
+    roots, master, sigs, pks, ids, jr, msig = _gen_committees(engine, V, t, n, 4, seed=41)
+    N = V * n
+    offs = list(range(0, N + 1, n))
+    # a normal batch first: the slot's workspace now holds a full share -> job map
+    out, st, ver = _dev_aggregate(engine, N, offs, [t] * V, sigs, pks, ids, jr, roots)
+    assert (st == 0).all() and ver.all() and all(out[v].tobytes() == msig[v] for v in range(V))
+    # (1) t = 0 on job 3, and an extra job V whose range decreases (off[V+1] < off[V]); the shares
+    #     array carries 8 trailing shares no job covers (off[n_jobs] < n_shares)
+    tt = [t] * V + [t]
+    tt[3] = 0
+    offs1 = offs + [N - 3]
+    extra_sigs = list(sigs) + list(sigs[:8])
+    out, st, ver = _dev_aggregate(engine, N + 8, offs1, tt, extra_sigs, list(pks) + list(pks[:8]),
+                                  list(ids) + list(ids[:8]), list(jr) + [0], roots)
+    assert st[3] == 6 and st[V] == 6
+    for v in range(V):
+        if v != 3:
+            assert st[v] == 0 and out[v].tobytes() == msig[v], v
+    assert not ver[3 * n:4 * n].any() and not ver[N:].any()
+    # (2) share_off[0] > 0: the first two validators' shares are outside every job
+    offs2 = offs[2:]
+    out, st, ver = _dev_aggregate(engine, N, offs2, [t] * (V - 2), sigs, pks, ids, jr[2:], roots)
+    assert (st == 0).all()
+    assert all(out[k].tobytes() == msig[k + 2] for k in range(V - 2))
+    assert not ver[:2 * n].any() and ver[2 * n:].all()
+
+
+def test_host_submit_wait_pipelined(engine):
+    """ssb_threshold_aggregate_batch_submit / ssb_batch_wait (zero-copy staging over PCIe): seven
+    batches submitted onto three slots before any wait -- every slot is reused while its previous
+    batch is pending, which must deliver that batch first -- then waited in reverse order; each
+    delivers exactly the fixture's statuses, combines and share verdicts.  The same with the public
+    keys from the decoded-key cache (the _cached_submit variant)."""
+    cases = _load("threshold_cases.json")["cases"]
+    roots, t, offs, sigs, pks, ids, jr = _golden_batch(cases, 3)
+    lib = engine._lib
+    assert lib.ssb_set_slot_streams(engine.handle, 1) == 0
+    assert lib.ssb_set_pipeline_depth(engine.handle, 3) == 0
+    try:
+        for cached in (False, True):
+            kw = {}
+            if cached:
+                uniq = sorted(set(pks))
+                table = np.frombuffer(b"".join(uniq), dtype=np.uint8)
+                from safestakeoperator_amd import _lib
+                assert lib.ssb_pk_cache_set(engine.handle, len(uniq), table.ctypes.data_as(_lib._u8p)) == 0
+                kw["pk_index"] = [uniq.index(p) for p in pks]
+            pend = [engine.submit_batch_raw(t, offs, b"".join(sigs), b"".join(pks), ids, jr, roots, **kw) for _ in range(7)]
+            for pb in reversed(pend):
+                out, st, err, ver = pb.wait()
+                for k in range(len(t)):
+                    c = cases[k % len(cases)]
+                    assert int(st[k]) == c["expected_status"], c["name"]
+                    if c["expected_status"] == 0:
+                        assert out[k].tobytes().hex() == c["expected_sig"], c["name"]
+                    elif c["expected_status"] in (2, 4):
+                        assert [int(err[k, 0]), int(err[k, 1])] == c["expected_payload"], c["name"]
+                    assert [bool(v) for v in ver[offs[k]:offs[k + 1]]] == c["share_verdicts"], c["name"]
+    finally:
+        lib.ssb_set_pipeline_depth(engine.handle, 1)
+        lib.ssb_set_slot_streams(engine.handle, 3)

@@ -45,7 +45,10 @@ def _worker(rank, world, port, q):
     sig = torch.randint(0, 256, (J, 96), dtype=torch.uint8, generator=g)
     st = torch.randint(0, 5, (J,), dtype=torch.int32, generator=g)
     bits, sigs, sts = exchange(ver, sig, st)
-    q.put((rank, [unpack_bits(bits[r], n) for r in range(world)], sigs.clone(), sts.clone(), ver, sig, st))
+    # numpy (pickled by value): torch tensors go through fd sharing, which races with this
+    # process's exit
+    q.put((rank, [unpack_bits(bits[r], n).numpy() for r in range(world)], sigs.numpy().copy(), sts.numpy().copy(),
+           ver.numpy(), sig.numpy(), st.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -68,9 +71,9 @@ def test_exchange_gloo_world2():
     for r in range(world):
         _, vers, sigs, sts, _, _, _ = res[r]
         for src in range(world):
-            assert torch.equal(vers[src], res[src][4])
-            assert torch.equal(sigs[src], res[src][5])
-            assert torch.equal(sts[src], res[src][6])
+            assert (vers[src] == res[src][4]).all()
+            assert (sigs[src] == res[src][5]).all()
+            assert (sts[src] == res[src][6]).all()
 
 
 # ---- strong scaling: one global batch split over ranks (uneven shards), results reassembled ----
@@ -144,3 +147,68 @@ def test_strong_scaling_reassembles_global_batch(world):
         assert (v == ver[:off[-1]]).all()
         assert (s == st).all() and (e.astype("uint64") == err).all()
         assert (sg[s == 0] == out[st == 0]).all()
+
+
+# ---- bench.py's own exchange step (BatchExchange): groups of pipelined batches, weak and strong ----
+def _stub_global(N_jobs, n):
+    """a deterministic 'engine' over a global batch: job j -> (status, sig bytes, err); share s -> verdict"""
+    j = torch.arange(N_jobs)
+    st = (j % 5 == 3).to(torch.int32) * 4
+    sig = ((j.view(-1, 1) * 7 + torch.arange(96).view(1, -1)) % 251).to(torch.uint8)
+    err = torch.stack([j % 3, j % 7], 1).to(torch.int64)
+    s = torch.arange(N_jobs * n)
+    ver = (s % 11 != 4).to(torch.uint8)
+    return ver, sig, st, err
+
+
+def _bx_worker(rank, world, port, q, strong):
+    import torch.distributed as dist
+    from safestakeoperator_amd.shard import BatchExchange, shard_jobs, shard_sizes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, J, G = 3, 41, 3                       # shares per job, global jobs, batches per group
+    off = list(range(0, J * n + 1, n))
+    gver, gsig, gst, gerr = _stub_global(J, n)
+    if strong:
+        j0, j1 = shard_jobs(off, world, rank)
+        sizes = shard_sizes(off, world)
+        loc = dict(ver=gver[j0 * n:j1 * n], out=gsig[j0:j1], st=gst[j0:j1], err=gerr[j0:j1])
+    else:
+        sizes = None
+        loc = dict(ver=gver ^ (rank & 1), out=gsig + rank, st=gst + rank, err=gerr)
+    bx = BatchExchange(strong=strong, sizes=sizes)
+    outs = [{k: v.clone() for k, v in loc.items()} for _ in range(G)]
+    for b in range(G):                       # the batches of one group differ in their statuses
+        outs[b]["st"] = outs[b]["st"] + 10 * b
+    bx.flush(outs)
+    ok, res = bx.check_last()
+    if strong:
+        full = all(torch.equal(r[0], gver) and torch.equal(r[1], gsig) and torch.equal(r[2], gst + 10 * b)
+                   and torch.equal(r[3], gerr) for b, r in enumerate(res))
+    else:
+        full = all(torch.equal(res[b][r][2], gst + r + 10 * b) and torch.equal(res[b][r][0], gver ^ (r & 1))
+                   for b in range(G) for r in range(world))
+    q.put((rank, bool(ok), bool(full)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("strong", [False, True], ids=["weak", "strong"])
+def test_bench_batch_exchange_gloo_world2(strong):
+    """The exchange step bench.py runs after each group of pipelined batches (shard.BatchExchange),
+    driven with a stub batch function over gloo at world 2: a group of 3 batches per collective;
+    weak -- every rank's gathered rows equal that rank's local outputs; strong (uneven 41-job global
+    batch) -- every batch of the group reassembles to the single-rank global result."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bx_worker, args=(r, world, port, q, strong)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(r[0] for r in res) == [0, 1]
+    assert all(r[1] and r[2] for r in res), res
