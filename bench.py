@@ -296,10 +296,9 @@ def main():
     # 20 slots + 2 hash streams 4.05 M.  With N > 1 the all-gather runs on RCCL's stream: it is
     # issued once per pipeline round (exchange_group), after the round's batches, so that stream is
     # not active beside the 20 slot queues.
-    # slot streams + the speculative-combine and tail streams (idle with one-stream slots, which run
-    # every stage on the slot's stream) + SSB_HASH_STREAMS (engine default 0) + one for torch
-    set_hw_queues(args.pipeline * args.slot_streams + 2 + int(os.environ.get("SSB_TAILS", "1") or 1)
-                  + int(os.environ.get("SSB_HASH_STREAMS", "0") or 0) + int(os.environ.get("SSB_G1_STREAMS", "0") or 0))
+    # slot streams + the context's speculative-combine and tail streams (idle with one-stream slots,
+    # which run every stage on the slot's stream) + one for torch
+    set_hw_queues(args.pipeline * args.slot_streams + 3)
 
     import numpy as np
     import torch
@@ -636,10 +635,7 @@ def main():
                                     % (args.config, V, n, t, n, n_roots)) + (" + final verify" if args.final_verify else ""),
                        "validators_per_gpu": V, "threshold": t, "operators": n, "roots": n_roots,
                        "parallelism": "dp%d (validator shards, RCCL all-gather of verdicts+signatures)" % world,
-                       "batches_in_flight": S, "streams_per_slot": args.slot_streams,
-                       "tail_streams": int(os.environ.get("SSB_TAILS", "1") or 1),
-                       "hash_streams": int(os.environ.get("SSB_HASH_STREAMS", "0") or 0),
-                       "post": os.environ.get("SSB_POST", "slot")},
+                       "batches_in_flight": S, "streams_per_slot": args.slot_streams},
             "batch_latency_ms": round(latency_ms, 3),
             "public_keys": ("compressed per batch (ssb_threshold_aggregate_batch_dev)" if args.compressed_pk else
                             "decompressed once at registration (ssb_pk_cache_set + _cached_dev), as lighthouse's "

@@ -28,6 +28,23 @@ if VARIANT:
     FLAGS += os.environ.get("SSB_VARIANT_DEFS", "").split()
 STAMP = LIB + ".srchash"
 OBJDIR = os.path.join(HERE, "build" + ("_" + VARIANT if VARIANT else ""))
+LLVM = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "llvm", "bin")
+
+# Kernels that may hold a private segment larger than the queue primer (k_scratch_prime): each runs
+# only inside a SYNCHRONOUS entry point (the call waits for its stream), so no two queues acquire
+# scratch for it at the same moment -- the failure the primer prevents (HSA_STATUS_ERROR_OUT_OF_
+# RESOURCES when twenty slot queues grew their scratch at once, round 2).  Every kernel of the batch
+# path (aggregate / verify, _dev and submit entry points) must fit the primer; the build fails
+# otherwise (check_private_segments).
+SYNC_ONLY_KERNELS = {
+    "k_sign": "ssb_sign_batch",
+    "k_sk_to_pk": "ssb_sk_to_pk_batch",
+    "k_pk_validate": "ssb_pk_validate_batch",
+    "k_combine_terms": "ssb_unsafe_aggregate_batch (255-bit products of unchecked shares)",
+    "k_dleq_verify": "ssb_dleq_verify_batch",
+    "k_feldman_share": "ssb_feldman_verify_batch",
+    "k_scratch_prime": "the primer itself",
+}
 
 
 def _inputs():
@@ -46,6 +63,60 @@ def _hash(paths, extra=""):
 
 def _source_hash():
     return _hash(_inputs())
+
+
+def _prime_bytes():
+    import re
+    with open(os.path.join(CSRC, "ssb_k_combine.hip")) as f:
+        return 4 * int(re.search(r"constexpr int PRIME_WORDS = (\d+);", f.read()).group(1))
+
+
+def kernel_resources(objs):
+    """{kernel: {"private": bytes, "vgpr": n, "agpr": n, "tu": file}} from the gfx950 code objects
+    embedded in the compiled objects (.hip_fatbin -> clang-offload-bundler -> llvm-readelf --notes)."""
+    import re
+    import tempfile
+    res = {}
+    with tempfile.TemporaryDirectory() as td:
+        for obj in objs:
+            fb, co = os.path.join(td, "fatbin"), os.path.join(td, "co")
+            if subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", ".hip_fatbin=" + fb, obj],
+                              capture_output=True).returncode != 0:
+                continue   # a host-only translation unit (no device code)
+            subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--" + ARCH, "--input=" + fb, "--output=" + co], check=True)
+            notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True,
+                                   capture_output=True, text=True).stdout
+            for blk in re.split(r"\n\s+- \.", notes):
+                m = re.search(r"\.name:\s+(\S+)", blk)
+                p = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+                if not (m and p):
+                    continue
+                mangled = m.group(1)
+                k = re.search(r"(k_[A-Za-z0-9_]+?)(?:I|E[ijPKNSvhmR])", mangled)
+                name = k.group(1) if k else mangled
+                v = re.search(r"\.vgpr_count:\s+(\d+)", blk)
+                a = re.search(r"\.agpr_count:\s+(\d+)", blk)
+                ent = dict(private=int(p.group(1)), vgpr=int(v.group(1)) if v else None,
+                           agpr=int(a.group(1)) if a else None, tu=os.path.basename(obj))
+                if name not in res or ent["private"] > res[name]["private"]:
+                    res[name] = ent
+    return res
+
+
+def check_private_segments(objs, out_json=None):
+    """Fails when a batch-path kernel's private segment exceeds the queue primer's per-lane array."""
+    import json
+    limit = _prime_bytes()
+    res = kernel_resources(objs)
+    bad = {k: v["private"] for k, v in res.items() if v["private"] > limit and k not in SYNC_ONLY_KERNELS}
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump(dict(primer_bytes=limit, sync_only=SYNC_ONLY_KERNELS, kernels=res), f, indent=1, sort_keys=True)
+    if bad:
+        raise RuntimeError("private segment above the queue primer's %d B/lane (k_scratch_prime) in batch-path "
+                           "kernels: %s" % (limit, bad))
+    return res
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -73,6 +144,9 @@ def build(force: bool = False, verbose: bool = True) -> str:
         os.replace(obj + ".tmp", obj)
         with open(stamp, "w") as f:
             f.write(h + "\n")
+    # private-segment guard (before the library is replaced): kernel_resources.json beside the objects
+    if os.path.exists(os.path.join(LLVM, "clang-offload-bundler")):
+        check_private_segments(objs, os.path.join(OBJDIR, "kernel_resources.json"))
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
     if verbose:
         print("[ssbls] linking:", " ".join(cmd), flush=True)

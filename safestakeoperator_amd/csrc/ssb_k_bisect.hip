@@ -208,17 +208,9 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
 
 namespace launch {
 
-// log2 of the tree's branching factor B: 4 (16-ary, default) or SSB_FB_BRANCH=4 / 16 / 2 / ...
-int fallback_log2_branch() {
-  static const int lb = [] {
-    const char* e = getenv("SSB_FB_BRANCH");
-    const int b = e ? atoi(e) : 16;
-    int l = 1;
-    while ((1 << l) < b && l < 8) ++l;
-    return l;
-  }();
-  return lb;
-}
+// log2 of the tree's branching factor: 16-ary (round 1 measured 16 against 4: one invalid share per
+// C2 batch costs 3 tested levels instead of 5)
+int fallback_log2_branch() { return 4; }
 int fallback_levels(size_t n) {
   const int lb = fallback_log2_branch();
   int L = 1;

@@ -122,147 +122,6 @@ __global__ void SSB_LB(64) k_msm_window(int c, const jac<F>* __restrict__ bsum, 
   msm_window_block<F>(blockIdx.x, sh, c, bsum, out_jac, out_q, out_p, negg1_pow, redo, lane_sum);
 }
 
-// ---- window sums and the G1 Horner as LANE-GROUP programs (ssb_lane_progs.h) ----
-// These stages are chains of point additions on a handful of workgroups -- latency, not
-// throughput: a G2 addition is 43 dependent Fp products on one lane but 6 product rounds on a
-// group of 8 lanes.  Every addition program checks its exceptional inputs (an operand at infinity,
-// equal or opposite points); a workgroup that met one flags `redo`, and the single-lane kernels
-// (k_msm_window / k_msm_horner, complete formulas) recompute exactly those windows / roots.
-template <class F> struct lane_pt;
-template <> struct lane_pt<fp2> {
-  static constexpr int G = lane::G2_ADD_G, NC = 6;
-  static constexpr int S0 = lane::G2_ADD_SCRATCH > lane::G2_DBL_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G2_DBL_SCRATCH;
-  template <class GR> static SSB_INL void add(GR& g, int a, int b, int d, uint32_t& e) { lane::g2_add(g, a, b, d, e); }
-  template <class GR> static SSB_INL void dbl(GR& g, int a, int d) { lane::g2_dbl(g, a, d); }
-};
-template <> struct lane_pt<fp> {
-  static constexpr int G = lane::G1_ADD_G, NC = 3;
-  static constexpr int S0 = lane::G1_ADD_SCRATCH > lane::G1_DBL_SCRATCH ? lane::G1_ADD_SCRATCH : lane::G1_DBL_SCRATCH;
-  template <class GR> static SSB_INL void add(GR& g, int a, int b, int d, uint32_t& e) { lane::g1_add(g, a, b, d, e); }
-  template <class GR> static SSB_INL void dbl(GR& g, int a, int d) { lane::g1_dbl(g, a, d); }
-};
-
-// One workgroup of NT threads per window, NG = NT / G groups; group t owns the m = 2^c / NG
-// consecutive buckets [t m, (t + 1) m) (the host launches it only when 2^c >= NG):
-//   S_t = sum_e B_{tm+e},  U_t = sum_e e B_{tm+e}          (running sums, 2(m-1) - 1 additions)
-//   suffix scan of S over the groups (log2 NG levels), U_t += [m] suffix_t for t >= 1,
-//   tree of U over the groups (log2 NG levels)   ->   sum_d d B_d  into lane_out[window].
-template <class F, int NT>
-__global__ void __launch_bounds__(NT) k_msm_window_lane(int c, const jac<F>* __restrict__ bsum, jac<F>* __restrict__ lane_out,
-                                                        uint32_t* __restrict__ redo) {
-  using namespace ssb::lane;
-  using T = lane_pt<F>;
-  constexpr int G = T::G, NG = NT / G, NC = T::NC;
-  constexpr int S = T::S0, U = S + NC, O = U + NC, X = O + NC, Y = X + NC, GS = Y + NC;
-  __shared__ fp lds[LP_NCODE_CONST + NG * GS];
-  __shared__ uint32_t flg[NG], has[NG], exc_any;
-  const int t = threadIdx.x / G, role = threadIdx.x % G;
-  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + t * GS, 0, 0, 0, (lu32*)&flg[t], role};
-  if (threadIdx.x == 0) exc_any = 0u;
-  lp_init_consts(g);
-  const int m = (1 << c) / NG;
-  const jac<F>* bk = bsum + (size_t)blockIdx.x * (1 << c);
-  lfp* base = (lfp*)lds + LP_NCODE_CONST;
-  auto load = [&](int slot, const jac<F>& p) { if (role < NC) g.s[slot + role] = ((const fp*)&p)[role]; };
-  auto copy = [&](int dst, int src) { if (role < NC) g.s[dst + role] = g.s[src + role]; };
-  uint32_t exc = 0;
-  bool hasU = m >= 2;
-  load(S, bk[t * m + m - 1]);
-  if (m >= 2) load(U, bk[t * m + m - 1]);
-  __syncthreads();
-  for (int e = m - 2; e >= 0; --e) {
-    load(O, bk[t * m + e]);
-    __syncthreads();
-    T::add(g, S, O, S, exc);
-    if (e >= 1) T::add(g, U, S, U, exc);
-  }
-  // suffix scan: S_t <- sum_{t' >= t} S_t'
-  for (int off = 1; off < NG; off <<= 1) {
-    copy(X, S);
-    __syncthreads();
-    const bool act = t + off < NG;
-    if (role < NC) g.s[O + role] = base[(act ? t + off : t) * GS + X + role];
-    __syncthreads();
-    uint32_t e2 = 0;
-    T::add(g, S, O, Y, e2);
-    if (act) { exc |= e2; copy(S, Y); }
-    __syncthreads();
-  }
-  // U_t += [m] S_t for t >= 1 (group 0's suffix carries weight 0)
-  for (int q = m; q > 1; q >>= 1) T::dbl(g, S, S);
-  if (m >= 2) {
-    uint32_t e2 = 0;
-    T::add(g, U, S, Y, e2);
-    if (t >= 1) { exc |= e2; copy(U, Y); }
-  } else {
-    if (t >= 1) copy(U, S);
-    hasU = t >= 1;
-  }
-  __syncthreads();
-  // tree over the groups
-  for (int h = NG / 2; h >= 1; h >>= 1) {
-    copy(X, U);
-    if (role == 0) has[t] = hasU ? 1u : 0u;
-    __syncthreads();
-    const bool act = t < h;
-    const int src = act ? t + h : t;
-    if (role < NC) g.s[O + role] = base[src * GS + X + role];
-    const bool ph = act && has[src];
-    __syncthreads();
-    uint32_t e2 = 0;
-    T::add(g, U, O, Y, e2);
-    if (ph) {
-      if (hasU) { exc |= e2; copy(U, Y); } else { copy(U, O); }
-      hasU = true;
-    }
-    __syncthreads();
-  }
-  if (exc) atomicOr(&exc_any, 1u);
-  __syncthreads();
-  if (t == 0 && role < NC) {
-    jac<F> r;
-    if (hasU) { for (int i = 0; i < NC; ++i) ((fp*)&r)[i] = g.s[U + i]; } else jac_set_inf(r);
-    if (role == 0) lane_out[blockIdx.x] = r;
-  }
-  if (threadIdx.x == 0) redo[blockIdx.x] = (exc_any || !hasU) ? 1u : 0u;
-}
-
-// G1 Horner per root on a group of 4 lanes: acc = W_{W-1}; acc = [2^c] acc + W_w, w = W-2 .. 0;
-// affine on the group's first lane.  redo[root] when an addition was exceptional.
-template <int NT>
-__global__ void __launch_bounds__(NT) k_msm_horner_lane(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
-                                                        g1_aff* __restrict__ out, uint32_t* __restrict__ redo) {
-  using namespace ssb::lane;
-  using T = lane_pt<fp>;
-  constexpr int G = T::G, NG = NT / G, NC = T::NC;
-  constexpr int A = T::S0, O = A + NC, GS = O + NC;
-  __shared__ fp lds[LP_NCODE_CONST + NG * GS];
-  __shared__ uint32_t flg[NG];
-  const int t = threadIdx.x / G, role = threadIdx.x % G;
-  const int r = blockIdx.x * NG + t;
-  const bool act = r < ngroups;
-  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + t * GS, 0, 0, 0, (lu32*)&flg[t], role};
-  lp_init_consts(g);
-  const g1_jac* ws = wsum + (size_t)(act ? r : 0) * W;
-  if (role < NC) g.s[A + role] = ((const fp*)&ws[W - 1])[role];
-  __syncthreads();
-  uint32_t exc = 0;
-  for (int w = W - 2; w >= 0; --w) {
-    for (int q = 0; q < c; ++q) T::dbl(g, A, A);
-    if (role < NC) g.s[O + role] = ((const fp*)&ws[w])[role];
-    __syncthreads();
-    T::add(g, A, O, A, exc);
-  }
-  if (act && role == 0) {
-    g1_jac a;
-    for (int i = 0; i < NC; ++i) ((fp*)&a)[i] = g.s[A + i];
-    g1_aff o;
-    jac_to_aff(o, a);
-    out[r] = o;
-    redo[r] = exc ? 1u : 0u;
-  }
-}
-
 // ---- narrow-window sums (msm_window_seq_block, ssb_blocks.h) ----
 template <class F>
 __global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* __restrict__ bsum,
@@ -453,64 +312,33 @@ void msm_sort(hipStream_t st, int n, const rlc_key& key, const uint32_t* sflags,
   hipLaunchKernelGGL(k_order_scatter, dim3((K + 255) / 256), dim3(256), 0, st, K, c1.base, cnt, bsum, order);
 }
 
-// Which MSM side runs its window reduce / Horner as lane-group kernels: SSB_MSM_LANE bit 0 = G1,
-// bit 1 = G2; default 0 (off).  Measured on MI355X (C2, 14 batches in flight, 20 timed steps):
-// the G1 side's window sums + Horner drop 3.06 -> 2.29 ms per batch but the G1 side is not on the
-// batch's critical path (the G2 side is) and the 64-lane groups' LDS and waves cost throughput:
-// 6.35 M -> 5.89 M partial sigs/s; the G2 window reduce goes 1.9 -> 2.6 ms (slower than one lane
-// per window).
-int msm_lane_mask() {
-  static const int m = [] { const char* e = getenv("SSB_MSM_LANE"); return e ? atoi(e) : 0; }();
-  return m;
-}
-constexpr int WL_NT2 = 256, WL_NT1 = 64, HL_NT = 64;
-
 void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
             const uint32_t* flags, const g2_aff* sig, g2_jac* bsum, g2_aff* pair_q, g1_aff* pair_p,
-            const g1_aff* negg1_pow, g2_jac* lane_sum, uint32_t* redo) {
+            const g1_aff* negg1_pow) {
   const uint32_t nb = c.ngroups * c.W << c.c;
   hipLaunchKernelGGL(k_msm_bucket<fp2>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, order, start,
                      cnt, ent, flags, sig, bsum);
-  const bool lanes = (msm_lane_mask() & 2) && (1u << c.c) >= (uint32_t)(WL_NT2 / lane_pt<fp2>::G);
-  if (lanes)
-    hipLaunchKernelGGL((k_msm_window_lane<fp2, WL_NT2>), dim3(c.ngroups * c.W), dim3(WL_NT2), 0, st, (int)c.c,
-                       (const g2_jac*)bsum, lane_sum, redo);
   hipLaunchKernelGGL(k_msm_window<fp2>, dim3(c.ngroups * c.W), dim3(64), 0, st, (int)c.c, (const g2_jac*)bsum,
-                     (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)(lanes ? redo : nullptr),
-                     (const g2_jac*)lane_sum);
+                     (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr, (const g2_jac*)nullptr);
 }
 
 void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
-            const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum, uint32_t* redo) {
+            const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum) {
   const uint32_t nb = c.ngroups * c.W << c.c;
   const uint32_t nw = c.ngroups * c.W;
   hipLaunchKernelGGL(k_msm_bucket<fp>, dim3((nb + (64u >> lj) - 1) / (64u >> lj)), dim3(64), 0, st, nb, c.base, lj, order, start,
                      cnt, ent, flags, pk, bsum);
-  const bool lanes = (msm_lane_mask() & 1) != 0;
-  if (lanes && (1u << c.c) >= (uint32_t)(WL_NT1 / lane_pt<fp>::G)) {
-    hipLaunchKernelGGL((k_msm_window_lane<fp, WL_NT1>), dim3(nw), dim3(WL_NT1), 0, st, (int)c.c, (const g1_jac*)bsum, wsum, redo);
-    hipLaunchKernelGGL(k_msm_window<fp>, dim3(nw), dim3(64), 0, st, (int)c.c, (const g1_jac*)bsum, wsum,
-                       (g1_aff*)nullptr, (g1_aff*)nullptr, (const g1_aff*)nullptr, (const uint32_t*)redo, (const g1_jac*)wsum);
-  } else if (c.c <= 4) {
+  if (c.c <= 4) {
     hipLaunchKernelGGL(k_msm_window_seq<fp>, dim3((nw + 63) / 64), dim3(64), 0, st, nw, (int)c.c, (const g1_jac*)bsum, wsum);
   } else {
     hipLaunchKernelGGL(k_msm_window<fp>, dim3(nw), dim3(64), 0, st, (int)c.c, (const g1_jac*)bsum, wsum,
                        (g1_aff*)nullptr, (g1_aff*)nullptr, (const g1_aff*)nullptr, (const uint32_t*)nullptr, (const g1_jac*)nullptr);
   }
-  if (lanes) {
-    uint32_t* hredo = redo + nw;
-    constexpr int NG = HL_NT / lane_pt<fp>::G;
-    hipLaunchKernelGGL(k_msm_horner_lane<HL_NT>, dim3((c.ngroups + NG - 1) / NG), dim3(HL_NT), 0, st, (int)c.ngroups, (int)c.c,
-                       (int)c.W, (const g1_jac*)wsum, root_sum, hredo);
-    hipLaunchKernelGGL(k_msm_horner, dim3((c.ngroups + 63) / 64), dim3(64), 0, st, (int)c.ngroups, (int)c.c, (int)c.W,
-                       (const g1_jac*)wsum, root_sum, (const uint32_t*)hredo);
-  } else {
-    hipLaunchKernelGGL(k_msm_horner, dim3((c.ngroups + 63) / 64), dim3(64), 0, st, (int)c.ngroups, (int)c.c, (int)c.W,
-                       (const g1_jac*)wsum, root_sum, (const uint32_t*)nullptr);
-  }
+  hipLaunchKernelGGL(k_msm_horner, dim3((c.ngroups + 63) / 64), dim3(64), 0, st, (int)c.ngroups, (int)c.c, (int)c.W,
+                     (const g1_jac*)wsum, root_sum, (const uint32_t*)nullptr);
 }
 
-bool msm_fused_ok(const msm_cfg& c1) { return msm_lane_mask() == 0 && c1.c <= 4; }
+bool msm_fused_ok(const msm_cfg& c1) { return c1.c <= 4; }
 
 h2c_fuse fuse_of(const h2c_ws* hw, int n_roots, g2_aff* out) {
   h2c_fuse h{0, nullptr, nullptr, nullptr, nullptr, 0, nullptr};

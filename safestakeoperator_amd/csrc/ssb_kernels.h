@@ -142,18 +142,16 @@ void hash_to_g2(hipStream_t st, int n, const uint8_t* roots, const dst_arg& dst,
 void msm_sort(hipStream_t st, int n, const rlc_key& key, const uint32_t* sflags, const uint32_t* pflags,
               const uint32_t* share_root, const msm_cfg& c2, const msm_cfg& c1, uint32_t K, uint32_t* cnt,
               uint32_t* start, uint32_t* cur, uint32_t* bsum, uint32_t* ent, uint32_t* order);
-// (lane_sum: W window points, redo: W words -- the lane-group window kernel's results and flags;
-// msm_g1's redo: ngroups * W + ngroups words, windows then roots)
 void msm_g2(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
             const uint32_t* flags, const g2_aff* sig, g2_jac* bsum, g2_aff* pair_q, g1_aff* pair_p,
-            const g1_aff* negg1_pow, g2_jac* lane_sum, uint32_t* redo);
+            const g1_aff* negg1_pow);
 void msm_g1(hipStream_t st, const msm_cfg& c, int lj, const uint32_t* order, const uint32_t* start, const uint32_t* cnt, const uint32_t* ent,
-            const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum, uint32_t* redo);
+            const uint32_t* flags, const g1_aff* pk, g1_jac* bsum, g1_jac* wsum, g1_aff* root_sum);
 // gflags[s] = DEC_IN_GROUP when signature s (decodable, not infinity) passes psi(P) == [x]P
 // subgroup checks: single-lane (default) or SSB_SUBGROUP=lane (8-lane groups + exact redo of exceptional shares)
 // msm_g2 + msm_g1 as three launches on one stream (bucket sums of both sides, window sums of both
-// sides, the G1 Horner): the two MSMs overlap on the device.  Only without lane-group window
-// kernels and with G1 windows of <= 16 buckets (msm_fused_ok).  With hw (the staged hash's
+// sides, the G1 Horner): the two MSMs overlap on the device.  Only with G1 windows of <= 16
+// buckets (msm_fused_ok).  With hw (the staged hash's
 // workspace, after h2c_u and subgroup_map's SWU map), the cofactor clearing rides along the
 // bucket sums and the affine output H[0..n_roots) along the window sums.
 bool msm_fused_ok(const msm_cfg& c1);

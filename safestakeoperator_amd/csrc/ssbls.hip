@@ -93,32 +93,11 @@ struct ssb_ctx {
   std::map<std::string, std::vector<evpair>> history;  // every launch while accumulating
   std::vector<evpair> pool;
   g1_aff* negg1_pow = nullptr;                         // device: [2^s](-g1), s = 0..63 (G2 MSM pairs)
-  // Context-wide streams for the kernels with the largest private segments (combine: up to 4.4 KB
-  // per lane, exact fallback: 2.6 KB), shared by all slots: the runtime reserves scratch per
-  // hardware queue for the largest kernel it has run, so these stay on two queues instead of
-  // every slot's.  spec: the speculative combines; tail: verdicts, exact fallback, exact combine.
+  // Context-wide streams of the three-stream (latency) configuration, shared by all its slots:
+  // spec runs the speculative combines, tail the verdicts, the exact fallback and the exact combine
+  // (the kernels with the largest private segments stay off the slots' queues).  One-stream slots
+  // run every stage on the slot's own stream and leave both idle.
   hipStream_t spec = nullptr, tail = nullptr;
-  // tail streams: slot i uses tails[i % ntails] (tails[0] == tail).  More than one lets the exact
-  // fallbacks of failed batches on different slots run concurrently (SSB_TAILS, default 1: the
-  // hardware queues are worth more as hash streams; a caller must give the process enough hardware
-  // queues -- slots + 2 + tails + hash streams -- or streams share queues and serialise).
-  static constexpr int MAX_TAILS = 4;
-  hipStream_t tails[MAX_TAILS] = {nullptr, nullptr, nullptr, nullptr};
-  int ntails = 1;
-  // hash streams (SSB_HASH_STREAMS, default 0): with one stream per slot, hash_to_G2 of slot i's
-  // batch runs on hashs[i % nhash] beside the slot's decode / subgroup / MSM chain instead of in
-  // front of it (the hash depends on the roots only; the Miller loops wait for it).  They pay off
-  // when the slots are few (14 slots + spec + 1 tail at the driver's 20 steps: H = 0 5.85 M,
-  // 6 7.19 M partial sigs/s); the default configuration instead spends every hardware queue on a
-  // slot (20 slots, hash on the slot's stream: 9.33 M; 20 slots + 2 hash streams oversubscribe the
-  // queues: 4.05 M).
-  static constexpr int MAX_HASH = 8;
-  hipStream_t hashs[MAX_HASH] = {};
-  int nhash = 0;
-  // G1-side streams (SSB_G1_STREAMS, default 0): the per-root G1 sums of slot i's batch run on
-  // g1s[i % ng1] beside the slot's G2 MSM instead of after it
-  hipStream_t g1s[MAX_HASH] = {nullptr, nullptr, nullptr, nullptr};
-  int ng1 = 0;
   // decoded public keys (ssb_pk_cache_set): affine points + DEC_* flags, indexed by the caller
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0;
   // RLC key of each batch: fresh from getrandom() per call (default), or expanded from the caller's
@@ -179,7 +158,7 @@ void pick_slot(ssb_ctx* ctx, void* stream) {
   ctx->next = (ctx->next + 1) % ctx->nslots;
 }
 
-hipStream_t slot_tail(ssb_ctx* ctx) { return ctx->tails[(int)(ctx->cur - ctx->sl) % ctx->ntails]; }
+hipStream_t slot_tail(ssb_ctx* ctx) { return ctx->tail; }
 
 int ensure_io(ssb_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->io_bytes) return SSB_OK;
@@ -206,10 +185,8 @@ int init_slot(ssb_slot& S, int streams) {
                         &S.ev_host})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
   // each new queue acquires its scratch now, alone (slots are created one after the other)
-  if (!getenv("SSB_NO_PRIME")) {
-    if (launch::prime_queue(S.stream)) return SSB_EHIP;
-    if (!S.shared) for (hipStream_t sd : S.side) if (launch::prime_queue(sd)) return SSB_EHIP;
-  }
+  if (launch::prime_queue(S.stream)) return SSB_EHIP;
+  if (!S.shared) for (hipStream_t sd : S.side) if (launch::prime_queue(sd)) return SSB_EHIP;
   return SSB_OK;
 }
 // the pending host-buffer batch of the slot: wait for it, copy its outputs to the caller's pointers
@@ -334,29 +311,17 @@ bool fallback_per_share() {
   const char* e = getenv("SSB_FALLBACK");
   return e && !strcmp(e, "share");
 }
-bool fallback_on_tail() {
-  const char* e = getenv("SSB_FB_STREAM");
-  return !(e && !strcmp(e, "slot"));
-}
-// One-stream slots run their whole batch on the slot's stream (SSB_POST=slot, the default): the
-// verdicts, the exact fallback (no-ops when the batch passed) and ONE combine from the verdicts
-// follow the final exponentiation in order, instead of a speculative combine on the shared spec
-// stream plus the exact path on a shared tail stream.  Every hardware queue then carries one slot
-// (measured C2 at the driver's 20 steps: a shared tail stream finishes the batches one at a time,
-// ~0.7 ms apart, once the pairing chains of all slots end together).  SSB_POST=tail keeps the
-// shared streams (the three-stream latency configuration always does).
-bool post_on_slot(const ssb_slot* s) {
-  static const bool slot = [] { const char* e = getenv("SSB_POST"); return !(e && !strcmp(e, "tail")); }();
-  return s->shared && slot;
-}
+// One-stream slots run their whole batch on the slot's stream: the verdicts, the exact fallback
+// (no-ops when the batch passed) and ONE combine from the verdicts follow the final exponentiation
+// in order -- every hardware queue carries one slot (round 2: a shared tail stream finished the
+// batches one at a time, ~0.7 ms apart, once the pairing chains of all slots ended together).  The
+// three-stream latency configuration runs them on the context's spec / tail streams.
+bool post_on_slot(const ssb_slot* s) { return s->shared; }
 msm_plan plan_msm(size_t n, size_t n_roots) {
   msm_plan p;
   const size_t g1n = n_roots ? n_roots : 1;
   p.g1_msm = g1_use_msm(n, n_roots);
   int c2 = msm_pick_c(n, 1, 3, 8), c1 = msm_pick_c(n, g1n, 2, 8);  // c <= 8: <= 4 buckets per window lane
-  // SSB_MSM_C2 / SSB_MSM_C1: force the window widths (experiments: latency vs work)
-  if (const char* e = getenv("SSB_MSM_C2")) c2 = std::max(3, std::min(8, atoi(e)));
-  if (const char* e = getenv("SSB_MSM_C1")) c1 = std::max(2, std::min(8, atoi(e)));
   auto keys = [&](int c, size_t g) { return (size_t)((64 + c - 1) / c) * g << c; };
   while (c1 > 2 && keys(c2, 1) + keys(c1, g1n) > MSM_KMAX) --c1;
   p.g2 = msm_cfg{(uint32_t)c2, (uint32_t)((64 + c2 - 1) / c2), 0u, 1u};
@@ -381,7 +346,6 @@ struct verify_ws {
   g2_jac* b2; g1_jac* b1; g1_jac* w1;                                              // MSM buckets / windows
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
   g2_jac* rsig; uint32_t* gst; uint8_t* gv0; uint8_t* gv1;                         // failed-batch group tests
-  g2_jac* w2; uint32_t* redo2; uint32_t* redo1;                                    // lane-group window kernels
   size_t npairs;
 };
 // Miller values of the pairs plus the levels of the 8-ary product tree
@@ -401,9 +365,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
          align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
          3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(n * sizeof(g2_jac)) +
-         align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
-         align_up(MSM_WMAX * sizeof(g2_jac)) + align_up(MSM_WMAX * 4) +
-         align_up(((size_t)p.g1.ngroups * (p.g1.W + 1) + 1) * 4);
+         align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
@@ -427,8 +389,6 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.rsig = c.take<g2_jac>(n);
   w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
   w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
-  w.w2 = c.take<g2_jac>(MSM_WMAX); w.redo2 = c.take<uint32_t>(MSM_WMAX);
-  w.redo1 = c.take<uint32_t>((size_t)w.plan.g1.ngroups * (w.plan.g1.W + 1) + 1);
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
@@ -440,10 +400,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
                bool* spec_done = nullptr) {
   rlc_key key;
   if (int rc = draw_rlc_key(ctx, rlc_seed, key)) return rc;
-  hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0];
-  if (ctx->cur->shared && ctx->nhash > 0) sh = ctx->hashs[(int)(ctx->cur - ctx->sl) % ctx->nhash];
-  hipStream_t s1 = ctx->cur->side[1];
-  if (ctx->cur->shared && ctx->ng1 > 0) s1 = ctx->g1s[(int)(ctx->cur - ctx->sl) % ctx->ng1];
+  hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0], s1 = ctx->cur->side[1];
   const msm_plan& P = w.plan;
   // One-stream slots: the G2 and G1 MSMs share launches (msm_both), and the hash_to_G2 stages ride
   // along the batch's own kernels -- the SWU map beside the subgroup checks, the cofactor clearing
@@ -469,7 +426,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   // the decode waited for a free wave slot behind the other slots' decode waves (~1.5 ms on the
   // last batches of the driver's run, profiles/r02_gate_timeline.txt)
   const bool clean = fuse_sort && n && ctx->cur->clean_cnt == w.cnt && ctx->cur->clean_tickets == w.tickets &&
-                     ctx->cur->clean_K >= P.K && !getenv("SSB_ALWAYS_PREP");
+                     ctx->cur->clean_K >= P.K;
   // this batch's counts / tickets are clean at its end only on the fused path (its scan and last
   // blocks reset them); any other path writes the workspace without leaving them clean
   if (fuse_sort) { ctx->cur->clean_cnt = w.cnt; ctx->cur->clean_tickets = w.tickets; ctx->cur->clean_K = P.K; }
@@ -537,7 +494,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   if (s1 != st) SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
     timed t(ctx, "k_msm_g1", s1);
-    launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cur, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p, w.redo1);
+    launch::msm_g1(s1, P.g1, P.lj1, w.order, w.start, w.cur, w.ent, w.flags, w.pk_aff, w.b1, w.w1, w.pair_p);
   } else {
     timed t(ctx, "k_sum_g1", s1);
     hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)n_roots), dim3(SEG_THREADS), 0, s1, (int)n_roots, w.rstart, w.rcnt, w.perm,
@@ -545,7 +502,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   if (s1 != st) SSB_HIP(hipEventRecord(ctx->cur->ev_r1, s1));
   if (n) on_decoded();
-  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cur, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w2, w.redo2); }
+  { timed t(ctx, "k_msm_g2"); launch::msm_g2(st, P.g2, P.lj2, w.order, w.start, w.cur, w.ent, w.flags, w.sig_aff, w.b2, w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow); }
   }
   if (!fused && s1 != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   if (!fuse_hash && sh != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
@@ -570,11 +527,9 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     }
     hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok, (int)n, (const uint32_t*)w.flags, d_verdict);
   }
-  // verdicts (+ the exact fallback when the batch failed) on the slot's tail stream: its kernels
-  // have the largest private segments, and the runtime reserves scratch per hardware queue for the
-  // largest kernel the queue has run (on every slot stream, 12 slots ran out of resources).
-  // SSB_FB_STREAM=slot puts them on the slot's own stream (few slots only).
-  const bool fb_tail = fallback_on_tail() && !post_on_slot(ctx->cur);
+  // the exact fallback when the batch failed: on the slot's own stream (one-stream slots), or the
+  // context's tail stream (three-stream configuration)
+  const bool fb_tail = !post_on_slot(ctx->cur);
   hipStream_t fbs = fb_tail ? tail : st;
   if (fb_tail && tail != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
@@ -615,16 +570,6 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   if (init_slot(ctx->sl[0], ctx->slot_streams) != SSB_OK) { delete ctx; return SSB_EHIP; }
   if (hipStreamCreateWithFlags(&ctx->spec, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx->sl[0]); delete ctx; return SSB_EHIP; }
-  ctx->tails[0] = ctx->tail;
-  if (const char* e = getenv("SSB_TAILS")) ctx->ntails = std::max(1, std::min(ssb_ctx::MAX_TAILS, atoi(e)));
-  for (int i = 1; i < ctx->ntails; ++i)
-    if (hipStreamCreateWithFlags(&ctx->tails[i], hipStreamNonBlocking) != hipSuccess) { ctx->ntails = i; break; }
-  if (const char* e = getenv("SSB_HASH_STREAMS")) ctx->nhash = std::max(0, std::min(ssb_ctx::MAX_HASH, atoi(e)));
-  for (int i = 0; i < ctx->nhash; ++i)
-    if (hipStreamCreateWithFlags(&ctx->hashs[i], hipStreamNonBlocking) != hipSuccess) { ctx->nhash = i; break; }
-  if (const char* e = getenv("SSB_G1_STREAMS")) ctx->ng1 = std::max(0, std::min(ssb_ctx::MAX_HASH, atoi(e)));
-  for (int i = 0; i < ctx->ng1; ++i)
-    if (hipStreamCreateWithFlags(&ctx->g1s[i], hipStreamNonBlocking) != hipSuccess) { ctx->ng1 = i; break; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
@@ -649,9 +594,6 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->negg1_pow) hipFree(ctx->negg1_pow);
   if (ctx->pkc_aff) hipFree(ctx->pkc_aff);
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
-  for (int i = 1; i < ctx->ntails; ++i) if (ctx->tails[i]) { hipStreamSynchronize(ctx->tails[i]); hipStreamDestroy(ctx->tails[i]); }
-  for (int i = 0; i < ctx->nhash; ++i) if (ctx->hashs[i]) { hipStreamSynchronize(ctx->hashs[i]); hipStreamDestroy(ctx->hashs[i]); }
-  for (int i = 0; i < ctx->ng1; ++i) if (ctx->g1s[i]) { hipStreamSynchronize(ctx->g1s[i]); hipStreamDestroy(ctx->g1s[i]); }
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
@@ -1064,7 +1006,6 @@ int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) SSB_HIP(hipStreamSynchronize(x));
-  for (int i = 1; i < ctx->ntails; ++i) SSB_HIP(hipStreamSynchronize(ctx->tails[i]));
   if (ctx->pkc_aff) { hipFree(ctx->pkc_aff); ctx->pkc_aff = nullptr; }
   if (ctx->pkc_flags) { hipFree(ctx->pkc_flags); ctx->pkc_flags = nullptr; }
   ctx->pkc_n = 0;

@@ -94,3 +94,20 @@ def test_plain_c_caller_golden_cases():
         want_ver += "".join("1" if v else "0" for v in c["share_verdicts"])
     assert out[len(cases)] == "verdicts " + want_ver
     assert out[len(cases) + 1] == "verify " + want_ver
+
+
+def test_batch_kernels_fit_the_queue_primer():
+    """Build guard (safestakeoperator_amd/build.py check_private_segments): every kernel the batch
+    path can launch on a slot queue has a private segment <= k_scratch_prime's per-lane array, so a
+    slot queue never has to grow its scratch while other queues run (HSA_STATUS_ERROR_OUT_OF_RESOURCES,
+    round 2); the larger ones are only launched by synchronous entry points."""
+    import glob
+    from safestakeoperator_amd import build as b
+    build(verbose=False)
+    objs = sorted(glob.glob(os.path.join(b.OBJDIR, "*.o")))
+    res = b.check_private_segments(objs)
+    limit = b._prime_bytes()
+    for k in ("k_decode_count", "k_subgroup_map", "k_msm_bucket2", "k_msm_window2", "k_miller_pairs", "k_fp12_prod8",
+              "k_final_lane", "k_fb_prep", "k_fb_rlc", "k_fb_level", "k_select_combine", "k_combine_terms_gls",
+              "k_combine_sum", "k_share_map"):
+        assert k in res and res[k]["private"] <= limit, (k, res.get(k))
