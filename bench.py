@@ -194,55 +194,65 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_coun
                 share_sigs=sigs, share_pks=pks, valid=valid, n_bad=len(bad))
 
 
-def cpu_baseline(wl, t, n, gpu_out=None, n_val=1024, threads=None, seconds=4.0):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(wl, t, n, gpu_out=None, n_val=4096, n_val_share=1024, threads=None, reps=5):
     """The plain-C oracle (oracle/bls_c.c, multi-threaded, `kind: "port"`) on a bounded sample of
-    the same workload: the first n_val validators x n shares of rank 0's batch, H(root) once per
-    root, two columns ("per-signature verify and RLC batch, both reported"):
+    the same workload, H(root) once per root, two columns ("per-signature verify and
+    RLC batch, both reported"), each the MEDIAN of `reps` (>= 5) whole passes:
       * rlc (the `value`): the batch-verify algorithm family the engine and lighthouse's
         verify_signature_sets use -- per share decompress + subgroup check + 64-bit [k]pk, [k]sig,
-        one multi-pairing and one final exponentiation, then the integer-Lagrange combine;
+        one multi-pairing and one final exponentiation, then the integer-Lagrange combine -- over the
+        first n_val validators x n shares of rank 0's batch;
       * per_share: every share verified on its own (2 Miller loops + final exponentiation each,
-        the reference's loop at generic_threshold.rs:149-169), 255-bit Lagrange combine.
+        the reference's loop at generic_threshold.rs:149-169), 255-bit Lagrange combine, over the
+        first n_val_share validators.
     Threads: the GPU box's CPU share (16 per GPU), fewer if the host has fewer.  Both columns are
     checked against the GPU's combined signatures for the same validators."""
     from oracle import bls_c
     threads = threads or max(1, min(16, os.cpu_count() or 1))
-    N = n_val * n
-    off = list(range(0, N + 1, n))
-    sigs = wl["sigs"][:96 * N]
-    pks = wl["pks"][:48 * N]
-    args = (off, [t] * n_val, sigs, pks, wl["ids"][:N], wl["job_root"][:n_val], wl["roots"], threads)
     bls_c.load()
 
-    reps = {}
+    def args_for(nv):
+        N = nv * n
+        return (list(range(0, N + 1, n)), [t] * nv, wl["sigs"][:96 * N], wl["pks"][:48 * N], wl["ids"][:N],
+                wl["job_root"][:nv], wl["roots"], threads)
 
-    def timed(fn):          # whole passes until `seconds` of CPU work per column
-        t0, k = time.perf_counter(), 0
-        while True:
+    def median_time(fn, k):
+        ts, res = [], None
+        for _ in range(k):
+            t0 = time.perf_counter()
             res = fn()
-            k += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-        reps[fn] = k
-        return res, (time.perf_counter() - t0) / k
+            ts.append(time.perf_counter() - t0)
+        return res, sorted(ts)[len(ts) // 2], ts
 
-    f_rlc = lambda: bls_c.threshold_batch_rlc(*args)
-    f_share = lambda: bls_c.threshold_batch(*args, verify_all=True)
-    (out, st, _, ver, batch_ok), dt_rlc = timed(f_rlc)
-    (out2, st2, _, ver2), dt_share = timed(f_share)
-    ok = bool((st == 0).all()) and bool(ver[:N].all()) and batch_ok and bool((st2 == 0).all()) and bool(ver2[:N].all())
+    a_rlc, a_share = args_for(n_val), args_for(n_val_share)
+    (out, st, _, ver, batch_ok), dt_rlc, ts_rlc = median_time(lambda: bls_c.threshold_batch_rlc(*a_rlc), reps)
+    (out2, st2, _, ver2), dt_share, ts_share = median_time(lambda: bls_c.threshold_batch(*a_share, verify_all=True), reps)
+    N, N2 = n_val * n, n_val_share * n
+    ok = bool((st == 0).all()) and bool(ver[:N].all()) and batch_ok and bool((st2 == 0).all()) and bool(ver2[:N2].all())
     if gpu_out is not None:
-        ok = ok and all(out[v].tobytes() == gpu_out[v].tobytes() == out2[v].tobytes() for v in range(n_val))
-    return dict(value=round(N / dt_rlc, 1), unit="partial_sigs/s", cores=threads, kind="port",
+        ok = ok and all(out[v].tobytes() == gpu_out[v].tobytes() for v in range(n_val))
+        ok = ok and all(out2[v].tobytes() == gpu_out[v].tobytes() for v in range(n_val_share))
+    return dict(value=round(N / dt_rlc, 1), unit="partial_sigs/s", cores=threads, kind="port", cpu_model=cpu_model(),
                 per_core=round(N / dt_rlc / threads, 1), combined_per_s=round(n_val / dt_rlc, 1),
-                seconds=round(dt_rlc, 2), matches_gpu=bool(ok),
-                per_share=dict(value=round(N / dt_share, 1), per_core=round(N / dt_share / threads, 1),
-                               combined_per_s=round(n_val / dt_share, 1), seconds=round(dt_share, 2)),
-                sample="%d validators x %d shares of the rank-0 C2 batch, %d / %d whole passes (rlc: batch verify + "
-                       "%d-of-%d combine; per_share: every share verified on its own), H(root) once per root, "
-                       "oracle/bls_c.c (plain C, 64-bit limbs), %d threads"
-                       % (n_val, n, reps[f_rlc], reps[f_share], t, n, threads),
-                seconds_total=round(dt_rlc * reps[f_rlc] + dt_share * reps[f_share], 2))
+                seconds=round(dt_rlc, 3), matches_gpu=bool(ok), repetitions=reps, statistic="median",
+                per_share=dict(value=round(N2 / dt_share, 1), per_core=round(N2 / dt_share / threads, 1),
+                               combined_per_s=round(n_val_share / dt_share, 1), seconds=round(dt_share, 3)),
+                sample="rlc: %d validators x %d shares of the rank-0 C2 batch (batch verify + %d-of-%d combine); "
+                       "per_share: the first %d validators (every share verified on its own); median of %d whole "
+                       "passes each; H(root) once per root; oracle/bls_c.c (plain C, 64-bit limbs), %d threads"
+                       % (n_val, n, t, n, n_val_share, reps, threads),
+                seconds_total=round(sum(ts_rlc) + sum(ts_share), 2))
 
 
 def main():
@@ -485,6 +495,48 @@ def main():
     eng.kernel_timing(False)
     latency_ms = sorted(lat)[1] * 1e3
 
+    # phase 1b: the roofline of the headline path's dominant kernel, k_subgroup_map (the fused
+    # one-stream path's subgroup checks, + the SWU map of the roots and the MSM sort's scatter
+    # riding along), and of k_decode_count, measured where the kernel fills the chip: a one-stream
+    # slot at depth 1 running ONE batch of R x the C2 batch (R = 8: 131,072 shares = 2,048 waves, two
+    # per SIMD -- the occupancy the kernel is built for).  The C2 batch alone is 256 waves on 1,024
+    # SIMDs; the pipelined run fills the chip with 20 of them, where per-launch times are shared.
+    rf = None
+    if not strong and not args.compressed_pk:
+        R = 8
+        rf_in = dict(sig=d_sig.repeat(R), pk=d_pkidx.repeat(R), ids=d_ids.repeat(R),
+                     off=torch.arange(0, R * N + 1, n, dtype=torch.int32, device=dev),
+                     t=torch.full((R * V,), t, dtype=torch.int32, device=dev), jr=d_jr.repeat(R))
+        rf_out = dict(out=torch.empty((R * V, 96), dtype=torch.uint8, device=dev),
+                      st=torch.empty((R * V,), dtype=torch.int32, device=dev),
+                      err=torch.empty((R * V, 2), dtype=torch.int64, device=dev),
+                      ver=torch.empty((R * N,), dtype=torch.uint8, device=dev))
+        if lib.ssb_set_slot_streams(eng.handle, 1) != 0 or lib.ssb_set_pipeline_depth(eng.handle, 1) != 0:
+            raise RuntimeError("ssb_set_slot_streams / ssb_set_pipeline_depth")
+        rs = torch.cuda.ExternalStream(lib.ssb_slot_stream(eng.handle, 0), device=dev)
+
+        def rf_step(i):
+            rc = lib.ssb_threshold_aggregate_batch_cached_dev(
+                eng.handle, R * V, R * N, rf_in["off"].data_ptr(), rf_in["t"].data_ptr(), rf_in["sig"].data_ptr(),
+                rf_in["pk"].data_ptr(), rf_in["ids"].data_ptr(), rf_in["jr"].data_ptr(), n_roots, d_roots.data_ptr(),
+                ctypes.cast(dst_arr, _lib._u8p), len(DST), (seed_base + 7777 + i) & (2 ** 64 - 1),
+                rf_out["out"].data_ptr(), rf_out["st"].data_ptr(), rf_out["err"].data_ptr(), rf_out["ver"].data_ptr(),
+                ctypes.c_void_p(rs.cuda_stream))
+            if rc != 0:
+                raise RuntimeError("roofline batch: %s" % lib.ssb_last_error(eng.handle))
+        rf_step(0)
+        torch.cuda.synchronize(dev)
+        eng.kernel_timing(True)
+        for i in range(3):
+            rf_step(1 + i)
+        torch.cuda.synchronize(dev)
+        rf = {k: eng.kernel_time(k) for k in ("k_subgroup", "k_decode")}
+        eng.kernel_timing(False)
+        rf_ok = (bool(((rf_out["st"].cpu().numpy() == 0) == np.tile(job_ok, R)).all())
+                 and bool((rf_out["ver"].cpu().numpy() == np.tile(valid, R)).all()))
+        rf = dict(R=R, shares=R * N, ok=rf_ok, ms={k: (v[0] / v[1] if v[1] else 0.0) for k, v in rf.items()})
+        del rf_in, rf_out
+
     # phase 2: the timed run, S batches in flight
     # (throughput configuration: S slots of args.slot_streams streams)
     if lib.ssb_set_slot_streams(eng.handle, args.slot_streams) != 0 or lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
@@ -616,6 +668,35 @@ def main():
         step_mads = sum(km.values())
         if args.final_verify:   # + the combined-signature verify: V shares, no combine
             step_mads += sum(v for k, v in kernel_mads(mads, V, 1, 1, n_roots).items() if k != "k_combine_fast")
+        # roofline: k_subgroup_map at full occupancy (phase 1b); the depth-1 C2 figure beside it
+        roof = None
+        if rf is not None and rf["ms"]["k_subgroup"] > 0:
+            mp = msm_plan(rf["shares"], n_roots)
+            sg_mads = rf["shares"] * mads["subgroup"]
+            dec_mads = rf["shares"] * mads["decode_sig"]
+            # algorithmic bytes per share of k_subgroup_map: the affine signature (g2_aff, 4 x 48 B +
+            # flag word) and three flag / root words read, two flag words written, and the sort's
+            # scatter (the share's root word read, one 4-byte entry written per MSM window)
+            sg_bytes_share = 196 + 3 * 4 + 2 * 4 + 4 + 4 * (mp["W2"] + mp["W1"])
+            pmc = pmc_traffic("k_subgroup_map")
+            roof = {"bound": "valu-int32-mad", "kernel": "k_subgroup_map",
+                    "achieved": round(sg_mads / (rf["ms"]["k_subgroup"] * 1e-3) / 1e12, 4),
+                    "peak": round(MAD_PEAK_MEASURED / 1e12, 2), "unit": "TMAD/s",
+                    "frac": round(sg_mads / (rf["ms"]["k_subgroup"] * 1e-3) / MAD_PEAK_MEASURED, 5),
+                    "traffic": pmc, "algorithmic_bytes": sg_bytes_share * rf["shares"],
+                    "traffic_over_algorithmic": round(pmc / (sg_bytes_share * rf["shares"]), 2) if pmc else None,
+                    "mads_per_launch": sg_mads, "avg_launch_ms": round(rf["ms"]["k_subgroup"], 4),
+                    "timing": "hipEvents on the slot's stream, one-stream slot at depth 1, one batch of %d x the C2 "
+                              "batch (%d shares = %d waves: the chip full at the kernel's two waves per SIMD); MADs = "
+                              "the subgroup checks only (the roots' SWU map riding along is < 1%%)" % (
+                                  rf["R"], rf["shares"], rf["shares"] // 64),
+                    "results_ok": rf["ok"],
+                    "k_decode_count": {"achieved": round(dec_mads / (rf["ms"]["k_decode"] * 1e-3) / 1e12, 4),
+                                       "frac": round(dec_mads / (rf["ms"]["k_decode"] * 1e-3) / MAD_PEAK_MEASURED, 5),
+                                       "avg_launch_ms": round(rf["ms"]["k_decode"], 4), "mads_per_launch": dec_mads},
+                    "depth1_c2": {"kernel": dom, "achieved": round(achieved, 4), "frac": round(achieved / peak, 5),
+                                  "avg_launch_ms": round(avg[dom], 4),
+                                  "timing": "one C2 batch alone, three-stream slot (256 waves on 1,024 SIMDs)"}}
         rec = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -657,10 +738,10 @@ def main():
                                "combined signatures (== the master key's signature)%s" % (
                                    V, N, "; the last exchange's gathered results == local" if world > 1 else ""),
             "invalid_shares_per_batch": wl["n_bad"],
-            "roofline": {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),
-                         "peak": round(peak, 2), "unit": "TMAD/s", "frac": round(achieved / peak, 5),
-                         "traffic": pmc_traffic(dom), "mads_per_launch": km[dom], "avg_launch_ms": round(avg[dom], 4),
-                         "timing": "hipEvents on the kernel's stream, pipeline depth 1"},
+            "roofline": roof or {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),
+                                 "peak": round(peak, 2), "unit": "TMAD/s", "frac": round(achieved / peak, 5),
+                                 "traffic": pmc_traffic(dom), "mads_per_launch": km[dom], "avg_launch_ms": round(avg[dom], 4),
+                                 "timing": "hipEvents on the kernel's stream, pipeline depth 1"},
             "step_roofline": {"mads_per_step_per_gpu": step_mads,
                               "achieved_TMAD_s": round(step_mads * world * args.steps / elapsed / 1e12, 4),
                               "frac": round(step_mads * args.steps / elapsed / MAD_PEAK_MEASURED, 5)},
@@ -668,7 +749,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline and not wl["n_bad"]:
             # about 10 s of host CPU work: whole passes over the C2 batch, >= 4 s per column
-            rec["cpu_baseline"] = cpu_baseline(wl, t, n, gpu_out=outs[0]["out"].cpu().numpy(), n_val=min(4096, V))
+            rec["cpu_baseline"] = cpu_baseline(wl, t, n, gpu_out=outs[0]["out"].cpu().numpy(), n_val=min(4096, V),
+                                               n_val_share=min(1024, V))
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()

@@ -30,13 +30,17 @@ SSB_INL void msm_entries(int i, uint64_t k, uint32_t g, const msm_cfg& c, uint32
 // one share's entries of both MSMs (the count pass, or with SCATTER the scatter pass of the sort);
 // a share whose root index is out of range has none (it cannot enter the batch)
 template <bool SCATTER>
-SSB_INL void msm_sort_lane(int i, const rlc_key& key, const uint32_t* __restrict__ share_root, const msm_cfg& c2,
-                           const msm_cfg& c1, uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
-  const uint32_t g = share_root[i];
+SSB_INL void msm_sort_lane_root(int i, uint32_t g, const rlc_key& key, const msm_cfg& c2, const msm_cfg& c1,
+                                uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
   if (g >= c1.ngroups) return;
   const uint64_t k = rlc_scalar_odd(key, (uint64_t)i);
   msm_entries<SCATTER>(i, k, 0u, c2, cnt, ent);
   msm_entries<SCATTER>(i, k, g, c1, cnt, ent);
+}
+template <bool SCATTER>
+SSB_INL void msm_sort_lane(int i, const rlc_key& key, const uint32_t* __restrict__ share_root, const msm_cfg& c2,
+                           const msm_cfg& c1, uint32_t* __restrict__ cnt, uint32_t* __restrict__ ent) {
+  msm_sort_lane_root<SCATTER>(i, share_root[i], key, c2, c1, cnt, ent);
 }
 
 // ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
@@ -230,6 +234,22 @@ SSB_INL void h2c_affine_block(uint32_t bid, int n, const g2_aff* __restrict__ q,
 // its share range.  (k_share_map clamps the ranges the same way.)
 SSB_INL bool job_ok(uint32_t b, uint32_t e, uint32_t t, uint32_t n_shares) {
   return t >= 1 && t <= SSB_MAX_T && b <= e && e <= n_shares;
+}
+// share -> (job, root): job j = the last j with off[j] <= s (binary search over off[0..n_jobs]).  A
+// share outside every well-formed job's range -- share_off not monotone, off[0] > 0,
+// off[n_jobs] < n_shares, or its job fails job_ok -- gets the sentinel 0xffffffff for both (no
+// H(root): never a candidate; the combine kernels skip it), so no kernel reads a stale entry of the
+// reused workspace or indexes a job array past n_jobs.  (tt == nullptr: no job_ok check.)
+SSB_INL void share_lookup(uint32_t s, const job_map& jm, uint32_t& job, uint32_t& root) {
+  int lo = 0, hi = jm.n_jobs;   // invariant (monotone off): off[lo] <= s < off[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (jm.off[mid] <= s) lo = mid; else hi = mid;
+  }
+  const uint32_t b = jm.off[lo], e = jm.off[lo + 1];
+  const bool in = jm.n_jobs > 0 && b <= s && s < e && (!jm.tt || job_ok(b, e, jm.tt[lo], jm.n_shares));
+  job = in ? (uint32_t)lo : 0xffffffffu;
+  root = in ? (jm.job_root ? jm.job_root[lo] : 0u) : 0xffffffffu;
 }
 SSB_INL void select_job(int j, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,

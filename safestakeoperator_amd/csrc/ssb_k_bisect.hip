@@ -55,13 +55,20 @@ __global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, in
   for (int s = t; s < n; s += PREP_THREADS)
     if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
 }
-// threads [0, n): rsig[s] = k_s sig_s;  [n, 2n): rpk[s] = k_s pk_s  (candidates only)
+// threads [0, n): rsig[s] = k_s sig_s;  [n, 2n): rpk[s] = k_s pk_s  (candidates only).  With
+// `verdict` it also writes, grid-wide, the verdicts the batch check decides: every share of a
+// passing batch, the non-candidates of a failing one (the candidates' follow from the group tests)
 __global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restrict__ ok,
                                    const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig_aff,
                                    const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
-                                   g1_jac* __restrict__ rpk) {
-  if (*ok) return;
+                                   g1_jac* __restrict__ rpk, uint8_t* __restrict__ verdict) {
+  const uint32_t pass = *ok;
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (verdict && g < n) {
+    const bool cand = (flags[g] & FLAG_CANDIDATE) != 0;
+    if (pass || !cand) verdict[g] = cand ? 1 : 0;
+  }
+  if (pass) return;
   // binary double-and-add (no window table): the private segment stays small -- every tail queue
   // reserves scratch for the largest kernel it has run, and this one is launched on every batch
   if (g < n) {
@@ -222,7 +229,7 @@ int fallback_levels(size_t n) {
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
-                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict) {
+                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict, bool fast_verdicts) {
   using namespace ssb::k;
   if (n <= 0 || n_roots <= 0) return;
   auto nb = [](size_t x, unsigned b) { return (unsigned)((x + b - 1) / b); };
@@ -230,7 +237,8 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   const int lb = fallback_log2_branch();
   hipLaunchKernelGGL(k_fb_prep, dim3(1), dim3(PREP_THREADS), 0, st, n, n_roots, L, lb, ok, share_root, cnt, start, cursor,
                      gst, perm);
-  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, key, ok, flags, sig, pk, rsig, rpk);
+  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, key, ok, flags, sig, pk, rsig, rpk,
+                     fast_verdicts ? verdict : (uint8_t*)nullptr);
   for (int l = 0; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;

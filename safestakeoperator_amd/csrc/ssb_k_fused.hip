@@ -11,8 +11,9 @@ namespace k {
 // blocks [0, nz): zero the sort's counts (and the order bins); then one lane per root: the hash's
 // expand_message_xmd + the two field elements (k_h2c_u)
 __global__ void SSB_LB(64) k_prep_fused(uint32_t nz, uint32_t K, uint32_t* __restrict__ cnt, uint32_t* __restrict__ tickets,
-                                        int n_roots, const uint8_t* __restrict__ roots, dst_arg dst, fp2* __restrict__ u) {
-  if (blockIdx.x == 0 && threadIdx.x < 4) tickets[threadIdx.x] = 0u;
+                                        uint32_t ntk, int n_roots, const uint8_t* __restrict__ roots, dst_arg dst,
+                                        fp2* __restrict__ u) {
+  if (blockIdx.x == 0) for (uint32_t i = threadIdx.x; i < ntk; i += 64) tickets[i] = 0u;
   if (blockIdx.x < nz) {
     for (uint32_t x = blockIdx.x * 64 * 16 + threadIdx.x; x < (blockIdx.x + 1) * 64 * 16 && x < K; x += 64) cnt[x] = 0u;
     return;
@@ -92,7 +93,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
                                            uint32_t* __restrict__ start, uint32_t* __restrict__ cur,
                                            uint32_t* __restrict__ order, uint32_t* __restrict__ tickets,
                                            int n_roots, const uint8_t* __restrict__ roots, dst_arg dst,
-                                           fp2* __restrict__ u) {
+                                           fp2* __restrict__ u, job_map jm) {
   const uint32_t part = blockIdx.x / nbd;
   if (part >= 3) {
     const int i = (int)(blockIdx.x - 3 * nbd) * 64 + threadIdx.x;
@@ -109,7 +110,12 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
   if (part == 2) {   // count pass; the last count block to finish runs the scans
     __shared__ uint32_t sh[64 + 512];
     __shared__ uint32_t last;
-    if (s < n) msm_sort_lane<false>(s, key, share_root, c2, c1, cnt, (uint32_t*)nullptr);
+    if (s < n) {
+      uint32_t g;
+      if (jm.n_jobs) { uint32_t j; share_lookup((uint32_t)s, jm, j, g); }   // (the decode blocks store it)
+      else g = share_root[s];
+      msm_sort_lane_root<false>(s, g, key, c2, c1, cnt, (uint32_t*)nullptr);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence();
@@ -125,6 +131,12 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
   }
   if (s >= n) return;
   if (part == 0) {
+    if (jm.n_jobs) {   // share -> (job, root) for the later launches (k_share_map's work)
+      uint32_t j, r;
+      share_lookup((uint32_t)s, jm, j, r);
+      jm.share_job[s] = j;
+      jm.share_root[s] = r;
+    }
     uint8_t b[96];
     for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
     g2_aff sig;
@@ -152,7 +164,8 @@ using namespace ssb::k;
 
 void prep_fused(hipStream_t st, const fused_sort& fs, int n_roots, const uint8_t* roots, const dst_arg& dst, const h2c_ws& hw) {
   const uint32_t nz = (fs.K + 64 * 16 - 1) / (64 * 16), nu = (uint32_t)(n_roots + 63) / 64;
-  hipLaunchKernelGGL(k_prep_fused, dim3(nz + nu), dim3(64), 0, st, nz, fs.K, fs.cnt, fs.tickets, n_roots, roots, dst, hw.u);
+  hipLaunchKernelGGL(k_prep_fused, dim3(nz + nu), dim3(64), 0, st, nz, fs.K, fs.cnt, fs.tickets, fs.ntk, n_roots, roots, dst,
+                     hw.u);
 }
 
 void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
@@ -168,11 +181,11 @@ void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk
   if (pk_index)
     hipLaunchKernelGGL(k_decode_count<true>, dim3(3 * nbd + nbu), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
                        cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt,
-                       fs.K, fs.start, fs.cur, fs.order, fs.tickets, u ? n_roots : 0, roots, d, uo);
+                       fs.K, fs.start, fs.cur, fs.order, fs.tickets, u ? n_roots : 0, roots, d, uo, fs.jm);
   else
     hipLaunchKernelGGL(k_decode_count<false>, dim3(3 * nbd + nbu), dim3(64), 0, st, n, nbd, sig96, pk48, pk_index, n_cache,
                        cache_aff, cache_flags, sig_aff, pk_aff, sflags, pflags, fs.key, fs.share_root, fs.c2, fs.c1, fs.cnt,
-                       fs.K, fs.start, fs.cur, fs.order, fs.tickets, u ? n_roots : 0, roots, d, uo);
+                       fs.K, fs.start, fs.cur, fs.order, fs.tickets, u ? n_roots : 0, roots, d, uo, fs.jm);
 }
 
 

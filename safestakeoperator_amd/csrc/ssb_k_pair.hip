@@ -149,5 +149,91 @@ __global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint
   }
 }
 
+// Miller loops, the product tree and ONE final exponentiation in one launch (the fused one-stream
+// path; k_miller_pairs + k_fp12_prod8 x 2 + k_final_lane in the other paths).  Block p computes pair
+// p's Miller value; the last block of each group of 8 to finish multiplies that group's values;
+// the last group to finish multiplies the group products and runs the final exponentiation -> *ok.
+// Completion tickets (tk[0]: groups done, tk[1 + i]: blocks of group i done), no block ever waits:
+// a block continues only with work whose inputs are complete, so the grid drains in every
+// schedule; the last block zeroes the tickets for the slot's next batch.  Saves three launches and
+// their dispatch gaps on the batch's latency-bound tail.  Blocks [npairs, ..) run the speculative
+// a-1 scan + combine, as in k_miller_pairs.  (The verdicts of a passing batch are written grid-wide
+// by the next launch, k_fb_rlc.)
+constexpr int MF_FE = FE_S0 + 12 + 12 + 84;
+constexpr int MF_SLOTS = ML_SLOTS > MF_FE ? ML_SLOTS : MF_FE;
+__global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__ Pa, const g2_aff* __restrict__ Qa,
+                                          fp12* __restrict__ f, spec_jobs sj, uint32_t* __restrict__ tk,
+                                          uint32_t* __restrict__ ok) {
+  using namespace ssb::lane;
+  __shared__ fp lds[LP_NCODE_CONST + MF_SLOTS];
+  __shared__ uint32_t flg, last;
+  const int p = blockIdx.x, lane_ = threadIdx.x;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  if (p >= npairs) {   // the speculative a-1 scan + combine, 64 jobs per block (candidate flags as verdicts)
+    const int j = (p - npairs) * 64 + lane_;
+    if (j >= sj.n_jobs) return;
+    select_job(j, sj.n_shares, sj.off, sj.tt, sj.ids, (const uint8_t*)nullptr, sj.flags, sj.sel, sj.status, sj.err);
+    const uint32_t fj = combine_fast_job(j, sj.off, sj.tt, sj.status, sj.sel, sj.ids, sj.sig_aff, sj.out96);
+    sj.fast[j] = fj;
+    if (!fj && sj.status[j] == SSB_DVF_OK) lagrange_job(j, sj.off, sj.tt, sj.ids, sj.sel, sj.lam);
+    return;
+  }
+  lp_init_consts(g);
+  {
+    const g1_aff P = Pa[p];
+    const g2_aff Q = Qa[p];
+    if (P.inf || Q.inf) {  // e(O, Q) = e(P, O) = 1  (uniform per workgroup)
+      if (lane_ == 0) f[p] = fp12_one();
+    } else {
+      const int F = ML_S0, B = F + 18;
+      if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
+      if (lane_ == 4) g.s[B + 4] = P.x;
+      if (lane_ == 5) g.s[B + 5] = P.y;
+      __syncthreads();
+      f12_miller(g, F, B);
+      if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
+    }
+  }
+  const int ng = (npairs + 7) / 8, gi = p / 8, gb = gi * 8, ge = min(npairs, gb + 8);
+  __threadfence();
+  __syncthreads();
+  if (lane_ == 0) last = atomicAdd(&tk[1 + gi], 1u) == (uint32_t)(ge - gb - 1) ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const int ACC = FE_S0, IN = ACC + 12, TMP = IN + 12;
+  if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)&f[gb])[lane_];
+  __syncthreads();
+  for (int i = gb + 1; i < ge; ++i) {
+    if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&f[i])[lane_];
+    __syncthreads();
+    f12_mul(g, ACC, IN, ACC);
+  }
+  if (lane_ < 12) ((fp*)&f[npairs + gi])[lane_] = g.s[ACC + lane_];
+  __threadfence();
+  __syncthreads();
+  if (lane_ == 0) last = atomicAdd(&tk[0], 1u) == (uint32_t)(ng - 1) ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)&f[npairs])[lane_];
+  __syncthreads();
+  for (int i = 1; i < ng; ++i) {
+    if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&f[npairs + i])[lane_];
+    __syncthreads();
+    f12_mul(g, ACC, IN, ACC);
+  }
+  f12_final_exp(g, ACC, TMP);
+  if (lane_ == 0) {  // == 1, read slot by slot (an fp12 local would sit in scratch)
+    bool one = true;
+    for (int k = 0; k < 12; ++k) {
+      const fp v = g.s[ACC + k];
+      one = one && (k == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v));
+    }
+    *ok = one ? 1u : 0u;
+  }
+  for (int i = lane_; i <= ng; i += 64) tk[i] = 0u;   // every block has passed its tickets
+}
+
 }  // namespace k
 }  // namespace ssb

@@ -7,25 +7,18 @@
 namespace ssb {
 namespace k {
 
-// share -> job and share -> root, one thread per SHARE: job j = the last j with off[j] <= s (binary
-// search over off[0..n_jobs]).  A share outside every well-formed job's range -- share_off not
-// monotone, off[0] > 0, off[n_jobs] < n_shares, or its job fails job_ok -- gets the sentinel
-// 0xffffffff for both (no H(root): never a candidate; the combine kernels skip it), so no later
-// kernel reads a stale entry of the reused workspace or indexes a job array past n_jobs.
+// share -> job and share -> root, one thread per share (share_lookup, ssb_blocks.h); the fused
+// one-stream path does the same lookups inside k_decode_count instead of a launch of its own
 __global__ void k_share_map(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                             const uint32_t* __restrict__ job_root, uint32_t* __restrict__ share_job,
                             uint32_t* __restrict__ share_root) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_shares) return;
-  int lo = 0, hi = n_jobs;   // invariant (monotone off): off[lo] <= s < off[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (off[mid] <= s) lo = mid; else hi = mid;
-  }
-  const uint32_t b = off[lo], e = off[lo + 1];
-  const bool in = n_jobs > 0 && b <= s && s < e && (!tt || job_ok(b, e, tt[lo], n_shares));
-  share_job[s] = in ? (uint32_t)lo : 0xffffffffu;
-  if (share_root) share_root[s] = in ? (job_root ? job_root[lo] : 0u) : 0xffffffffu;
+  const job_map jm{n_jobs, n_shares, off, tt, job_root, share_job, share_root};
+  uint32_t j, r;
+  share_lookup(s, jm, j, r);
+  share_job[s] = j;
+  if (share_root) share_root[s] = r;
 }
 __global__ void SSB_LB(64) k_decode(int n, const uint8_t* __restrict__ sig96,
                                                const uint8_t* __restrict__ pk48, int group_check,

@@ -18,6 +18,12 @@ struct spec_jobs {
   uint32_t* sel; int32_t* status; uint64_t* err; const g2_aff* sig_aff; uint32_t* fast; uint8_t* out96; fr* lam;
 };
 
+// share -> (job, root) of an aggregate batch (share_lookup, ssb_blocks.h)
+struct job_map {
+  int n_jobs; uint32_t n_shares; const uint32_t* off; const uint32_t* tt; const uint32_t* job_root;
+  uint32_t* share_job; uint32_t* share_root;
+};
+
 // One bucket MSM of the RLC sums (ssb_k_msm.hip): c-bit windows, W = ceil(64 / c) of them,
 // `ngroups` independent sums; bucket key = base + ((group * W + window) << c) + digit.
 struct msm_cfg { uint32_t c, W, base, ngroups; };
@@ -67,6 +73,11 @@ __global__ void k_fallback_lane(int n, const uint32_t* __restrict__ ok, const ui
 __global__ void k_miller_pairs(int npairs, const g1_aff* __restrict__ P, const g2_aff* __restrict__ Q,
                                fp12* __restrict__ f, spec_jobs sj);
 __global__ void k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out);
+// Miller loops + product tree + final exponentiation in one launch (fused one-stream path):
+// tk: 1 + ceil(npairs / 8) completion tickets (zero on entry, zero again on exit); f: npairs +
+// ceil(npairs / 8) values
+__global__ void k_miller_final(int npairs, const g1_aff* __restrict__ P, const g2_aff* __restrict__ Q,
+                               fp12* __restrict__ f, spec_jobs sj, uint32_t* __restrict__ tk, uint32_t* __restrict__ ok);
 __global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok, int nv,
                              const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdict);
 __global__ void k_sign(int n, const uint8_t* __restrict__ sk32le, const uint32_t* __restrict__ root_idx,
@@ -172,7 +183,12 @@ struct fused_sort {
   rlc_key key; const uint32_t* share_root; msm_cfg c2, c1; uint32_t K;
   uint32_t* cnt; uint32_t* start; uint32_t* cur; uint32_t* ent; uint32_t* order;
   const uint32_t* pflags; uint32_t n_roots; uint32_t* flags;
-  uint32_t* tickets;   // 4 words, zeroed by prep_fused: [0] count blocks done, [1] G1 windows, [2] clears
+  uint32_t* tickets;   // ntk words, zeroed by prep_fused: [0] count blocks done, [1] G1 windows, [2] clears,
+                       // [4 ..) k_miller_final's groups
+  uint32_t ntk;
+  // jobs given (aggregate path): decode_count computes share -> (job, root) itself, writing
+  // jm.share_job / jm.share_root (== share_root above) -- no k_share_map launch in front of the batch
+  job_map jm;
 };
 // the subgroup checks with (hw != nullptr) the hash's SWU map of n_roots roots and (fs != nullptr)
 // the sort's scatter in the same launch; with fs the lanes also write the combined share flags
@@ -198,7 +214,7 @@ int fallback_levels(size_t n);
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
                      uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
-                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict);
+                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict, bool fast_verdicts);
 // first use of a new queue: acquire its scratch for the largest slot kernel while the other queues
 // are idle (ssb_k_combine.hip); synchronous, 0 on success
 int prime_queue(hipStream_t st);

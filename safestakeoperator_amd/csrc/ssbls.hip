@@ -339,7 +339,10 @@ struct verify_ws {
   g1_aff* pair_p;     // pair P points: root sums, then [2^(c w)](-g1)
   g2_aff* sig_aff; g1_aff* pk_aff; uint32_t* flags; uint32_t* sflags; uint32_t* pflags; uint32_t* gflags; uint32_t* gexc;
   fp12* f; uint32_t* ok;
-  uint32_t* tickets;   // fused launches: completion tickets of the blocks (zeroed per batch by k_prep_fused)
+  uint32_t* tickets;   // fused launches: completion tickets of the blocks (zeroed by k_prep_fused, and
+                       // again by the blocks that consume them): [0, 4) sort / windows / clears,
+                       // [4, 4 + ntk_miller) k_miller_final's
+  uint32_t ntk;
   char* hws;          // staged hash_to_G2 workspace
   uint32_t* cnt; uint32_t* start; uint32_t* cur; uint32_t* sbsum; uint32_t* ent;   // MSM counting sort
   uint32_t* order;                                                                 // buckets by count
@@ -360,6 +363,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
   const size_t np = n_roots + MSM_WMAX;
   return align_up(np * sizeof(g2_aff)) + align_up(np * sizeof(g1_aff)) + align_up(n * sizeof(g2_aff)) +
          align_up(n * sizeof(g1_aff)) + align_up(n * 4) * 5 + align_up(fp12_slots(np) * sizeof(fp12)) + align_up(4) +
+         align_up((4 + 1 + (np + 7) / 8) * 4) +
          align_up(launch::hash_ws_bytes(n_roots)) + 4 * align_up((size_t)p.K * 4) + align_up(1024 * 4) +
          align_up(p.n_ent * 4) + align_up(((size_t)p.g2.W << p.g2.c) * sizeof(g2_jac)) +
          align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
@@ -376,7 +380,9 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
   w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
   w.gflags = c.take<uint32_t>(n); w.gexc = c.take<uint32_t>(n);
-  w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1); w.tickets = c.take<uint32_t>(4);
+  w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1);
+  w.ntk = 4 + 1 + (uint32_t)((np + 7) / 8);
+  w.tickets = c.take<uint32_t>(w.ntk);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   w.cnt = c.take<uint32_t>(w.plan.K); w.start = c.take<uint32_t>(w.plan.K); w.cur = c.take<uint32_t>(w.plan.K);
   w.sbsum = c.take<uint32_t>(1024); w.ent = c.take<uint32_t>(w.plan.n_ent); w.order = c.take<uint32_t>(w.plan.K);
@@ -393,11 +399,23 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   return w;
 }
 
+// The fused one-stream path (every stage on the slot's stream, the counting sort and the hash
+// stages riding along the per-share launches): one-stream slot, a per-root G1 bucket MSM with
+// windows of <= 16 buckets, and the sort's keys within FUSED_SORT_KMAX.
+bool fused_sort_path(const ssb_slot* S, size_t n, size_t n_roots) {
+  if (!S->shared || !n || !n_roots) return false;
+  const msm_plan P = plan_msm(n, n_roots);
+  const char* sgp = getenv("SSB_SUBGROUP");
+  return P.g1_msm && launch::msm_fused_ok(P.g1) && !(sgp && sgp[0] == 'l') && P.K <= launch::FUSED_SORT_KMAX;
+}
+
+// jm (aggregate path on the fused path): the share -> (job, root) map is computed by the decode
+// launch (d_share_root == jm->share_root) instead of a k_share_map launch in front of the batch
 template <class F>
 int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const uint8_t* d_sig, const uint8_t* d_pk,
                const uint32_t* d_pk_index, const uint32_t* d_share_root, const uint8_t* d_roots, const dst_arg& dst, uint64_t rlc_seed,
                uint8_t* d_verdict, F on_decoded, hipStream_t tail, const spec_jobs* sj = nullptr,
-               bool* spec_done = nullptr) {
+               bool* spec_done = nullptr, const job_map* jm = nullptr) {
   rlc_key key;
   if (int rc = draw_rlc_key(ctx, rlc_seed, key)) return rc;
   hipStream_t st = ctx->cur->stream, sh = ctx->cur->side[0], s1 = ctx->cur->side[1];
@@ -412,8 +430,9 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   const launch::h2c_ws hw = launch::carve_h2c(w.hws, n_roots);
   // ... and the MSM entries' counting sort rides along the decode and the subgroup checks
   const bool fuse_sort = fuse_hash && P.K <= launch::FUSED_SORT_KMAX;
+  if (jm && !fuse_sort) { ctx->err = "internal: share map expected on the fused path"; return SSB_EINVAL; }
   const launch::fused_sort fs{key, d_share_root, P.g2, P.g1, P.K, w.cnt, w.start, w.cur, w.ent, w.order,
-                              w.pflags, (uint32_t)n_roots, w.flags, w.tickets};
+                              w.pflags, (uint32_t)n_roots, w.flags, w.tickets, w.ntk, jm ? *jm : job_map{}};
   // hash_to_G2 per root runs beside decode / RLC / sums; the Miller loops wait for it
   // (events only between distinct streams: on one stream the order is given, and every record or
   // wait is one more packet in the slot's queue)
@@ -506,17 +525,24 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   if (!fused && s1 != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_r1, 0));
   if (!fuse_hash && sh != st) SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_hash, 0));
-  {
-    // one-stream slots: the speculative combine rides along the Miller loops (a few latency-bound
-    // blocks), so a passing batch's tail is only no-op launches
-    spec_jobs sjv{};
-    unsigned nbsp = 0;
-    if (sj && sj->n_jobs > 0 && st == ctx->cur->stream) { sjv = *sj; nbsp = (unsigned)((sj->n_jobs + 63) / 64); }
-    if (spec_done) *spec_done = nbsp > 0;
+  // one-stream slots: the speculative combine rides along the Miller loops (a few latency-bound
+  // blocks), so a passing batch's tail is only no-op launches
+  spec_jobs sjv{};
+  unsigned nbsp = 0;
+  if (sj && sj->n_jobs > 0 && st == ctx->cur->stream) { sjv = *sj; nbsp = (unsigned)((sj->n_jobs + 63) / 64); }
+  if (spec_done) *spec_done = nbsp > 0;
+  // the fused path: Miller loops, product tree and final exponentiation in ONE launch (completion
+  // tickets of the fused path's workspace); the fast verdicts then come grid-wide from k_fb_rlc
+  const bool miller_final = fuse_sort && !fallback_per_share();
+  if (miller_final) {
     timed t(ctx, "k_miller");
-    hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs + nbsp), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f, sjv);
-  }
-  {
+    hipLaunchKernelGGL(k_miller_final, dim3((unsigned)w.npairs + nbsp), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f, sjv,
+                       w.tickets + 4, w.ok);
+  } else {
+    {
+      timed t(ctx, "k_miller");
+      hipLaunchKernelGGL(k_miller_pairs, dim3((unsigned)w.npairs + nbsp), dim3(64), 0, st, (int)w.npairs, w.pair_p, w.H, w.f, sjv);
+    }
     timed t(ctx, "k_final");
     int np = (int)w.npairs;
     fp12* cur = w.f;
@@ -525,7 +551,10 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
       hipLaunchKernelGGL(k_fp12_prod8, dim3((unsigned)nparts), dim3(64), 0, st, np, cur, cur + np);
       cur += np; np = nparts;
     }
-    hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok, (int)n, (const uint32_t*)w.flags, d_verdict);
+    // (the per-share fallback leaves the fast verdicts to k_final_lane; the group-test fallback
+    // writes them grid-wide in k_fb_rlc)
+    hipLaunchKernelGGL(k_final_lane, dim3(1), dim3(64), 0, st, np, cur, w.ok, (int)n, (const uint32_t*)w.flags,
+                       fallback_per_share() ? d_verdict : (uint8_t*)nullptr);
   }
   // the exact fallback when the batch failed: on the slot's own stream (one-stream slots), or the
   // context's tail stream (three-stream configuration)
@@ -537,13 +566,14 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   }
   if (n) {
     timed t(ctx, "k_fallback_verify", fbs);
-    // (the fast verdicts -- a passing batch, non-candidates -- were written by k_final_lane)
+    // (the fast verdicts -- a passing batch, non-candidates -- come from k_final_lane on the per-share
+    // path, from k_fb_rlc on the group-test path)
     if (fallback_per_share())
       hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, fbs, (int)n, w.ok, w.flags,
                          d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
     else
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff,
-                              w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict);
+                              w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rsig, w.rpk, w.gv0, w.gv1, d_verdict, true);
   }
   if (!fb_tail && tail != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));
@@ -882,7 +912,11 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
-  if (n) hipLaunchKernelGGL(k_share_map, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root);
+  // share -> (job, root): in the decode launch on the fused path, else a launch of its own
+  const bool fmap = fused_sort_path(ctx->cur, n, n_roots);
+  const job_map jm{(int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root};
+  if (n && !fmap)
+    hipLaunchKernelGGL(k_share_map, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root);
   // speculative combine (selection from the decode flags) on its own stream, beside the pairing chain
   auto spec = [&] {
     hipStreamWaitEvent(sc, ctx->cur->ev_dec, 0);
@@ -899,7 +933,8 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
                      out_sig96, lam};
   bool spec_in_window = false;
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict,
-                       [&] { if (!on_slot) spec(); }, tl, on_slot ? &sj : nullptr, &spec_in_window))) return rc;
+                       [&] { if (!on_slot) spec(); }, tl, on_slot ? &sj : nullptr, &spec_in_window, fmap ? &jm : nullptr)))
+    return rc;
   if (!n && !on_slot) spec();
   // exact path: only if the RLC batch failed (every kernel a no-op when w.ok == 1, the speculative
   // combine stands) -- on the shared tail stream, or on the slot's stream; one-stream slots whose
