@@ -2,7 +2,7 @@
 average counter value per dispatch; HBM bytes per launch = 2 x FETCH_SIZE (gfx950 reports half of
 wide coalesced reads, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, FETCH/WRITE_SIZE in KB.
 
-    python bench_tools/pmc_summary.py gpurun_out/<tag>  > summary.json
+    python bench_tools/pmc_summary.py gpurun_out/<tag> [--by-grid] > summary.json
 """
 import csv
 import glob
@@ -16,12 +16,15 @@ def short(name):
     return name.replace("(anonymous namespace)::", "").split("(")[0].replace("ssb::k::", "")
 
 
-def main(root):
+def main(root, by_grid=False):
     vals = defaultdict(lambda: defaultdict(list))
     for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
                 k = short(row.get("Kernel_Name", ""))
+                if by_grid:   # one entry per launch shape (e.g. the roofline batch vs the C2 batches)
+                    gs = [v for c, v in row.items() if c and c.startswith("Grid_Size")]
+                    k = "%s@%s" % (k, "x".join(gs))
                 c = row.get("Counter_Name", "")
                 try:
                     v = float(row.get("Counter_Value", "nan"))
@@ -42,4 +45,4 @@ def main(root):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], by_grid="--by-grid" in sys.argv)

@@ -190,27 +190,33 @@ __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* _
                                          g1_jac* __restrict__ w1, h2c_fuse h, window2_tail tl) {
   __shared__ __attribute__((aligned(16))) char lds[WINDOW2_LDS];
   __shared__ uint32_t last;
+  SSB_TRACE_T0();
   uint32_t bid = blockIdx.x;
   if (bid < nblk2) {
     msm_window_block<fp2>(bid, (g2_jac*)lds, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow, (const uint32_t*)nullptr,
                           (const g2_jac*)nullptr);
+    SSB_TRACE(TR_W2_G2);
     return;
   }
   bid -= nblk2;
   if (bid < nblk1) {
     if (!tl.tickets) { msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1); return; }
     if (bid * 64 + threadIdx.x < ngw1) msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1);
+    SSB_TRACE(TR_W2_G1);
     if (last_block(&tl.tickets[1], nblk1, &last)) {
       for (int g = threadIdx.x; g < tl.ngroups1; g += 64) msm_horner_lane(g, c1, tl.W1, w1, tl.root_sum);
       if (threadIdx.x == 0) tl.tickets[1] = 0u;   // clean for the slot's next batch
+      SSB_TRACE(TR_W2_HORNER);
     }
     return;
   }
   bid -= nblk1;
   h2c_clear_block(bid, (fp*)lds, h.n, h.q, h.hj, h.exc);
+  SSB_TRACE(TR_W2_CLEAR);
   if (tl.tickets && last_block(&tl.tickets[2], (uint32_t)(h.n + 7) / 8, &last)) {
     for (uint32_t b = 0; b * 64 < (uint32_t)h.n; ++b) h2c_affine_block(b, h.n, h.q, h.hj, h.exc, h.exact_all, h.out);
     if (threadIdx.x == 0) tl.tickets[2] = 0u;
+    SSB_TRACE(TR_W2_AFFINE);
   }
 }
 
@@ -394,3 +400,5 @@ void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, 
 
 }  // namespace launch
 }  // namespace ssb
+
+SSB_TRACE_READER(msm)

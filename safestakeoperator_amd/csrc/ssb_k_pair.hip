@@ -167,6 +167,7 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
   using namespace ssb::lane;
   __shared__ fp lds[LP_NCODE_CONST + MF_SLOTS];
   __shared__ uint32_t flg, last;
+  SSB_TRACE_T0();
   const int p = blockIdx.x, lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
   if (p >= npairs) {   // the speculative a-1 scan + combine, 64 jobs per block (candidate flags as verdicts)
@@ -194,6 +195,7 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
       if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
     }
   }
+  SSB_TRACE(TR_MF_MILLER);
   const int ng = (npairs + 7) / 8, gi = p / 8, gb = gi * 8, ge = min(npairs, gb + 8);
   __threadfence();
   __syncthreads();
@@ -210,6 +212,7 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
     f12_mul(g, ACC, IN, ACC);
   }
   if (lane_ < 12) ((fp*)&f[npairs + gi])[lane_] = g.s[ACC + lane_];
+  SSB_TRACE(TR_MF_GROUP);
   __threadfence();
   __syncthreads();
   if (lane_ == 0) last = atomicAdd(&tk[0], 1u) == (uint32_t)(ng - 1) ? 1u : 0u;
@@ -223,6 +226,7 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
     __syncthreads();
     f12_mul(g, ACC, IN, ACC);
   }
+  SSB_TRACE(TR_MF_PRODUCT);
   f12_final_exp(g, ACC, TMP);
   if (lane_ == 0) {  // == 1, read slot by slot (an fp12 local would sit in scratch)
     bool one = true;
@@ -233,7 +237,10 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
     *ok = one ? 1u : 0u;
   }
   for (int i = lane_; i <= ng; i += 64) tk[i] = 0u;   // every block has passed its tickets
+  SSB_TRACE(TR_MF_FINAL);
 }
 
 }  // namespace k
 }  // namespace ssb
+
+SSB_TRACE_READER(pair)

@@ -5,6 +5,38 @@
 #include "ssb_units.h"
 #include "../../include/ssbls.h"
 
+// Experiment builds only (SSB_VARIANT_DEFS=-DSSB_TRACE_TAIL, bench_tools/trace_tail.py): the tail
+// kernels record per-block start / end wall-clock stamps (100 MHz) in a device buffer of their
+// translation unit (read back by ssb_debug_trace_<tu>), so the critical path inside a fused launch
+// can be read without perturbing it; the product library compiles these to nothing.
+#ifdef SSB_TRACE_TAIL
+enum { TR_W2_G2 = 1, TR_W2_G1, TR_W2_HORNER, TR_W2_CLEAR, TR_W2_AFFINE, TR_MF_MILLER, TR_MF_GROUP, TR_MF_PRODUCT, TR_MF_FINAL };
+static __device__ unsigned long long ssb_trace_buf[4 * 2048];
+static __device__ unsigned int ssb_trace_n;
+#define SSB_TRACE_T0() const unsigned long long trace_t0_ = wall_clock64()
+#define SSB_TRACE(tag)                                                                      \
+  do {                                                                                      \
+    if (threadIdx.x == 0) {                                                                 \
+      const unsigned i_ = atomicAdd(&ssb_trace_n, 1u) & 2047u;                              \
+      ssb_trace_buf[4 * i_] = (tag); ssb_trace_buf[4 * i_ + 1] = blockIdx.x;                \
+      ssb_trace_buf[4 * i_ + 2] = trace_t0_; ssb_trace_buf[4 * i_ + 3] = wall_clock64();    \
+    }                                                                                       \
+  } while (0)
+#define SSB_TRACE_READER(tu)                                                                \
+  extern "C" int ssb_debug_trace_##tu(unsigned long long* out) {                            \
+    unsigned int n = 0, z = 0;                                                              \
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(ssb_trace_n), 4) != hipSuccess) return -1;       \
+    if (n > 2048) n = 2048;                                                                 \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ssb_trace_buf), 32 * (size_t)n) != hipSuccess) return -1; \
+    hipMemcpyToSymbol(HIP_SYMBOL(ssb_trace_n), &z, 4);                                      \
+    return (int)n;                                                                          \
+  }
+#else
+#define SSB_TRACE_T0() ((void)0)
+#define SSB_TRACE(tag) ((void)0)
+#define SSB_TRACE_READER(tu)
+#endif
+
 namespace ssb {
 
 // DST passed by value to the hashing kernels

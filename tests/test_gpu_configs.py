@@ -186,3 +186,52 @@ def test_c5_per_gpu_slice(engine, distinct_roots):
     o_out, o_st, o_err, o_ver = _c_oracle(wl, sample, t, n)
     assert (o_st == 0).all() and o_ver[:len(sample) * n].all()
     assert all(out[v].tobytes() == o_out[k].tobytes() for k, v in enumerate(sample))
+
+
+def test_twenty_slots_every_batch_in_fallback(engine):
+    """20 one-stream slots in flight at once (the bench's configuration) with 1% invalid shares in
+    EVERY batch, so every slot queue runs the exact group-test fallback -- the path whose larger
+    kernels could grow a queue's scratch while the other queues run (round 2's
+    HSA_STATUS_ERROR_OUT_OF_RESOURCES; every batch kernel now fits the queue primer, build guard).
+    Twenty batches submitted through the asynchronous host path before any wait, each with its own
+    invalid set: every verdict / status / combine == the construction truth, and the first and the
+    last batch == the C oracle on the same bytes."""
+    V, t, n, R, S = 512, 3, 4, 8, 20
+    wl = bench.make_workload(engine, V, t, n, R, 31, invalid_rate=0.0)
+    N = V * n
+    wrong = engine.sign_batch([11 + i for i in range(N // 50)], [0] * (N // 50), [bytes([7]) * 32])
+    rng = np.random.default_rng(77)
+    batches = []
+    for b in range(S):
+        bad = sorted(rng.choice(N, size=N // 100, replace=False).tolist())
+        sigs = bytearray(wl["sigs"])
+        for k, i in enumerate(bad):
+            sigs[96 * i:96 * (i + 1)] = wrong[(k + b) % len(wrong)]
+        valid = np.ones(N, dtype=np.uint8)
+        valid[bad] = 0
+        batches.append((bytes(sigs), valid))
+    lib = engine._lib
+    assert lib.ssb_set_slot_streams(engine.handle, 1) == 0
+    assert lib.ssb_set_pipeline_depth(engine.handle, S) == 0
+    try:
+        offs = list(range(0, N + 1, n))
+        pend = [engine.submit_batch_raw([t] * V, offs, sg, wl["pks"], wl["ids"], wl["job_root"], wl["roots"])
+                for sg, _ in batches]
+        res = [p.wait() for p in pend]
+    finally:
+        lib.ssb_set_pipeline_depth(engine.handle, 1)
+        lib.ssb_set_slot_streams(engine.handle, 3)
+    msig = engine.sign_batch(wl["master"], wl["job_root"], wl["roots"])
+    for (sg, valid), (out, st, err, ver) in zip(batches, res):
+        assert (ver == valid).all()
+        per_job = valid.reshape(V, n).sum(axis=1)
+        assert ((st == 0) == (per_job >= t)).all()
+        ok = np.nonzero(per_job >= t)[0]
+        assert all(out[v].tobytes() == msig[v] for v in ok)
+    for b in (0, S - 1):
+        sg, _ = batches[b]
+        o_out, o_st, o_err, o_ver = bls_c.threshold_batch(list(range(0, N + 1, n)), [t] * V, sg, wl["pks"], wl["ids"],
+                                                          wl["job_root"], wl["roots"], THREADS, verify_all=True)
+        out, st, err, ver = res[b]
+        assert (ver == o_ver[:N]).all() and (st == o_st).all() and (err == o_err).all()
+        assert (out[st == 0] == o_out[o_st == 0]).all()
