@@ -38,6 +38,20 @@ def main():
     for r in win:
         ends[r[2]] = max(ends[r[2]], r[1])
     print("queue finish (ms): " + " ".join("%.1f" % ((e - t0) / 1e6) for e in sorted(ends.values())))
+    # per queue (batch), the end of each stage relative to the release: what the last batches wait on
+    per_q = collections.defaultdict(dict)
+    for r in win:
+        if r[3].startswith("__amd") or r[3].startswith("at::"):
+            continue
+        k = r[3].split("<")[0]
+        per_q[r[2]][k] = max(per_q[r[2]].get(k, 0), r[1])
+    stages = ["k_decode_count", "k_subgroup_map", "k_msm_bucket2", "k_msm_window2", "k_miller_final",
+              "k_fb_rlc", "k_fb_level", "k_combine_sum"]
+    print("per-queue stage ends (ms), by queue finish:")
+    print("  " + " ".join("%9s" % s.replace("k_", "")[:9] for s in stages) + "  last")
+    for q, d in sorted(per_q.items(), key=lambda kv: max(kv[1].values())):
+        print("  " + " ".join("%9.2f" % ((d[s] - t0) / 1e6) if s in d else "%9s" % "-" for s in stages) +
+              "  %.2f" % ((max(d.values()) - t0) / 1e6))
     step = a.bin * 1e6
     for b in range(int(math.ceil((t1 - t0) / step))):
         lo, hi = t0 + b * step, t0 + (b + 1) * step

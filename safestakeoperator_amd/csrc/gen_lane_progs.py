@@ -766,7 +766,8 @@ class Emitter:
     def __init__(self, sch):
         self.s, self.G = sch, sch.G
         self.lines = []
-        self.tables = []
+        self.tables = []      # (name, words): per-stage packed code rows, [role][NW] uint32
+        self.cur = None       # codes of the stage being emitted (lists of G values)
 
     def sel(self, codes):
         """per-role values (< 2^16) -> a C expression of `role`: packed immediates for small
@@ -794,9 +795,35 @@ class Emitter:
             return "LP_SEL16X2(0x%016xull, 0x%016xull)" % (lo, hi)
         if len(set(codes)) == 1:
             return "%du" % codes[0]
-        name = "%s_t%d" % (self.s.p.name, len(self.tables))
-        self.tables.append((name, codes))
-        return "LP_SELT(%s)" % name
+        # one packed row per lane and stage (LP_CODES at the stage's top loads the lane's row with
+        # 16-byte loads, one memory round trip per stage instead of one per table)
+        idx = len(self.cur)
+        self.cur.append(codes)
+        return "LP_CW(@TAB@, @NW@, %d)" % idx
+
+    def begin_stage(self):
+        self.cur = []
+        self.stage_start = len(self.lines)
+
+    def end_stage(self):
+        """Pack the stage's code lists into a table and patch the stage's lines."""
+        codes, self.cur = self.cur, None
+        if not codes:
+            return
+        G = self.G
+        nw = (len(codes) + 1) // 2
+        nw = (nw + 3) // 4 * 4
+        name = "%s_s%d" % (self.s.p.name, len(self.tables))
+        words = []
+        for r in range(G):
+            row = [0] * nw
+            for i, c in enumerate(codes):
+                row[i // 2] |= c[r] << (16 * (i & 1))
+            words += row
+        self.tables.append((name, words))
+        for k in range(self.stage_start, len(self.lines)):
+            self.lines[k] = self.lines[k].replace("@TAB@", name).replace("@NW@", str(nw))
+        self.lines.insert(self.stage_start + 2, "    LP_CODES(%s, %d);" % (name, nw))
 
     def bits(self, bits):
         v = 0
@@ -917,6 +944,7 @@ class Emitter:
         for (kind, items) in s.stages:
             for p0 in range(0, len(items), G):
                 chunk = items[p0:p0 + G]
+                self.begin_stage()
                 out.append("  {  // %s %s" % (kind, " ".join("".join(str(x) for x in it) for it in chunk)))
                 out.append("    LP_DECL_T;")
                 if kind == "prod":
@@ -976,17 +1004,20 @@ class Emitter:
                         out.append("    LP_FOR(%d) lp_chk(g, LP_T, %s);" % (G, self.sel(cb)))
                 out.append("    LP_SYNC();")
                 out.append("  }")
+                self.end_stage()
         if staged:
             for p0 in range(0, nout, G):
                 n = min(G, nout - p0)
                 src = [C_SCR + stage_base + p0 + r for r in range(n)] + [0] * (G - n)
                 dst = [C_D + p0 + r for r in range(n)] + [junk] * (G - n)
+                self.begin_stage()
                 out.append("  {  // copy outputs %d..%d" % (p0, p0 + n - 1))
                 out.append("    LP_DECL_T;")
                 out.append("    LP_FOR(%d) lp_ld(LP_T, g, %s);" % (G, self.sel(src)))
                 out.append("    LP_FOR(%d) lp_st(g, %s, LP_T);" % (G, self.sel(dst)))
                 out.append("    LP_SYNC();")
                 out.append("  }")
+                self.end_stage()
         self.n_scr_total = n_scr_total
         return out
 
@@ -1006,8 +1037,8 @@ def emit_header(progs):
         body = em.emit()
         nprod = len(sch.prods)
         nmat = sch.n_mats
-        for name, codes in em.tables:
-            hdr.append("SSB_LP_TABLE uint16_t %s[%d] = {%s};" % (name, len(codes), ", ".join(map(str, codes))))
+        for name, words in em.tables:
+            hdr.append("SSB_LP_TABLE uint32_t %s[%d] = {%s};" % (name, len(words), ", ".join("0x%x" % w for w in words)))
         hdr.append("// %s: G=%d, %d products in %d rounds (%.0f%% lane use), %d materialisations, %d outputs, "
                    "%d scratch slots, %d stages"
                    % (P.name, P.G, nprod, sch.n_rounds, 100.0 * nprod / max(1, sch.n_rounds * P.G), nmat,

@@ -21,8 +21,10 @@ SSB_INL void msm_entries(int i, uint64_t k, uint32_t g, const msm_cfg& c, uint32
   for (uint32_t w = 0; w < c.W; ++w) {
     const uint32_t d = (uint32_t)((k >> (c.c * w)) & mask);
     if (!d) continue;
-    const uint32_t key = c.base + ((g * c.W + w) << c.c) + d;
-    if (SCATTER) ent[atomicAdd(&cnt[key], 1u)] = (uint32_t)i;
+    // merged: all windows of the group share its buckets; the entry names the window's base
+    const uint32_t key = c.merged ? c.base + (g << c.c) + d : c.base + ((g * c.W + w) << c.c) + d;
+    const uint32_t e = c.merged ? ((uint32_t)i << 4) | w : (uint32_t)i;
+    if (SCATTER) ent[atomicAdd(&cnt[key], 1u)] = e;
     else atomicAdd(&cnt[key], 1u);
   }
 }
@@ -46,11 +48,14 @@ SSB_INL void msm_sort_lane(int i, const rlc_key& key, const uint32_t* __restrict
 // ---- bucket sums: J = 2^lj lanes per bucket, 64/J buckets per workgroup, buckets in `order` ----
 // (block bodies take their block index and LDS explicitly, so one launch can run the G2 and the
 // G1 side's blocks side by side: k_msm_bucket2 / k_msm_window2 below)
+// (pow != nullptr: a merged MSM -- entry = share << 4 | window, point = pow[pidx[share] * PKPOW_W + window],
+// the cached key's precomputed base [2^(4 window)] pk)
 template <class F>
 SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t base, int lj, const uint32_t* __restrict__ order,
                               const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
                               const uint32_t* __restrict__ ent, const uint32_t* __restrict__ flags,
-                              const aff<F>* __restrict__ pts, jac<F>* __restrict__ bsum) {
+                              const aff<F>* __restrict__ pts, jac<F>* __restrict__ bsum,
+                              const aff<F>* __restrict__ pow = nullptr, const uint32_t* __restrict__ pidx = nullptr) {
   const int lane = threadIdx.x, J = 1 << lj, j = lane & (J - 1);
   const uint32_t ob = bid * (64u >> lj) + (uint32_t)(lane >> lj);
   const uint32_t key = ob < nb ? order[base + ob] : 0u, b = key - base;
@@ -64,9 +69,16 @@ SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t ba
     // bucket launch runs two waves per SIMD, which hide each other's latency (round 2: the former
     // software-pipelined loop, two points live, held 256 VGPRs + 165 AGPRs = one wave per SIMD;
     // C2 at 20 steps 11.2 -> 12.1 M partial sigs/s)
-    for (uint32_t x = s + j; x < e; x += J) {
-      const uint32_t i = ent[x];
-      if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pts[i]; jac_add_aff_inl(acc, acc, q); }
+    if (pow) {
+      for (uint32_t x = s + j; x < e; x += J) {
+        const uint32_t en = ent[x], i = en >> 4;
+        if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pow[(size_t)pidx[i] * PKPOW_W + (en & 15u)]; jac_add_aff_inl(acc, acc, q); }
+      }
+    } else {
+      for (uint32_t x = s + j; x < e; x += J) {
+        const uint32_t i = ent[x];
+        if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pts[i]; jac_add_aff_inl(acc, acc, q); }
+      }
     }
   }
   for (int h = J >> 1; h >= 1; h >>= 1) {
@@ -110,9 +122,10 @@ SSB_INL void msm_window_block(uint32_t bid, jac<F>* sh, int c, const jac<F>* __r
     for (int e = m - 1; e >= 1; --e) { jac<F> o = bk[t * m + e]; jac_add(S, S, o); jac_add(U, U, S); }
     jac<F> o = bk[t * m]; jac_add(S, S, o);
   }
-  // suffix scan over the lanes: S_t <- sum_{t' >= t} S_t'
+  // suffix scan over the lanes: S_t <- sum_{t' >= t} S_t'  (blocks wider than 64 lanes: the lanes
+  // past 64 only keep the barriers)
   for (int off = 1; off < L; off <<= 1) {
-    sh[t] = S;
+    if (t < 64) sh[t] = S;
     __syncthreads();
     if (t + off < L) { jac<F> o = sh[t + off]; jac_add(S, S, o); }
     __syncthreads();
@@ -122,7 +135,7 @@ SSB_INL void msm_window_block(uint32_t bid, jac<F>* sh, int c, const jac<F>* __r
     jac_add(U, U, S);
   }
   for (int h = L >> 1; h >= 1; h >>= 1) {
-    sh[t] = U;
+    if (t < 64) sh[t] = U;
     __syncthreads();
     if (t < h) { jac<F> o = sh[t + h]; jac_add(U, U, o); }
     __syncthreads();
@@ -213,7 +226,7 @@ SSB_INL void h2c_clear_block(uint32_t bid, fp* lds, int n, const g2_aff* __restr
 // with exact_all: the test knob SSB_H2C_EXACT) is redone exactly, hj[i] serving as its temporary
 SSB_INL void h2c_affine_block(uint32_t bid, int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
                               const uint32_t* __restrict__ exc, int exact_all, g2_aff* __restrict__ out) {
-  const int i = bid * 64 + threadIdx.x;
+  const int i = bid * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g2_jac s;
   if (exc[i] || exact_all) {

@@ -134,6 +134,8 @@ __global__ void SSB_LB(64) k_msm_window_seq(uint32_t ngw, int c, const jac<F>* _
 struct msm_bucket_args {
   uint32_t nb, base; int lj; const uint32_t* order; const uint32_t* start; const uint32_t* cnt; const uint32_t* ent;
 };
+// the G1 side's merged MSM (msm_cfg::merged): the cached keys' precomputed bases and the shares' cache indices
+struct g1_pre_args { const g1_aff* pow; const uint32_t* pidx; };
 // hash_to_G2 stages riding along (nblk of their own; 0 = none): the SWU map beside the subgroup
 // checks, the cofactor clearing beside the bucket sums, the affine output beside the window sums
 struct h2c_fuse { int n; const fp2* u; g2_aff* q; g2_jac* hj; uint32_t* exc; int exact_all; g2_aff* out; };
@@ -145,13 +147,14 @@ struct h2c_fuse { int n; const fp2* u; g2_aff* q; g2_jac* hj; uint32_t* exc; int
 #endif
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_B2_WAVES))) k_msm_bucket2(uint32_t nblk2, msm_bucket_args a2, msm_bucket_args a1,
                                          const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig,
-                                         const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1) {
+                                         const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1,
+                                         g1_pre_args pre) {
   __shared__ g2_jac sh[64];
   if (blockIdx.x < nblk2)
     msm_bucket_block<fp2>(blockIdx.x, sh, a2.nb, a2.base, a2.lj, a2.order, a2.start, a2.cnt, a2.ent, flags, sig, b2);
   else
     msm_bucket_block<fp>(blockIdx.x - nblk2, (g1_jac*)sh, a1.nb, a1.base, a1.lj, a1.order, a1.start, a1.cnt, a1.ent, flags,
-                         pk, b1);
+                         pk, b1, pre.pow, pre.pidx);
 }
 // (the cofactor clearing's lane programs need 32 KB of LDS per block: they ride with the window
 // sums, a launch of few blocks, not with the bucket sums, whose many blocks the LDS would thin out)
@@ -172,7 +175,22 @@ SSB_INL void msm_horner_lane(int g, int c, int W, const g1_jac* __restrict__ wsu
   jac_to_aff(a, acc);
   out[g] = a;
 }
-struct window2_tail { uint32_t* tickets; int ngroups1, W1; g1_aff* root_sum; };
+struct window2_tail { uint32_t* tickets; int ngroups1, W1; g1_aff* root_sum; int merged; };
+// the merged G1 MSM's per-root reduce, one lane per root: root_sum[r] = sum_{d=1}^{15} d B_{r,d} by
+// running sums (28 additions) -- no per-window sums and no Horner (60 doublings + 15 additions per
+// root on one lane, the window launch's longest chain at 1.8 ms before the precomputed bases)
+SSB_INL void msm_root_lane(int r, const g1_jac* __restrict__ b1, g1_aff* __restrict__ out) {
+  const g1_jac* bk = b1 + ((size_t)r << 4);
+  g1_jac S = bk[15], U = S;
+  for (int d = 14; d >= 1; --d) {
+    g1_jac o = bk[d];
+    jac_add(S, S, o);
+    jac_add(U, U, S);
+  }
+  g1_aff a;
+  jac_to_aff(a, U);
+  out[r] = a;
+}
 SSB_INL bool last_block(uint32_t* ticket, uint32_t nblocks, uint32_t* flag_lds) {
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -200,6 +218,12 @@ __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* _
   }
   bid -= nblk2;
   if (bid < nblk1) {
+    if (tl.merged) {   // the merged G1 MSM: one reduce per root, straight to root_sum
+      const int r = (int)bid * 64 + threadIdx.x;
+      if (r < tl.ngroups1) msm_root_lane(r, b1, tl.root_sum);
+      SSB_TRACE(TR_W2_G1);
+      return;
+    }
     if (!tl.tickets) { msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1); return; }
     if (bid * 64 + threadIdx.x < ngw1) msm_window_seq_block<fp>(bid, ngw1, c1, b1, w1);
     SSB_TRACE(TR_W2_G1);
@@ -355,18 +379,22 @@ h2c_fuse fuse_of(const h2c_ws* hw, int n_roots, g2_aff* out) {
 void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int lj1, const uint32_t* order,
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
-              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw, int n_roots, g2_aff* H, uint32_t* tickets) {
+              g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw, int n_roots, g2_aff* H, uint32_t* tickets,
+              const g1_aff* pk_pow, const uint32_t* pk_index) {
   const h2c_fuse h = fuse_of(hw, n_roots, H);
-  const uint32_t nb2 = c2.ngroups * c2.W << c2.c, nb1 = c1.ngroups * c1.W << c1.c;
+  const uint32_t nb2 = msm_nbuckets(c2), nb1 = msm_nbuckets(c1);
+  const g1_pre_args pre{c1.merged ? pk_pow : nullptr, c1.merged ? pk_index : nullptr};
   const uint32_t nblk2 = (nb2 + (64u >> lj2) - 1) / (64u >> lj2), nblk1 = (nb1 + (64u >> lj1) - 1) / (64u >> lj1);
   const uint32_t nbc = h.n ? (uint32_t)(h.n + 7) / 8 : 0u, nba = h.n ? (uint32_t)(h.n + 63) / 64 : 0u;
   const msm_bucket_args a2{nb2, c2.base, lj2, order, start, cnt, ent}, a1{nb1, c1.base, lj1, order, start, cnt, ent};
-  hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1), dim3(64), 0, st, nblk2, a2, a1, flags, sig, pk, b2, b1);
-  const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W, nbw1 = (nw1 + 63) / 64;
-  const window2_tail tl{tickets, (int)c1.ngroups, (int)c1.W, root_sum};
+  hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1), dim3(64), 0, st, nblk2, a2, a1, flags, sig, pk, b2, b1, pre);
+  const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W;
+  const uint32_t nbw1 = c1.merged ? (c1.ngroups + 63) / 64 : (nw1 + 63) / 64;
+  const window2_tail tl{tickets, (int)c1.ngroups, (int)c1.W, root_sum, (int)c1.merged};
   hipLaunchKernelGGL(k_msm_window2, dim3(nw2 + nbw1 + nbc), dim3(64), 0, st, nw2, (int)c2.c, (const g2_jac*)b2,
                      pair_q, pair_p, negg1_pow, nbw1, nw1, (int)c1.c, (const g1_jac*)b1, wsum1, h, tl);
   if (tickets) return;   // the Horner and the affine H ran in the window launch's last blocks
+  // (a merged G1 side has no Horner and always runs with tickets -- run_verify checks)
   const uint32_t nbh = (c1.ngroups + 63) / 64;
   hipLaunchKernelGGL(k_msm_horner2, dim3(nbh + nba), dim3(64), 0, st, nbh, (int)c1.ngroups, (int)c1.c, (int)c1.W,
                      (const g1_jac*)wsum1, root_sum, h);

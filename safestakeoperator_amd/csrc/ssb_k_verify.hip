@@ -86,6 +86,29 @@ __global__ void SSB_LB2(64) k_decode_pk(int n, const uint8_t* __restrict__ pk48,
   pflags[s] = unit_decode_pk(pk, b);
   pk_aff[s] = pk;
 }
+// the key cache's precomputed bases for the merged G1 MSM: pow[PKPOW_W s + w] = [2^(4 w)] pk_s (keys that
+// did not decode to a usable point are never read: their shares are no candidates)
+__global__ void SSB_LB2(64) k_pk_pow(int n, const g1_aff* __restrict__ pk_aff, const uint32_t* __restrict__ pflags,
+                                     g1_aff* __restrict__ pow) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  g1_aff* o = pow + (size_t)s * PKPOW_W;
+  const g1_aff a = pk_aff[s];
+  o[0] = a;
+  const uint32_t f = pflags[s];
+  if (!(f & DEC_OK) || (f & DEC_INF)) {
+    for (uint32_t w = 1; w < PKPOW_W; ++w) o[w] = a;
+    return;
+  }
+  g1_jac p;
+  jac_from_aff(p, a);
+  for (uint32_t w = 1; w < PKPOW_W; ++w) {
+    for (int q = 0; q < 4; ++q) jac_dbl(p, p);
+    g1_aff t;
+    jac_to_aff(t, p);
+    o[w] = t;
+  }
+}
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
                         const uint32_t* __restrict__ gflags, const uint32_t* __restrict__ share_root, uint32_t n_roots,
                         uint32_t* __restrict__ flags) {

@@ -58,7 +58,13 @@ struct job_map {
 
 // One bucket MSM of the RLC sums (ssb_k_msm.hip): c-bit windows, W = ceil(64 / c) of them,
 // `ngroups` independent sums; bucket key = base + ((group * W + window) << c) + digit.
-struct msm_cfg { uint32_t c, W, base, ngroups; };
+// merged (the G1 side with the public-key cache's precomputed bases [2^(c w)] pk, c = 4, W = 16):
+// every window of a group shares ONE set of buckets, key = base + (group << c) + digit, and the
+// entry carries its window (entry = share << 4 | window): the digit d of window w adds
+// [2^(c w)] pk_i to bucket d, so sum_d d B_d is the whole sum -- no per-window sums, no Horner.
+struct msm_cfg { uint32_t c, W, base, ngroups, merged; };
+SSB_INL uint32_t msm_nbuckets(const msm_cfg& c) { return (c.merged ? c.ngroups : c.ngroups * c.W) << c.c; }
+constexpr uint32_t PKPOW_W = 16;   // precomputed bases per cached public key ([2^(4 w)] pk, w < 16)
 
 namespace k {
 constexpr int SUM_THREADS = 128;   // k_sum_* block size
@@ -91,6 +97,8 @@ __global__ void k_decode_sig(int n, const uint8_t* __restrict__ sig96, g2_aff* _
 __global__ void k_pk_gather(int n, const uint32_t* __restrict__ pk_index, uint32_t n_cache,
                             const g1_aff* __restrict__ cache_aff, const uint32_t* __restrict__ cache_flags,
                             g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ pflags);
+__global__ void k_pk_pow(int n, const g1_aff* __restrict__ pk_aff, const uint32_t* __restrict__ pflags,
+                         g1_aff* __restrict__ pow);
 __global__ void k_decode_pk(int n, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff,
                             uint32_t* __restrict__ pflags);
 __global__ void k_flags(int n, const uint32_t* __restrict__ sflags, const uint32_t* __restrict__ pflags,
@@ -202,7 +210,8 @@ void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
               g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw = nullptr, int n_roots = 0, g2_aff* H = nullptr,
-              uint32_t* tickets = nullptr);
+              uint32_t* tickets = nullptr, const g1_aff* pk_pow = nullptr, const uint32_t* pk_index = nullptr);
+// (c1.merged: the G1 side reads the cached keys' precomputed bases pk_pow[pk_index[share] * PKPOW_W + window])
 // (with tickets: the G1 Horner and the affine H(root) run in the window launch's last G1-window /
 // last clearing block instead of a launch of their own)
 // The counting sort of the MSM entries in two launches that ride along the batch's kernels

@@ -50,7 +50,7 @@ struct grp {       // passed BY VALUE to the programs (lives in registers)
 #else
 #define SSB_LP_FN inline
 #endif
-#define SSB_LP_TABLE constexpr
+#define SSB_LP_TABLE alignas(16) constexpr
 #if defined(__HIP_DEVICE_COMPILE__)
 #define LP_DECL_T fp T_
 #define LP_FOR(G) for (int role = g.role, once_ = 1; once_; once_ = 0)
@@ -69,12 +69,52 @@ struct grp {       // passed BY VALUE to the programs (lives in registers)
 #define LP_SEL16(imm) ((uint32_t)((imm) >> (16 * role)) & 0xffffu)
 #define LP_SEL16X2(lo, hi) ((uint32_t)((role < 4 ? (lo) : (hi)) >> (16 * (role & 3))) & 0xffffu)
 #define LP_SELT(tab) ((uint32_t)(tab)[role])
+// Per-stage code rows of the G = 64 programs: tab[role * nw .. + nw) holds the lane's 16-bit codes of
+// one stage, two per word.  The device loads its row once at the top of the stage (nw / 4 16-byte
+// loads, one memory round trip); the host reads the table directly inside its role loop.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LP_CODES(tab, nw) lp_u4c cw_[(nw) / 4]; lp_load_codes<(nw) / 4>(cw_, (tab) + (size_t)g.role * (nw))
+#define LP_CW(tab, nw, i) ((cw_[(i) / 8][((i) / 2) & 3] >> (16 * ((i) & 1))) & 0xffffu)
+#else
+#define LP_CODES(tab, nw) ((void)0)
+#define LP_CW(tab, nw, i) (((uint32_t)(tab)[role * (nw) + (i) / 2] >> (16 * ((i) & 1))) & 0xffffu)
+#endif
 #define LP_BIT(imm) ((uint32_t)((imm) >> role) & 1u)
 
 SSB_INL lfp* lp_ptr(const grp& g, uint32_t c) {
   const int base = c >= 512u ? g.d - 512 : (c >= 480u ? g.b - 480 : (c >= 448u ? g.a - 448 : -48));
   return c < (uint32_t)LP_NCODE_CONST ? g.k + c : g.s + ((int)c + base);
 }
+// Slot moves as three 16-byte LDS accesses (ds_read_b128 / ds_write_b128): through a computed slot
+// pointer the compiler no longer sees fp's 16-byte alignment and splits a plain struct copy into
+// ds_read2_b32 pairs (six per slot, each a separate LDS round trip when its limbs are consumed).
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint32_t lp_u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t lp_u4c __attribute__((ext_vector_type(4)));
+template <int N> SSB_INL void lp_load_codes(lp_u4c* cw, const uint32_t* row) {
+  const lp_u4c* p = (const lp_u4c*)row;
+#pragma unroll
+  for (int k = 0; k < N; ++k) cw[k] = p[k];
+}
+SSB_INL fp lp_get(const lfp* p) {
+  const SSB_LDS lp_u4* q = (const SSB_LDS lp_u4*)p;
+  const lp_u4 a = q[0], b = q[1], c = q[2];
+  fp r;
+  r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
+  r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
+  r.l[8] = c.x; r.l[9] = c.y; r.l[10] = c.z; r.l[11] = c.w;
+  return r;
+}
+SSB_INL void lp_put(lfp* p, const fp& v) {
+  SSB_LDS lp_u4* q = (SSB_LDS lp_u4*)p;
+  q[0] = lp_u4{v.l[0], v.l[1], v.l[2], v.l[3]};
+  q[1] = lp_u4{v.l[4], v.l[5], v.l[6], v.l[7]};
+  q[2] = lp_u4{v.l[8], v.l[9], v.l[10], v.l[11]};
+}
+#else
+SSB_INL fp lp_get(const lfp* p) { return *p; }
+SSB_INL void lp_put(lfp* p, const fp& v) { *p = v; }
+#endif
 
 // ---- 12-limb helpers without modular reduction ----
 SSB_INL void lp_add_raw(fp& x, const fp& v) {
@@ -92,25 +132,25 @@ SSB_INL void lp_sel(fp& r, const fp& a, const fp& b, uint32_t s) {  // r = s ? a
   for (int i = 0; i < 12; ++i) r.l[i] = s ? a.l[i] : b.l[i];
 }
 
-template <class GR> SSB_INL void lp_ld(fp& x, const GR& g, uint32_t c) { x = *lp_ptr(g, c); }
-template <class GR> SSB_INL void lp_ld_neg(fp& x, const GR& g, uint32_t c) { lp_pminus(x, *lp_ptr(g, c)); }
+template <class GR> SSB_INL void lp_ld(fp& x, const GR& g, uint32_t c) { x = lp_get(lp_ptr(g, c)); }
+template <class GR> SSB_INL void lp_ld_neg(fp& x, const GR& g, uint32_t c) { lp_pminus(x, lp_get(lp_ptr(g, c))); }
 template <class GR> SSB_INL void lp_ld_sgn(fp& x, const GR& g, uint32_t c, uint32_t s) {
-  const fp v = *lp_ptr(g, c);
+  const fp v = lp_get(lp_ptr(g, c));
   fp n; lp_pminus(n, v);
   lp_sel(x, n, v, s);
 }
-template <class GR> SSB_INL void lp_acc(fp& x, const GR& g, uint32_t c) { lp_add_raw(x, *lp_ptr(g, c)); }
+template <class GR> SSB_INL void lp_acc(fp& x, const GR& g, uint32_t c) { lp_add_raw(x, lp_get(lp_ptr(g, c))); }
 template <class GR> SSB_INL void lp_acc_neg(fp& x, const GR& g, uint32_t c) {
-  fp n; lp_pminus(n, *lp_ptr(g, c));
+  fp n; lp_pminus(n, lp_get(lp_ptr(g, c)));
   lp_add_raw(x, n);
 }
 template <class GR> SSB_INL void lp_acc_sgn(fp& x, const GR& g, uint32_t c, uint32_t s) {
-  const fp v = *lp_ptr(g, c);
+  const fp v = lp_get(lp_ptr(g, c));
   fp n; lp_pminus(n, v);
   fp t; lp_sel(t, n, v, s);
   lp_add_raw(x, t);
 }
-template <class GR> SSB_INL void lp_st(const GR& g, uint32_t c, const fp& v) { *lp_ptr(g, c) = v; }
+template <class GR> SSB_INL void lp_st(const GR& g, uint32_t c, const fp& v) { lp_put(lp_ptr(g, c), v); }
 
 // modular doubling / addition of reduced values (< p)
 SSB_INL void lp_csub(fp& x, const uint32_t* mp);
@@ -154,10 +194,10 @@ SSB_INL void la_neg(lacc& x, const fp& v, uint32_t c) {
   for (int i = 0; i < 12; ++i) x.b[i] = (uint64_t)v.l[i] * c + x.b[i];
 }
 SSB_INL void la_mix(lacc& x, const fp& v, uint32_t cp, uint32_t cn) { la_pos(x, v, cp); la_neg(x, v, cn); }
-template <class GR> SSB_INL void la_ld_pos(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_pos(x, *lp_ptr(g, code), c); }
-template <class GR> SSB_INL void la_ld_neg(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_neg(x, *lp_ptr(g, code), c); }
+template <class GR> SSB_INL void la_ld_pos(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_pos(x, lp_get(lp_ptr(g, code)), c); }
+template <class GR> SSB_INL void la_ld_neg(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_neg(x, lp_get(lp_ptr(g, code)), c); }
 template <class GR> SSB_INL void la_ld_mix(lacc& x, const GR& g, uint32_t code, uint32_t cp, uint32_t cn) {
-  la_mix(x, *lp_ptr(g, code), cp, cn);
+  la_mix(x, lp_get(lp_ptr(g, code)), cp, cn);
 }
 constexpr double LA_INV_PHI = 1.0 / (436277738.0 + 1.0) * (1.0 - 1e-12);  // 1 / ((p >> 352) + 1), rounded down
 SSB_INL void la_fin(fp& r, const lacc& x, uint32_t K, bool exact) {

@@ -100,6 +100,7 @@ struct ssb_ctx {
   hipStream_t spec = nullptr, tail = nullptr;
   // decoded public keys (ssb_pk_cache_set): affine points + DEC_* flags, indexed by the caller
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0;
+  g1_aff* pkc_pow = nullptr;   // [pkc_n][PKPOW_W] precomputed bases [2^(4 w)] pk (nullptr: allocation failed)
   // RLC key of each batch: fresh from getrandom() per call (default), or expanded from the caller's
   // seed (ssb_set_rlc_deterministic: reproducible runs / tests only)
   bool rlc_deterministic = false;
@@ -317,20 +318,35 @@ bool fallback_per_share() {
 // batches one at a time, ~0.7 ms apart, once the pairing chains of all slots ended together).  The
 // three-stream latency configuration runs them on the context's spec / tail streams.
 bool post_on_slot(const ssb_slot* s) { return s->shared; }
-msm_plan plan_msm(size_t n, size_t n_roots) {
+// g1_pre: the public keys come from the cache, which holds their precomputed bases (ctx->pkc_pow):
+// the G1 side is one merged 4-bit MSM per root (msm_cfg::merged)
+msm_plan plan_msm(size_t n, size_t n_roots, bool g1_pre = false) {
   msm_plan p;
   const size_t g1n = n_roots ? n_roots : 1;
   p.g1_msm = g1_use_msm(n, n_roots);
   int c2 = msm_pick_c(n, 1, 3, 8), c1 = msm_pick_c(n, g1n, 2, 8);  // c <= 8: <= 4 buckets per window lane
   auto keys = [&](int c, size_t g) { return (size_t)((64 + c - 1) / c) * g << c; };
   while (c1 > 2 && keys(c2, 1) + keys(c1, g1n) > MSM_KMAX) --c1;
-  p.g2 = msm_cfg{(uint32_t)c2, (uint32_t)((64 + c2 - 1) / c2), 0u, 1u};
-  p.g1 = msm_cfg{(uint32_t)c1, p.g1_msm ? (uint32_t)((64 + c1 - 1) / c1) : 0u, (uint32_t)keys(c2, 1), (uint32_t)g1n};
+  p.g2 = msm_cfg{(uint32_t)c2, (uint32_t)((64 + c2 - 1) / c2), 0u, 1u, 0u};
+  p.g1 = msm_cfg{(uint32_t)c1, p.g1_msm ? (uint32_t)((64 + c1 - 1) / c1) : 0u, (uint32_t)keys(c2, 1), (uint32_t)g1n, 0u};
   p.K = (uint32_t)(keys(c2, 1) + (p.g1_msm ? keys(c1, g1n) : 0));
   p.lj2 = msm_pick_lj(n, 1, c2);
   p.lj1 = msm_pick_lj(n, g1n, c1);
+  if (g1_pre && p.g1_msm) {
+    p.g1 = msm_cfg{4u, PKPOW_W, (uint32_t)keys(c2, 1), (uint32_t)g1n, 1u};
+    p.K = (uint32_t)(keys(c2, 1) + (g1n << 4));
+    p.lj1 = msm_pick_lj(n * PKPOW_W, g1n, 4);   // every window's entries land in the root's 16 buckets
+  }
   p.n_ent = n * (p.g2.W + p.g1.W);
   return p;
+}
+// workspace sizes: the larger of the two G1 layouts (a slot's workspace serves both)
+msm_plan plan_size(size_t n, size_t n_roots) {
+  msm_plan a = plan_msm(n, n_roots, false);
+  const msm_plan b = plan_msm(n, n_roots, true);
+  a.K = std::max(a.K, b.K);
+  a.n_ent = std::max(a.n_ent, b.n_ent);
+  return a;
 }
 
 struct verify_ws {
@@ -359,7 +375,7 @@ inline size_t fp12_slots(size_t np) {
 }
 
 size_t verify_ws_bytes(size_t n, size_t n_roots) {
-  const msm_plan p = plan_msm(n, n_roots);
+  const msm_plan p = plan_size(n, n_roots);
   const size_t np = n_roots + MSM_WMAX;
   return align_up(np * sizeof(g2_aff)) + align_up(np * sizeof(g1_aff)) + align_up(n * sizeof(g2_aff)) +
          align_up(n * sizeof(g1_aff)) + align_up(n * 4) * 5 + align_up(fp12_slots(np) * sizeof(fp12)) + align_up(4) +
@@ -372,9 +388,10 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots);
 }
 
-verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
+verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) {
   verify_ws w;
-  w.plan = plan_msm(n, n_roots);
+  const msm_plan sz = plan_size(n, n_roots);   // (the same layout for both G1 forms)
+  w.plan = plan_msm(n, n_roots, g1_pre);
   const size_t np = n_roots + MSM_WMAX;
   w.H = c.take<g2_aff>(np); w.pair_p = c.take<g1_aff>(np);
   w.sig_aff = c.take<g2_aff>(n); w.pk_aff = c.take<g1_aff>(n);
@@ -384,11 +401,11 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
   w.ntk = 4 + 1 + (uint32_t)((np + 7) / 8);
   w.tickets = c.take<uint32_t>(w.ntk);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
-  w.cnt = c.take<uint32_t>(w.plan.K); w.start = c.take<uint32_t>(w.plan.K); w.cur = c.take<uint32_t>(w.plan.K);
-  w.sbsum = c.take<uint32_t>(1024); w.ent = c.take<uint32_t>(w.plan.n_ent); w.order = c.take<uint32_t>(w.plan.K);
-  w.b2 = c.take<g2_jac>((size_t)w.plan.g2.W << w.plan.g2.c);
-  w.b1 = c.take<g1_jac>((size_t)w.plan.g1.ngroups * w.plan.g1.W << w.plan.g1.c);
-  w.w1 = c.take<g1_jac>((size_t)w.plan.g1.ngroups * w.plan.g1.W);
+  w.cnt = c.take<uint32_t>(sz.K); w.start = c.take<uint32_t>(sz.K); w.cur = c.take<uint32_t>(sz.K);
+  w.sbsum = c.take<uint32_t>(1024); w.ent = c.take<uint32_t>(sz.n_ent); w.order = c.take<uint32_t>(sz.K);
+  w.b2 = c.take<g2_jac>((size_t)sz.g2.W << sz.g2.c);
+  w.b1 = c.take<g1_jac>((size_t)sz.g1.ngroups * sz.g1.W << sz.g1.c);   // >= the merged layout's ngroups << 4
+  w.w1 = c.take<g1_jac>((size_t)sz.g1.ngroups * sz.g1.W);
   w.rpk = c.take<g1_jac>(n);
   w.rcnt = c.take<uint32_t>(n_roots); w.rstart = c.take<uint32_t>(n_roots); w.rcur = c.take<uint32_t>(n_roots);
   w.perm = c.take<uint32_t>(n);
@@ -402,11 +419,19 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots) {
 // The fused one-stream path (every stage on the slot's stream, the counting sort and the hash
 // stages riding along the per-share launches): one-stream slot, a per-root G1 bucket MSM with
 // windows of <= 16 buckets, and the sort's keys within FUSED_SORT_KMAX.
-bool fused_sort_path(const ssb_slot* S, size_t n, size_t n_roots) {
+bool fused_sort_path(const ssb_slot* S, size_t n, size_t n_roots, bool g1_pre = false) {
   if (!S->shared || !n || !n_roots) return false;
-  const msm_plan P = plan_msm(n, n_roots);
+  const msm_plan P = plan_msm(n, n_roots, g1_pre);
   const char* sgp = getenv("SSB_SUBGROUP");
   return P.g1_msm && launch::msm_fused_ok(P.g1) && !(sgp && sgp[0] == 'l') && P.K <= launch::FUSED_SORT_KMAX;
+}
+
+// the merged G1 MSM over the key cache's precomputed bases: cached keys, bases present, and the
+// fused one-stream path (the only one whose launches know the merged layout)
+bool g1_pre_path(const ssb_ctx* ctx, const uint32_t* pk_index, size_t n, size_t n_roots) {
+  if (!pk_index || !ctx->pkc_pow || getenv("SSB_NO_PKPOW")) return false;
+  const msm_plan P = plan_msm(n, n_roots, true);
+  return P.g1.merged && fused_sort_path(ctx->cur, n, n_roots, true);
 }
 
 // jm (aggregate path on the fused path): the share -> (job, root) map is computed by the decode
@@ -506,9 +531,10 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
   if (fused) {
     if (n) on_decoded();
     timed t(ctx, "k_msm_g2");
+    if (P.g1.merged && !(fuse_sort && d_pk_index && ctx->pkc_pow)) { ctx->err = "internal: merged G1 MSM off the fused cached path"; return SSB_EINVAL; }
     launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cur, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
                      w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p, fuse_hash ? &hw : nullptr,
-                     (int)n_roots, w.H, fuse_sort ? w.tickets : nullptr);
+                     (int)n_roots, w.H, fuse_sort ? w.tickets : nullptr, (const g1_aff*)ctx->pkc_pow, d_pk_index);
   } else {
   if (s1 != st) SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {
@@ -624,6 +650,7 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->negg1_pow) hipFree(ctx->negg1_pow);
   if (ctx->pkc_aff) hipFree(ctx->pkc_aff);
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
+  if (ctx->pkc_pow) hipFree(ctx->pkc_pow);
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
   delete ctx;
@@ -904,7 +931,8 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_user, 0));
   }
   carve c{(char*)ctx->cur->ws};
-  verify_ws w = carve_verify(c, n, n_roots);
+  const bool pre = g1_pre_path(ctx, pk_index, n, n_roots);
+  verify_ws w = carve_verify(c, n, n_roots, pre);
   uint32_t* share_job = c.take<uint32_t>(n);
   uint32_t* share_root = c.take<uint32_t>(n);
   uint32_t* sel = c.take<uint32_t>(n);
@@ -913,7 +941,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
   // share -> (job, root): in the decode launch on the fused path, else a launch of its own
-  const bool fmap = fused_sort_path(ctx->cur, n, n_roots);
+  const bool fmap = fused_sort_path(ctx->cur, n, n_roots, pre);
   const job_map jm{(int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root};
   if (n && !fmap)
     hipLaunchKernelGGL(k_share_map, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root);
@@ -984,7 +1012,7 @@ int verify_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint32_t* pk_i
     SSB_HIP(hipStreamWaitEvent(st, ctx->cur->ev_user, 0));
   }
   carve c{(char*)ctx->cur->ws};
-  verify_ws w = carve_verify(c, n, n_roots);
+  verify_ws w = carve_verify(c, n, n_roots, g1_pre_path(ctx, pk_index, n, n_roots));
   // root indices >= n_roots: those shares are skipped by the sums and get verdict 0
   hipStream_t tl = post_on_slot(ctx->cur) ? st : slot_tail(ctx);
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, root_idx, roots32, d, rlc_seed, verdicts, [] {},
@@ -1043,6 +1071,7 @@ int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) SSB_HIP(hipStreamSynchronize(x));
   if (ctx->pkc_aff) { hipFree(ctx->pkc_aff); ctx->pkc_aff = nullptr; }
   if (ctx->pkc_flags) { hipFree(ctx->pkc_flags); ctx->pkc_flags = nullptr; }
+  if (ctx->pkc_pow) { hipFree(ctx->pkc_pow); ctx->pkc_pow = nullptr; }
   ctx->pkc_n = 0;
   if (!n) return SSB_OK;
   uint8_t* d_in = nullptr;
@@ -1055,6 +1084,12 @@ int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
   hipStream_t st = ctx->sl[0].stream;
   SSB_HIP(hipMemcpyAsync(d_in, pk48, n * 48, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_decode_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_in, ctx->pkc_aff, ctx->pkc_flags);
+  // the precomputed bases of the batch path's merged G1 MSM (plan_msm g1_pre): registration-time
+  // work, like the decompression; without them (allocation failed) batches use the windowed G1 MSM
+  if (hipMalloc(&ctx->pkc_pow, n * PKPOW_W * sizeof(g1_aff)) != hipSuccess) { ctx->pkc_pow = nullptr; (void)hipGetLastError(); }
+  if (ctx->pkc_pow)
+    hipLaunchKernelGGL(k_pk_pow, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const g1_aff*)ctx->pkc_aff,
+                       (const uint32_t*)ctx->pkc_flags, ctx->pkc_pow);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipStreamSynchronize(st));
   hipFree(d_in);
