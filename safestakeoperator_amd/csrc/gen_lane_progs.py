@@ -494,6 +494,31 @@ def programs():
         T2, (l0, l1, l4) = miller_add_h(T, ((B(0), B(1)), (B(2), B(3))), (B(4), B(5)))
         return flat12(f12_mul_014(f, l0, l1, l4)) + flat(*T2)
     define("MILLER_ADDSTEP", 18, 6, 64, miller_addstep)
+
+    # Two Miller loops in one (a pairing check's e(P1, Q1) e(P2, Q2) before the final
+    # exponentiation): f <- f^2 l_{T1,T1}(P1) l_{T2,T2}(P2), both T doubled -- the squaring of f is
+    # shared, and the two lines' products ride in the same rounds.  A = f (12) | T1 (6) | T2 (6),
+    # B = (xP1, yP1, xP2, yP2)
+    def miller_iter2():
+        f = sym_fp12(A)
+        T1 = ((A(12), A(13)), (A(14), A(15)), (A(16), A(17)))
+        T2 = ((A(18), A(19)), (A(20), A(21)), (A(22), A(23)))
+        T1n, la = miller_dbl_h(T1, (B(0), B(1)))
+        T2n, lb = miller_dbl_h(T2, (B(2), B(3)))
+        g = f12_mul_014(f12_mul_014(f12_sqr(f), *la), *lb)
+        return flat12(g) + flat(*T1n) + flat(*T2n)
+    define("MILLER_ITER2", 24, 4, 64, miller_iter2)
+
+    # f <- f l_{T1,Q1}(P1) l_{T2,Q2}(P2), T1 += Q1, T2 += Q2.  B = (xQ1, yQ1, xP1, yP1, xQ2, yQ2, xP2, yP2)
+    def miller_addstep2():
+        f = sym_fp12(A)
+        T1 = ((A(12), A(13)), (A(14), A(15)), (A(16), A(17)))
+        T2 = ((A(18), A(19)), (A(20), A(21)), (A(22), A(23)))
+        T1n, la = miller_add_h(T1, ((B(0), B(1)), (B(2), B(3))), (B(4), B(5)))
+        T2n, lb = miller_add_h(T2, ((B(6), B(7)), (B(8), B(9))), (B(10), B(11)))
+        g = f12_mul_014(f12_mul_014(f, *la), *lb)
+        return flat12(g) + flat(*T1n) + flat(*T2n)
+    define("MILLER_ADDSTEP2", 24, 12, 64, miller_addstep2)
     return ps
 
 

@@ -87,15 +87,19 @@ __global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restri
   }
 }
 
-constexpr int BS_ML0 = lane::MILLER_ITER_SCRATCH > lane::MILLER_ADDSTEP_SCRATCH ? lane::MILLER_ITER_SCRATCH
-                                                                               : lane::MILLER_ADDSTEP_SCRATCH;
-constexpr int BS_S0 = BS_ML0 > lane::FP12_MUL_SCRATCH ? BS_ML0 : lane::FP12_MUL_SCRATCH;
-constexpr int BS_SLOTS = BS_S0 + 18 + 6 + 18 + 84;
+constexpr int bs_max(int a, int b) { return a > b ? a : b; }
+constexpr int BS_S0 = bs_max(bs_max(bs_max(lane::MILLER_ITER_SCRATCH, lane::MILLER_ADDSTEP_SCRATCH),
+                                    bs_max(lane::MILLER_ITER2_SCRATCH, lane::MILLER_ADDSTEP2_SCRATCH)),
+                             lane::FP12_MUL_SCRATCH);
+// F: f | T1 | T2 (24), B: the pairs (12), BP: 4 work slots, TMP: the final exponentiation's 84
+constexpr int BS_SLOTS = BS_S0 + 24 + 12 + 4 + 84;
 
 // One level of the group tree.  Workgroups (one wave) stride over the level's groups (control
 // flow uniform per group): sums of the group's k_i pk_i and k_i sig_i (lane-strided, LDS tree),
-// affine, then the two lane-program Miller loops, product, final exponentiation.  (A two-wave
-// variant running both Miller loops at once halved the resident workgroups and measured slower.)
+// affine, then ONE two-pair lane-program Miller loop (f12_miller2: e(S_pk, H(r)) and e(-g1, S_sig)
+// share the squarings of f; 1.33 single loops of latency instead of 2), final exponentiation.  (A
+// two-wave variant running the two loops on two waves halved the resident workgroups and measured
+// slower.)
 // gv_prev / gv_cur: per-group results of the previous / this level (1 pass, 0 fail).
 constexpr int LV_THREADS = 64;
 __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots, const uint32_t* __restrict__ ok,
@@ -115,7 +119,7 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
   const int lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
   lp_init_consts(g);
-  const int F1 = BS_S0, B = F1 + 18, F2 = B + 6, TMP = F2 + 18;
+  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
   const uint32_t lg = (uint32_t)(lb * (L - 1 - l));
   const uint64_t Gs = 1ull << lg;
   const uint32_t* gl = gst + (size_t)l * (n_roots + 1);
@@ -174,26 +178,25 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
     if (ncand) {
       const g1_aff P = sP;
       const g2_aff Q = sQ;
-      if (!P.inf) {                            // e(S_pk, H(r)) before the final exponentiation
-        const g2_aff h = H[r];
-        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&h)[lane_];
-        if (lane_ == 4) g.s[B + 4] = P.x;
-        if (lane_ == 5) g.s[B + 5] = P.y;
+      const g1_aff ng = g1_neg_generator();
+      const g2_aff h = H[r];
+      if (!P.inf && !Q.inf) {                  // e(S_pk, H(r)) e(-g1, S_sig), one two-pair loop
+        if (lane_ < 4) { g.s[B + lane_] = ((const fp*)&h)[lane_]; g.s[B + 6 + lane_] = ((const fp*)&Q)[lane_]; }
+        if (lane_ == 4) { g.s[B + 4] = P.x; g.s[B + 10] = ng.x; }
+        if (lane_ == 5) { g.s[B + 5] = P.y; g.s[B + 11] = ng.y; }
+        __syncthreads();
+        f12_miller2(g, F1, B, BP);
+      } else if (!P.inf || !Q.inf) {           // one pair at infinity: e(O, .) = e(., O) = 1
+        const g2_aff q = P.inf ? Q : h;
+        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&q)[lane_];
+        if (lane_ == 4) g.s[B + 4] = P.inf ? ng.x : P.x;
+        if (lane_ == 5) g.s[B + 5] = P.inf ? ng.y : P.y;
         __syncthreads();
         f12_miller(g, F1, B);
       } else {
         const fp12 one = fp12_one();
         if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&one)[lane_];
         __syncthreads();
-      }
-      if (!Q.inf) {                            // e(-g1, S_sig)
-        const g1_aff ng = g1_neg_generator();
-        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
-        if (lane_ == 4) g.s[B + 4] = ng.x;
-        if (lane_ == 5) g.s[B + 5] = ng.y;
-        __syncthreads();
-        f12_miller(g, F2, B);
-        f12_mul(g, F1, F2, F1);
       }
       f12_final_exp(g, F1, TMP);
       __syncthreads();

@@ -50,9 +50,11 @@ __global__ void SSB_LB(64) k_miller_pairs(int npairs, const g1_aff* __restrict__
 // failed (a no-op otherwise).  A bounded grid of 64-lane workgroups strides over the shares; each
 // candidate runs two lane-program Miller loops, one Fp12 product and one final exponentiation out of
 // LDS (the single-lane form needs ~9 KB of scratch per lane, which a full-size grid cannot reserve
-// on every hardware queue).
-constexpr int FB_S0 = ML_S0 > lane::FP12_MUL_SCRATCH ? ML_S0 : lane::FP12_MUL_SCRATCH;
-constexpr int FB_SLOTS = FB_S0 + 18 + 6 + 18 + 84;
+// on every hardware queue).  The two Miller loops run as one two-pair loop (f12_miller2).
+constexpr int fb_max(int a, int b) { return a > b ? a : b; }
+constexpr int FB_S0 = fb_max(fb_max(ML_S0, fb_max(lane::MILLER_ITER2_SCRATCH, lane::MILLER_ADDSTEP2_SCRATCH)),
+                             lane::FP12_MUL_SCRATCH);
+constexpr int FB_SLOTS = FB_S0 + 24 + 12 + 4 + 84;
 __global__ void SSB_LB(64) k_fallback_lane(int n, const uint32_t* __restrict__ ok,
                                                       const uint32_t* __restrict__ flags,
                                                       const uint32_t* __restrict__ share_root,
@@ -65,23 +67,18 @@ __global__ void SSB_LB(64) k_fallback_lane(int n, const uint32_t* __restrict__ o
   const int lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
   lp_init_consts(g);
-  const int F1 = FB_S0, B = F1 + 18, F2 = B + 6, TMP = F2 + 18;
+  const int F1 = FB_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
   for (int s = blockIdx.x; s < n; s += gridDim.x) {
     if (!(flags[s] & FLAG_CANDIDATE)) continue;  // uniform per workgroup; verdict written by k_final_lane
     const g1_aff pk = pk_aff[s];
     const g2_aff h = H[share_root[s]], sg = sig_aff[s];
     const g1_aff ng = g1_neg_generator();
-    if (lane_ < 4) g.s[B + lane_] = ((const fp*)&h)[lane_];
-    if (lane_ == 4) g.s[B + 4] = pk.x;
-    if (lane_ == 5) g.s[B + 5] = pk.y;
+    // e(pk, H(m)) e(-g1, sig) before the final exponentiation (candidates: pk, sig not infinity)
+    if (lane_ < 4) { g.s[B + lane_] = ((const fp*)&h)[lane_]; g.s[B + 6 + lane_] = ((const fp*)&sg)[lane_]; }
+    if (lane_ == 4) { g.s[B + 4] = pk.x; g.s[B + 10] = ng.x; }
+    if (lane_ == 5) { g.s[B + 5] = pk.y; g.s[B + 11] = ng.y; }
     __syncthreads();
-    f12_miller(g, F1, B);                     // e(pk, H(m)) before the final exponentiation
-    if (lane_ < 4) g.s[B + lane_] = ((const fp*)&sg)[lane_];
-    if (lane_ == 4) g.s[B + 4] = ng.x;
-    if (lane_ == 5) g.s[B + 5] = ng.y;
-    __syncthreads();
-    f12_miller(g, F2, B);                     // e(-g1, sig)
-    f12_mul(g, F1, F2, F1);
+    f12_miller2(g, F1, B, BP);
     f12_final_exp(g, F1, TMP);
     if (lane_ == 0) {
       fp12 e;

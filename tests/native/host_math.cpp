@@ -174,7 +174,18 @@ static void lane_selftest(const uint8_t* seed32) {
       // values differ by an Fp2 factor per line, which the final exponentiation removes)
       lane::f12_miller(g, F, Bq); lane::ld12(r2, g.s + F);
       fp12 e1, e2; final_exponentiation(e1, f1); final_exponentiation(e2, r2); ok += fp12_eq(e1, e2); ++n;
-      ok += !fp12_eq(f1, r2); ++n; } }
+      ok += !fp12_eq(f1, r2); ++n; }
+    { // two-pair Miller loop of (pk, P) and (-g1, Q): == the product of the two single loops after
+      // the final exponentiation
+      const int F = h.U(100), Bq = h.U(130), Bp = h.U(142);
+      g.s[Bq] = P.x.c0; g.s[Bq + 1] = P.x.c1; g.s[Bq + 2] = P.y.c0; g.s[Bq + 3] = P.y.c1; g.s[Bq + 4] = pk.x; g.s[Bq + 5] = pk.y;
+      g.s[Bq + 6] = Q.x.c0; g.s[Bq + 7] = Q.x.c1; g.s[Bq + 8] = Q.y.c0; g.s[Bq + 9] = Q.y.c1; g.s[Bq + 10] = ng.x; g.s[Bq + 11] = ng.y;
+      lane::f12_miller2(g, F, Bq, Bp); lane::ld12(r2, g.s + F);
+      fp12 m, e1, e2; fp12_mul(m, f1, f2); final_exponentiation(e1, m); final_exponentiation(e2, r2); ok += fp12_eq(e1, e2); ++n;
+      // and (pk, P) with (-pk, P): a check that holds, e(pk, P) e(-pk, P) == 1
+      g1_aff npk = pk; fp_neg(npk.y, pk.y);
+      g.s[Bq + 6] = P.x.c0; g.s[Bq + 7] = P.x.c1; g.s[Bq + 8] = P.y.c0; g.s[Bq + 9] = P.y.c1; g.s[Bq + 10] = npk.x; g.s[Bq + 11] = npk.y;
+      lane::f12_miller2(g, F, Bq, Bp); lane::f12_final_exp(g, F, h.U(12)); lane::ld12(r2, g.s + F); ok += fp12_is_one(r2); ++n; } }
   printf("%d %d\n", ok, n);
 }
 

@@ -235,3 +235,67 @@ def test_twenty_slots_every_batch_in_fallback(engine):
         out, st, err, ver = res[b]
         assert (ver == o_ver[:N]).all() and (st == o_st).all() and (err == o_err).all()
         assert (out[st == 0] == o_out[o_st == 0]).all()
+
+
+def _cached_one_stream(engine, wl, V, t, n, slots=2):
+    """ssb_threshold_aggregate_batch_cached_dev on one-stream slots (bench.py's timed path: keys from
+    the decoded-key cache, the fused launches): (out96, status, err, verdicts)."""
+    import ctypes
+    import torch
+    lib = engine._lib
+    dev = torch.device("cuda", 0)
+    N = V * n
+    u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    cache = np.frombuffer(wl["pks"], dtype=np.uint8)
+    assert lib.ssb_pk_cache_set(engine.handle, N, cache.ctypes.data_as(_lib._u8p)) == 0
+    d_sig, d_roots = u8(wl["sigs"]), u8(b"".join(wl["roots"]))
+    d_idx = torch.arange(0, N, dtype=torch.int32, device=dev)
+    d_ids = torch.tensor(wl["ids"], dtype=torch.int64, device=dev)
+    d_off = torch.arange(0, N + 1, n, dtype=torch.int32, device=dev)
+    d_t = torch.full((V,), t, dtype=torch.int32, device=dev)
+    d_jr = torch.tensor(wl["job_root"], dtype=torch.int32, device=dev)
+    dst = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
+    assert lib.ssb_set_slot_streams(engine.handle, 1) == 0, lib.ssb_last_error(engine.handle)
+    assert lib.ssb_set_pipeline_depth(engine.handle, slots) == 0, lib.ssb_last_error(engine.handle)
+    try:
+        runs = []
+        for k in range(slots):
+            out = torch.zeros((V, 96), dtype=torch.uint8, device=dev)
+            st = torch.zeros((V,), dtype=torch.int32, device=dev)
+            err = torch.zeros((V, 2), dtype=torch.int64, device=dev)
+            ver = torch.zeros((N,), dtype=torch.uint8, device=dev)
+            rc = lib.ssb_threshold_aggregate_batch_cached_dev(
+                engine.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(), d_idx.data_ptr(), d_ids.data_ptr(),
+                d_jr.data_ptr(), len(wl["roots"]), d_roots.data_ptr(), ctypes.cast(dst, _lib._u8p), len(DST), 0x5AFE + k,
+                out.data_ptr(), st.data_ptr(), err.data_ptr(), ver.data_ptr(), None)
+            assert rc == 0, lib.ssb_last_error(engine.handle)
+            runs.append((out, st, err, ver))
+        torch.cuda.synchronize()
+        return [tuple(x.cpu().numpy() for x in r) for r in runs]
+    finally:
+        lib.ssb_set_pipeline_depth(engine.handle, 1)
+        lib.ssb_set_slot_streams(engine.handle, 3)
+        assert lib.ssb_pk_cache_set(engine.handle, 0, None) == 0
+
+
+@pytest.mark.parametrize("g1", ["merged", "windowed"])
+@pytest.mark.parametrize("rate", [0.0, 0.01, 0.95], ids=["valid", "invalid_1pct", "invalid_95pct"])
+def test_c2_cached_one_stream_matches_c_oracle(engine, monkeypatch, g1, rate):
+    """bench.py's timed path: one-stream slots, keys from the cache.  merged: the G1 sums read the
+    cache's precomputed bases [2^(4w)] pk (one 16-bucket MSM per root, no Horner); windowed
+    (SSB_NO_PKPOW=1): the per-window G1 MSM + Horner.  At 95% invalid shares most buckets are empty
+    (infinity inputs to every reduction) and every batch runs the group-test fallback with its
+    two-pair Miller loops.  Every verdict, status and combined signature == the C oracle on the
+    same bytes."""
+    if g1 == "windowed":
+        monkeypatch.setenv("SSB_NO_PKPOW", "1")
+    V, t, n, R = 4096, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=3, invalid_rate=rate)
+    runs = _cached_one_stream(engine, wl, V, t, n)
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
+    for out, st, err, ver in runs:
+        assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
+        assert (st == o_st).all() and (err.astype(np.uint64) == o_err.astype(np.uint64)).all()
+        ok = st == 0
+        assert (out[ok] == o_out[ok]).all()
+        _check_against_truth(wl, V, t, n, out, st, err, ver)
