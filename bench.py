@@ -117,14 +117,23 @@ def kernel_mads(mads, V, t, n, n_roots, pk_cached=True):
     p = msm_plan(N, n_roots)
     small = mads["combine_small_t3"] if t <= 3 else (mads["combine_small_t5"] if t <= 5 else mads["combine_small_t10"])
     npairs = n_roots + p["W2"]
+    if pk_cached and p["g1_msm"]:
+        # the merged G1 MSM over the cache's precomputed bases (plan_msm g1_pre): 16 entries per share
+        # into the root's 16 buckets, one 15-bucket running sum per root, no Horner
+        g1n, lj1 = p["groups1"], 0
+        while lj1 < 6 and N / g1n / 2 ** (lj1 + 1) >= 8:
+            lj1 += 1
+        g1 = (N * 16 * (1 - 1 / 16) * mads["madd_g1"] + g1n * 16 * ((1 << lj1) - 1) * mads["sum_g1_add"]
+              + g1n * (2 * 14 * mads["sum_g1_add"] + mads["to_affine_g1"]))
+    else:
+        g1 = (msm_mads(mads, N, p["c1"], p["W1"], p["lj1"], p["groups1"], "g1")
+              + p["groups1"] * ((p["W1"] - 1) * (p["c1"] * mads["dbl_g1"] + mads["sum_g1_add"]) + mads["to_affine_g1"]))
     return {
         "k_hash_to_g2": n_roots * mads["hash_to_g2"],
         "k_decode": N * (mads["decode_sig"] + (0.0 if pk_cached else mads["decode_pk"])),
         "k_subgroup": N * mads["subgroup"],
         "k_msm_g2": msm_mads(mads, N, p["c2"], p["W2"], p["lj2"], 1, "g2") + p["W2"] * mads["to_affine_g2"],
-        "k_msm_g1": (msm_mads(mads, N, p["c1"], p["W1"], p["lj1"], p["groups1"], "g1")
-                     + p["groups1"] * ((p["W1"] - 1) * (p["c1"] * mads["dbl_g1"] + mads["sum_g1_add"])
-                                       + mads["to_affine_g1"])) if p["g1_msm"] else 0.0,
+        "k_msm_g1": g1 if p["g1_msm"] else 0.0,
         "k_rlc_pk": 0.0 if p["g1_msm"] else N * mads["rlc_pk"],
         "k_sum_g1": 0.0 if p["g1_msm"] else N * mads["sum_g1_add"] + n_roots * mads["to_affine_g1"],
         "k_miller": npairs * mads["miller_pair"],
