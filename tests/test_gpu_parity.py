@@ -343,6 +343,19 @@ def test_large_configs_properties(engine, V, t, n):
     sample = list(range(0, V, V // 512))
     msig = engine.sign_batch([master[v] for v in sample], [jr[v] for v in sample], roots)
     assert all(out[v].tobytes() == msig[k] for k, v in enumerate(sample))
+    # and the same 512 validators through the independent C oracle (every share verified on its
+    # own, the reference's scan and 255-bit Lagrange combine): identical bytes, not only the engine
+    # agreeing with its own signer
+    from oracle import bls_c
+    used = sorted({jr[v] for v in sample})
+    remap = {r: k for k, r in enumerate(used)}
+    o_off = list(range(0, len(sample) * n + 1, n))
+    o_out, o_st, o_err, o_ver = bls_c.threshold_batch(
+        o_off, [t] * len(sample), b"".join(sigs[n * v + i] for v in sample for i in range(n)),
+        b"".join(pks[n * v + i] for v in sample for i in range(n)), [ids[n * v + i] for v in sample for i in range(n)],
+        [remap[jr[v]] for v in sample], [roots[r] for r in used], 16, verify_all=True)
+    assert (o_st == 0).all() and o_ver[:len(sample) * n].all()
+    assert all(out[v].tobytes() == o_out[k].tobytes() for k, v in enumerate(sample))
 
 
 def test_combined_verify_on_device(engine):
