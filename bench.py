@@ -429,19 +429,27 @@ def main():
                                               h_in["roots"], seed=(seed_base + i) & (2 ** 64 - 1),
                                               pk_index=h_in["pkidx"] if use_cache[0] else None)
             return
-        with torch.cuda.stream(s):
-            # the slot's output buffers are rewritten by this batch: order it after the all-gather
-            # of the slot's previous batch (a stream wait, the host does not block)
-            for w in pending.pop(k, []):
-                w.wait()
-            rc = fn(
-                eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), src["d_sig"].data_ptr(), pk_arg.data_ptr(),
-                src["d_ids"].data_ptr(), src["d_jr"].data_ptr(), n_roots, src["d_roots"].data_ptr(),
-                ctypes.cast(dst_arr, _lib._u8p), len(DST),
-                (seed_base + i) & (2 ** 64 - 1), o["out"].data_ptr(), o["st"].data_ptr(), o["err"].data_ptr(),
-                o["ver"].data_ptr(), ctypes.c_void_p(s.cuda_stream))
-            if rc != 0:
-                raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
+        # the slot's output buffers are rewritten by this batch: order it after the all-gather of the
+        # slot's previous batch (a stream wait, the host does not block)
+        pend = pending.pop(k, [])
+        if pend:
+            with torch.cuda.stream(s):
+                for w in pend:
+                    w.wait()
+        # (the argument tuple of slot k is built once: the timed loop's host time per submit is the
+        # library's, not Python's -- the last batch of a round starts that much later)
+        key = (k, use_cache[0], s.cuda_stream)
+        a = call_args.get(key)
+        if a is None:
+            a = call_args[key] = (
+                (eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), src["d_sig"].data_ptr(), pk_arg.data_ptr(),
+                 src["d_ids"].data_ptr(), src["d_jr"].data_ptr(), n_roots, src["d_roots"].data_ptr(),
+                 ctypes.cast(dst_arr, _lib._u8p), len(DST)),
+                (o["out"].data_ptr(), o["st"].data_ptr(), o["err"].data_ptr(), o["ver"].data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+        rc = fn(*a[0], (seed_base + i) & (2 ** 64 - 1), *a[1])
+        if rc != 0:
+            raise RuntimeError("ssb_threshold_aggregate_batch_dev: %s" % lib.ssb_last_error(eng.handle))
+        if True:
             if args.final_verify:
                 # a-8: every combined signature against its validator's master key, same slot and
                 # stream, after the combine (a job that did not combine holds zero bytes: verdict 0)
@@ -456,6 +464,7 @@ def main():
         if len(group) >= S:
             exchange_group()
 
+    call_args = {}  # per (slot, key variant): the submit call's fixed arguments
     group = []      # slots whose results are not exchanged yet
     xchg = BatchExchange(strong, sizes=sizes, device=cdev) if dist is not None else None
 

@@ -22,19 +22,24 @@
 namespace ssb {
 namespace k {
 
-// One workgroup: counting sort of the shares by root (cnt, start, perm) and the group starts of
-// every level (gst[l][r], n_roots + 1 words per level).  Phases separated by workgroup barriers
-// (global atomics and stores of one workgroup are ordered by them).
-constexpr int PREP_THREADS = 1024;
-__global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, int L, int lb, const uint32_t* __restrict__ ok,
-                                                        const uint32_t* __restrict__ share_root, uint32_t* __restrict__ cnt,
-                                                        uint32_t* __restrict__ start, uint32_t* __restrict__ cursor,
-                                                        uint32_t* __restrict__ gst, uint32_t* __restrict__ perm) {
-  if (*ok) return;
-  const int t = threadIdx.x;
-  for (int r = t; r < n_roots; r += PREP_THREADS) cnt[r] = 0u;
+// One workgroup (the last block of k_fb_rlc's grid): counting sort of the shares by root (cnt,
+// start, perm) and the group starts of every level (gst[l][r], n_roots + 1 words per level).
+// Phases separated by workgroup barriers (global atomics and stores of one workgroup are ordered
+// by them).  (It used to be a launch of its own, k_fb_prep: one more no-op launch on every passing
+// batch's tail.)
+struct fb_prep_args { int n_roots, L, lb; const uint32_t* share_root; uint32_t* cnt; uint32_t* start; uint32_t* cursor;
+                      uint32_t* gst; uint32_t* perm; };
+SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
+  const int t = threadIdx.x, NT = blockDim.x, n_roots = a.n_roots, L = a.L, lb = a.lb;
+  const uint32_t* __restrict__ share_root = a.share_root;
+  uint32_t* __restrict__ cnt = a.cnt;
+  uint32_t* __restrict__ start = a.start;
+  uint32_t* __restrict__ cursor = a.cursor;
+  uint32_t* __restrict__ gst = a.gst;
+  uint32_t* __restrict__ perm = a.perm;
+  for (int r = t; r < n_roots; r += NT) cnt[r] = 0u;
   __syncthreads();
-  for (int s = t; s < n; s += PREP_THREADS)
+  for (int s = t; s < n; s += NT)
     if (share_root[s] < (uint32_t)n_roots) atomicAdd(&cnt[share_root[s]], 1u);
   __syncthreads();
   if (t == 0) {
@@ -52,17 +57,22 @@ __global__ void __launch_bounds__(PREP_THREADS) k_fb_prep(int n, int n_roots, in
     g[n_roots] = acc;
   }
   __syncthreads();
-  for (int s = t; s < n; s += PREP_THREADS)
+  for (int s = t; s < n; s += NT)
     if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
 }
 // threads [0, n): rsig[s] = k_s sig_s;  [n, 2n): rpk[s] = k_s pk_s  (candidates only).  With
 // `verdict` it also writes, grid-wide, the verdicts the batch check decides: every share of a
 // passing batch, the non-candidates of a failing one (the candidates' follow from the group tests)
+// (the grid's last block runs the counting sort by root, fb_prep_block)
 __global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restrict__ ok,
                                    const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig_aff,
                                    const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
-                                   g1_jac* __restrict__ rpk, uint8_t* __restrict__ verdict) {
+                                   g1_jac* __restrict__ rpk, uint8_t* __restrict__ verdict, fb_prep_args prep) {
   const uint32_t pass = *ok;
+  if (blockIdx.x == gridDim.x - 1) {   // uniform per block
+    if (!pass) fb_prep_block(n, prep);
+    return;
+  }
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (verdict && g < n) {
     const bool cand = (flags[g] & FLAG_CANDIDATE) != 0;
@@ -238,10 +248,9 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   auto nb = [](size_t x, unsigned b) { return (unsigned)((x + b - 1) / b); };
   const int L = fallback_levels((size_t)n);
   const int lb = fallback_log2_branch();
-  hipLaunchKernelGGL(k_fb_prep, dim3(1), dim3(PREP_THREADS), 0, st, n, n_roots, L, lb, ok, share_root, cnt, start, cursor,
-                     gst, perm);
-  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, key, ok, flags, sig, pk, rsig, rpk,
-                     fast_verdicts ? verdict : (uint8_t*)nullptr);
+  const fb_prep_args prep{n_roots, L, lb, share_root, cnt, start, cursor, gst, perm};
+  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64) + 1), dim3(64), 0, st, n, key, ok, flags, sig, pk, rsig, rpk,
+                     fast_verdicts ? verdict : (uint8_t*)nullptr, prep);
   for (int l = 0; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;

@@ -107,7 +107,7 @@ def test_batch_kernels_fit_the_queue_primer():
     objs = sorted(glob.glob(os.path.join(b.OBJDIR, "*.o")))
     res = b.check_private_segments(objs)
     limit = b._prime_bytes()
-    for k in ("k_decode_count", "k_subgroup_map", "k_msm_bucket2", "k_msm_window2", "k_miller_pairs", "k_fp12_prod8",
-              "k_final_lane", "k_fb_prep", "k_fb_rlc", "k_fb_level", "k_select_combine", "k_combine_terms_gls",
+    for k in ("k_decode_count", "k_subgroup_map", "k_msm_bucket2", "k_msm_window2", "k_miller_pairs", "k_miller_final",
+              "k_fp12_prod8", "k_final_lane", "k_fb_rlc", "k_fb_level", "k_select_combine", "k_combine_terms_gls",
               "k_combine_sum", "k_share_map"):
         assert k in res and res[k]["private"] <= limit, (k, res.get(k))
