@@ -142,14 +142,17 @@ def kernel_mads(mads, V, t, n, n_roots, pk_cached=True):
     }
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, shares=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (FETCH_SIZE x 2 on
     gfx950 + WRITE_SIZE, separate passes; bench_tools/pmc_summary.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        e = d.get(kernel, {})
+        if shares and e.get("hbm_bytes_per_share"):   # measured on one batch size, scaled per share
+            return round(e["hbm_bytes_per_share"] * shares)
+        return e.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -696,7 +699,12 @@ def main():
             # flag word) and three flag / root words read, two flag words written, and the sort's
             # scatter (the share's root word read, one 4-byte entry written per MSM window)
             sg_bytes_share = 196 + 3 * 4 + 2 * 4 + 4 + 4 * (mp["W2"] + mp["W1"])
-            pmc = pmc_traffic("k_subgroup_map")
+            pmc = pmc_traffic("k_subgroup_map", rf["shares"])
+            try:
+                with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+                    sq = json.load(f).get("k_subgroup_map", {}).get("sq")
+            except (OSError, ValueError):
+                sq = None
             roof = {"bound": "valu-int32-mad", "kernel": "k_subgroup_map",
                     "achieved": round(sg_mads / (rf["ms"]["k_subgroup"] * 1e-3) / 1e12, 4),
                     "peak": round(MAD_PEAK_MEASURED / 1e12, 2), "unit": "TMAD/s",
@@ -709,9 +717,11 @@ def main():
                               "the subgroup checks only (the roots' SWU map riding along is < 1%%)" % (
                                   rf["R"], rf["shares"], rf["shares"] // 64),
                     "results_ok": rf["ok"],
+                    "pmc_sq": sq,   # SQ_INSTS_VALU / wave and VALU-active / busy cycle: roofline batch and pipelined C2
                     "k_decode_count": {"achieved": round(dec_mads / (rf["ms"]["k_decode"] * 1e-3) / 1e12, 4),
                                        "frac": round(dec_mads / (rf["ms"]["k_decode"] * 1e-3) / MAD_PEAK_MEASURED, 5),
-                                       "avg_launch_ms": round(rf["ms"]["k_decode"], 4), "mads_per_launch": dec_mads},
+                                       "avg_launch_ms": round(rf["ms"]["k_decode"], 4), "mads_per_launch": dec_mads,
+                                       "traffic": pmc_traffic("k_decode_count", rf["shares"])},
                     "depth1_c2": {"kernel": dom, "achieved": round(achieved, 4), "frac": round(achieved / peak, 5),
                                   "avg_launch_ms": round(avg[dom], 4),
                                   "timing": "one C2 batch alone, three-stream slot (256 waves on 1,024 SIMDs)"}}
