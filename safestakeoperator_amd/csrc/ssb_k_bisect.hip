@@ -14,8 +14,16 @@
 // (the batch check's soundness, 2^-63 per group); a failing single-share group is exactly the
 // reference's verify (k_i != 0 mod r), so it gets verdict 0.  Children of a passing group are not
 // tested; a group whose share range equals its failed parent's inherits the failure untested.
-// Work at 1% invalid shares (C2: 64 roots x 256): ~3.5k group checks (4-ary: ~2.1k, in 5 levels)
-// instead of 16,384 per-share checks; at one invalid share, 96.  Every kernel here is a no-op (uniform early exit) when the batch passed.
+// Launches (all on the slot's stream, each a uniform no-op when the batch passed):
+//   k_fb_rlc     verdicts the batch check decides, the candidates' scalars k_i, counting sort by root
+//   k_fb_root    level 0's S_r = sum k_i sig_i per root as a 4-bit-digit bucket sum (no per-share
+//                products); e(PK_r, H(r)) is the batch check's own Miller value
+//   k_fb_level 0 one check per root
+//   k_fb_single  <= FB_SINGLE_MAX shares in failing roots: each checked alone (no products, one
+//                pairing check deep) -- one invalid share per C2 batch: 256 single checks
+//   k_fb_sparse  otherwise: k_i sig_i, k_i pk_i for the failing roots' candidates, then
+//   k_fb_level l the 16-ary levels below the root (work at 1% invalid shares, C2: ~3.5k group checks
+//                instead of 16,384 per-share checks)
 #include "ssb_kernels.h"
 #include "ssb_lane_ops.h"
 
@@ -23,12 +31,12 @@ namespace ssb {
 namespace k {
 
 // One workgroup (the last block of k_fb_rlc's grid): counting sort of the shares by root (cnt,
-// start, perm) and the group starts of every level (gst[l][r], n_roots + 1 words per level).
-// Phases separated by workgroup barriers (global atomics and stores of one workgroup are ordered
-// by them).  (It used to be a launch of its own, k_fb_prep: one more no-op launch on every passing
-// batch's tail.)
+// start, perm) and the group starts of every level (gst[l][r], n_roots + 1 words per level); it
+// also zeroes k_fb_root's per-root tickets.  Phases separated by workgroup barriers (global atomics
+// and stores of one workgroup are ordered by them).  (It used to be a launch of its own, k_fb_prep:
+// one more no-op launch on every passing batch's tail.)
 struct fb_prep_args { int n_roots, L, lb; const uint32_t* share_root; uint32_t* cnt; uint32_t* start; uint32_t* cursor;
-                      uint32_t* gst; uint32_t* perm; };
+                      uint32_t* gst; uint32_t* perm; uint32_t* rtk; uint32_t* nfail; };
 SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   const int t = threadIdx.x, NT = blockDim.x, n_roots = a.n_roots, L = a.L, lb = a.lb;
   const uint32_t* __restrict__ share_root = a.share_root;
@@ -37,7 +45,8 @@ SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   uint32_t* __restrict__ cursor = a.cursor;
   uint32_t* __restrict__ gst = a.gst;
   uint32_t* __restrict__ perm = a.perm;
-  for (int r = t; r < n_roots; r += NT) cnt[r] = 0u;
+  for (int r = t; r < n_roots; r += NT) { cnt[r] = 0u; a.rtk[r] = 0u; }
+  if (t == 0) *a.nfail = 0u;
   __syncthreads();
   for (int s = t; s < n; s += NT)
     if (share_root[s] < (uint32_t)n_roots) atomicAdd(&cnt[share_root[s]], 1u);
@@ -60,49 +69,233 @@ SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   for (int s = t; s < n; s += NT)
     if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
 }
-// threads [0, n): rsig[s] = k_s sig_s;  [n, 2n): rpk[s] = k_s pk_s  (candidates only).  With
+// Threads [0, n): the candidates' RLC scalars k64[s] (the main check's own, rlc_scalar_odd).  With
 // `verdict` it also writes, grid-wide, the verdicts the batch check decides: every share of a
-// passing batch, the non-candidates of a failing one (the candidates' follow from the group tests)
-// (the grid's last block runs the counting sort by root, fb_prep_block)
+// passing batch, the non-candidates of a failing one (the candidates' follow from the group tests).
+// The grid's last block runs the counting sort by root (fb_prep_block).
 __global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restrict__ ok,
-                                   const uint32_t* __restrict__ flags, const g2_aff* __restrict__ sig_aff,
-                                   const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
-                                   g1_jac* __restrict__ rpk, uint8_t* __restrict__ verdict, fb_prep_args prep) {
+                                   const uint32_t* __restrict__ flags, uint64_t* __restrict__ k64,
+                                   uint8_t* __restrict__ verdict, fb_prep_args prep) {
   const uint32_t pass = *ok;
   if (blockIdx.x == gridDim.x - 1) {   // uniform per block
     if (!pass) fb_prep_block(n, prep);
     return;
   }
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (verdict && g < n) {
-    const bool cand = (flags[g] & FLAG_CANDIDATE) != 0;
-    if (pass || !cand) verdict[g] = cand ? 1 : 0;
-  }
-  if (pass) return;
-  // binary double-and-add (no window table): the private segment stays small -- every tail queue
-  // reserves scratch for the largest kernel it has run, and this one is launched on every batch
-  if (g < n) {
-    if (flags[g] & FLAG_CANDIDATE) {
-      const uint64_t k = rlc_scalar_odd(key, (uint64_t)g);
-      const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
-      g2_jac r; jac_mul_aff(r, sig_aff[g], kw, 2); rsig[g] = r;
-    }
-  } else if (g < 2 * n) {
-    const int s = g - n;
-    if (flags[s] & FLAG_CANDIDATE) {
-      const uint64_t k = rlc_scalar_odd(key, (uint64_t)s);
-      const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
-      g1_jac r; jac_mul_aff(r, pk_aff[s], kw, 2); rpk[s] = r;
-    }
-  }
+  if (g >= n) return;
+  const bool cand = (flags[g] & FLAG_CANDIDATE) != 0;
+  if (verdict && (pass || !cand)) verdict[g] = cand ? 1 : 0;
+  if (!pass && cand) k64[g] = rlc_scalar_odd(key, (uint64_t)g);
 }
 
+// Level 0 of the tree (one group per root) without per-share products: the root's group check is
+//     e(PK_r, H(r)) * e(-g1, S_r) == 1,   PK_r = sum_{i in r} k_i pk_i,  S_r = sum_{i in r} k_i sig_i
+// over the root's candidates -- and e(PK_r, H(r)) before the final exponentiation is the main check's
+// own Miller value f[r] (pair r of the batch check is (PK_r, H(r)), ssbls.hip run_verify), so only S_r
+// is new: a Pippenger sum with 4-bit digits, 16 windows x 15 buckets per root, ~16 mixed additions
+// per share instead of a 64-bit double-and-add in G2 AND G1 per share (the former k_fb_rlc).
+// Block (r, q) owns windows 4q .. 4q+3 of root r, lane (w, d) = bucket d of window 4q + w: the
+// root's shares are sorted into the 64 buckets in LDS (chunks of FR_CHUNK shares), each lane sums
+// its bucket, a 16-lane suffix scan and tree give W_w = sum_d d B_{w,d}, and
+// X_q = sum_w 2^(4w) W_{4q+w}.  The last of the root's four blocks (completion ticket rtk[r], zeroed
+// by fb_prep_block) forms S_r = sum_q 2^(16q) X_q and runs the check: one lane-program Miller loop
+// e(-g1, S_r), times f[r], final exponentiation.  gv0[group of r] and, on a pass, the verdicts of
+// the root's candidates.  Product-free: the failing roots' per-share products follow in k_fb_sparse.
+constexpr int FR_CHUNK = 512;
+// at most this many shares in failing roots after level 0: k_fb_single checks them one by one
+constexpr uint32_t FB_SINGLE_MAX = 1024;
 constexpr int bs_max(int a, int b) { return a > b ? a : b; }
 constexpr int BS_S0 = bs_max(bs_max(bs_max(lane::MILLER_ITER_SCRATCH, lane::MILLER_ADDSTEP_SCRATCH),
                                     bs_max(lane::MILLER_ITER2_SCRATCH, lane::MILLER_ADDSTEP2_SCRATCH)),
                              lane::FP12_MUL_SCRATCH);
 // F: f | T1 | T2 (24), B: the pairs (12), BP: 4 work slots, TMP: the final exponentiation's 84
 constexpr int BS_SLOTS = BS_S0 + 24 + 12 + 4 + 84;
+
+// LDS of k_fb_root: the root's bucket lists (the point trees move through cross-lane shuffles, so
+// the block's LDS stays small enough for two waves per SIMD)
+struct fr_bucket_lds { uint32_t list[4 * FR_CHUNK]; uint32_t cnt[64], off[64], cur[64]; };
+SSB_INL g2_jac shfl_down_g2(const g2_jac& p, int off) {
+  g2_jac r;
+  const int* a = (const int*)&p;
+  int* b = (int*)&r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(g2_jac) / 4); ++i) b[i] = __shfl_down(a[i], (unsigned)off, 64);
+  return r;
+}
+__global__ void SSB_LB2(64) k_fb_root(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ start,
+                                    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
+                                    const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64,
+                                    const g2_aff* __restrict__ sig_aff, g2_jac* __restrict__ X, g2_aff* __restrict__ T,
+                                    uint32_t* __restrict__ rtk) {
+  if (*ok) return;   // uniform: the batch passed
+  const int r = blockIdx.x >> 2, q = blockIdx.x & 3;
+  if (r >= n_roots) return;
+  const uint32_t nr = cnt[r], sb = start[r];
+  if (!nr) return;   // no group (the root's four blocks all leave here: no ticket)
+  __shared__ fr_bucket_lds ub;
+  __shared__ uint32_t last;
+  const int lane_ = threadIdx.x, wl = lane_ >> 4, d = lane_ & 15;
+  g2_jac acc;
+  jac_set_inf(acc);
+  for (uint32_t c0 = 0; c0 < nr; c0 += FR_CHUNK) {
+    const uint32_t m = nr - c0 < (uint32_t)FR_CHUNK ? nr - c0 : (uint32_t)FR_CHUNK;
+    ub.cnt[lane_] = 0u;
+    __syncthreads();
+    for (uint32_t x = lane_; x < m; x += 64) {
+      const uint32_t s = perm[sb + c0 + x];
+      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
+      for (int w = 0; w < 4; ++w) { const uint32_t dg = (kq >> (4 * w)) & 15u; if (dg) atomicAdd(&ub.cnt[w * 16 + dg], 1u); }
+    }
+    __syncthreads();
+    if (lane_ == 0) {
+      uint32_t a = 0;
+      for (int i = 0; i < 64; ++i) { ub.off[i] = a; ub.cur[i] = a; a += ub.cnt[i]; }
+    }
+    __syncthreads();
+    for (uint32_t x = lane_; x < m; x += 64) {
+      const uint32_t s = perm[sb + c0 + x];
+      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t dg = (kq >> (4 * w)) & 15u;
+        if (dg) ub.list[atomicAdd(&ub.cur[w * 16 + dg], 1u)] = s;
+      }
+    }
+    __syncthreads();
+    const uint32_t e = ub.off[lane_] + ub.cnt[lane_];
+    for (uint32_t i = ub.off[lane_]; i < e; ++i) { const g2_aff p = sig_aff[ub.list[i]]; jac_add_aff_inl(acc, acc, p); }
+    __syncthreads();
+  }
+  // W_w = sum_d d B_{w,d}: suffix sums S_d = sum_{d' >= d} B_{w,d'} over the window's 16 lanes (lane
+  // d = 0 holds no bucket), then the sum of S_1 .. S_15
+  for (int off = 1; off < 16; off <<= 1) {
+    const g2_jac o = shfl_down_g2(acc, off);
+    if (d + off < 16) jac_add_inl(acc, acc, o);
+  }
+  if (d == 0) jac_set_inf(acc);
+  for (int h = 8; h >= 1; h >>= 1) {
+    const g2_jac o = shfl_down_g2(acc, h);
+    if (d < h) jac_add_inl(acc, acc, o);
+  }
+  // X_q = sum_w 2^(4w) W_{4q+w}  (lanes 0, 16, 32, 48)
+  if (d == 0) for (int i = 0; i < 4 * wl; ++i) jac_dbl_inl(acc, acc);
+  for (int h = 32; h >= 16; h >>= 1) {
+    const g2_jac o = shfl_down_g2(acc, h);
+    if (lane_ < h && d == 0) jac_add_inl(acc, acc, o);
+  }
+  if (lane_ == 0) X[4 * r + q] = acc;
+  __threadfence();
+  __syncthreads();
+  if (lane_ == 0) last = atomicAdd(&rtk[r], 1u) == 3u ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // S_r = sum_q 2^(16q) X_q -> T[r] (affine, for level 0's check in k_fb_level)
+  g2_jac t;
+  jac_set_inf(t);
+  if (lane_ < 4) { t = X[4 * r + lane_]; for (int i = 0; i < 16 * lane_; ++i) jac_dbl_inl(t, t); }
+  for (int h = 2; h >= 1; h >>= 1) {
+    const g2_jac o = shfl_down_g2(t, h);
+    if (lane_ < h) jac_add_inl(t, t, o);
+  }
+  if (lane_ == 0) {
+    g2_aff Q;
+    jac_to_aff(Q, t);
+    T[r] = Q;
+    rtk[r] = 0u;
+  }
+}
+
+// The per-share products the levels below 0 sum, for the candidates of the roots whose level-0
+// check failed only: threads [0, n) rsig[s] = k_s sig_s, [n, 2n) rpk[s] = k_s pk_s.
+// Binary double-and-add (no window table): the private segment stays small -- every slot queue
+// reserves scratch for the largest kernel it has run, and this one is launched on every batch.
+__global__ void SSB_LB2(64) k_fb_sparse(int n, int n_roots, const uint32_t* __restrict__ ok,
+                                      const uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
+                                      const uint32_t* __restrict__ gst0, const uint8_t* __restrict__ gv0,
+                                      const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
+                                      const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
+                                      g1_jac* __restrict__ rpk, const uint32_t* __restrict__ nfail) {
+  if (*ok || *nfail <= FB_SINGLE_MAX) return;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = g < n ? g : g - n;
+  if (s >= n || !(flags[s] & FLAG_CANDIDATE)) return;
+  const uint32_t r = share_root[s];
+  if (r >= (uint32_t)n_roots || gv0[gst0[r]]) return;   // the root passed: its shares are decided
+  const uint64_t k = k64[s];
+  const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+  if (g < n) { g2_jac o; jac_mul_aff(o, sig_aff[s], kw, 2); rsig[s] = o; }
+  else { g1_jac o; jac_mul_aff(o, pk_aff[s], kw, 2); rpk[s] = o; }
+}
+
+// the Fp12 value in slots F .. F+11 == 1, one slot per lane (an fp12 local would take 144 registers);
+// a workgroup-wide vote, so every lane gets the answer (and the slots are free again on return)
+SSB_INL bool f12_slots_one(const lane::grp& g, int F) {
+  __syncthreads();
+  const int lane_ = threadIdx.x;
+  bool one = true;
+  if (lane_ < 12) { const fp v = g.s[F + lane_]; one = lane_ == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v); }
+  return __syncthreads_and(one ? 1 : 0) != 0;
+}
+
+// e(P, h) * e(-g1, Q) == 1 with the workgroup's lane programs (one two-pair loop when both pairs are
+// finite; e(O, .) = e(., O) = 1), then the final exponentiation.  Uniform per workgroup.
+SSB_INL bool pair_check(lane::grp& g, const g1_aff& P, const g2_aff& Q, const g2_aff& h, int F1, int B, int BP, int TMP) {
+  using namespace ssb::lane;
+  const int lane_ = threadIdx.x;
+  const g1_aff ng = g1_neg_generator();
+  if (!P.inf && !Q.inf) {                  // e(S_pk, H(r)) e(-g1, S_sig), one two-pair loop
+    if (lane_ < 4) { g.s[B + lane_] = ((const fp*)&h)[lane_]; g.s[B + 6 + lane_] = ((const fp*)&Q)[lane_]; }
+    if (lane_ == 4) { g.s[B + 4] = P.x; g.s[B + 10] = ng.x; }
+    if (lane_ == 5) { g.s[B + 5] = P.y; g.s[B + 11] = ng.y; }
+    __syncthreads();
+    f12_miller2(g, F1, B, BP);
+  } else if (!P.inf || !Q.inf) {           // one pair at infinity
+    const g2_aff q = P.inf ? Q : h;
+    if (lane_ < 4) g.s[B + lane_] = ((const fp*)&q)[lane_];
+    if (lane_ == 4) g.s[B + 4] = P.inf ? ng.x : P.x;
+    if (lane_ == 5) g.s[B + 5] = P.inf ? ng.y : P.y;
+    __syncthreads();
+    f12_miller(g, F1, B);
+  } else {
+    const fp12 one = fp12_one();
+    if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&one)[lane_];
+    __syncthreads();
+  }
+  f12_final_exp(g, F1, TMP);
+  return f12_slots_one(g, F1);
+}
+
+// Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
+// e(pk_s, H(r)) * e(-g1, sig_s) == 1 -- exactly the reference's verify, no RLC scalar, no per-share
+// products, one pairing check deep instead of k_fb_sparse + the levels below the root.  Blocks
+// stride over the root-sorted order (a failing root's shares are contiguous there: one per block).
+__global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nfail,
+                                      const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                                      const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst0,
+                                      const uint8_t* __restrict__ gv0, const uint32_t* __restrict__ flags,
+                                      const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ H,
+                                      const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
+                                      uint8_t* __restrict__ verdict) {
+  using namespace ssb::lane;
+  if (*ok || *nfail > FB_SINGLE_MAX) return;   // uniform
+  __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
+  __shared__ uint32_t flg;
+  const int lane_ = threadIdx.x;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  bool init = false;
+  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
+  const uint32_t total = start[n_roots - 1] + cnt[n_roots - 1];
+  for (uint32_t x = blockIdx.x; x < total; x += gridDim.x) {
+    const uint32_t s = perm[x];
+    const uint32_t r = share_root[s];
+    if (!(flags[s] & FLAG_CANDIDATE) || gv0[gst0[r]]) continue;
+    if (!init) { lp_init_consts(g); init = true; }
+    const bool pass = pair_check(g, pk_aff[s], sig_aff[s], H[r], F1, B, BP, TMP);
+    if (lane_ == 0) verdict[s] = pass ? 1 : 0;
+  }
+}
 
 // One level of the group tree.  Workgroups (one wave) stride over the level's groups (control
 // flow uniform per group): sums of the group's k_i pk_i and k_i sig_i (lane-strided, LDS tree),
@@ -118,9 +311,11 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
                                               const uint32_t* __restrict__ flags, const g2_jac* __restrict__ rsig,
                                               const g1_jac* __restrict__ rpk, const g2_aff* __restrict__ H,
                                               const uint8_t* __restrict__ gv_prev, uint8_t* __restrict__ gv_cur,
-                                              uint8_t* __restrict__ verdict) {
+                                              uint8_t* __restrict__ verdict, const g2_aff* __restrict__ T,
+                                              const fp12* __restrict__ froot, uint32_t* __restrict__ nfail) {
   using namespace ssb::lane;
   if (*ok) return;  // uniform: the batch passed
+  if (l > 0 && *nfail <= FB_SINGLE_MAX) return;   // (k_fb_single decides the few shares of failing roots)
   __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ g2_jac red[64];
   __shared__ g1_aff sP;
@@ -156,6 +351,26 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
         continue;
       }
     }
+    bool pass = true;
+    if (l == 0 && T) {   // level 0 (one group per root): e(PK_r, H(r)) is the batch check's froot[r], S_r = T[r]
+      const g2_aff Q = T[r];
+      const int FR = TMP + 72;
+      if (Q.inf) {
+        if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&froot[r])[lane_];
+        __syncthreads();
+      } else {
+        const g1_aff ng = g1_neg_generator();
+        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
+        if (lane_ == 4) g.s[B + 4] = ng.x;
+        if (lane_ == 5) g.s[B + 5] = ng.y;
+        if (lane_ < 12) g.s[FR + lane_] = ((const fp*)&froot[r])[lane_];
+        __syncthreads();
+        f12_miller(g, F1, B);
+        f12_mul(g, F1, FR, F1);
+      }
+      f12_final_exp(g, F1, TMP);
+      pass = f12_slots_one(g, F1);
+    } else {
     // sums over the group's candidates
     if (lane_ == 0) ncand = 0u;
     __syncthreads();
@@ -184,37 +399,12 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
     }
     if (lane_ == 0) { g1_aff p; jac_to_aff(p, acc1); sP = p; }
     __syncthreads();
-    bool pass = true;
-    if (ncand) {
-      const g1_aff P = sP;
-      const g2_aff Q = sQ;
-      const g1_aff ng = g1_neg_generator();
-      const g2_aff h = H[r];
-      if (!P.inf && !Q.inf) {                  // e(S_pk, H(r)) e(-g1, S_sig), one two-pair loop
-        if (lane_ < 4) { g.s[B + lane_] = ((const fp*)&h)[lane_]; g.s[B + 6 + lane_] = ((const fp*)&Q)[lane_]; }
-        if (lane_ == 4) { g.s[B + 4] = P.x; g.s[B + 10] = ng.x; }
-        if (lane_ == 5) { g.s[B + 5] = P.y; g.s[B + 11] = ng.y; }
-        __syncthreads();
-        f12_miller2(g, F1, B, BP);
-      } else if (!P.inf || !Q.inf) {           // one pair at infinity: e(O, .) = e(., O) = 1
-        const g2_aff q = P.inf ? Q : h;
-        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&q)[lane_];
-        if (lane_ == 4) g.s[B + 4] = P.inf ? ng.x : P.x;
-        if (lane_ == 5) g.s[B + 5] = P.inf ? ng.y : P.y;
-        __syncthreads();
-        f12_miller(g, F1, B);
-      } else {
-        const fp12 one = fp12_one();
-        if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&one)[lane_];
-        __syncthreads();
-      }
-      f12_final_exp(g, F1, TMP);
-      __syncthreads();
-      fp12 e;
-      ld12(e, g.s + F1);
-      pass = fp12_is_one(e);
+    if (ncand) pass = pair_check(g, sP, sQ, H[r], F1, B, BP, TMP);
     }
-    if (lane_ == 0) gv_cur[gid] = pass ? 1 : 0;
+    if (lane_ == 0) {
+      gv_cur[gid] = pass ? 1 : 0;
+      if (l == 0 && !pass) atomicAdd(nfail, cnt[r]);   // shares in failing roots
+    }
     if (pass || lg == 0)
       for (uint64_t k = a + lane_; k < b; k += 64) {
         const uint32_t s = perm[k];
@@ -240,26 +430,46 @@ int fallback_levels(size_t n) {
 }
 
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
-                     const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
-                     uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
-                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict, bool fast_verdicts) {
+                     const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, const fp12* froot,
+                     const fb_ws& fw, uint8_t* verdict, bool fast_verdicts) {
   using namespace ssb::k;
   if (n <= 0 || n_roots <= 0) return;
   auto nb = [](size_t x, unsigned b) { return (unsigned)((x + b - 1) / b); };
   const int L = fallback_levels((size_t)n);
   const int lb = fallback_log2_branch();
-  const fb_prep_args prep{n_roots, L, lb, share_root, cnt, start, cursor, gst, perm};
-  hipLaunchKernelGGL(k_fb_rlc, dim3(nb(2 * (size_t)n, 64) + 1), dim3(64), 0, st, n, key, ok, flags, sig, pk, rsig, rpk,
+  const fb_prep_args prep{n_roots, L, lb, share_root, fw.cnt, fw.start, fw.cursor, fw.gst, fw.perm, fw.rtk, fw.nfail};
+  hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + 1), dim3(64), 0, st, n, key, ok, flags, fw.k64,
                      fast_verdicts ? verdict : (uint8_t*)nullptr, prep);
-  for (int l = 0; l < L; ++l) {
+  hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, n_roots, ok, (const uint32_t*)fw.start,
+                     (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, flags, (const uint64_t*)fw.k64, sig, fw.X, fw.T,
+                     fw.rtk);
+  {
+    const unsigned grid = (unsigned)(n_roots < 2048 ? n_roots : 2048);
+    hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, 0, L, lb, n_roots, ok, (const uint32_t*)fw.start,
+                       (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, flags,
+                       (const g2_jac*)fw.rsig, (const g1_jac*)fw.rpk, H, (const uint8_t*)fw.gv1, fw.gv0, verdict,
+                       (const g2_aff*)fw.T, froot, fw.nfail);
+  }
+  if (L == 1) return;
+  {
+    const unsigned grid = (unsigned)(n < 2048 ? n : 2048);
+    hipLaunchKernelGGL(k_fb_single, dim3(grid), dim3(64), 0, st, n_roots, ok, (const uint32_t*)fw.nfail,
+                       (const uint32_t*)fw.start, (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst,
+                       (const uint8_t*)fw.gv0, flags, share_root, H, sig, pk, verdict);
+  }
+  hipLaunchKernelGGL(k_fb_sparse, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, n_roots, ok, flags, share_root,
+                     (const uint32_t*)fw.gst, (const uint8_t*)fw.gv0, (const uint64_t*)fw.k64, sig, pk, fw.rsig, fw.rpk,
+                     (const uint32_t*)fw.nfail);
+  for (int l = 1; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;
     const unsigned grid = (unsigned)(bound < 2048 ? bound : 2048);
-    uint8_t* cur = (l & 1) ? gv1 : gv0;
-    const uint8_t* prev = (l & 1) ? gv0 : gv1;
-    hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, lb, n_roots, ok, (const uint32_t*)start,
-                       (const uint32_t*)cnt, (const uint32_t*)perm, (const uint32_t*)gst, flags, (const g2_jac*)rsig,
-                       (const g1_jac*)rpk, H, prev, cur, verdict);
+    uint8_t* cur = (l & 1) ? fw.gv1 : fw.gv0;
+    const uint8_t* prev = (l & 1) ? fw.gv0 : fw.gv1;
+    hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, lb, n_roots, ok, (const uint32_t*)fw.start,
+                       (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, flags,
+                       (const g2_jac*)fw.rsig, (const g1_jac*)fw.rpk, H, prev, cur, verdict, (const g2_aff*)nullptr,
+                       (const fp12*)nullptr, fw.nfail);
   }
 }
 

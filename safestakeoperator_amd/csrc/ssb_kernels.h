@@ -248,14 +248,24 @@ void decode_count(hipStream_t st, int n, const uint8_t* sig96, const uint8_t* pk
 // (the exclusive scan of the counts and the bucket order run in decode_count's last count block)
 void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, uint32_t* gflags, uint32_t* exc);
 // Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups
-// (ssb_k_bisect.hip); no-op when *ok.  Workspace: cnt/start/cursor n_roots words, perm n words,
-// gst fallback_levels(n) * (n_roots + 1) words, rsig/rpk n points, gv0/gv1 n + n_roots bytes.
+// (ssb_k_bisect.hip); no-op when *ok.  froot: the batch check's Miller values, f[r] = e(PK_r, H(r))
+// before the final exponentiation for r < n_roots.  Workspace (fb_ws): cnt/start/cursor/rtk n_roots
+// words, perm n words, k64 n scalars, X 4 n_roots points, T n_roots points, gst fallback_levels(n) * (n_roots + 1)
+// words, rsig/rpk n points, gv0/gv1 n + n_roots bytes, nfail one word.
+struct fb_ws {
+  uint32_t *cnt, *start, *cursor, *perm, *gst, *rtk, *nfail;
+  uint64_t* k64;
+  g2_jac* X;
+  g2_aff* T;
+  g2_jac* rsig;
+  g1_jac* rpk;
+  uint8_t *gv0, *gv1;
+};
 int fallback_log2_branch();
 int fallback_levels(size_t n);
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
-                     const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, uint32_t* cnt,
-                     uint32_t* start, uint32_t* cursor, uint32_t* perm, uint32_t* gst, g2_jac* rsig, g1_jac* rpk,
-                     uint8_t* gv0, uint8_t* gv1, uint8_t* verdict, bool fast_verdicts);
+                     const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, const fp12* froot,
+                     const fb_ws& fw, uint8_t* verdict, bool fast_verdicts);
 // first use of a new queue: acquire its scratch for the largest slot kernel while the other queues
 // are idle (ssb_k_combine.hip); synchronous, 0 on success
 int prime_queue(hipStream_t st);

@@ -299,3 +299,24 @@ def test_c2_cached_one_stream_matches_c_oracle(engine, monkeypatch, g1, rate):
         ok = st == 0
         assert (out[ok] == o_out[ok]).all()
         _check_against_truth(wl, V, t, n, out, st, err, ver)
+
+
+@pytest.mark.parametrize("count", [1, 3, 8], ids=["one", "three", "eight"])
+def test_c2_cached_one_stream_few_invalid(engine, count):
+    """A few invalid shares per C2 batch (bench.py --invalid-count): level 0 of the fallback checks
+    each root against the batch check's own Miller value e(PK_r, H(r)) and a per-root bucket sum of
+    k_i sig_i (k_fb_root); with at most FB_SINGLE_MAX (1,024) shares in failing roots -- one or
+    three failing roots of 256 -- they are checked one by one (k_fb_single), with more (eight roots)
+    through the per-share products and the 16-ary levels.  Every verdict, status and combined
+    signature == the C oracle on the same bytes."""
+    V, t, n, R = 4096, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=4, invalid_count=count)
+    runs = _cached_one_stream(engine, wl, V, t, n)
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
+    assert int((o_ver[:V * n] == 0).sum()) == count
+    for out, st, err, ver in runs:
+        assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
+        assert (st == o_st).all() and (err.astype(np.uint64) == o_err.astype(np.uint64)).all()
+        ok = st == 0
+        assert (out[ok] == o_out[ok]).all()
+        _check_against_truth(wl, V, t, n, out, st, err, ver)
