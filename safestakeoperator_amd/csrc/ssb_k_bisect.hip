@@ -103,7 +103,7 @@ __global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restri
 // the root's candidates.  Product-free: the failing roots' per-share products follow in k_fb_sparse.
 constexpr int FR_CHUNK = 512;
 // at most this many shares in failing roots after level 0: k_fb_single checks them one by one
-constexpr uint32_t FB_SINGLE_MAX = 1024;
+constexpr uint32_t FB_SINGLE_MAX = 384;
 constexpr int bs_max(int a, int b) { return a > b ? a : b; }
 constexpr int BS_S0 = bs_max(bs_max(bs_max(lane::MILLER_ITER_SCRATCH, lane::MILLER_ADDSTEP_SCRATCH),
                                     bs_max(lane::MILLER_ITER2_SCRATCH, lane::MILLER_ADDSTEP2_SCRATCH)),

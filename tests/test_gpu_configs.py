@@ -305,8 +305,8 @@ def test_c2_cached_one_stream_matches_c_oracle(engine, monkeypatch, g1, rate):
 def test_c2_cached_one_stream_few_invalid(engine, count):
     """A few invalid shares per C2 batch (bench.py --invalid-count): level 0 of the fallback checks
     each root against the batch check's own Miller value e(PK_r, H(r)) and a per-root bucket sum of
-    k_i sig_i (k_fb_root); with at most FB_SINGLE_MAX (1,024) shares in failing roots -- one or
-    three failing roots of 256 -- they are checked one by one (k_fb_single), with more (eight roots)
+    k_i sig_i (k_fb_root); with at most FB_SINGLE_MAX (384) shares in failing roots -- one failing
+    root of 256 -- they are checked one by one (k_fb_single), with more (three or eight roots)
     through the per-share products and the 16-ary levels.  Every verdict, status and combined
     signature == the C oracle on the same bytes."""
     V, t, n, R = 4096, 3, 4, 64
