@@ -24,6 +24,11 @@
 //   k_fb_sparse  otherwise: k_i sig_i, k_i pk_i for the failing roots' candidates, then
 //   k_fb_level l the 16-ary levels below the root (work at 1% invalid shares, C2: ~3.5k group checks
 //                instead of 16,384 per-share checks)
+// lane-program kernels at two waves per SIMD (256 registers, the rest spilled within the queue
+// primer's private segment): under load they no longer wait for a whole SIMD's register file
+#ifndef SSB_WAVES_PER_EU
+#define SSB_WAVES_PER_EU 2
+#endif
 #include "ssb_kernels.h"
 #include "ssb_lane_ops.h"
 

@@ -1,6 +1,11 @@
 // ssb_k_pair.hip -- kernels (gfx950): lane-program Miller loops, Fp12 products and the final exponentiation.
 // Launched from ssbls.hip (declarations in ssb_kernels.h); one TU per kernel family so the
 // library compiles in parallel.
+// lane-program kernels at two waves per SIMD (256 registers, the rest spilled within the queue
+// primer's private segment): under load they no longer wait for a whole SIMD's register file
+#ifndef SSB_WAVES_PER_EU
+#define SSB_WAVES_PER_EU 2
+#endif
 #include "ssb_kernels.h"
 #include "ssb_blocks.h"
 #include "ssb_lane_ops.h"
