@@ -46,7 +46,7 @@ def main():
         k = r[3].split("<")[0]
         per_q[r[2]][k] = max(per_q[r[2]].get(k, 0), r[1])
     stages = ["k_decode_count", "k_subgroup_map", "k_msm_bucket2", "k_msm_window2", "k_miller_final",
-              "k_fb_rlc", "k_fb_root", "k_fb_single", "k_fb_sparse", "k_fb_level", "k_combine_sum"]
+              "k_fb_rlc", "k_fb_root", "k_fb_single", "k_fb_sparse", "k_fb_level", "k_select_combine", "k_combine_sum"]
     print("per-queue stage ends (ms), by queue finish:")
     print("  " + " ".join("%9s" % s.replace("k_", "")[:9] for s in stages) + "  last")
     for q, d in sorted(per_q.items(), key=lambda kv: max(kv[1].values())):

@@ -16,9 +16,8 @@
 // tested; a group whose share range equals its failed parent's inherits the failure untested.
 // Launches (all on the slot's stream, each a uniform no-op when the batch passed):
 //   k_fb_rlc     verdicts the batch check decides, the candidates' scalars k_i, counting sort by root
-//   k_fb_root    level 0's S_r = sum k_i sig_i per root as a 4-bit-digit bucket sum (no per-share
-//                products); e(PK_r, H(r)) is the batch check's own Miller value
-//   k_fb_level 0 one check per root
+//   k_fb_root    level 0, one check per root: S_r = sum k_i sig_i as a 4-bit-digit bucket sum (no
+//                per-share products); e(PK_r, H(r)) is the batch check's own Miller value
 //   k_fb_single  <= FB_SINGLE_MAX shares in failing roots: each checked alone (no products, one
 //                pairing check deep) -- one invalid share per C2 batch: 256 single checks
 //   k_fb_sparse  otherwise: k_i sig_i, k_i pk_i for the failing roots' candidates, then
@@ -116,102 +115,6 @@ constexpr int BS_S0 = bs_max(bs_max(bs_max(lane::MILLER_ITER_SCRATCH, lane::MILL
 // F: f | T1 | T2 (24), B: the pairs (12), BP: 4 work slots, TMP: the final exponentiation's 84
 constexpr int BS_SLOTS = BS_S0 + 24 + 12 + 4 + 84;
 
-// LDS of k_fb_root: the root's bucket lists (the point trees move through cross-lane shuffles, so
-// the block's LDS stays small enough for two waves per SIMD)
-struct fr_bucket_lds { uint32_t list[4 * FR_CHUNK]; uint32_t cnt[64], off[64], cur[64]; };
-SSB_INL g2_jac shfl_down_g2(const g2_jac& p, int off) {
-  g2_jac r;
-  const int* a = (const int*)&p;
-  int* b = (int*)&r;
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(g2_jac) / 4); ++i) b[i] = __shfl_down(a[i], (unsigned)off, 64);
-  return r;
-}
-__global__ void SSB_LB2(64) k_fb_root(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ start,
-                                    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
-                                    const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64,
-                                    const g2_aff* __restrict__ sig_aff, g2_jac* __restrict__ X, g2_aff* __restrict__ T,
-                                    uint32_t* __restrict__ rtk) {
-  if (*ok) return;   // uniform: the batch passed
-  const int r = blockIdx.x >> 2, q = blockIdx.x & 3;
-  if (r >= n_roots) return;
-  const uint32_t nr = cnt[r], sb = start[r];
-  if (!nr) return;   // no group (the root's four blocks all leave here: no ticket)
-  __shared__ fr_bucket_lds ub;
-  __shared__ uint32_t last;
-  const int lane_ = threadIdx.x, wl = lane_ >> 4, d = lane_ & 15;
-  g2_jac acc;
-  jac_set_inf(acc);
-  for (uint32_t c0 = 0; c0 < nr; c0 += FR_CHUNK) {
-    const uint32_t m = nr - c0 < (uint32_t)FR_CHUNK ? nr - c0 : (uint32_t)FR_CHUNK;
-    ub.cnt[lane_] = 0u;
-    __syncthreads();
-    for (uint32_t x = lane_; x < m; x += 64) {
-      const uint32_t s = perm[sb + c0 + x];
-      if (!(flags[s] & FLAG_CANDIDATE)) continue;
-      const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
-      for (int w = 0; w < 4; ++w) { const uint32_t dg = (kq >> (4 * w)) & 15u; if (dg) atomicAdd(&ub.cnt[w * 16 + dg], 1u); }
-    }
-    __syncthreads();
-    if (lane_ == 0) {
-      uint32_t a = 0;
-      for (int i = 0; i < 64; ++i) { ub.off[i] = a; ub.cur[i] = a; a += ub.cnt[i]; }
-    }
-    __syncthreads();
-    for (uint32_t x = lane_; x < m; x += 64) {
-      const uint32_t s = perm[sb + c0 + x];
-      if (!(flags[s] & FLAG_CANDIDATE)) continue;
-      const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
-      for (int w = 0; w < 4; ++w) {
-        const uint32_t dg = (kq >> (4 * w)) & 15u;
-        if (dg) ub.list[atomicAdd(&ub.cur[w * 16 + dg], 1u)] = s;
-      }
-    }
-    __syncthreads();
-    const uint32_t e = ub.off[lane_] + ub.cnt[lane_];
-    for (uint32_t i = ub.off[lane_]; i < e; ++i) { const g2_aff p = sig_aff[ub.list[i]]; jac_add_aff_inl(acc, acc, p); }
-    __syncthreads();
-  }
-  // W_w = sum_d d B_{w,d}: suffix sums S_d = sum_{d' >= d} B_{w,d'} over the window's 16 lanes (lane
-  // d = 0 holds no bucket), then the sum of S_1 .. S_15
-  for (int off = 1; off < 16; off <<= 1) {
-    const g2_jac o = shfl_down_g2(acc, off);
-    if (d + off < 16) jac_add_inl(acc, acc, o);
-  }
-  if (d == 0) jac_set_inf(acc);
-  for (int h = 8; h >= 1; h >>= 1) {
-    const g2_jac o = shfl_down_g2(acc, h);
-    if (d < h) jac_add_inl(acc, acc, o);
-  }
-  // X_q = sum_w 2^(4w) W_{4q+w}  (lanes 0, 16, 32, 48)
-  if (d == 0) for (int i = 0; i < 4 * wl; ++i) jac_dbl_inl(acc, acc);
-  for (int h = 32; h >= 16; h >>= 1) {
-    const g2_jac o = shfl_down_g2(acc, h);
-    if (lane_ < h && d == 0) jac_add_inl(acc, acc, o);
-  }
-  if (lane_ == 0) X[4 * r + q] = acc;
-  __threadfence();
-  __syncthreads();
-  if (lane_ == 0) last = atomicAdd(&rtk[r], 1u) == 3u ? 1u : 0u;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // S_r = sum_q 2^(16q) X_q -> T[r] (affine, for level 0's check in k_fb_level)
-  g2_jac t;
-  jac_set_inf(t);
-  if (lane_ < 4) { t = X[4 * r + lane_]; for (int i = 0; i < 16 * lane_; ++i) jac_dbl_inl(t, t); }
-  for (int h = 2; h >= 1; h >>= 1) {
-    const g2_jac o = shfl_down_g2(t, h);
-    if (lane_ < h) jac_add_inl(t, t, o);
-  }
-  if (lane_ == 0) {
-    g2_aff Q;
-    jac_to_aff(Q, t);
-    T[r] = Q;
-    rtk[r] = 0u;
-  }
-}
-
 // The per-share products the levels below 0 sum, for the candidates of the roots whose level-0
 // check failed only: threads [0, n) rsig[s] = k_s sig_s, [n, 2n) rpk[s] = k_s pk_s.
 // Binary double-and-add (no window table): the private segment stays small -- every slot queue
@@ -272,6 +175,138 @@ SSB_INL bool pair_check(lane::grp& g, const g1_aff& P, const g2_aff& Q, const g2
   return f12_slots_one(g, F1);
 }
 
+// LDS of k_fb_root: the root's bucket lists (the point trees move through cross-lane shuffles, so
+// the block's LDS stays small enough for two waves per SIMD)
+struct fr_bucket_lds { uint32_t list[4 * FR_CHUNK]; uint32_t cnt[64], off[64], cur[64]; };
+union fr_lds { fr_bucket_lds b; fp s[lane::LP_NCODE_CONST + BS_SLOTS]; };
+SSB_INL g2_jac shfl_down_g2(const g2_jac& p, int off) {
+  g2_jac r;
+  const int* a = (const int*)&p;
+  int* b = (int*)&r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(g2_jac) / 4); ++i) b[i] = __shfl_down(a[i], (unsigned)off, 64);
+  return r;
+}
+__global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __restrict__ ok,
+                                     const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                                     const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst,
+                                     const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64,
+                                     const g2_aff* __restrict__ sig_aff, const fp12* __restrict__ froot,
+                                     g2_jac* __restrict__ X, uint32_t* __restrict__ rtk, uint8_t* __restrict__ gv0,
+                                     uint32_t* __restrict__ nfail, uint8_t* __restrict__ verdict) {
+  using namespace ssb::lane;
+  if (*ok) return;   // uniform: the batch passed
+  const int r = blockIdx.x >> 2, q = blockIdx.x & 3;
+  if (r >= n_roots) return;
+  const uint32_t nr = cnt[r], sb = start[r];
+  if (!nr) return;   // no group (the root's four blocks all leave here: no ticket)
+  __shared__ fr_lds u;
+  fr_bucket_lds& ub = u.b;
+  __shared__ uint32_t flg, last;
+  const int lane_ = threadIdx.x, wl = lane_ >> 4, d = lane_ & 15;
+  g2_jac acc;
+  jac_set_inf(acc);
+  for (uint32_t c0 = 0; c0 < nr; c0 += FR_CHUNK) {
+    const uint32_t m = nr - c0 < (uint32_t)FR_CHUNK ? nr - c0 : (uint32_t)FR_CHUNK;
+    ub.cnt[lane_] = 0u;
+    __syncthreads();
+    for (uint32_t x = lane_; x < m; x += 64) {
+      const uint32_t s = perm[sb + c0 + x];
+      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
+      for (int w = 0; w < 4; ++w) { const uint32_t dg = (kq >> (4 * w)) & 15u; if (dg) atomicAdd(&ub.cnt[w * 16 + dg], 1u); }
+    }
+    __syncthreads();
+    if (lane_ == 0) {
+      uint32_t a = 0;
+      for (int i = 0; i < 64; ++i) { ub.off[i] = a; ub.cur[i] = a; a += ub.cnt[i]; }
+    }
+    __syncthreads();
+    for (uint32_t x = lane_; x < m; x += 64) {
+      const uint32_t s = perm[sb + c0 + x];
+      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t dg = (kq >> (4 * w)) & 15u;
+        if (dg) ub.list[atomicAdd(&ub.cur[w * 16 + dg], 1u)] = s;
+      }
+    }
+    __syncthreads();
+    const uint32_t e = ub.off[lane_] + ub.cnt[lane_];
+    for (uint32_t i = ub.off[lane_]; i < e; ++i) { const g2_aff p = sig_aff[ub.list[i]]; jac_add_aff_inl(acc, acc, p); }
+    __syncthreads();
+  }
+  // W_w = sum_d d B_{w,d}: suffix sums S_d = sum_{d' >= d} B_{w,d'} over the window's 16 lanes (lane
+  // d = 0 holds no bucket), then the sum of S_1 .. S_15
+  for (int off = 1; off < 16; off <<= 1) {
+    const g2_jac o = shfl_down_g2(acc, off);
+    if (d + off < 16) jac_add(acc, acc, o);
+  }
+  if (d == 0) jac_set_inf(acc);
+  for (int h = 8; h >= 1; h >>= 1) {
+    const g2_jac o = shfl_down_g2(acc, h);
+    if (d < h) jac_add(acc, acc, o);
+  }
+  // X_q = sum_w 2^(4w) W_{4q+w}  (lanes 0, 16, 32, 48)
+  if (d == 0) for (int i = 0; i < 4 * wl; ++i) jac_dbl(acc, acc);
+  for (int h = 32; h >= 16; h >>= 1) {
+    const g2_jac o = shfl_down_g2(acc, h);
+    if (lane_ < h && d == 0) jac_add(acc, acc, o);
+  }
+  if (lane_ == 0) X[4 * r + q] = acc;
+  __threadfence();
+  __syncthreads();
+  if (lane_ == 0) last = atomicAdd(&rtk[r], 1u) == 3u ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // S_r = sum_q 2^(16q) X_q, then the root's check FE(f[r] * e(-g1, S_r)) == 1
+  g2_jac t;
+  jac_set_inf(t);
+  if (lane_ < 4) { t = X[4 * r + lane_]; for (int i = 0; i < 16 * lane_; ++i) jac_dbl(t, t); }
+  for (int h = 2; h >= 1; h >>= 1) {
+    const g2_jac o = shfl_down_g2(t, h);
+    if (lane_ < h) jac_add(t, t, o);
+  }
+  g2_aff Q;
+  Q.inf = true;
+  if (lane_ == 0) jac_to_aff(Q, t);
+  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+  grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  lp_init_consts(g);
+  const int F1 = BS_S0, B = F1 + 24, TMP = B + 12 + 4, FR = TMP + 72;
+  if (lane_ == 0) flg = Q.inf ? 1u : 0u;
+  if (lane_ == 0 && !Q.inf) {
+    g.s[B + 0] = Q.x.c0; g.s[B + 1] = Q.x.c1; g.s[B + 2] = Q.y.c0; g.s[B + 3] = Q.y.c1;
+    const g1_aff ng = g1_neg_generator();
+    g.s[B + 4] = ng.x; g.s[B + 5] = ng.y;
+  }
+  __syncthreads();
+  const bool qinf = flg != 0;
+  __syncthreads();
+  if (qinf) {   // e(-g1, O) = 1: the root's value is f[r] alone
+    if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&froot[r])[lane_];
+    __syncthreads();
+  } else {
+    if (lane_ < 12) g.s[FR + lane_] = ((const fp*)&froot[r])[lane_];
+    __syncthreads();
+    f12_miller(g, F1, B);
+    f12_mul(g, F1, FR, F1);
+  }
+  f12_final_exp(g, F1, TMP);
+  const bool pass = f12_slots_one(g, F1);
+  if (lane_ == 0) {
+    gv0[gst[r]] = pass ? 1 : 0;
+    if (!pass) atomicAdd(nfail, nr);   // shares in failing roots
+    rtk[r] = 0u;
+  }
+  if (pass || L == 1)   // (L == 1: level 0 is the single-share level)
+    for (uint32_t k = sb + lane_; k < sb + nr; k += 64) {
+      const uint32_t s = perm[k];
+      if (flags[s] & FLAG_CANDIDATE) verdict[s] = pass ? 1 : 0;
+    }
+}
+
 // Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
 // e(pk_s, H(r)) * e(-g1, sig_s) == 1 -- exactly the reference's verify, no RLC scalar, no per-share
 // products, one pairing check deep instead of k_fb_sparse + the levels below the root.  Blocks
@@ -310,17 +345,19 @@ __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__
 // slower.)
 // gv_prev / gv_cur: per-group results of the previous / this level (1 pass, 0 fail).
 constexpr int LV_THREADS = 64;
+// (the group sums and the two-pair loop do not fit 256 registers: one wave per SIMD, whatever the
+// TU asks -- a waves_per_eu(1) attribute here would lift the shared out-of-line callees to 512 for
+// every kernel of the TU)
 __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots, const uint32_t* __restrict__ ok,
                                               const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
                                               const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst,
                                               const uint32_t* __restrict__ flags, const g2_jac* __restrict__ rsig,
                                               const g1_jac* __restrict__ rpk, const g2_aff* __restrict__ H,
                                               const uint8_t* __restrict__ gv_prev, uint8_t* __restrict__ gv_cur,
-                                              uint8_t* __restrict__ verdict, const g2_aff* __restrict__ T,
-                                              const fp12* __restrict__ froot, uint32_t* __restrict__ nfail) {
+                                              uint8_t* __restrict__ verdict, const uint32_t* __restrict__ nfail) {
   using namespace ssb::lane;
   if (*ok) return;  // uniform: the batch passed
-  if (l > 0 && *nfail <= FB_SINGLE_MAX) return;   // (k_fb_single decides the few shares of failing roots)
+  if (*nfail <= FB_SINGLE_MAX) return;   // (level 0 ran in k_fb_root; k_fb_single decides few failing shares)   // (k_fb_single decides the few shares of failing roots)
   __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ g2_jac red[64];
   __shared__ g1_aff sP;
@@ -357,25 +394,7 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
       }
     }
     bool pass = true;
-    if (l == 0 && T) {   // level 0 (one group per root): e(PK_r, H(r)) is the batch check's froot[r], S_r = T[r]
-      const g2_aff Q = T[r];
-      const int FR = TMP + 72;
-      if (Q.inf) {
-        if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&froot[r])[lane_];
-        __syncthreads();
-      } else {
-        const g1_aff ng = g1_neg_generator();
-        if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
-        if (lane_ == 4) g.s[B + 4] = ng.x;
-        if (lane_ == 5) g.s[B + 5] = ng.y;
-        if (lane_ < 12) g.s[FR + lane_] = ((const fp*)&froot[r])[lane_];
-        __syncthreads();
-        f12_miller(g, F1, B);
-        f12_mul(g, F1, FR, F1);
-      }
-      f12_final_exp(g, F1, TMP);
-      pass = f12_slots_one(g, F1);
-    } else {
+    {
     // sums over the group's candidates
     if (lane_ == 0) ncand = 0u;
     __syncthreads();
@@ -406,10 +425,7 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
     __syncthreads();
     if (ncand) pass = pair_check(g, sP, sQ, H[r], F1, B, BP, TMP);
     }
-    if (lane_ == 0) {
-      gv_cur[gid] = pass ? 1 : 0;
-      if (l == 0 && !pass) atomicAdd(nfail, cnt[r]);   // shares in failing roots
-    }
+    if (lane_ == 0) gv_cur[gid] = pass ? 1 : 0;
     if (pass || lg == 0)
       for (uint64_t k = a + lane_; k < b; k += 64) {
         const uint32_t s = perm[k];
@@ -445,16 +461,9 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   const fb_prep_args prep{n_roots, L, lb, share_root, fw.cnt, fw.start, fw.cursor, fw.gst, fw.perm, fw.rtk, fw.nfail};
   hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + 1), dim3(64), 0, st, n, key, ok, flags, fw.k64,
                      fast_verdicts ? verdict : (uint8_t*)nullptr, prep);
-  hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, n_roots, ok, (const uint32_t*)fw.start,
-                     (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, flags, (const uint64_t*)fw.k64, sig, fw.X, fw.T,
-                     fw.rtk);
-  {
-    const unsigned grid = (unsigned)(n_roots < 2048 ? n_roots : 2048);
-    hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, 0, L, lb, n_roots, ok, (const uint32_t*)fw.start,
-                       (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, flags,
-                       (const g2_jac*)fw.rsig, (const g1_jac*)fw.rpk, H, (const uint8_t*)fw.gv1, fw.gv0, verdict,
-                       (const g2_aff*)fw.T, froot, fw.nfail);
-  }
+  hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
+                     (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, flags,
+                     (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict);
   if (L == 1) return;
   {
     const unsigned grid = (unsigned)(n < 2048 ? n : 2048);
@@ -473,8 +482,8 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
     const uint8_t* prev = (l & 1) ? fw.gv0 : fw.gv1;
     hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, lb, n_roots, ok, (const uint32_t*)fw.start,
                        (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, flags,
-                       (const g2_jac*)fw.rsig, (const g1_jac*)fw.rpk, H, prev, cur, verdict, (const g2_aff*)nullptr,
-                       (const fp12*)nullptr, fw.nfail);
+                       (const g2_jac*)fw.rsig, (const g1_jac*)fw.rpk, H, prev, cur, verdict,
+                       (const uint32_t*)fw.nfail);
   }
 }
 

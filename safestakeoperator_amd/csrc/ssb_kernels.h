@@ -250,13 +250,12 @@ void subgroup(hipStream_t st, int n, const uint32_t* sflags, const g2_aff* sig, 
 // Exact verdicts of a failed batch by group testing on a 16-ary tree of root-aligned share groups
 // (ssb_k_bisect.hip); no-op when *ok.  froot: the batch check's Miller values, f[r] = e(PK_r, H(r))
 // before the final exponentiation for r < n_roots.  Workspace (fb_ws): cnt/start/cursor/rtk n_roots
-// words, perm n words, k64 n scalars, X 4 n_roots points, T n_roots points, gst fallback_levels(n) * (n_roots + 1)
+// words, perm n words, k64 n scalars, X 4 n_roots points, gst fallback_levels(n) * (n_roots + 1)
 // words, rsig/rpk n points, gv0/gv1 n + n_roots bytes, nfail one word.
 struct fb_ws {
   uint32_t *cnt, *start, *cursor, *perm, *gst, *rtk, *nfail;
   uint64_t* k64;
   g2_jac* X;
-  g2_aff* T;
   g2_jac* rsig;
   g1_jac* rpk;
   uint8_t *gv0, *gv1;

@@ -365,7 +365,7 @@ struct verify_ws {
   g2_jac* b2; g1_jac* b1; g1_jac* w1;                                              // MSM buckets / windows
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
   g2_jac* rsig; uint32_t* gst; uint8_t* gv0; uint8_t* gv1;                         // failed-batch group tests
-  uint64_t* k64; g2_jac* fbX; g2_aff* fbT; uint32_t* rtk; uint32_t* nfail;                                     // (level 0 per root)
+  uint64_t* k64; g2_jac* fbX; uint32_t* rtk; uint32_t* nfail;                                     // (level 0 per root)
   size_t npairs;
 };
 // Miller values of the pairs plus the levels of the 8-ary product tree
@@ -387,8 +387,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
          3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(n * sizeof(g2_jac)) +
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
-         align_up(n * 8) + align_up(4 * n_roots * sizeof(g2_jac)) + align_up(n_roots * sizeof(g2_aff)) +
-         align_up(n_roots * 4) + align_up(4);
+         align_up(n * 8) + align_up(4 * n_roots * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) {
@@ -415,7 +414,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.rsig = c.take<g2_jac>(n);
   w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
   w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
-  w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(4 * n_roots); w.fbT = c.take<g2_aff>(n_roots); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
+  w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(4 * n_roots); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
@@ -603,7 +602,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
                          d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
     else
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, w.f,
-                              launch::fb_ws{w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rtk, w.nfail, w.k64, w.fbX, w.fbT, w.rsig, w.rpk,
+                              launch::fb_ws{w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rtk, w.nfail, w.k64, w.fbX, w.rsig, w.rpk,
                                             w.gv0, w.gv1}, d_verdict, true);
   }
   if (!fb_tail && tail != st) {
