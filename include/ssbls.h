@@ -95,15 +95,16 @@ const char* ssb_last_error(const ssb_ctx* ctx);
 /* Slots x streams-per-slot limits: the HIP runtime reserves scratch on every hardware queue for the
  * largest kernel that queue has run, and 8 slots x 3 streams exhausted it on an MI355X
  * (HSA_STATUS_ERROR_OUT_OF_RESOURCES: the side streams run the large-scratch kernels) while
- * one-stream slots run clean up to SSB_MAX_SLOT_STREAMS. */
-#define SSB_MAX_SLOT_STREAMS 24
+ * one-stream slots run clean up to SSB_MAX_SLOT_STREAMS (20: with round 3's kernels, whose
+ * largest batch-path private segment is 2.4 KB per lane, 24 one-stream slots failed the same way). */
+#define SSB_MAX_SLOT_STREAMS 20
 #define SSB_MAX_THREE_STREAM_SLOTS 5
 /* SSB_OK if `depth` slots of `streams` streams are a supported configuration (streams 1 or 3,
  * depth x streams <= SSB_MAX_SLOT_STREAMS, three-stream slots at most SSB_MAX_THREE_STREAM_SLOTS),
  * SSB_EINVAL otherwise.  No GPU needed; ssb_set_pipeline_depth / ssb_set_slot_streams refuse what
  * this refuses. */
 int ssb_check_pipeline_config(int depth, int streams);
-/* Number of pipeline slots (1..24, default 1).  Each slot owns its streams and workspace; calls of
+/* Number of pipeline slots (1..20, default 1).  Each slot owns its streams and workspace; calls of
  * ssb_threshold_aggregate_batch_dev go to the slots round robin, so up to `depth` independent
  * batches are in flight and overlap on the device (e.g. the duties of consecutive slots).  Each
  * call's outputs are ready when the caller's `stream` reaches them. */

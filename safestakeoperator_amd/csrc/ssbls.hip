@@ -672,7 +672,7 @@ int ssb_check_pipeline_config(int depth, int streams) {
 int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
   if (!ctx) return SSB_EINVAL;
   if (ssb_check_pipeline_config(depth, ctx->slot_streams) != SSB_OK) {
-    ctx->err = "pipeline depth x streams per slot outside the supported range (one-stream slots: depth 1..24; three-stream slots: depth 1..5)";
+    ctx->err = "pipeline depth x streams per slot outside the supported range (one-stream slots: depth 1..20; three-stream slots: depth 1..5)";
     return SSB_EINVAL;
   }
   SSB_HIP(hipSetDevice(ctx->device));

@@ -28,12 +28,12 @@ def test_create_without_gpu_fails_cleanly():
 
 def test_pipeline_config_guard():
     """ssb_check_pipeline_config (the rule ssb_set_pipeline_depth / ssb_set_slot_streams enforce):
-    24 one-stream slots and 5 three-stream slots are accepted, 8 x 3 (which exhausted the per-queue
-    scratch reservations on an MI355X) and out-of-range values are refused."""
+    20 one-stream slots and 5 three-stream slots are accepted; 8 x 3 and 24 x 1 (which exhausted the
+    per-queue scratch reservations on an MI355X) and out-of-range values are refused."""
     lib = _lib.load()
     ok = lambda d, s: lib.ssb_check_pipeline_config(d, s) == 0
-    assert ok(1, 1) and ok(14, 1) and ok(20, 1) and ok(24, 1) and ok(1, 3) and ok(5, 3)
-    assert not ok(8, 3) and not ok(6, 3) and not ok(25, 1) and not ok(0, 1) and not ok(4, 2)
+    assert ok(1, 1) and ok(14, 1) and ok(20, 1) and ok(1, 3) and ok(5, 3)
+    assert not ok(8, 3) and not ok(6, 3) and not ok(21, 1) and not ok(24, 1) and not ok(25, 1) and not ok(0, 1) and not ok(4, 2)
     # a null context is refused before any HIP call
     assert lib.ssb_set_pipeline_depth(None, 4) == -1 and lib.ssb_set_slot_streams(None, 3) == -1
 
