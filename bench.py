@@ -267,6 +267,21 @@ def cpu_baseline(wl, t, n, gpu_out=None, n_val=4096, n_val_share=1024, threads=N
                 seconds_total=round(sum(ts_rlc) + sum(ts_share), 2))
 
 
+def launch_command(n, argv, port):
+    """The torch.distributed.run command bench.py --gpus N runs itself when no launcher set WORLD_SIZE."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    return subprocess.call(launch_command(n, argv, port))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -301,7 +316,22 @@ def main():
     ap.add_argument("--invalid-rate", type=float, default=0.0,
                     help="fraction of shares signed over the wrong root (the RLC batch fails; exact verdicts "
                          "come from the per-share fallback).  The headline is the all-valid C2 batch.")
+    ap.add_argument("--sustained-steps", type=int, default=200,
+                    help="length of the sustained-rate run reported as value_sustained (0: skip)")
+    ap.add_argument("--collector-windows", type=int, default=200,
+                    help="4,096-job windows pushed through the native per-slot collector for value_collector (0: skip)")
+    ap.add_argument("--collector-threads", type=int, default=8, help="native submitter threads of value_collector")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group even at one rank (rehearses RCCL's stream beside the slot "
+                         "queues on one GPU: torchrun --nproc-per-node 1 ... --force-dist)")
     args = ap.parse_args()
+    # --gpus N without an external launcher: start the N ranks here, BEFORE anything touches the GPU
+    # (this process only waits for them), one process per GPU over RCCL, and exit with their status
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if os.environ.get("WORLD_SIZE") is not None and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (os.environ["WORLD_SIZE"], args.gpus), file=sys.stderr)
+        sys.exit(2)
     if args.config is None:
         args.config = "C4_global" if args.scaling == "strong" else "C2"
     strong = args.scaling == "strong"
@@ -331,7 +361,7 @@ def main():
     # --dist-backend gloo: rehearsal of the N > 1 path on fewer GPUs than ranks (ranks share
     # devices round robin, the collectives run on host copies); the measured path is RCCL.
     gpu = local % max(1, torch.cuda.device_count()) if args.dist_backend == "gloo" else local
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         if args.dist_backend == "nccl":
@@ -601,7 +631,8 @@ def main():
         torch.cuda.synchronize(dev)
         return check_slots(host=use_host[0])
 
-    def timed_run():
+    def timed_run(steps=None):
+        steps = args.steps if steps is None else steps
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -616,7 +647,7 @@ def main():
         ev = []
         t0 = time.perf_counter()
         host_ms = []
-        for i in range(args.steps):
+        for i in range(steps):
             th = time.perf_counter()
             if dbg:   # when the slot's stream reaches / finishes this batch
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -663,11 +694,50 @@ def main():
         elapsed_host = timed_run()
         ok_host = ok_host and check_slots(host=True)
         use_host[0] = False
-    ok_st = ok_comb = ok_head and ok_other and ok_timed and ok_x and ok_host
+    # sustained rate: the same path for --sustained-steps batches (a continuous per-slot service
+    # rather than the driver's burst of `steps` batches, every one in flight at once)
+    elapsed_sus, ok_sus = None, True
+    if args.sustained_steps > 0:
+        ok_sus = warm_and_check()
+        elapsed_sus = timed_run(args.sustained_steps)
+        ok_sus = ok_sus and check_slots()
+    # the reference-side caller's path: jobs pushed one by one through the library's native per-slot
+    # collector (ssb_collector_submit, what HotstuffOperatorCommittee::sign calls under --features hip)
+    # by native submitter threads, 4,096-job windows, `S` windows in flight, keys as rows of the
+    # decoded-key table (ssb_pk_cache_add), timed from the first submit to the last result
+    coll = None
+    if args.collector_windows > 0 and not strong:
+        from safestakeoperator_amd.collector import NativeCollector, collbench_run
+        torch.cuda.synchronize(dev)
+        streams.clear()
+        col = NativeCollector(eng, max_jobs=V, max_shares=V * n, window_s=0.005, in_flight=S)
+        try:
+            rows = col.rows(wl["share_pks"])
+            collbench_run(col, wl, V, n, t, rows, S * V, threads=args.collector_threads)          # warm-up
+            n_jobs = args.collector_windows * V
+            if dist is not None:
+                dist.barrier()
+            c_sec, c_res = collbench_run(col, wl, V, n, t, rows, n_jobs, threads=args.collector_threads)
+            cw = col.stats()
+            cprof = col.profile()
+        finally:
+            col.close()
+        vv = np.arange(n_jobs) % V
+        vbits = (valid.reshape(V, n).astype(np.uint64) << np.arange(n, dtype=np.uint64)).sum(axis=1)
+        c_ok = (bool((c_res["done"] == 1).all()) and bool((c_res["rc"] == 0).all())
+                and bool(((c_res["status"] == 0) == job_ok[vv]).all()) and bool((c_res["verdicts"] == vbits[vv]).all())
+                and bool((c_res["sig96"][job_ok[vv]] == msig_arr[vv[job_ok[vv]]]).all()))
+        coll = dict(seconds=c_sec, jobs=n_jobs, windows=cw[0], ok=c_ok, profile=cprof)
+    ok_st = ok_comb = ok_head and ok_other and ok_timed and ok_x and ok_host and ok_sus and (coll is None or coll["ok"])
     if dist is not None:
-        tt = torch.tensor([elapsed, elapsed_other], dtype=torch.float64, device=cdev)
+        tt = torch.tensor([elapsed, elapsed_other, elapsed_sus or 0.0, coll["seconds"] if coll else 0.0],
+                          dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, elapsed_other = float(tt[0].item()), float(tt[1].item())
+        if elapsed_sus:
+            elapsed_sus = float(tt[2].item())
+        if coll:
+            coll["seconds"] = float(tt[3].item())
         okt = torch.tensor([1 if (ok_st and ok_comb) else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_all = bool(okt.item())
@@ -756,6 +826,22 @@ def main():
                              "(ssb_verify_batch_cached_dev, RLC batch); combined_sigs_per_s counts verified ones" % V
                              if args.final_verify else None),
             "value_host_buffers": (round(V_glob * n * args.steps / elapsed_host, 1) if elapsed_host else None),
+            "value_sustained": (round(V_glob * n * args.sustained_steps / elapsed_sus, 1) if elapsed_sus else None),
+            "sustained": ("the headline path for %d batches (%d in flight), results of every slot's last batch checked"
+                          % (args.sustained_steps, S)) if elapsed_sus else None,
+            "value_collector": (round(coll["jobs"] * n * world / coll["seconds"], 1) if coll else None),
+            "collector": (dict(jobs_per_gpu=coll["jobs"], windows=coll["windows"], window_jobs=V, in_flight=S,
+                               submitter_threads=args.collector_threads, seconds=round(coll["seconds"], 4),
+                               combined_sigs_per_s=round(coll["jobs"] * world / coll["seconds"], 1),
+                               frac_of_value=round(coll["jobs"] * n * world / coll["seconds"] / value, 3),
+                               frac_of_sustained=(round(coll["jobs"] * n * world / coll["seconds"] /
+                                                        (V_glob * n * args.sustained_steps / elapsed_sus), 3)
+                                                  if elapsed_sus else None),
+                               worker_profile_incl_warmup=coll["profile"],
+                               path="ssb_collector_submit per job from native threads (bench_tools/collbench.cpp) -> "
+                                    "4,096-job windows -> ssb_threshold_aggregate_batch_cached_dev on %d one-stream "
+                                    "slots; timed first submit -> last result; every job's status, verdicts and "
+                                    "combined signature checked" % S) if coll else None),
             "host_buffers": "every batch's inputs start in, and its results end in, ordinary host memory: "
                             "ssb_threshold_aggregate_batch%s_submit copies them into the slot's pinned device-mapped "
                             "staging buffer, the kernels read / write it in place over PCIe, ssb_batch_wait delivers "

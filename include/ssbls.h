@@ -82,6 +82,9 @@ extern "C" {
                                                  share_off[j+1] < share_off[j] or > n_shares;
                                                  err = {t, share count}.  The host-pointer entry
                                                  points refuse such a batch with SSB_EINVAL. */
+#define SSB_DVF_ENGINE_ERROR 7                /* the job's batch did not complete (HIP error): no
+                                                 output; err[0] = the hipError_t.  Never a reference
+                                                 result -- a lost batch never reads as SSB_DVF_OK. */
 
 /* Maximum threshold t supported per job, and maximum DST length. */
 #define SSB_MAX_T 64
@@ -232,8 +235,72 @@ int ssb_threshold_aggregate_batch_cached_submit(ssb_ctx* ctx, size_t n_jobs, con
                                                 const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
                                                 uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
                                                 uint64_t* out_err, uint8_t* share_verdicts, uint64_t* ticket);
-/* Wait for a submitted batch and deliver its outputs (SSB_OK at once if already delivered). */
+/* Wait for a submitted batch and deliver its outputs (SSB_OK at once if already delivered;
+ * SSB_EHIP if the batch did not complete -- its statuses are then SSB_DVF_ENGINE_ERROR).
+ * LIFETIME: the library keeps the output pointers a _submit call received and writes into them
+ * when the batch is delivered -- inside ssb_batch_wait, or earlier inside any later call that
+ * delivers the slot's pending batch (the next submit to that slot, ssb_set_pipeline_depth,
+ * ssb_set_slot_streams, ssb_pk_cache_set / _add when they wait, ssb_kernel_timing, ssb_destroy).
+ * The caller keeps out_sig96 / out_status / out_err / share_verdicts valid until ssb_batch_wait
+ * on the ticket has returned. */
 int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket);
+
+/* ---- Per-slot collector --------------------------------------------------------
+ * The batched caller in front of ssb_threshold_aggregate_batch_cached_dev that SafeStake's per-duty
+ * tasks use instead of one threshold_aggregate call each (HotstuffOperatorCommittee::sign,
+ * src/validation/impls/hotstuff.rs:141-169; the call at :165-166).  Any number of threads submit
+ * jobs concurrently (lock-free reservation in the open window, the job's bytes copied straight into
+ * the window's pinned, device-mapped buffer); one worker thread closes a window when it holds
+ * max_jobs jobs / max_shares shares, when its first job has waited window_us, or on flush, and
+ * launches it on the next of `in_flight` one-stream pipeline slots with the public keys from the key
+ * table (ssb_pk_cache_add).  Up to `in_flight` windows run on the device while the next one fills;
+ * every job's result is exactly threshold_aggregate's for that job alone (generic_threshold.rs:132-175).
+ * The collector takes the context over (one-stream slots, pipeline depth in_flight): while it
+ * exists, use the context only through ssb_collector_* calls. */
+typedef struct ssb_collector ssb_collector;
+typedef struct ssb_job_result {
+  uint8_t sig96[96];     /* the combined signature (status SSB_DVF_OK) */
+  uint64_t err[2];       /* DvfError fields of the status (ssbls.h status tags) */
+  uint64_t verdicts;     /* bit i: share i's verify result (the first 64 shares) */
+  int32_t status;        /* SSB_DVF_* ; SSB_DVF_ENGINE_ERROR when the job's batch failed (rc) */
+  int32_t rc;            /* SSB_OK, or the negative SSB_E* code of the job's batch */
+  uint32_t n_shares;
+  uint32_t done;         /* 0 while pending; 1 (written last, release) when the fields are final */
+} ssb_job_result;
+/* Called on the collector's worker thread when a job's result is final (after `done` is set); must
+ * not block or call ssb_collector_* functions (e.g. complete a future / send on a channel and
+ * return).  With a callback the result must stay valid until the callback has returned. */
+typedef void (*ssb_job_done_fn)(void* user, const ssb_job_result* result);
+
+/* in_flight: 1..SSB_MAX_SLOT_STREAMS one-stream pipeline slots; up to 2 x in_flight windows are on the
+ * device (one running and one queued per slot, so a slot's stream never idles while the worker
+ * delivers); max_shares: share capacity of a window (>= 64); window_us: how long the first job of a
+ * window waits for company. */
+int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, uint32_t window_us, int in_flight,
+                         ssb_collector** out);
+/* Drains: every submitted job is delivered before it returns.  The context stays usable. */
+void ssb_collector_destroy(ssb_collector* col);
+/* ssb_pk_cache_add through the collector (serialised with its launches). */
+int ssb_collector_register_keys(ssb_collector* col, size_t n, const uint8_t* pk48, uint32_t* out_index);
+/* One threshold_aggregate job: t, n shares (1 <= t <= SSB_MAX_T, n <= 64; the caller has done the
+ * reference's two DifferentLength checks), sig96[n], pk_index[n] (rows of the key table), ids[n],
+ * the 32-byte signing root.  `result` (caller-owned, valid until done) receives the outcome; `cb`
+ * (may be NULL) is then called with `user`.  Thread-safe; blocks only while every window buffer is
+ * busy (back-pressure). */
+int ssb_collector_submit(ssb_collector* col, uint32_t t, uint32_t n, const uint8_t* sig96, const uint32_t* pk_index,
+                         const uint64_t* ids, const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb,
+                         void* user);
+/* Block until result->done (the job must have been submitted to this collector). */
+int ssb_collector_wait(ssb_collector* col, const ssb_job_result* result);
+/* Close the open window now and wait until every job submitted before the call is delivered. */
+int ssb_collector_flush(ssb_collector* col);
+/* Counters since creation: windows launched, jobs and shares delivered. */
+int ssb_collector_stats(ssb_collector* col, uint64_t* windows, uint64_t* jobs, uint64_t* shares);
+/* Worker-thread profile since creation: time closing + launching windows, delivering results, and
+ * waiting for a device window to free up (every window on the device busy), and how many submits
+ * waited for a new window. */
+int ssb_collector_profile(ssb_collector* col, double* seal_ms, double* deliver_ms, double* backpressure_ms,
+                          uint64_t* full_waits);
 
 /* Same, all array arguments are device pointers; `stream` is a hipStream_t (NULL = default).
  * The caller owns the job shapes: share_off must be non-decreasing with share_off[n_jobs] ==
@@ -254,6 +321,13 @@ int ssb_threshold_aggregate_batch_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shar
  * into that table instead of 48 compressed bytes.  A key that does not decode, decodes to
  * infinity, or an index >= n makes the share invalid (verdict 0), as in the compressed path. */
 int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48);
+/* Incremental registration (a committee's operator keys when it is built: DvfSigner::spawn,
+ * src/node/dvfcore.rs:144-235, OperatorCommittee::from_definition, src/validation/operator_committees.rs:13-30):
+ * out_index[i] = the table row of pk48[i].  A key already in the table (from this call, an earlier
+ * add, or a _set) keeps its row; new keys are decoded (and their merged-MSM bases precomputed) into
+ * rows after the existing ones, so indices stay stable and batches already in flight are unaffected.
+ * Synchronous; when the table's capacity doubles it first waits for every in-flight batch. */
+int ssb_pk_cache_add(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint32_t* out_index);
 int ssb_threshold_aggregate_batch_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares,
                                              const uint32_t* share_off, const uint32_t* t,
                                              const uint8_t* sig96, const uint32_t* pk_index,

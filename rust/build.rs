@@ -13,7 +13,7 @@ use std::process::Command;
 // the translation units of libssbls.so (safestakeoperator_amd/build.py SOURCES)
 const SOURCES: &[&str] = &[
     "ssbls.hip", "ssb_k_lane.hip", "ssb_k_verify.hip", "ssb_k_pair.hip", "ssb_k_hash.hip", "ssb_k_combine.hip",
-    "ssb_k_msm.hip", "ssb_k_bisect.hip", "ssb_k_wire.hip", "ssb_k_dkg.hip", "ssb_k_fused.hip",
+    "ssb_k_msm.hip", "ssb_k_bisect.hip", "ssb_k_wire.hip", "ssb_k_dkg.hip", "ssb_k_fused.hip", "ssb_collector.hip",
 ];
 
 fn main() {

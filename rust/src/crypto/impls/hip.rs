@@ -228,7 +228,7 @@ pub fn aggregate_batch(t: usize, jobs: &[ThresholdJob]) -> Vec<Result<Signature,
 
 /// The reference's scan order (generic_threshold.rs:149-169): shares up to the t-th accepted one,
 /// ids already accepted skipped unverified; every verified-and-invalid share is logged.
-fn log_invalid_shares(t: usize, ids: &[u64], verdicts: &[u8]) {
+pub(crate) fn log_invalid_shares(t: usize, ids: &[u64], verdicts: &[u8]) {
     let mut accepted: Vec<u64> = Vec::with_capacity(t);
     for (id, v) in ids.iter().zip(verdicts) {
         if accepted.contains(id) {

@@ -48,6 +48,19 @@ SIGNATURES = {
                                                                    _u64p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),
     "ssb_batch_wait": (ctypes.c_int, [_ctx, ctypes.c_uint64]),
     "ssb_pk_cache_set": (ctypes.c_int, [_ctx, _sz, _u8p]),
+    "ssb_pk_cache_add": (ctypes.c_int, [_ctx, _sz, _u8p, _u32p]),
+    "ssb_collector_create": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "ssb_collector_destroy": (None, [ctypes.c_void_p]),
+    "ssb_collector_register_keys": (ctypes.c_int, [ctypes.c_void_p, _sz, _u8p, _u32p]),
+    "ssb_collector_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_collector_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_collector_flush": (ctypes.c_int, [ctypes.c_void_p]),
+    "ssb_collector_stats": (ctypes.c_int, [ctypes.c_void_p, _u64p, _u64p, _u64p]),
+    "ssb_collector_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _u64p]),
     "ssb_verify_batch_dev": (ctypes.c_int, [_ctx, _sz, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz,
                                             ctypes.c_void_p, _u8p, _sz, ctypes.c_uint64, ctypes.c_void_p,
                                             ctypes.c_void_p]),
@@ -70,6 +83,17 @@ SIGNATURES = {
     "ssb_decode_wire_sigs_dev": (ctypes.c_int, [_ctx, _sz, ctypes.c_void_p, _sz, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_void_p]),
 }
+
+
+class JobResult(ctypes.Structure):
+    """ssb_job_result (include/ssbls.h): one collector job's outcome."""
+    _fields_ = [("sig96", ctypes.c_uint8 * 96), ("err", ctypes.c_uint64 * 2), ("verdicts", ctypes.c_uint64),
+                ("status", ctypes.c_int32), ("rc", ctypes.c_int32), ("n_shares", ctypes.c_uint32),
+                ("done", ctypes.c_uint32)]
+
+
+# ssb_job_done_fn: void (*)(void* user, const ssb_job_result* result)
+JOB_DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(JobResult))
 
 
 def header_symbols():

@@ -20,7 +20,7 @@ VARIANT = os.environ.get("SSB_VARIANT", "")
 LIB = os.path.join(HERE, "libssbls%s.so" % ("_" + VARIANT if VARIANT else ""))
 SOURCES = ["ssbls.hip", "ssb_k_lane.hip", "ssb_k_verify.hip", "ssb_k_pair.hip", "ssb_k_hash.hip",
            "ssb_k_combine.hip", "ssb_k_msm.hip", "ssb_k_bisect.hip", "ssb_k_wire.hip", "ssb_k_dkg.hip",
-           "ssb_k_fused.hip"]
+           "ssb_k_fused.hip", "ssb_collector.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SSB_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]
@@ -157,5 +157,29 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
+COLLBENCH_SRC = os.path.join(HERE, "..", "bench_tools", "collbench.cpp")
+COLLBENCH_LIB = os.path.join(HERE, "..", "bench_tools", "libcollbench.so")
+
+
+def build_collbench(verbose: bool = True) -> str:
+    """bench_tools/libcollbench.so: the native submitter threads of bench.py's value_collector
+    (benchmark / test infrastructure, linked against libssbls.so)."""
+    build(verbose=verbose)
+    want = _hash([COLLBENCH_SRC, os.path.join(HERE, "..", "include", "ssbls.h")], "collbench")
+    stamp = COLLBENCH_LIB + ".srchash"
+    if os.path.exists(COLLBENCH_LIB) and os.path.exists(stamp) and open(stamp).read().strip() == want:
+        return COLLBENCH_LIB
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", COLLBENCH_LIB + ".tmp", COLLBENCH_SRC,
+           "-L" + HERE, "-l:" + os.path.basename(LIB), "-Wl,-rpath,$ORIGIN/../safestakeoperator_amd"]
+    if verbose:
+        print("[ssbls] building:", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(COLLBENCH_LIB + ".tmp", COLLBENCH_LIB)
+    with open(stamp, "w") as f:
+        f.write(want + "\n")
+    return COLLBENCH_LIB
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_collbench()

@@ -8,10 +8,13 @@ Many such tasks run concurrently, one per validator, and every call pays a full 
 share.
 
 `SlotCollector` is the batched caller that replaces those per-task calls: tasks `submit` their
-`ThresholdJob` and get a `concurrent.futures.Future`; one worker thread owns the engine (a context
-must not be used from two threads at once, include/ssbls.h) and flushes the pending jobs as ONE
-`threshold_aggregate_batch` per distinct threshold when either `max_jobs` are pending or the
-oldest pending job has waited `window_s` (the aggregation window), or on `flush()`.  Each future
+`ThresholdJob` and get a `concurrent.futures.Future`.  On an engine it runs on the library's native
+collector (`NativeCollector`, include/ssbls.h "Per-slot collector", csrc/ssb_collector.hip): the
+job's bytes go straight into the open window's pinned buffer, public keys become rows of the
+engine's decoded-key table (registered once, `ssb_pk_cache_add`), and up to `in_flight` windows run
+on the device while the next fills.  A window closes at `max_jobs` jobs, after `window_s`, or on
+`flush()`.  With a `batch_fn` instead (CPU tests), one worker thread runs ONE
+`batch_fn(t, jobs)` per distinct threshold of each window.  Each future
 resolves to exactly what `threshold_aggregate` returns for that job alone: the 96-byte combined
 signature, or the reference's `DvfError` raised from `Future.result()`.  Batching changes nothing
 observable per job: every job's verify-then-combine is independent, and the RLC batch check falls
@@ -19,33 +22,130 @@ back to exact per-share verdicts when any share in the batch is invalid.  The ba
 linear combination is keyed by a secret the library draws per call (include/ssbls.h), so shares
 from different validators' committees cannot be crafted to cancel each other out in one batch.
 """
+import ctypes
+import itertools
 import threading
 import time
 from concurrent.futures import Future
 from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
 
-from .threshold import MAX_T, DvfError, Engine, ThresholdJob, ThresholdSignature, job_shape_error
+import numpy as np
+
+from . import _lib
+from .threshold import (MAX_T, DifferentLength, DvfError, Engine, ThresholdJob, ThresholdSignature, _error_from,
+                        job_shape_error)
+
+MAX_JOB_SHARES = 64   # ssb_collector_submit: shares per job
+
+
+class NativeCollector:
+    """ssb_collector (include/ssbls.h): lock-free submission into pinned windows, one worker thread in
+    the library, `in_flight` windows on the device.  Takes the engine's context over while it lives."""
+
+    def __init__(self, engine: Engine, max_jobs: int = 4096, max_shares: Optional[int] = None, window_s: float = 0.005,
+                 in_flight: int = 20):
+        self.engine = engine
+        self._lib = engine._lib
+        h = ctypes.c_void_p()
+        ms = int(max_shares) if max_shares is not None else max(64, 16 * int(max_jobs))
+        rc = self._lib.ssb_collector_create(engine.handle, int(max_jobs), ms, int(round(window_s * 1e6)),
+                                            int(in_flight), ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError("ssb_collector_create failed (%d): %s" % (rc, self._lib.ssb_last_error(engine.handle)))
+        self._h = h
+        self._rows: Dict[bytes, int] = {}
+        self._rows_lock = threading.Lock()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def rows(self, pks: Sequence[bytes]) -> np.ndarray:
+        """Key-table rows of these public keys, registering the ones not seen before."""
+        with self._rows_lock:
+            new = [p for p in dict.fromkeys(bytes(p) for p in pks) if p not in self._rows]
+            if new:
+                buf = np.frombuffer(b"".join(new), dtype=np.uint8)
+                idx = np.zeros(len(new), dtype=np.uint32)
+                rc = self._lib.ssb_collector_register_keys(self._h, len(new), buf.ctypes.data_as(_lib._u8p),
+                                                           idx.ctypes.data_as(_lib._u32p))
+                if rc != 0:
+                    raise RuntimeError("ssb_collector_register_keys failed (%d)" % rc)
+                self._rows.update(zip(new, idx.tolist()))
+            return np.fromiter((self._rows[bytes(p)] for p in pks), dtype=np.uint32, count=len(pks))
+
+    def submit(self, t: int, sig96: np.ndarray, rows: np.ndarray, ids: np.ndarray, root: bytes, result: "_lib.JobResult",
+               cb=None, user: int = 0) -> None:
+        """One job (arrays already packed: sig96 uint8[n*96], rows uint32[n], ids uint64[n]); `result`
+        and the arrays stay alive until the job is done."""
+        n = len(ids)
+        rc = self._lib.ssb_collector_submit(self._h, int(t), n, sig96.ctypes.data if n else None,
+                                            rows.ctypes.data if n else None, ids.ctypes.data if n else None,
+                                            root, ctypes.addressof(result), cb, ctypes.c_void_p(user))
+        if rc != 0:
+            raise RuntimeError("ssb_collector_submit failed (%d)" % rc)
+
+    def wait(self, result: "_lib.JobResult") -> None:
+        self._lib.ssb_collector_wait(self._h, ctypes.addressof(result))
+
+    def flush(self) -> None:
+        self._lib.ssb_collector_flush(self._h)
+
+    def stats(self) -> Tuple[int, int, int]:
+        w, j, s = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._lib.ssb_collector_stats(self._h, ctypes.byref(w), ctypes.byref(j), ctypes.byref(s))
+        return int(w.value), int(j.value), int(s.value)
+
+    def profile(self) -> dict:
+        """Worker-thread profile: ms closing + launching windows, delivering, waiting on the device;
+        submits that waited for a new window."""
+        a, b, c, w = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        self._lib.ssb_collector_profile(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(w))
+        return dict(seal_ms=round(a.value, 3), deliver_ms=round(b.value, 3), backpressure_ms=round(c.value, 3),
+                    full_waits=int(w.value))
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.ssb_collector_destroy(self._h)   # drains every submitted job
+            self._h = None
+
+
+def result_of(r: "_lib.JobResult") -> Union[bytes, DvfError, Exception]:
+    """The job's threshold_aggregate outcome from its ssb_job_result."""
+    if r.status == 0:
+        return bytes(r.sig96)
+    return _error_from(int(r.status), int(r.err[0]), int(r.err[1]))
 
 BatchFn = Callable[[int, Sequence[ThresholdJob]], List[Union[bytes, DvfError]]]
 
 
 class SlotCollector:
-    """Aggregation window over `threshold_aggregate` calls (one worker thread, one engine)."""
+    """Aggregation window over `threshold_aggregate` calls: the engine's native collector, or (with a
+    `batch_fn`, CPU tests) one Python worker thread calling batch_fn per window and threshold."""
 
     def __init__(self, engine: Optional[Engine] = None, max_jobs: int = 4096, window_s: float = 0.005,
-                 batch_fn: Optional[BatchFn] = None):
+                 batch_fn: Optional[BatchFn] = None, in_flight: int = 20):
         if max_jobs < 1 or window_s < 0:
             raise ValueError("max_jobs >= 1 and window_s >= 0")
         self._engine = engine
         self._max = int(max_jobs)
         self._window = float(window_s)
-        # batch_fn(t, jobs) -> per-job results; default: the engine's batched entry point
-        self._batch_fn = batch_fn or self._engine_batch
+        self._native: Optional[NativeCollector] = None
+        self.batches: List[int] = []          # sizes of the batches submitted (observability)
+        if batch_fn is None:
+            from .threshold import default_engine
+            self._native = NativeCollector(engine or default_engine(), max_jobs=max_jobs, window_s=window_s,
+                                           in_flight=in_flight)
+            self._inflight: Dict[int, Tuple[Future, "_lib.JobResult", tuple]] = {}
+            self._ids = itertools.count(1)
+            self._cb = _lib.JOB_DONE_FN(self._done)   # kept alive as long as the collector
+            self._closed = False
+            return
+        self._batch_fn = batch_fn
         self._cv = threading.Condition()
         self._pending: List[Tuple[int, ThresholdJob, Future, float]] = []
         self._flushing = False                # flush(): drain everything pending without waiting
         self._closed = False
-        self.batches: List[int] = []          # sizes of the batches submitted (observability)
         self._worker = threading.Thread(target=self._run, name="ssb-slot-collector", daemon=True)
         self._worker.start()
 
@@ -64,6 +164,8 @@ class SlotCollector:
             fut.set_running_or_notify_cancel()
             fut.set_exception(ValueError(bad))
             return fut
+        if self._native is not None:
+            return self._submit_native(int(threshold), job, fut)
         with self._cv:
             if self._closed:
                 raise RuntimeError("collector closed")
@@ -79,8 +181,56 @@ class SlotCollector:
         """Blocking form with the reference's signature and error behaviour."""
         return self.submit(threshold, ThresholdJob(sigs, pks, ids, msg)).result(timeout)
 
+    # -- native path --
+    def _submit_native(self, t: int, job: ThresholdJob, fut: Future) -> Future:
+        # the reference's two length checks (generic_threshold.rs:133-138), before the engine
+        if len(job.sigs) != len(job.pks):
+            return self._fail(fut, DifferentLength(len(job.sigs), len(job.pks)))
+        if len(job.sigs) != len(job.ids):
+            return self._fail(fut, DifferentLength(len(job.sigs), len(job.ids)))
+        if len(job.sigs) > MAX_JOB_SHARES:
+            return self._fail(fut, ValueError("more than %d shares in one job" % MAX_JOB_SHARES))
+        if self._closed:
+            raise RuntimeError("collector closed")
+        n = len(job.sigs)
+        sig = np.frombuffer(b"".join(bytes(s) for s in job.sigs), dtype=np.uint8) if n else np.zeros(1, np.uint8)
+        rows = self._native.rows(job.pks) if n else np.zeros(1, np.uint32)
+        ids = np.asarray([int(i) for i in job.ids], dtype=np.uint64) if n else np.zeros(1, np.uint64)
+        if not n:
+            ids = ids[:0]
+        root = bytes(job.msg)
+        res = _lib.JobResult()
+        key = next(self._ids)
+        self._inflight[key] = (fut, res, (sig, rows, ids, root))   # alive until delivered
+        try:
+            self._native.submit(t, sig, rows, ids, root, res, self._cb, key)
+        except BaseException:
+            self._inflight.pop(key, None)
+            raise
+        return fut
+
+    @staticmethod
+    def _fail(fut: Future, e: Exception) -> Future:
+        fut.set_running_or_notify_cancel()
+        fut.set_exception(e)
+        return fut
+
+    def _done(self, user, res_p) -> None:
+        """ssb_job_done_fn, on the library's worker thread."""
+        fut, res, _ = self._inflight.pop(int(user or 0))
+        if not fut.set_running_or_notify_cancel():
+            return
+        r = result_of(res)
+        if isinstance(r, Exception):
+            fut.set_exception(r)
+        else:
+            fut.set_result(r)
+
     def flush(self) -> None:
         """Submit everything pending now and wait until it has been processed."""
+        if self._native is not None:
+            self._native.flush()
+            return
         with self._cv:
             futs = [p[2] for p in self._pending]
             if futs:
@@ -90,6 +240,13 @@ class SlotCollector:
             f.exception()                     # waits; results stay on the futures
 
     def close(self) -> None:
+        if self._native is not None:
+            if not self._closed:
+                self._closed = True
+                self._native.flush()
+                self.native_stats = self._native.stats()   # (windows, jobs, shares)
+                self._native.close()
+            return
         with self._cv:
             self._closed = True
             self._cv.notify()
@@ -147,3 +304,35 @@ class SlotCollector:
                         f.set_exception(r)
                     else:
                         f.set_result(r)
+
+
+# numpy view of ssb_job_result (include/ssbls.h), for arrays of results filled by native code
+JOB_RESULT_DTYPE = np.dtype([("sig96", np.uint8, 96), ("err", "<u8", 2), ("verdicts", "<u8"), ("status", "<i4"),
+                             ("rc", "<i4"), ("n_shares", "<u4"), ("done", "<u4")], align=True)
+assert JOB_RESULT_DTYPE.itemsize == ctypes.sizeof(_lib.JobResult)
+
+
+def collbench_run(col: NativeCollector, wl: dict, V: int, n: int, t: int, rows: np.ndarray, n_jobs: int,
+                  threads: int = 8) -> Tuple[float, np.ndarray]:
+    """bench_tools/libcollbench.so: `threads` native submitters push n_jobs jobs (job k = validator
+    k % V of the workload) through the collector; (seconds first submit -> last result, results)."""
+    import os
+    from .build import build_collbench
+    lib = ctypes.CDLL(build_collbench(verbose=False))
+    fn = lib.ssb_collbench_run
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.POINTER(ctypes.c_double)]
+    sig = np.frombuffer(wl["sigs"], dtype=np.uint8)
+    ids = np.asarray(wl["ids"], dtype=np.uint64)
+    roots = np.frombuffer(b"".join(wl["roots"]), dtype=np.uint8)
+    jr = np.asarray(wl["job_root"], dtype=np.uint32)
+    rows = np.ascontiguousarray(rows, dtype=np.uint32)
+    res = np.zeros(n_jobs, dtype=JOB_RESULT_DTYPE)
+    sec = ctypes.c_double()
+    rc = fn(col.handle, int(threads), int(n_jobs), V, n, t, sig.ctypes.data, rows.ctypes.data, ids.ctypes.data,
+            roots.ctypes.data, jr.ctypes.data, res.ctypes.data, ctypes.byref(sec))
+    if rc != 0:
+        raise RuntimeError("ssb_collbench_run failed (%d)" % rc)
+    return float(sec.value), res

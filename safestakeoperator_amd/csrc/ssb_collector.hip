@@ -1,0 +1,429 @@
+// ssb_collector.hip -- the per-slot collector: the native batched caller in front
+// of ssb_threshold_aggregate_batch_cached_dev (include/ssbls.h, "Per-slot collector").
+//
+// Reference call site: every committee's duty ends with ONE
+// ThresholdSignature::new(t).threshold_aggregate(sigs, pks, ids, msg) (HotstuffOperatorCommittee::sign,
+// src/validation/impls/hotstuff.rs:141-169, the call at :165-166), thousands of them per slot, each a
+// handful of shares.  Here those calls become ssb_collector_submit: the job's bytes go straight into
+// the open window's pinned, device-mapped buffer, and the window runs as one engine batch.
+//
+// Concurrency.  Submitters reserve (job, share range) in the open window with ONE atomic fetch_add on
+// a packed word (bit 63 closed | jobs << 32 | shares): jobs and shares are handed out in order, so
+// the jobs that fit form a prefix and their share ranges are contiguous (share_off is written by the
+// submitters themselves).  A reservation past the capacity asks the worker to close the window and
+// retries in the next one.  The worker closes a window with fetch_or(closed): the reservations made
+// before it are exactly `jobs` of the returned word; it waits until all of them have settled
+// (copied, or given up as overflow), deduplicates the signing roots (hash_to_G2 runs once per
+// distinct root), and launches the window on the next one-stream pipeline slot.  Up to `in_flight`
+// windows run on the device while the next fills; a window's buffer is reused only after its event
+// completes, and results are delivered in launch order.
+#include <hip/hip_runtime.h>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/ssbls.h"
+
+namespace ssb { int ctx_device(const ssb_ctx* ctx); }
+
+namespace {
+
+constexpr uint64_t CLOSED = 1ull << 63;
+constexpr uint32_t MAX_JOB_SHARES = 64;
+inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+struct window {
+  uint8_t* h = nullptr;   // pinned host buffer (inputs, then the engine's outputs)
+  uint8_t* d = nullptr;   // its device address
+  size_t i_sig = 0, i_pk = 0, i_ids = 0, i_off = 0, i_t = 0, i_jr = 0, i_roots = 0, o_sig = 0, o_st = 0, o_err = 0, o_ver = 0;
+  std::atomic<uint64_t> resv{0};
+  std::atomic<uint32_t> settled{0};
+  std::atomic<uint32_t> committed{0};
+  std::atomic<int64_t> t_first{0};
+  std::vector<ssb_job_result*> res;
+  std::vector<ssb_job_done_fn> cb;
+  std::vector<void*> user;
+  std::vector<uint8_t> root_in;   // per job, the 32-byte root as submitted
+  hipEvent_t ev = nullptr;
+  uint64_t seq = 0;
+  uint32_t nj = 0, ns = 0;
+  int rc = SSB_OK;
+  uint32_t* off() { return (uint32_t*)(h + i_off); }
+};
+
+}  // namespace
+
+struct ssb_collector {
+  ssb_ctx* ctx = nullptr;
+  int device = 0;
+  uint32_t J = 0, N = 0, in_flight = 1;
+  int64_t window_ns = 0;
+  std::vector<window*> all;
+  std::atomic<window*> open{nullptr};
+  std::deque<window*> inflight, freel;
+  std::mutex mu;                   // worker state, the queues, the condition variables
+  std::condition_variable cv_worker, cv_submit, cv_done;
+  std::mutex ctx_mu;               // the engine context: launches and key registration
+  uint64_t seal_upto = 0;          // a submitter found window seq <= this full: close it
+  uint32_t max_windows = 1;        // windows on the device: two per slot (one running, one queued)
+  std::atomic<bool> stopping{false};
+  uint64_t seq_next = 1, flush_upto = 0, delivered_seq = 0;
+  uint32_t slot_rr = 0;
+  std::atomic<uint64_t> n_windows{0}, n_jobs{0}, n_shares{0};
+  // profile (worker thread): ns spent closing + launching windows, delivering results, waiting for a
+  // device window to free up; submitter waits for a new window
+  std::atomic<uint64_t> ns_seal{0}, ns_deliver{0}, ns_backpressure{0}, n_full_waits{0};
+  std::thread worker;
+  std::vector<uint32_t> rtab;      // worker-only: root dedup table (index + 1)
+
+  void reset(window* w) {
+    w->resv.store(0, std::memory_order_relaxed);
+    w->settled.store(0, std::memory_order_relaxed);
+    w->committed.store(0, std::memory_order_relaxed);
+    w->t_first.store(0, std::memory_order_relaxed);
+    w->off()[0] = 0;
+    w->nj = w->ns = 0;
+    w->rc = SSB_OK;
+    w->seq = seq_next++;
+  }
+  void seal(window* w);
+  void deliver(window* w);
+  void run();
+};
+
+namespace {
+
+void wait_new_window(ssb_collector* c, window* w) {
+  c->n_full_waits.fetch_add(1, std::memory_order_relaxed);
+  std::unique_lock<std::mutex> lk(c->mu);
+  c->cv_submit.wait(lk, [&] { return c->open.load(std::memory_order_acquire) != w || c->stopping; });
+}
+
+}  // namespace
+
+// close-time work on the worker thread: distinct roots, the job -> root map, then the launch
+void ssb_collector::seal(window* w) {
+  const uint32_t nj = w->committed.load(std::memory_order_acquire);
+  w->nj = nj;
+  w->ns = nj ? w->off()[nj] : 0;
+  uint32_t* jr = (uint32_t*)(w->h + w->i_jr);
+  uint8_t* roots = w->h + w->i_roots;
+  const uint32_t mask = (uint32_t)rtab.size() - 1;
+  std::fill(rtab.begin(), rtab.end(), 0u);
+  uint32_t nr = 0;
+  for (uint32_t j = 0; j < nj; ++j) {
+    const uint8_t* r = w->root_in.data() + 32 * (size_t)j;
+    uint64_t k;
+    memcpy(&k, r, 8);
+    uint32_t hsh = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+    for (;;) {
+      const uint32_t e = rtab[hsh];
+      if (!e) {
+        memcpy(roots + 32 * (size_t)nr, r, 32);
+        rtab[hsh] = ++nr;
+        jr[j] = nr - 1;
+        break;
+      }
+      if (!memcmp(roots + 32 * (size_t)(e - 1), r, 32)) { jr[j] = e - 1; break; }
+      hsh = (hsh + 1) & mask;
+    }
+  }
+  static const uint8_t dst[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";   // src/crypto/impls/blst.rs:11
+  std::lock_guard<std::mutex> g(ctx_mu);
+  const int k = (int)(slot_rr++ % in_flight);
+  void* st = ssb_slot_stream(ctx, k);
+  uint8_t* d = w->d;
+  w->rc = ssb_threshold_aggregate_batch_cached_dev(
+      ctx, nj, w->ns, (const uint32_t*)(d + w->i_off), (const uint32_t*)(d + w->i_t), d + w->i_sig,
+      (const uint32_t*)(d + w->i_pk), (const uint64_t*)(d + w->i_ids), (const uint32_t*)(d + w->i_jr), nr, d + w->i_roots,
+      dst, sizeof(dst) - 1, 0, d + w->o_sig, (int32_t*)(d + w->o_st), (uint64_t*)(d + w->o_err), d + w->o_ver, st);
+  if (w->rc == SSB_OK && hipEventRecord(w->ev, (hipStream_t)st) != hipSuccess) w->rc = SSB_EHIP;
+  n_windows.fetch_add(1, std::memory_order_relaxed);
+}
+
+void ssb_collector::deliver(window* w) {
+  const int32_t* st = (const int32_t*)(w->h + w->o_st);
+  const uint64_t* er = (const uint64_t*)(w->h + w->o_err);
+  const uint8_t* sg = w->h + w->o_sig;
+  const uint8_t* vr = w->h + w->o_ver;
+  const uint32_t* off = w->off();
+  for (uint32_t j = 0; j < w->nj; ++j) {
+    ssb_job_result* r = w->res[j];
+    const uint32_t b = off[j], n = off[j + 1] - off[j];
+    r->n_shares = n;
+    r->rc = w->rc;
+    if (w->rc == SSB_OK) {
+      memcpy(r->sig96, sg + 96 * (size_t)j, 96);
+      r->status = st[j];
+      r->err[0] = er[2 * (size_t)j];
+      r->err[1] = er[2 * (size_t)j + 1];
+      uint64_t bits = 0;
+      for (uint32_t i = 0; i < n && i < 64; ++i) bits |= (uint64_t)(vr[b + i] != 0) << i;
+      r->verdicts = bits;
+    } else {
+      memset(r->sig96, 0, 96);
+      r->status = SSB_DVF_ENGINE_ERROR;
+      r->err[0] = (uint64_t)(int64_t)w->rc;
+      r->err[1] = 0;
+      r->verdicts = 0;
+    }
+    __atomic_store_n(&r->done, 1u, __ATOMIC_RELEASE);
+    if (w->cb[j]) w->cb[j](w->user[j], r);
+  }
+  n_jobs.fetch_add(w->nj, std::memory_order_relaxed);
+  n_shares.fetch_add(w->ns, std::memory_order_relaxed);
+}
+
+void ssb_collector::run() {
+  hipSetDevice(device);
+  std::unique_lock<std::mutex> lk(mu);
+  for (;;) {
+    // deliver finished windows, in launch order
+    bool delivered = false;
+    while (!inflight.empty()) {
+      window* f = inflight.front();
+      if (f->rc == SSB_OK) {
+        const hipError_t q = hipEventQuery(f->ev);
+        if (q == hipErrorNotReady) break;
+        if (q != hipSuccess) f->rc = SSB_EHIP;
+      }
+      inflight.pop_front();
+      lk.unlock();
+      const int64_t d0 = now_ns();
+      deliver(f);
+      ns_deliver.fetch_add((uint64_t)(now_ns() - d0), std::memory_order_relaxed);
+      lk.lock();
+      delivered_seq = f->seq;
+      freel.push_back(f);
+      delivered = true;
+    }
+    if (delivered) cv_done.notify_all();
+    window* w = open.load(std::memory_order_relaxed);
+    const uint64_t r = w->resv.load(std::memory_order_acquire);
+    const uint32_t nres = (uint32_t)(r >> 32) & 0x7fffffffu;
+    const int64_t t0 = w->t_first.load(std::memory_order_relaxed);
+    const int64_t now = now_ns();
+    const bool due = nres > 0 && (seal_upto >= w->seq || stopping || flush_upto >= w->seq || nres >= J ||
+                                  (t0 && now - t0 >= window_ns));
+    if (due) {
+      if (inflight.size() >= max_windows || freel.empty()) {   // every device window busy: wait for the oldest
+        window* f = inflight.front();
+        lk.unlock();
+        const int64_t b0 = now_ns();
+        if (f->rc == SSB_OK && hipEventSynchronize(f->ev) != hipSuccess) f->rc = SSB_EHIP;
+        ns_backpressure.fetch_add((uint64_t)(now_ns() - b0), std::memory_order_relaxed);
+        lk.lock();
+        continue;
+      }
+      window* nw = freel.front();
+      freel.pop_front();
+      reset(nw);
+      open.store(nw, std::memory_order_release);
+      cv_submit.notify_all();
+      lk.unlock();
+      const int64_t s0 = now_ns();
+      const uint32_t pre = (uint32_t)(w->resv.fetch_or(CLOSED, std::memory_order_acq_rel) >> 32) & 0x7fffffffu;
+      while (w->settled.load(std::memory_order_acquire) < pre) cpu_relax();   // submitters mid-copy
+      seal(w);
+      ns_seal.fetch_add((uint64_t)(now_ns() - s0), std::memory_order_relaxed);
+      lk.lock();
+      inflight.push_back(w);
+      continue;
+    }
+    if (stopping && nres == 0 && inflight.empty()) break;
+    // sleep until the window is due, a submitter fills it, or (with windows on the device) 20 us
+    int64_t wait = inflight.empty() ? (int64_t)1000000000 : (int64_t)20000;
+    if (nres > 0 && t0) wait = std::min<int64_t>(wait, std::max<int64_t>(0, t0 + window_ns - now));
+    else if (nres > 0) wait = std::min<int64_t>(wait, 20000);
+    if (wait > 0) cv_worker.wait_for(lk, std::chrono::nanoseconds(wait));
+  }
+  cv_done.notify_all();
+}
+
+namespace {
+void free_windows(ssb_collector* c) {
+  for (window* w : c->all) {
+    if (w->ev) hipEventDestroy(w->ev);
+    if (w->h) hipHostFree(w->h);
+    delete w;
+  }
+  c->all.clear();
+}
+// wake the worker about a change of a window's reservation word (which it reads outside `mu`):
+// taking `mu` first means the worker is either before its check or already waiting (no lost wakeup)
+void poke_worker(ssb_collector* c, const window* full) {
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    // per window: a late overflow on an already closed window must not close its successor
+    if (full && full->seq > c->seal_upto) c->seal_upto = full->seq;
+  }
+  c->cv_worker.notify_one();
+}
+}  // namespace
+
+extern "C" {
+
+int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, uint32_t window_us, int in_flight,
+                         ssb_collector** out) {
+  if (!out) return SSB_EINVAL;
+  *out = nullptr;
+  if (!ctx || max_jobs == 0 || max_jobs > (1u << 24) || max_shares < MAX_JOB_SHARES || max_shares > (1u << 28) ||
+      in_flight < 1 || ssb_check_pipeline_config(in_flight, 1) != SSB_OK)
+    return SSB_EINVAL;
+  int rc;
+  if ((rc = ssb_set_slot_streams(ctx, 1)) || (rc = ssb_set_pipeline_depth(ctx, in_flight))) return rc;
+  ssb_collector* c = new (std::nothrow) ssb_collector();
+  if (!c) return SSB_ENOMEM;
+  c->ctx = ctx;
+  c->device = ssb::ctx_device(ctx);
+  c->J = max_jobs;
+  c->N = max_shares;
+  c->in_flight = (uint32_t)in_flight;
+  c->max_windows = 2u * (uint32_t)in_flight;
+  c->window_ns = (int64_t)window_us * 1000;
+  uint32_t rt = 1;
+  while (rt < 2 * max_jobs) rt <<= 1;
+  c->rtab.assign(rt, 0u);
+  if (hipSetDevice(c->device) != hipSuccess) { delete c; return SSB_EHIP; }
+  const size_t J = max_jobs, N = max_shares;
+  for (int i = 0; i < 2 * in_flight + 2; ++i) {
+    window* w = new (std::nothrow) window();
+    if (!w) { free_windows(c); delete c; return SSB_ENOMEM; }
+    c->all.push_back(w);
+    size_t o = 0;
+    auto at = [&](size_t bytes) { const size_t r = o; o += al(bytes); return r; };
+    w->i_sig = at(N * 96); w->i_pk = at(N * 4); w->i_ids = at(N * 8); w->i_off = at((J + 1) * 4); w->i_t = at(J * 4);
+    w->i_jr = at(J * 4); w->i_roots = at(J * 32); w->o_sig = at(J * 96); w->o_st = at(J * 4); w->o_err = at(J * 16);
+    w->o_ver = at(N);
+    if (hipHostMalloc((void**)&w->h, o, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&w->d, w->h, 0) != hipSuccess ||
+        hipEventCreateWithFlags(&w->ev, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      if (w->h) { hipHostFree(w->h); w->h = nullptr; }
+      free_windows(c);
+      delete c;
+      return SSB_ENOMEM;
+    }
+    w->res.assign(J, nullptr);
+    w->cb.assign(J, nullptr);
+    w->user.assign(J, nullptr);
+    w->root_in.assign(J * 32, 0);
+    c->freel.push_back(w);
+  }
+  window* w0 = c->freel.front();
+  c->freel.pop_front();
+  c->reset(w0);
+  c->open.store(w0);
+  c->worker = std::thread([c] { c->run(); });
+  *out = c;
+  return SSB_OK;
+}
+
+void ssb_collector_destroy(ssb_collector* c) {
+  if (!c) return;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->stopping.store(true);
+  }
+  c->cv_worker.notify_all();
+  c->cv_submit.notify_all();
+  if (c->worker.joinable()) c->worker.join();
+  free_windows(c);
+  delete c;
+}
+
+int ssb_collector_register_keys(ssb_collector* c, size_t n, const uint8_t* pk48, uint32_t* out_index) {
+  if (!c) return SSB_EINVAL;
+  std::lock_guard<std::mutex> g(c->ctx_mu);
+  return ssb_pk_cache_add(c->ctx, n, pk48, out_index);
+}
+
+int ssb_collector_submit(ssb_collector* c, uint32_t t, uint32_t n, const uint8_t* sig96, const uint32_t* pk_index,
+                         const uint64_t* ids, const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb,
+                         void* user) {
+  if (!c || !result || !root32 || t == 0 || t > SSB_MAX_T || n > MAX_JOB_SHARES || (n && (!sig96 || !pk_index || !ids)))
+    return SSB_EINVAL;
+  __atomic_store_n(&result->done, 0u, __ATOMIC_RELAXED);
+  for (;;) {
+    if (c->stopping.load(std::memory_order_acquire)) return SSB_EINVAL;   // (a submit must not race destroy)
+    window* w = c->open.load(std::memory_order_acquire);
+    const uint64_t old = w->resv.fetch_add((1ull << 32) | n, std::memory_order_acq_rel);
+    if (old & CLOSED) {   // the worker closed this window after we loaded it: retry in the next one
+      if (c->stopping) return SSB_EINVAL;
+      wait_new_window(c, w);
+      continue;
+    }
+    const uint32_t j = (uint32_t)(old >> 32) & 0x7fffffffu, s = (uint32_t)old;
+    if (j >= c->J || (uint64_t)s + n > c->N) {   // full: have it closed, retry in the next window
+      w->settled.fetch_add(1, std::memory_order_release);
+      poke_worker(c, w);
+      if (c->stopping) return SSB_EINVAL;
+      wait_new_window(c, w);
+      continue;
+    }
+    if (j == 0) w->t_first.store(now_ns(), std::memory_order_relaxed);
+    uint8_t* h = w->h;
+    memcpy(h + w->i_sig + 96 * (size_t)s, sig96, 96 * (size_t)n);
+    memcpy(h + w->i_pk + 4 * (size_t)s, pk_index, 4 * (size_t)n);
+    memcpy(h + w->i_ids + 8 * (size_t)s, ids, 8 * (size_t)n);
+    w->off()[j + 1] = s + n;
+    ((uint32_t*)(h + w->i_t))[j] = t;
+    memcpy(w->root_in.data() + 32 * (size_t)j, root32, 32);
+    w->res[j] = result;
+    w->cb[j] = cb;
+    w->user[j] = user;
+    w->committed.fetch_add(1, std::memory_order_release);
+    w->settled.fetch_add(1, std::memory_order_release);
+    if (j == 0 || j + 1 == c->J) poke_worker(c, nullptr);   // a window starts (its timer) / is full
+    return SSB_OK;
+  }
+}
+
+int ssb_collector_wait(ssb_collector* c, const ssb_job_result* r) {
+  if (!c || !r) return SSB_EINVAL;
+  if (__atomic_load_n(&r->done, __ATOMIC_ACQUIRE)) return SSB_OK;
+  std::unique_lock<std::mutex> lk(c->mu);
+  c->cv_done.wait(lk, [&] { return __atomic_load_n(&r->done, __ATOMIC_ACQUIRE) != 0; });
+  return SSB_OK;
+}
+
+int ssb_collector_flush(ssb_collector* c) {
+  if (!c) return SSB_EINVAL;
+  std::unique_lock<std::mutex> lk(c->mu);
+  window* w = c->open.load(std::memory_order_acquire);
+  const bool empty = ((w->resv.load(std::memory_order_acquire) >> 32) & 0x7fffffffu) == 0;
+  const uint64_t target = empty ? w->seq - 1 : w->seq;
+  if (target > c->flush_upto) c->flush_upto = target;
+  c->cv_worker.notify_one();
+  c->cv_done.wait(lk, [&] { return c->delivered_seq >= target; });
+  return SSB_OK;
+}
+
+int ssb_collector_profile(ssb_collector* c, double* seal_ms, double* deliver_ms, double* backpressure_ms,
+                          uint64_t* full_waits) {
+  if (!c) return SSB_EINVAL;
+  if (seal_ms) *seal_ms = c->ns_seal.load() * 1e-6;
+  if (deliver_ms) *deliver_ms = c->ns_deliver.load() * 1e-6;
+  if (backpressure_ms) *backpressure_ms = c->ns_backpressure.load() * 1e-6;
+  if (full_waits) *full_waits = c->n_full_waits.load();
+  return SSB_OK;
+}
+
+int ssb_collector_stats(ssb_collector* c, uint64_t* windows, uint64_t* jobs, uint64_t* shares) {
+  if (!c) return SSB_EINVAL;
+  if (windows) *windows = c->n_windows.load();
+  if (jobs) *jobs = c->n_jobs.load();
+  if (shares) *shares = c->n_shares.load();
+  return SSB_OK;
+}
+
+}  // extern "C"

@@ -23,6 +23,8 @@
 #include <string>
 #include <vector>
 #include <map>
+#include <set>
+#include <unordered_map>
 #include <mutex>
 #include <algorithm>
 #include <cmath>
@@ -98,13 +100,20 @@ struct ssb_ctx {
   // (the kernels with the largest private segments stay off the slots' queues).  One-stream slots
   // run every stage on the slot's own stream and leave both idle.
   hipStream_t spec = nullptr, tail = nullptr;
-  // decoded public keys (ssb_pk_cache_set): affine points + DEC_* flags, indexed by the caller
-  g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0;
-  g1_aff* pkc_pow = nullptr;   // [pkc_n][PKPOW_W] precomputed bases [2^(4 w)] pk (nullptr: allocation failed)
+  // decoded public keys (ssb_pk_cache_set / ssb_pk_cache_add): affine points + DEC_* flags, indexed
+  // by the caller; rows [0, pkc_n) are live, the arrays hold pkc_cap rows
+  g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0, pkc_cap = 0;
+  g1_aff* pkc_pow = nullptr;   // [pkc_cap][PKPOW_W] precomputed bases [2^(4 w)] pk (nullptr: allocation failed)
+  // ssb_pk_cache_add: compressed key -> its row (first occurrence), built lazily after a _set
+  std::unordered_map<std::string, uint32_t> pkc_map;
+  bool pkc_map_valid = true;
+  std::vector<uint8_t> pkc_set_keys;   // the keys of the last _set while pkc_map is not built
+  uint8_t* pkc_stage = nullptr; size_t pkc_stage_bytes = 0;   // device staging of the keys being added
   // RLC key of each batch: fresh from getrandom() per call (default), or expanded from the caller's
   // seed (ssb_set_rlc_deterministic: reproducible runs / tests only)
   bool rlc_deterministic = false;
   uint64_t ticket_gen = 0;          // host-buffer batch tickets: (generation << 8) | slot
+  std::set<uint64_t> failed_tickets;   // host batches whose completion failed (ssb_batch_wait -> SSB_EHIP)
 };
 
 namespace {
@@ -190,27 +199,38 @@ int init_slot(ssb_slot& S, int streams) {
   if (!S.shared) for (hipStream_t sd : S.side) if (launch::prime_queue(sd)) return SSB_EHIP;
   return SSB_OK;
 }
-// the pending host-buffer batch of the slot: wait for it, copy its outputs to the caller's pointers
-hipError_t deliver_host(ssb_slot& S) {
+// the pending host-buffer batch of the slot: wait for it, copy its outputs to the caller's pointers.
+// If the wait fails the batch is lost: every job's status becomes SSB_DVF_ENGINE_ERROR (a lost batch
+// never reads as SSB_DVF_OK in zero-filled outputs) and the ticket is remembered, so ssb_batch_wait
+// on it returns SSB_EHIP whichever call delivered it.
+hipError_t deliver_host(ssb_ctx* ctx, ssb_slot& S) {
   if (!S.host_ticket) return hipSuccess;
-  S.host_ticket = 0;
   const hipError_t e = hipEventSynchronize(S.ev_host);
-  if (e != hipSuccess) return e;
   const auto& h = S.ho;
+  const uint64_t ticket = S.host_ticket;
+  S.host_ticket = 0;
+  if (e != hipSuccess) {
+    for (size_t j = 0; j < h.nj; ++j) { h.st[j] = SSB_DVF_ENGINE_ERROR; h.err[2 * j] = (uint64_t)(int64_t)e; h.err[2 * j + 1] = 0; }
+    memset(h.sig, 0, h.nj * 96);
+    if (h.ver && h.n) memset(h.ver, 0, h.n);
+    ctx->failed_tickets.insert(ticket);
+    ctx->err = std::string("batch completion failed: ") + hipGetErrorString(e);
+    return e;
+  }
   memcpy(h.sig, S.hst + h.o_sig, h.nj * 96);
   memcpy(h.st, S.hst + h.o_st, h.nj * 4);
   memcpy(h.err, S.hst + h.o_err, h.nj * 16);
   if (h.ver && h.n) memcpy(h.ver, S.hst + h.o_ver, h.n);
   return hipSuccess;
 }
-void sync_slot(ssb_slot& S) {
-  deliver_host(S);
+void sync_slot(ssb_ctx* ctx, ssb_slot& S) {
+  deliver_host(ctx, S);
   if (S.stream) hipStreamSynchronize(S.stream);
   if (!S.shared) for (hipStream_t sd : S.side) if (sd) hipStreamSynchronize(sd);
   if (S.out_pending) hipEventSynchronize(S.ev_out);
 }
-void free_slot(ssb_slot& S) {
-  deliver_host(S);
+void free_slot(ssb_ctx* ctx, ssb_slot& S) {
+  deliver_host(ctx, S);
   if (S.ws) hipFree(S.ws);
   if (S.hst) hipHostFree(S.hst);
   if (!S.shared) for (hipStream_t sd : S.side) if (sd) hipStreamDestroy(sd);
@@ -615,6 +635,10 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
 
 }  // namespace
 
+namespace ssb {
+int ctx_device(const ssb_ctx* ctx) { return ctx->device; }   // (ssb_collector.hip)
+}
+
 extern "C" {
 
 int ssb_create(ssb_ctx** out, int device_ordinal) {
@@ -629,14 +653,14 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   ctx->device = device_ordinal;
   if (init_slot(ctx->sl[0], ctx->slot_streams) != SSB_OK) { delete ctx; return SSB_EHIP; }
   if (hipStreamCreateWithFlags(&ctx->spec, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx->sl[0]); delete ctx; return SSB_EHIP; }
+      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
     for (int i = 0; i < 64; ++i) { jac_to_aff(h[i], p); jac_dbl(p, p); }
     if (hipMalloc(&ctx->negg1_pow, sizeof(h)) != hipSuccess ||
         hipMemcpy(ctx->negg1_pow, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
-      free_slot(ctx->sl[0]); delete ctx; return SSB_EHIP;
+      free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP;
     }
   }
   *out = ctx;
@@ -646,7 +670,7 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
 void ssb_destroy(ssb_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
-  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
+  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx, ctx->sl[i]);
   for (auto& kv : ctx->timers) { if (kv.second.a) hipEventDestroy(kv.second.a); if (kv.second.b) hipEventDestroy(kv.second.b); }
   for (auto& kv : ctx->history) for (auto& p : kv.second) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   for (auto& p : ctx->pool) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
@@ -655,8 +679,9 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->pkc_aff) hipFree(ctx->pkc_aff);
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
   if (ctx->pkc_pow) hipFree(ctx->pkc_pow);
+  if (ctx->pkc_stage) hipFree(ctx->pkc_stage);
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
-  for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx->sl[i]);
+  for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx, ctx->sl[i]);
   delete ctx;
 }
 
@@ -680,9 +705,11 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
     if (init_slot(ctx->sl[i], ctx->slot_streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
     ctx->nslots = i + 1;
   }
-  for (int i = depth; i < ctx->nslots; ++i) { sync_slot(ctx->sl[i]); free_slot(ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
+  for (int i = depth; i < ctx->nslots; ++i) { sync_slot(ctx, ctx->sl[i]); free_slot(ctx, ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
   ctx->nslots = depth;
   ctx->next = 0;
+  // the synchronous entry points run on ctx->cur: never leave it on a removed (reset) slot
+  ctx->cur = &ctx->sl[0];
   return SSB_OK;
 }
 
@@ -694,7 +721,7 @@ int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
   }
   if (streams == ctx->slot_streams) return SSB_OK;
   SSB_HIP(hipSetDevice(ctx->device));
-  for (int i = 0; i < ctx->nslots; ++i) { sync_slot(ctx->sl[i]); free_slot(ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
+  for (int i = 0; i < ctx->nslots; ++i) { sync_slot(ctx, ctx->sl[i]); free_slot(ctx, ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
   ctx->slot_streams = streams;
   for (int i = 0; i < ctx->nslots; ++i)
     if (init_slot(ctx->sl[i], streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
@@ -734,7 +761,7 @@ int ssb_last_kernel_ms(const ssb_ctx* ctx_c, const char* name, float* ms) {
 
 int ssb_kernel_timing(ssb_ctx* ctx, int on) {
   if (!ctx) return SSB_EINVAL;
-  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
+  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx, ctx->sl[i]);
   for (auto& kv : ctx->history) for (auto& p : kv.second) ctx->pool.push_back(p);
   ctx->history.clear();
   ctx->accumulate = on == 1;
@@ -1067,37 +1094,134 @@ int ssb_verify_batch_cached_dev(ssb_ctx* ctx, size_t n, const uint32_t* pk_index
   return verify_dev(ctx, n, nullptr, pk_index, sig96, root_idx, n_roots, roots32, dst, dst_len, rlc_seed, verdicts, stream);
 }
 
-int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
-  if (!ctx) return SSB_EINVAL;
-  if (n && !pk48) { ctx->err = "null pk48"; return SSB_EINVAL; }
-  SSB_HIP(hipSetDevice(ctx->device));
-  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx->sl[i]);
-  for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) SSB_HIP(hipStreamSynchronize(x));
+}  // extern "C"
+namespace {
+void pkc_free(ssb_ctx* ctx) {
   if (ctx->pkc_aff) { hipFree(ctx->pkc_aff); ctx->pkc_aff = nullptr; }
   if (ctx->pkc_flags) { hipFree(ctx->pkc_flags); ctx->pkc_flags = nullptr; }
   if (ctx->pkc_pow) { hipFree(ctx->pkc_pow); ctx->pkc_pow = nullptr; }
-  ctx->pkc_n = 0;
-  if (!n) return SSB_OK;
-  uint8_t* d_in = nullptr;
-  if (hipMalloc(&ctx->pkc_aff, n * sizeof(g1_aff)) != hipSuccess || hipMalloc(&ctx->pkc_flags, n * 4) != hipSuccess ||
-      hipMalloc(&d_in, n * 48) != hipSuccess) {
+  ctx->pkc_n = ctx->pkc_cap = 0;
+}
+// every slot and context stream idle: in-flight batches read the table through the pointers they
+// were launched with
+int pkc_quiesce(ssb_ctx* ctx) {
+  for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx, ctx->sl[i]);
+  for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) SSB_HIP(hipStreamSynchronize(x));
+  return SSB_OK;
+}
+// room for `need` rows; growing (capacity doubles) moves the live rows to the new arrays after every
+// in-flight batch has finished -- registration-time work, amortised over the doublings
+int pkc_reserve(ssb_ctx* ctx, size_t need) {
+  if (need <= ctx->pkc_cap) return SSB_OK;
+  if (int rc = pkc_quiesce(ctx)) return rc;
+  const size_t cap = std::max<size_t>({need, 2 * ctx->pkc_cap, (size_t)1024});
+  g1_aff* a = nullptr; uint32_t* f = nullptr; g1_aff* p = nullptr;
+  if (hipMalloc(&a, cap * sizeof(g1_aff)) != hipSuccess || hipMalloc(&f, cap * 4) != hipSuccess) {
+    if (a) hipFree(a);
+    (void)hipGetLastError();
     ctx->err = "hipMalloc public-key cache failed";
-    if (d_in) hipFree(d_in);
     return SSB_ENOMEM;
   }
-  hipStream_t st = ctx->sl[0].stream;
-  SSB_HIP(hipMemcpyAsync(d_in, pk48, n * 48, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_decode_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_in, ctx->pkc_aff, ctx->pkc_flags);
   // the precomputed bases of the batch path's merged G1 MSM (plan_msm g1_pre): registration-time
   // work, like the decompression; without them (allocation failed) batches use the windowed G1 MSM
-  if (hipMalloc(&ctx->pkc_pow, n * PKPOW_W * sizeof(g1_aff)) != hipSuccess) { ctx->pkc_pow = nullptr; (void)hipGetLastError(); }
+  if (hipMalloc(&p, cap * PKPOW_W * sizeof(g1_aff)) != hipSuccess) { p = nullptr; (void)hipGetLastError(); }
+  hipStream_t st = ctx->sl[0].stream;
+  const size_t n = ctx->pkc_n;
+  if (n) {
+    SSB_HIP(hipMemcpyAsync(a, ctx->pkc_aff, n * sizeof(g1_aff), hipMemcpyDeviceToDevice, st));
+    SSB_HIP(hipMemcpyAsync(f, ctx->pkc_flags, n * 4, hipMemcpyDeviceToDevice, st));
+    if (p && ctx->pkc_pow)
+      SSB_HIP(hipMemcpyAsync(p, ctx->pkc_pow, n * PKPOW_W * sizeof(g1_aff), hipMemcpyDeviceToDevice, st));
+    else if (p)
+      hipLaunchKernelGGL(k_pk_pow, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const g1_aff*)a, (const uint32_t*)f, p);
+    SSB_HIP(hipGetLastError());
+    SSB_HIP(hipStreamSynchronize(st));
+  }
+  const size_t live = ctx->pkc_n;
+  pkc_free(ctx);
+  ctx->pkc_aff = a; ctx->pkc_flags = f; ctx->pkc_pow = p; ctx->pkc_n = live; ctx->pkc_cap = cap;
+  return SSB_OK;
+}
+// decode n compressed keys into rows [row, row + n) (+ their precomputed bases); synchronous.  Runs
+// on slot 0's stream: rows below `row` -- the only ones an in-flight batch can index -- are untouched.
+int pkc_fill(ssb_ctx* ctx, size_t row, size_t n, const uint8_t* pk48) {
+  if (!n) return SSB_OK;
+  if (n * 48 > ctx->pkc_stage_bytes) {
+    if (ctx->pkc_stage) { hipFree(ctx->pkc_stage); ctx->pkc_stage = nullptr; ctx->pkc_stage_bytes = 0; }
+    const size_t want = std::max<size_t>(n * 48, 48 * 1024);
+    if (hipMalloc(&ctx->pkc_stage, want) != hipSuccess) { ctx->pkc_stage = nullptr; ctx->err = "hipMalloc key staging failed"; return SSB_ENOMEM; }
+    ctx->pkc_stage_bytes = want;
+  }
+  hipStream_t st = ctx->sl[0].stream;
+  SSB_HIP(hipMemcpyAsync(ctx->pkc_stage, pk48, n * 48, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_decode_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const uint8_t*)ctx->pkc_stage,
+                     ctx->pkc_aff + row, ctx->pkc_flags + row);
   if (ctx->pkc_pow)
-    hipLaunchKernelGGL(k_pk_pow, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const g1_aff*)ctx->pkc_aff,
-                       (const uint32_t*)ctx->pkc_flags, ctx->pkc_pow);
+    hipLaunchKernelGGL(k_pk_pow, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const g1_aff*)(ctx->pkc_aff + row),
+                       (const uint32_t*)(ctx->pkc_flags + row), ctx->pkc_pow + row * PKPOW_W);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipStreamSynchronize(st));
-  hipFree(d_in);
+  return SSB_OK;
+}
+}  // namespace
+extern "C" {
+
+int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
+  if (!ctx) return SSB_EINVAL;
+  if (n && !pk48) { ctx->err = "null pk48"; return SSB_EINVAL; }
+  if (n > (size_t)UINT32_MAX) { ctx->err = "too many keys"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  if (int rc = pkc_quiesce(ctx)) return rc;
+  pkc_free(ctx);
+  ctx->pkc_map.clear();
+  ctx->pkc_set_keys.clear();
+  ctx->pkc_map_valid = true;
+  if (!n) return SSB_OK;
+  int rc;
+  if ((rc = pkc_reserve(ctx, n))) return rc;
+  if ((rc = pkc_fill(ctx, 0, n, pk48))) return rc;
   ctx->pkc_n = n;
+  // the key -> row index for a later ssb_pk_cache_add is built from these bytes on first use
+  ctx->pkc_set_keys.assign(pk48, pk48 + n * 48);
+  ctx->pkc_map_valid = false;
+  return SSB_OK;
+}
+
+int ssb_pk_cache_add(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint32_t* out_index) {
+  if (!ctx) return SSB_EINVAL;
+  if (n == 0) return SSB_OK;
+  if (!pk48 || !out_index) { ctx->err = "null pointer"; return SSB_EINVAL; }
+  SSB_HIP(hipSetDevice(ctx->device));
+  if (!ctx->pkc_map_valid) {   // after a _set: index its rows (first occurrence of each key)
+    ctx->pkc_map.clear();
+    ctx->pkc_map.reserve(ctx->pkc_set_keys.size() / 48);
+    for (size_t r = 0; r * 48 < ctx->pkc_set_keys.size(); ++r)
+      ctx->pkc_map.emplace(std::string((const char*)ctx->pkc_set_keys.data() + 48 * r, 48), (uint32_t)r);
+    std::vector<uint8_t>().swap(ctx->pkc_set_keys);
+    ctx->pkc_map_valid = true;
+  }
+  // new distinct keys of this call, in order
+  std::vector<uint8_t> fresh;
+  std::unordered_map<std::string, uint32_t> local;
+  size_t next = ctx->pkc_n;
+  for (size_t i = 0; i < n; ++i) {
+    std::string k((const char*)pk48 + 48 * i, 48);
+    auto it = ctx->pkc_map.find(k);
+    if (it != ctx->pkc_map.end()) { out_index[i] = it->second; continue; }
+    auto jt = local.find(k);
+    if (jt != local.end()) { out_index[i] = jt->second; continue; }
+    if (next >= (size_t)UINT32_MAX) { ctx->err = "key table full"; return SSB_EINVAL; }
+    local.emplace(std::move(k), (uint32_t)next);
+    out_index[i] = (uint32_t)next++;
+    fresh.insert(fresh.end(), pk48 + 48 * i, pk48 + 48 * i + 48);
+  }
+  const size_t nf = fresh.size() / 48;
+  if (!nf) return SSB_OK;
+  int rc;
+  if ((rc = pkc_reserve(ctx, ctx->pkc_n + nf))) return rc;
+  if ((rc = pkc_fill(ctx, ctx->pkc_n, nf, fresh.data()))) return rc;
+  ctx->pkc_n += nf;
+  for (auto& kv : local) ctx->pkc_map.emplace(kv.first, kv.second);
   return SSB_OK;
 }
 
@@ -1127,7 +1251,7 @@ int submit_impl(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const ui
   // the next slot round robin; its previous host batch is delivered before its staging is reused
   const int k = ctx->next;
   ssb_slot& S = ctx->sl[k];
-  SSB_HIP(deliver_host(S));
+  SSB_HIP(deliver_host(ctx, S));
   size_t o = 0;
   auto at = [&](size_t bytes) { const size_t r = o; o += align_up(bytes); return r; };
   const size_t i_sig = at(n * 96), i_pk = at(pk_index ? n * 4 : n * 48), i_ids = at(n * 8), i_off = at((n_jobs + 1) * 4), i_t = at(n_jobs * 4),
@@ -1194,10 +1318,17 @@ int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket) {
   if (!ctx) return SSB_EINVAL;
   if (ticket == 0) return SSB_OK;
   const int k = (int)(ticket & 0xff);
-  if (k >= ctx->nslots || (ticket >> 8) > ctx->ticket_gen) { ctx->err = "unknown ticket"; return SSB_EINVAL; }
-  ssb_slot& S = ctx->sl[k];
-  if (S.host_ticket != ticket) return SSB_OK;   // already delivered (its slot was reused, or waited before)
-  SSB_HIP(deliver_host(S));
+  // only generations never issued are unknown; any issued ticket that no live slot holds was
+  // delivered (its slot reused, waited before, or removed by ssb_set_pipeline_depth /
+  // ssb_set_slot_streams / ssb_pk_cache_*, which deliver first) -- unless its delivery failed
+  if ((ticket >> 8) == 0 || (ticket >> 8) > ctx->ticket_gen || k >= SSB_MAX_SLOTS) { ctx->err = "unknown ticket"; return SSB_EINVAL; }
+  if (k < ctx->nslots && ctx->sl[k].host_ticket == ticket) (void)deliver_host(ctx, ctx->sl[k]);
+  auto it = ctx->failed_tickets.find(ticket);
+  if (it != ctx->failed_tickets.end()) {
+    ctx->failed_tickets.erase(it);
+    ctx->err = "the batch did not complete (HIP error); its statuses are SSB_DVF_ENGINE_ERROR";
+    return SSB_EHIP;
+  }
   return SSB_OK;
 }
 

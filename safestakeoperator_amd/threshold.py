@@ -32,7 +32,7 @@ INFINITY_SIGNATURE = bytes([0xC0]) + bytes(95)          # bls::INFINITY_SIGNATUR
 
 SSB_OK = 0
 DVF_OK, DVF_DIFFERENT_LENGTH, DVF_INSUFFICIENT_SIGNATURES, DVF_INVALID_OPERATOR_ID, \
-    DVF_INSUFFICIENT_VALID_SIGNATURES, DVF_BAD_SIGNATURE_ENCODING, DVF_INVALID_JOB = range(7)
+    DVF_INSUFFICIENT_VALID_SIGNATURES, DVF_BAD_SIGNATURE_ENCODING, DVF_INVALID_JOB, DVF_ENGINE_ERROR = range(8)
 MAX_T = 64
 
 
@@ -109,6 +109,8 @@ def _error_from(status: int, e0: int, e1: int) -> Optional[DvfError]:
         return DifferentLength(e0, e1)
     if status == DVF_INVALID_JOB:      # _dev callers only (t or share range outside the limits)
         return ValueError("job outside the engine's limits: t = %d, %d shares" % (e0, e1))
+    if status == DVF_ENGINE_ERROR:     # the job's batch did not complete: never a reference result
+        return RuntimeError("engine error: the batch did not complete (code %d)" % (e0 - (1 << 64) if e0 >= 1 << 63 else e0))
     raise RuntimeError("unknown status %d" % status)
 
 
@@ -124,11 +126,49 @@ class Engine:
             raise RuntimeError("ssb_create(device=%d) failed with %d (no usable GPU?)" % (device, rc))
         self._h = h
         self.device = device
+        # host-buffer batches not yet waited for, by ticket: the library writes their outputs into
+        # the PendingBatch's arrays when the batch is delivered -- possibly inside a later call that
+        # reuses the slot (include/ssbls.h, ssb_batch_wait LIFETIME) -- so they stay alive here
+        self._pending = {}
 
     def close(self):
         if getattr(self, "_h", None):
-            self._lib.ssb_destroy(self._h)
+            self._lib.ssb_destroy(self._h)   # (delivers every pending batch first)
             self._h = None
+            self._pending = {}
+
+    def _delivered_all(self):
+        """Every pending host batch has been delivered by the library (set_pipeline_depth,
+        set_slot_streams, pk_cache_set / pk_cache_add, kernel_timing deliver them all)."""
+        self._pending.clear()
+
+    def set_pipeline_depth(self, depth: int):
+        self._check(self._lib.ssb_set_pipeline_depth(self._h, int(depth)), "ssb_set_pipeline_depth")
+        self._delivered_all()
+
+    def set_slot_streams(self, streams: int):
+        self._check(self._lib.ssb_set_slot_streams(self._h, int(streams)), "ssb_set_slot_streams")
+        self._delivered_all()
+
+    def pk_cache_set(self, pks) -> None:
+        """ssb_pk_cache_set: the decoded-key table = these keys, row i = key i."""
+        buf = np.frombuffer(b"".join(pks) if not isinstance(pks, (bytes, bytearray, np.ndarray)) else pks, dtype=np.uint8)
+        if buf.size % 48:
+            raise ValueError("public keys are 48 bytes")
+        self._check(self._lib.ssb_pk_cache_set(self._h, buf.size // 48, buf.ctypes.data_as(_lib._u8p)), "ssb_pk_cache_set")
+        self._delivered_all()
+
+    def pk_cache_add(self, pks) -> np.ndarray:
+        """ssb_pk_cache_add: register keys (a committee's operator keys), return their stable rows."""
+        buf = np.frombuffer(b"".join(pks) if not isinstance(pks, (bytes, bytearray, np.ndarray)) else pks, dtype=np.uint8)
+        if buf.size % 48:
+            raise ValueError("public keys are 48 bytes")
+        n = buf.size // 48
+        idx = np.zeros(max(n, 1), dtype=np.uint32)
+        if n:
+            self._check(self._lib.ssb_pk_cache_add(self._h, n, buf.ctypes.data_as(_lib._u8p), idx.ctypes.data_as(_lib._u32p)),
+                        "ssb_pk_cache_add")
+        return idx[:n]
 
     def __del__(self):
         try:
@@ -166,6 +206,7 @@ class Engine:
         """Start (accumulate every launch, or with last_only the last launch of each stage for
         last_kernel_ms) or stop the engine's event timing; off by default."""
         self._check(self._lib.ssb_kernel_timing(self._h, (2 if last_only else 1) if on else 0), "ssb_kernel_timing")
+        self._delivered_all()
 
     def kernel_time(self, name: str):
         """(total ms, launches) accumulated since kernel_timing(True)."""
@@ -379,6 +420,11 @@ class Engine:
             pb.st.ctypes.data_as(_lib._i32p), pb.err.ctypes.data_as(_lib._u64p), pb.ver.ctypes.data_as(_lib._u8p),
             ctypes.byref(tk)), "ssb_threshold_aggregate_batch_submit")
         pb.ticket = tk.value
+        # this submit delivered the slot's previous batch (same slot = the ticket's low byte)
+        slot = pb.ticket & 0xFF
+        for t in [t for t in self._pending if t & 0xFF == slot]:
+            del self._pending[t]
+        self._pending[pb.ticket] = pb
         return pb
 
     def unsafe_aggregate_batch_raw(self, share_off: Sequence[int], sigs: bytes, ids: Sequence[int]):
@@ -410,7 +456,10 @@ class PendingBatch:
         self.ver = np.zeros(max(N, 1), dtype=np.uint8)
 
     def wait(self):
-        self.engine._check(self.engine._lib.ssb_batch_wait(self.engine._h, self.ticket), "ssb_batch_wait")
+        try:
+            self.engine._check(self.engine._lib.ssb_batch_wait(self.engine._h, self.ticket), "ssb_batch_wait")
+        finally:
+            self.engine._pending.pop(self.ticket, None)
         return self.out[:self.J], self.st[:self.J], self.err[:self.J], self.ver[:self.N]
 
 

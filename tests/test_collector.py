@@ -121,12 +121,15 @@ def test_engine_failure_reaches_every_job():
 
 
 @pytest.mark.gpu
-def test_collector_on_engine(engine):
+def test_collector_on_engine():
+    """SlotCollector on its own engine (the native collector takes a context over)."""
+    from safestakeoperator_amd import Engine
     cases = _cases()
-    with SlotCollector(engine, max_jobs=4096, window_s=0.01) as col:
-        futs = [(col.submit(c["t"], _job(c)), _expected(c)) for c in cases for _ in range(3)]
-        for f, want in futs:
-            _check(f, want)
+    with Engine(0) as eng:
+        with SlotCollector(eng, max_jobs=4096, window_s=0.01, in_flight=2) as col:
+            futs = [(col.submit(c["t"], _job(c)), _expected(c)) for c in cases for _ in range(3)]
+            for f, want in futs:
+                _check(f, want)
 
 
 def test_malformed_job_fails_alone():

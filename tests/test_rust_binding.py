@@ -35,7 +35,9 @@ def test_patches_apply_in_order(tmp_path):
         assert r.returncode == 0, f"{os.path.basename(p)}: {r.stderr}"
         subprocess.run(["git", "apply", p], cwd=tmp_path, check=True, capture_output=True)
     hot = (tmp_path / "src/validation/impls/hotstuff.rs").read_text()
-    assert "SLOT_COLLECTOR" in hot and 'cfg(not(feature = "hip"))' in hot
+    assert "slot_collector::threshold_aggregate" in hot and 'cfg(not(feature = "hip"))' in hot
+    oc = (tmp_path / "src/validation/operator_committees.rs").read_text()
+    assert "register_committee_keys(&def.operator_public_keys)" in oc
     gt = (tmp_path / "src/crypto/generic_threshold.rs").read_text()
     assert "fn threshold_aggregate_batch" in gt and "pub struct ThresholdJob" in gt
 
