@@ -157,12 +157,17 @@ def pmc_traffic(kernel, shares=None):
         return None
 
 
-def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_count=0, v0=0):
+def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_count=0, v0=0, bad_operator=0, ids="seq"):
     """Synthetic committees: deterministic keys (seed 0x5AFE57A4E, rank), Shamir shares, partial
     signatures from the engine's batched signer (H(m)*sk), public keys sk*g1.  invalid_rate: that
     fraction of the shares (deterministic choice) signs the NEXT root instead -- a valid G2 point
     that fails verification (SURVEY.md §8d C2/C4 invalid variants).  v0: index of the first
-    validator (a rank's shard of one global batch: validators v0 .. v0+V-1 of seed `rank`)."""
+    validator (a rank's shard of one global batch: validators v0 .. v0+V-1 of seed `rank`).
+    bad_operator: every share of the operator with that id is invalid (a faulty / malicious operator,
+    the reference skips and logs its shares: generic_threshold.rs:166-168).
+    ids: "seq" -- operator ids 1..n in every committee (the reference's tests and DKG helper); "registry"
+    -- n distinct pseudo-random ids in [1, 2^16) per committee, as registry operator ids arrive from the
+    contract (src/node/node.rs:470-474, validator.releated_operators)."""
     seed = b"ssbls-bench" + (0x5AFE57A4E).to_bytes(8, "little") + rank.to_bytes(4, "little")
     roots = [hashlib.sha256(seed + b"root" + i.to_bytes(4, "little")).digest() for i in range(n_roots)]
 
@@ -178,14 +183,28 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_coun
         for k in range(1, t):
             coef[v, k] = h(b"c", vb, k.to_bytes(4, "little"))
     master = coef[:, 0].tolist()
+    if ids == "registry":
+        idm = np.empty((V, n), dtype=object)
+        for v in range(V):
+            vb = (v0 + v).to_bytes(4, "little")
+            got, k = [], 0
+            while len(got) < n:
+                x = 1 + int.from_bytes(hashlib.sha256(seed + b"id" + vb + k.to_bytes(4, "little")).digest()[:4], "little") % 65535
+                if x not in got:
+                    got.append(x)
+                k += 1
+            idm[v, :] = got
+    else:
+        idm = np.asarray([list(range(1, n + 1))] * V, dtype=object)
     shares = np.empty((V, n), dtype=object)
-    for i in range(1, n + 1):
+    for i in range(n):
+        x = idm[:, i]
         acc = coef[:, t - 1].copy()
         for k in range(t - 2, -1, -1):
-            acc = (acc * i + coef[:, k]) % R_ORDER
-        shares[:, i - 1] = acc
+            acc = (acc * x + coef[:, k]) % R_ORDER
+        shares[:, i] = acc
     share_sk = shares.reshape(-1).tolist()
-    ids = list(range(1, n + 1)) * V
+    ids = [int(x) for x in idm.reshape(-1).tolist()]
     jr = [(v0 + v) % n_roots for v in range(V)]
     share_root = [r for r in jr for _ in range(n)]
     bad = [i for i in range(len(share_sk))
@@ -194,6 +213,8 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_coun
     if invalid_count:                                  # exactly that many, spread over the batch
         N = len(share_sk)
         bad = sorted(set(bad) | {(k * (N // invalid_count) + 4099 * (k + 1)) % N for k in range(invalid_count)})
+    if bad_operator:                                   # every share of that operator id
+        bad = sorted(set(bad) | {i for i, x in enumerate(ids) if x == bad_operator})
     sign_root = list(share_root)
     for i in bad:
         sign_root[i] = (share_root[i] + 1) % n_roots
@@ -316,6 +337,11 @@ def main():
     ap.add_argument("--invalid-rate", type=float, default=0.0,
                     help="fraction of shares signed over the wrong root (the RLC batch fails; exact verdicts "
                          "come from the per-share fallback).  The headline is the all-valid C2 batch.")
+    ap.add_argument("--bad-operator", type=int, default=0,
+                    help="every share of the operator with this id is invalid (a faulty operator in every committee)")
+    ap.add_argument("--ids", default="seq", choices=("seq", "registry"),
+                    help="operator ids: 1..n per committee (seq), or distinct pseudo-random registry ids in [1, 2^16) "
+                         "per committee (registry, src/node/node.rs:470-474)")
     ap.add_argument("--sustained-steps", type=int, default=200,
                     help="length of the sustained-rate run reported as value_sustained (0: skip)")
     ap.add_argument("--collector-windows", type=int, default=200,
@@ -394,9 +420,11 @@ def main():
         j0, j1 = shard_jobs(goff, world, rank)
         sizes = shard_sizes(goff, world)
         V = j1 - j0
-        wl = make_workload(eng, V, t, n, n_roots, 0, args.invalid_rate, args.invalid_count, v0=j0)
+        wl = make_workload(eng, V, t, n, n_roots, 0, args.invalid_rate, args.invalid_count, v0=j0,
+                           bad_operator=args.bad_operator, ids=args.ids)
     else:
-        wl = make_workload(eng, V, t, n, n_roots, rank, args.invalid_rate, args.invalid_count)
+        wl = make_workload(eng, V, t, n, n_roots, rank, args.invalid_rate, args.invalid_count,
+                           bad_operator=args.bad_operator, ids=args.ids)
     N = V * n
     valid = np.asarray(wl["valid"], dtype=np.uint8)
     job_ok = valid.reshape(V, n).sum(axis=1) >= t
@@ -852,6 +880,9 @@ def main():
                                "combined signatures (== the master key's signature)%s" % (
                                    V, N, "; the last exchange's gathered results == local" if world > 1 else ""),
             "invalid_shares_per_batch": wl["n_bad"],
+            "operator_ids": ("registry: distinct pseudo-random ids in [1, 2^16) per committee" if args.ids == "registry"
+                             else "1..%d in every committee" % n),
+            "bad_operator": args.bad_operator or None,
             "roofline": roof or {"bound": "valu-int32-mad", "kernel": dom, "achieved": round(achieved, 4),
                                  "peak": round(peak, 2), "unit": "TMAD/s", "frac": round(achieved / peak, 5),
                                  "traffic": pmc_traffic(dom), "mads_per_launch": km[dom], "avg_launch_ms": round(avg[dom], 4),

@@ -34,6 +34,11 @@
 namespace ssb {
 namespace k {
 
+using launch::fb_jobs;
+// committee stage: at most this many suspect shares are checked one by one (beyond it the tree decides)
+constexpr uint32_t FB_SUSPECT_MAX = 2048;
+constexpr unsigned EX_SINGLE_BLOCKS = 512;
+
 // One workgroup (the last block of k_fb_rlc's grid): counting sort of the shares by root (cnt,
 // start, perm) and the group starts of every level (gst[l][r], n_roots + 1 words per level); it
 // also zeroes k_fb_root's per-root tickets.  Phases separated by workgroup barriers (global atomics
@@ -73,16 +78,105 @@ SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   for (int s = t; s < n; s += NT)
     if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
 }
+// ---- committee stage (aggregate batches): consistency of each job's shares ------------------------
+// All valid shares of a job lie on one polynomial of degree t - 1 (generic_threshold.rs:59-80: the
+// key split; src/crypto/impls/blst.rs:19-39: the combine relies on it), so any t + 1 of them satisfy
+// the t-th divided difference  sum_i sig_i / prod_{j != i} (x_i - x_j) = O, i.e. with integer
+// coefficients c_i = L / prod_{j != i} (x_i - x_j)  (L the lcm of the denominators; ids 1..4:
+// -1, 3, -3, 1)  sum_i c_i sig_i = O.  A job whose shares break one of its relations holds an
+// invalid share: its candidates become SUSPECT (checked one by one) and the rest of the batch is
+// re-checked at once by excluding them from the batch check (k_fb_excl).  The relation is only a
+// partition heuristic -- every verdict still comes from a pairing check (an adversary who makes
+// invalid shares satisfy it only sends them into the exclusion check, which then fails, and the
+// tree below decides).  Ids whose coefficients overflow 63 bits, duplicates and t > REL_TMAX give
+// no relation (the job is left to the exclusion check).
+constexpr int REL_TMAX = 16;
+SSB_INL int64_t rel_gcd(int64_t a, int64_t b) {
+  if (a < 0) a = -a;
+  if (b < 0) b = -b;
+  while (b) { const int64_t t = a % b; a = b; b = t; }
+  return a;
+}
+SSB_INL bool rel_coeffs(int64_t* c, const uint64_t* x, int m) {
+  int64_t L = 1;
+  for (int i = 0; i < m; ++i) {
+    if (x[i] >= (1ull << 62)) return false;
+    int64_t d = 1;
+    for (int j = 0; j < m; ++j) {
+      if (j == i) continue;
+      const int64_t df = (int64_t)x[i] - (int64_t)x[j];
+      if (df == 0 || __builtin_mul_overflow(d, df, &d)) return false;
+    }
+    c[i] = d;
+    const int64_t a = d < 0 ? -d : d, g = rel_gcd(L, a);
+    if (__builtin_mul_overflow(L / g, a, &L)) return false;
+  }
+  for (int i = 0; i < m; ++i) c[i] = L / c[i];
+  return true;
+}
+// job j: the relations over its first t candidates plus each further candidate; on a broken one
+// every candidate of the job is marked SUSPECT and listed (slist, nS)
+SSB_INL void consist_job(int j, uint32_t n, const fb_jobs& jb, uint32_t* __restrict__ flags,
+                         const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS) {
+  const uint32_t b = jb.off[j], e = jb.off[j + 1], t = jb.tt[j];
+  if (e < b || e > n || t == 0 || t > (uint32_t)REL_TMAX) return;
+  uint32_t base[REL_TMAX];
+  uint64_t x[REL_TMAX + 1];
+  int64_t c[REL_TMAX + 1];
+  uint32_t nb = 0;
+  bool sus = false;
+  for (uint32_t s = b; s < e && !sus; ++s) {
+    if (!(flags[s] & FLAG_CANDIDATE)) continue;
+    if (nb < t) { base[nb++] = s; continue; }
+    for (uint32_t i = 0; i < t; ++i) x[i] = jb.ids[base[i]];
+    x[t] = jb.ids[s];
+    if (!rel_coeffs(c, x, (int)t + 1)) continue;
+    uint64_t mx = 0;
+    for (uint32_t i = 0; i <= t; ++i) { const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]); mx = m > mx ? m : mx; }
+    const int nbits = mx ? 64 - __builtin_clzll(mx) : 0;
+    g2_jac acc;
+    jac_set_inf(acc);
+    for (int bit = nbits - 1; bit >= 0; --bit) {
+      jac_dbl(acc, acc);
+      for (uint32_t i = 0; i <= t; ++i) {
+        const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
+        if ((m >> bit) & 1ull) {
+          g2_aff q = sig_aff[i < t ? base[i] : s];
+          if (c[i] < 0) fp2_neg(q.y, q.y);
+          jac_add_aff(acc, acc, q);
+        }
+      }
+    }
+    sus = !jac_is_inf(acc);
+  }
+  if (!sus) return;
+  for (uint32_t s = b; s < e; ++s)
+    if (flags[s] & FLAG_CANDIDATE) {
+      atomicOr(&flags[s], (uint32_t)FLAG_SUSPECT);
+      const uint32_t k = atomicAdd(nS, 1u);
+      if (k < FB_SUSPECT_MAX) slist[k] = s;
+    }
+}
+
 // Threads [0, n): the candidates' RLC scalars k64[s] (the main check's own, rlc_scalar_odd).  With
 // `verdict` it also writes, grid-wide, the verdicts the batch check decides: every share of a
 // passing batch, the non-candidates of a failing one (the candidates' follow from the group tests).
+// Blocks after the shares' (jobs given): the committee consistency of 64 jobs each (consist_job).
 // The grid's last block runs the counting sort by root (fb_prep_block).
 __global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restrict__ ok,
-                                   const uint32_t* __restrict__ flags, uint64_t* __restrict__ k64,
-                                   uint8_t* __restrict__ verdict, fb_prep_args prep) {
+                                   uint32_t* __restrict__ flags, uint64_t* __restrict__ k64,
+                                   uint8_t* __restrict__ verdict, fb_prep_args prep, fb_jobs jobs,
+                                   const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ slist,
+                                   uint32_t* __restrict__ nS) {
   const uint32_t pass = *ok;
   if (blockIdx.x == gridDim.x - 1) {   // uniform per block
     if (!pass) fb_prep_block(n, prep);
+    return;
+  }
+  const int nbs = (n + 63) / 64;
+  if ((int)blockIdx.x >= nbs) {        // committee consistency
+    const int j = ((int)blockIdx.x - nbs) * 64 + (int)threadIdx.x;
+    if (!pass && j < jobs.n_jobs) consist_job(j, (uint32_t)n, jobs, flags, sig_aff, slist, nS);
     return;
   }
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -124,8 +218,9 @@ __global__ void SSB_LB2(64) k_fb_sparse(int n, int n_roots, const uint32_t* __re
                                       const uint32_t* __restrict__ gst0, const uint8_t* __restrict__ gv0,
                                       const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
                                       const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
-                                      g1_jac* __restrict__ rpk, const uint32_t* __restrict__ nfail) {
-  if (*ok || *nfail <= FB_SINGLE_MAX) return;
+                                      g1_jac* __restrict__ rpk, const uint32_t* __restrict__ nfail,
+                                      const uint32_t* __restrict__ xok) {
+  if (*ok || *nfail <= FB_SINGLE_MAX || (xok && *xok)) return;
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = g < n ? g : g - n;
   if (s >= n || !(flags[s] & FLAG_CANDIDATE)) return;
@@ -179,30 +274,23 @@ SSB_INL bool pair_check(lane::grp& g, const g1_aff& P, const g2_aff& Q, const g2
 // the block's LDS stays small enough for two waves per SIMD)
 struct fr_bucket_lds { uint32_t list[4 * FR_CHUNK]; uint32_t cnt[64], off[64], cur[64]; };
 union fr_lds { fr_bucket_lds b; fp s[lane::LP_NCODE_CONST + BS_SLOTS]; };
-SSB_INL g2_jac shfl_down_g2(const g2_jac& p, int off) {
-  g2_jac r;
+template <class P> SSB_INL P shfl_down_pt(const P& p, int off) {
+  P r;
   const int* a = (const int*)&p;
   int* b = (int*)&r;
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(g2_jac) / 4); ++i) b[i] = __shfl_down(a[i], (unsigned)off, 64);
+  for (int i = 0; i < (int)(sizeof(P) / 4); ++i) b[i] = __shfl_down(a[i], (unsigned)off, 64);
   return r;
 }
-__global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __restrict__ ok,
-                                     const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
-                                     const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst,
-                                     const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64,
-                                     const g2_aff* __restrict__ sig_aff, const fp12* __restrict__ froot,
-                                     g2_jac* __restrict__ X, uint32_t* __restrict__ rtk, uint8_t* __restrict__ gv0,
-                                     uint32_t* __restrict__ nfail, uint8_t* __restrict__ verdict) {
-  using namespace ssb::lane;
-  if (*ok) return;   // uniform: the batch passed
-  const int r = blockIdx.x >> 2, q = blockIdx.x & 3;
-  if (r >= n_roots) return;
-  const uint32_t nr = cnt[r], sb = start[r];
-  if (!nr) return;   // no group (the root's four blocks all leave here: no ticket)
-  __shared__ fr_lds u;
-  fr_bucket_lds& ub = u.b;
-  __shared__ uint32_t flg, last;
+SSB_INL g2_jac shfl_down_g2(const g2_jac& p, int off) { return shfl_down_pt(p, off); }
+
+// X_q = sum_w 2^(4w) W_{4q+w} over the listed shares (bits 16q .. 16q+15 of their scalars k64):
+// the shares are sorted into 64 buckets (4 windows x 16 digits) in LDS, chunk by chunk; lane (w, d)
+// sums bucket d of window w; a 16-lane suffix scan and tree give W = sum_d d B_d; lanes 0, 16, 32, 48
+// shift and add.  Result in lane 0.  Shares without `need` in their flags are skipped.
+SSB_FN g2_jac quarter_sum(fr_bucket_lds& ub, const uint32_t* __restrict__ list, uint32_t nr,
+                           const uint32_t* __restrict__ flags, uint32_t need, const uint64_t* __restrict__ k64,
+                           const g2_aff* __restrict__ sig_aff, int q) {
   const int lane_ = threadIdx.x, wl = lane_ >> 4, d = lane_ & 15;
   g2_jac acc;
   jac_set_inf(acc);
@@ -211,8 +299,8 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
     ub.cnt[lane_] = 0u;
     __syncthreads();
     for (uint32_t x = lane_; x < m; x += 64) {
-      const uint32_t s = perm[sb + c0 + x];
-      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      const uint32_t s = list[c0 + x];
+      if ((flags[s] & need) != need) continue;
       const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
       for (int w = 0; w < 4; ++w) { const uint32_t dg = (kq >> (4 * w)) & 15u; if (dg) atomicAdd(&ub.cnt[w * 16 + dg], 1u); }
     }
@@ -223,8 +311,8 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
     }
     __syncthreads();
     for (uint32_t x = lane_; x < m; x += 64) {
-      const uint32_t s = perm[sb + c0 + x];
-      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      const uint32_t s = list[c0 + x];
+      if ((flags[s] & need) != need) continue;
       const uint32_t kq = (uint32_t)(k64[s] >> (16 * q));
       for (int w = 0; w < 4; ++w) {
         const uint32_t dg = (kq >> (4 * w)) & 15u;
@@ -240,19 +328,84 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
   // d = 0 holds no bucket), then the sum of S_1 .. S_15
   for (int off = 1; off < 16; off <<= 1) {
     const g2_jac o = shfl_down_g2(acc, off);
-    if (d + off < 16) jac_add(acc, acc, o);
+    if (d + off < 16) jac_add_inl(acc, acc, o);
   }
   if (d == 0) jac_set_inf(acc);
   for (int h = 8; h >= 1; h >>= 1) {
     const g2_jac o = shfl_down_g2(acc, h);
-    if (d < h) jac_add(acc, acc, o);
+    if (d < h) jac_add_inl(acc, acc, o);
   }
   // X_q = sum_w 2^(4w) W_{4q+w}  (lanes 0, 16, 32, 48)
-  if (d == 0) for (int i = 0; i < 4 * wl; ++i) jac_dbl(acc, acc);
+  if (d == 0) for (int i = 0; i < 4 * wl; ++i) jac_dbl_inl(acc, acc);
   for (int h = 32; h >= 16; h >>= 1) {
     const g2_jac o = shfl_down_g2(acc, h);
-    if (lane_ < h && d == 0) jac_add(acc, acc, o);
+    if (lane_ < h && d == 0) jac_add_inl(acc, acc, o);
   }
+  return acc;
+}
+// sum_q 2^(16q) X[q] (q < 4), affine, in lane 0 (Q.inf on the other lanes)
+SSB_FN g2_aff combine_quarters(const g2_jac* __restrict__ X) {
+  const int lane_ = threadIdx.x;
+  g2_jac t;
+  jac_set_inf(t);
+  if (lane_ < 4) { t = X[lane_]; for (int i = 0; i < 16 * lane_; ++i) jac_dbl_inl(t, t); }
+  for (int h = 2; h >= 1; h >>= 1) {
+    const g2_jac o = shfl_down_g2(t, h);
+    if (lane_ < h) jac_add_inl(t, t, o);
+  }
+  g2_aff Q;
+  Q.inf = true;
+  if (lane_ == 0) jac_to_aff(Q, t);
+  return Q;
+}
+// Miller value m(P, Q) (lane program) into slots F1 .. F1+11 of the workgroup's LDS, or 1 when P or
+// Q is infinity.  P, Q are read from lane 0; uniform.
+SSB_FN void miller_one(lane::grp& g, const g1_aff& P, const g2_aff& Q, int F1, int B, uint32_t& flg) {
+  using namespace ssb::lane;
+  const int lane_ = threadIdx.x;
+  if (lane_ == 0) {
+    flg = (P.inf || Q.inf) ? 1u : 0u;
+    if (!(P.inf || Q.inf)) {
+      g.s[B + 0] = Q.x.c0; g.s[B + 1] = Q.x.c1; g.s[B + 2] = Q.y.c0; g.s[B + 3] = Q.y.c1;
+      g.s[B + 4] = P.x; g.s[B + 5] = P.y;
+    }
+  }
+  __syncthreads();
+  const bool one = flg != 0;
+  __syncthreads();
+  if (one) {
+    const fp12 o = fp12_one();
+    if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&o)[lane_];
+    __syncthreads();
+  } else {
+    f12_miller(g, F1, B);
+  }
+}
+
+__global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __restrict__ ok,
+                                     const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                                     const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst,
+                                     const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64,
+                                     const g2_aff* __restrict__ sig_aff, const fp12* __restrict__ froot,
+                                     g2_jac* __restrict__ X, uint32_t* __restrict__ rtk, uint8_t* __restrict__ gv0,
+                                     uint32_t* __restrict__ nfail, uint8_t* __restrict__ verdict, int n,
+                                     const uint32_t* __restrict__ xok, uint32_t* __restrict__ nS) {
+  using namespace ssb::lane;
+  if (*ok) return;   // uniform: the batch passed
+  if (nS && blockIdx.x == 0 && threadIdx.x == 0) *nS = 0u;   // (k_fb_excl, the last reader, has finished)
+  if (xok && *xok) {   // the committee stage decided every candidate: the non-suspects passed
+    for (int s = blockIdx.x * 64 + threadIdx.x; s < n; s += gridDim.x * 64)
+      if ((flags[s] & (FLAG_CANDIDATE | FLAG_SUSPECT)) == FLAG_CANDIDATE) verdict[s] = 1;
+    return;
+  }
+  const int r = blockIdx.x >> 2, q = blockIdx.x & 3;
+  if (r >= n_roots) return;
+  const uint32_t nr = cnt[r], sb = start[r];
+  if (!nr) return;   // no group (the root's four blocks all leave here: no ticket)
+  __shared__ fr_lds u;
+  __shared__ uint32_t flg, last;
+  const int lane_ = threadIdx.x;
+  const g2_jac acc = quarter_sum(u.b, perm + sb, nr, flags, FLAG_CANDIDATE, k64, sig_aff, q);
   if (lane_ == 0) X[4 * r + q] = acc;
   __threadfence();
   __syncthreads();
@@ -261,38 +414,15 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
   if (!last) return;
   __threadfence();
   // S_r = sum_q 2^(16q) X_q, then the root's check FE(f[r] * e(-g1, S_r)) == 1
-  g2_jac t;
-  jac_set_inf(t);
-  if (lane_ < 4) { t = X[4 * r + lane_]; for (int i = 0; i < 16 * lane_; ++i) jac_dbl(t, t); }
-  for (int h = 2; h >= 1; h >>= 1) {
-    const g2_jac o = shfl_down_g2(t, h);
-    if (lane_ < h) jac_add(t, t, o);
-  }
-  g2_aff Q;
-  Q.inf = true;
-  if (lane_ == 0) jac_to_aff(Q, t);
+  const g2_aff Q = combine_quarters(X + 4 * r);
   __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
   grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
   lp_init_consts(g);
   const int F1 = BS_S0, B = F1 + 24, TMP = B + 12 + 4, FR = TMP + 72;
-  if (lane_ == 0) flg = Q.inf ? 1u : 0u;
-  if (lane_ == 0 && !Q.inf) {
-    g.s[B + 0] = Q.x.c0; g.s[B + 1] = Q.x.c1; g.s[B + 2] = Q.y.c0; g.s[B + 3] = Q.y.c1;
-    const g1_aff ng = g1_neg_generator();
-    g.s[B + 4] = ng.x; g.s[B + 5] = ng.y;
-  }
+  miller_one(g, g1_neg_generator(), Q, F1, B, flg);   // e(-g1, O) = 1: the root's value is f[r] alone
+  if (lane_ < 12) g.s[FR + lane_] = ((const fp*)&froot[r])[lane_];
   __syncthreads();
-  const bool qinf = flg != 0;
-  __syncthreads();
-  if (qinf) {   // e(-g1, O) = 1: the root's value is f[r] alone
-    if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&froot[r])[lane_];
-    __syncthreads();
-  } else {
-    if (lane_ < 12) g.s[FR + lane_] = ((const fp*)&froot[r])[lane_];
-    __syncthreads();
-    f12_miller(g, F1, B);
-    f12_mul(g, F1, FR, F1);
-  }
+  f12_mul(g, F1, FR, F1);
   f12_final_exp(g, F1, TMP);
   const bool pass = f12_slots_one(g, F1);
   if (lane_ == 0) {
@@ -307,6 +437,124 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
     }
 }
 
+// -sum k_i pk_i over the suspects of one root's segment of the root-sorted order (lane 0; infinity
+// on the other lanes): products on the lanes, a lane tree
+SSB_FN g1_aff neg_suspect_sum(uint32_t sb, uint32_t nr, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
+                              const uint64_t* __restrict__ k64, const g1_aff* __restrict__ pk_aff) {
+  const int lane_ = threadIdx.x;
+  g1_jac acc;
+  jac_set_inf(acc);
+  for (uint32_t k = sb + lane_; k < sb + nr; k += 64) {
+    const uint32_t s = perm[k];
+    if (!(flags[s] & FLAG_SUSPECT)) continue;
+    const uint64_t kk = k64[s];
+    const uint32_t kw[2] = {(uint32_t)kk, (uint32_t)(kk >> 32)};
+    g1_jac p;
+    jac_mul_aff(p, pk_aff[s], kw, 2);
+    jac_add(acc, acc, p);
+  }
+  for (int h = 32; h >= 1; h >>= 1) {
+    const g1_jac o = shfl_down_pt(acc, h);
+    if (lane_ < h) jac_add(acc, acc, o);
+  }
+  g1_aff P;
+  P.inf = true;
+  if (lane_ == 0 && !jac_is_inf(acc)) { jac_to_aff(P, acc); fp_neg(P.y, P.y); }
+  return P;
+}
+
+// The committee stage's checks (after k_fb_rlc's consistency pass listed the suspects, nS <=
+// FB_SUSPECT_MAX; otherwise a no-op and the tree decides):
+//   * the EXCLUSION check -- the batch check without the suspects:
+//       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
+//       E_r = sum_{suspects of root r} k_i pk_i  (block r: products on the lanes, a lane tree),
+//       X   = sum_{suspects} k_i sig_i          (blocks n_roots .. +3: 4-bit-digit bucket sums),
+//     where ftot is the batch check's own Miller product (k_miller_final) -- by bilinearity this is
+//     the RLC check over every non-suspect candidate with the batch's own scalars (soundness 2^-63),
+//     at the cost of one Miller loop per root holding suspects: *xok = 1 decides them all valid;
+//   * every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's verify
+//     (blocks n_roots + 4 ..).
+// The pair blocks finish with completion tickets (xtk[0]: pairs, xtk[1]: X's quarters); the last
+// pair multiplies ftot by the n_roots + 1 Miller values and runs ONE final exponentiation.
+__global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nS,
+                                     const uint32_t* __restrict__ slist, const uint32_t* __restrict__ start,
+                                     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
+                                     const uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
+                                     const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
+                                     const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H,
+                                     const fp12* __restrict__ ftot, fp12* __restrict__ fex, g2_jac* __restrict__ X4,
+                                     uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict) {
+  using namespace ssb::lane;
+  if (*ok) return;   // uniform: the batch passed
+  const uint32_t ns = *nS;
+  const int blk = blockIdx.x, lane_ = threadIdx.x;
+  if (ns == 0 || ns > FB_SUSPECT_MAX) {   // nothing to exclude / too many suspects: the tree decides
+    if (blk == 0 && lane_ == 0) *xok = 0u;
+    return;
+  }
+  __shared__ fr_lds u;
+  __shared__ uint32_t flg, last;
+  grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
+  if (blk >= n_roots + 4) {   // the suspects, one pairing check each
+    bool init = false;
+    for (uint32_t x = (uint32_t)(blk - n_roots - 4); x < ns; x += gridDim.x - (unsigned)(n_roots + 4)) {
+      const uint32_t s = slist[x];
+      const uint32_t r = share_root[s];
+      if (!init) { lp_init_consts(g); init = true; }
+      const bool pass = pair_check(g, pk_aff[s], sig_aff[s], H[r], F1, B, BP, TMP);
+      if (lane_ == 0) verdict[s] = pass ? 1 : 0;
+    }
+    return;
+  }
+  int pair;   // the exclusion pair this block computes: root r, or n_roots for X
+  if (blk < n_roots) {
+    const int r = blk;
+    const g1_aff P = neg_suspect_sum(start[r], cnt[r], perm, flags, k64, pk_aff);   // -E_r (lane 0)
+    __syncthreads();
+    lp_init_consts(g);
+    miller_one(g, P, H[r], F1, B, flg);
+    pair = r;
+  } else {
+    const int q = blk - n_roots;
+    const g2_jac acc = quarter_sum(u.b, slist, ns, flags, FLAG_SUSPECT, k64, sig_aff, q);
+    if (lane_ == 0) X4[q] = acc;
+    __threadfence();
+    __syncthreads();
+    if (lane_ == 0) last = atomicAdd(&xtk[1], 1u) == 3u ? 1u : 0u;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const g2_aff Q = combine_quarters(X4);
+    __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+    lp_init_consts(g);
+    g1_aff G = g1_neg_generator();
+    fp_neg(G.y, G.y);   // +g1
+    miller_one(g, G, Q, F1, B, flg);
+    if (lane_ == 0) xtk[1] = 0u;
+    pair = n_roots;
+  }
+  if (lane_ < 12) ((fp*)&fex[pair])[lane_] = g.s[F1 + lane_];
+  __threadfence();
+  __syncthreads();
+  if (lane_ == 0) last = atomicAdd(&xtk[0], 1u) == (uint32_t)n_roots ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // ftot * prod of the n_roots + 1 exclusion values, ONE final exponentiation
+  const int ACC = F1, IN = F1 + 12;
+  if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)ftot)[lane_];
+  __syncthreads();
+  for (int i = 0; i <= n_roots; ++i) {
+    if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&fex[i])[lane_];
+    __syncthreads();
+    f12_mul(g, ACC, IN, ACC);
+  }
+  f12_final_exp(g, ACC, TMP);
+  const bool pass = f12_slots_one(g, ACC);
+  if (lane_ == 0) { *xok = pass ? 1u : 0u; xtk[0] = 0u; }
+}
+
 // Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
 // e(pk_s, H(r)) * e(-g1, sig_s) == 1 -- exactly the reference's verify, no RLC scalar, no per-share
 // products, one pairing check deep instead of k_fb_sparse + the levels below the root.  Blocks
@@ -317,9 +565,9 @@ __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__
                                       const uint8_t* __restrict__ gv0, const uint32_t* __restrict__ flags,
                                       const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ H,
                                       const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
-                                      uint8_t* __restrict__ verdict) {
+                                      uint8_t* __restrict__ verdict, const uint32_t* __restrict__ xok) {
   using namespace ssb::lane;
-  if (*ok || *nfail > FB_SINGLE_MAX) return;   // uniform
+  if (*ok || *nfail > FB_SINGLE_MAX || (xok && *xok)) return;   // uniform
   __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ uint32_t flg;
   const int lane_ = threadIdx.x;
@@ -354,10 +602,11 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
                                               const uint32_t* __restrict__ flags, const g2_jac* __restrict__ rsig,
                                               const g1_jac* __restrict__ rpk, const g2_aff* __restrict__ H,
                                               const uint8_t* __restrict__ gv_prev, uint8_t* __restrict__ gv_cur,
-                                              uint8_t* __restrict__ verdict, const uint32_t* __restrict__ nfail) {
+                                              uint8_t* __restrict__ verdict, const uint32_t* __restrict__ nfail,
+                                              const uint32_t* __restrict__ xok) {
   using namespace ssb::lane;
-  if (*ok) return;  // uniform: the batch passed
-  if (*nfail <= FB_SINGLE_MAX) return;   // (level 0 ran in k_fb_root; k_fb_single decides few failing shares)   // (k_fb_single decides the few shares of failing roots)
+  if (*ok || (xok && *xok)) return;  // uniform: the batch passed / the committee stage decided it
+  if (*nfail <= FB_SINGLE_MAX) return;   // (level 0 ran in k_fb_root; k_fb_single decides the few shares of failing roots)
   __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ g2_jac red[64];
   __shared__ g1_aff sP;
@@ -450,30 +699,40 @@ int fallback_levels(size_t n) {
   return L;
 }
 
-void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
+void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, const fp12* froot,
-                     const fb_ws& fw, uint8_t* verdict, bool fast_verdicts) {
+                     const fb_ws& fw, uint8_t* verdict, bool fast_verdicts, const fb_jobs& jobs) {
   using namespace ssb::k;
   if (n <= 0 || n_roots <= 0) return;
   auto nb = [](size_t x, unsigned b) { return (unsigned)((x + b - 1) / b); };
   const int L = fallback_levels((size_t)n);
   const int lb = fallback_log2_branch();
+  // the committee stage needs the jobs, the batch check's Miller product and the stage's workspace
+  const bool committee = jobs.n_jobs > 0 && fw.slist && fw.nS && fw.xtk && fw.xok && fw.fex && fw.ftot;
+  const fb_jobs cj = committee ? jobs : fb_jobs{0, nullptr, nullptr, nullptr};
+  const uint32_t* xok = committee ? fw.xok : nullptr;
   const fb_prep_args prep{n_roots, L, lb, share_root, fw.cnt, fw.start, fw.cursor, fw.gst, fw.perm, fw.rtk, fw.nfail};
-  hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + 1), dim3(64), 0, st, n, key, ok, flags, fw.k64,
-                     fast_verdicts ? verdict : (uint8_t*)nullptr, prep);
+  hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + nb((size_t)cj.n_jobs, 64) + 1), dim3(64), 0, st, n, key, ok, flags,
+                     fw.k64, fast_verdicts ? verdict : (uint8_t*)nullptr, prep, cj, sig, fw.slist, fw.nS);
+  if (committee)
+    hipLaunchKernelGGL(k_fb_excl, dim3((unsigned)n_roots + 4 + EX_SINGLE_BLOCKS), dim3(64), 0, st, n_roots, ok,
+                       (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
+                       (const uint32_t*)fw.perm, (const uint32_t*)flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
+                       fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
-                     (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, flags,
-                     (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict);
+                     (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
+                     (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,
+                     committee ? fw.nS : (uint32_t*)nullptr);
   if (L == 1) return;
   {
     const unsigned grid = (unsigned)(n < 2048 ? n : 2048);
     hipLaunchKernelGGL(k_fb_single, dim3(grid), dim3(64), 0, st, n_roots, ok, (const uint32_t*)fw.nfail,
                        (const uint32_t*)fw.start, (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst,
-                       (const uint8_t*)fw.gv0, flags, share_root, H, sig, pk, verdict);
+                       (const uint8_t*)fw.gv0, (const uint32_t*)flags, share_root, H, sig, pk, verdict, xok);
   }
-  hipLaunchKernelGGL(k_fb_sparse, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, n_roots, ok, flags, share_root,
-                     (const uint32_t*)fw.gst, (const uint8_t*)fw.gv0, (const uint64_t*)fw.k64, sig, pk, fw.rsig, fw.rpk,
-                     (const uint32_t*)fw.nfail);
+  hipLaunchKernelGGL(k_fb_sparse, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, n_roots, ok, (const uint32_t*)flags,
+                     share_root, (const uint32_t*)fw.gst, (const uint8_t*)fw.gv0, (const uint64_t*)fw.k64, sig, pk, fw.rsig,
+                     fw.rpk, (const uint32_t*)fw.nfail, xok);
   for (int l = 1; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;
@@ -481,9 +740,9 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
     uint8_t* cur = (l & 1) ? fw.gv1 : fw.gv0;
     const uint8_t* prev = (l & 1) ? fw.gv0 : fw.gv1;
     hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, lb, n_roots, ok, (const uint32_t*)fw.start,
-                       (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, flags,
+                       (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                        (const g2_jac*)fw.rsig, (const g1_jac*)fw.rpk, H, prev, cur, verdict,
-                       (const uint32_t*)fw.nfail);
+                       (const uint32_t*)fw.nfail, xok);
   }
 }
 

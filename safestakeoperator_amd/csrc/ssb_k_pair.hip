@@ -229,6 +229,9 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
     f12_mul(g, ACC, IN, ACC);
   }
   SSB_TRACE(TR_MF_PRODUCT);
+  // the product before the final exponentiation, for the exclusion check of a failed batch
+  // (k_fb_excl: the batch check without its suspect shares, by bilinearity from this value)
+  if (lane_ < 12) ((fp*)&f[npairs + ng])[lane_] = g.s[ACC + lane_];
   f12_final_exp(g, ACC, TMP);
   if (lane_ == 0) {  // == 1, read slot by slot (an fp12 local would sit in scratch)
     bool one = true;

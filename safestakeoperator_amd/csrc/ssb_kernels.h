@@ -115,7 +115,7 @@ __global__ void k_miller_pairs(int npairs, const g1_aff* __restrict__ P, const g
 __global__ void k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out);
 // Miller loops + product tree + final exponentiation in one launch (fused one-stream path):
 // tk: 1 + ceil(npairs / 8) completion tickets (zero on entry, zero again on exit); f: npairs +
-// ceil(npairs / 8) values
+// ceil(npairs / 8) + 1 values (the last: the product before the final exponentiation)
 __global__ void k_miller_final(int npairs, const g1_aff* __restrict__ P, const g2_aff* __restrict__ Q,
                                fp12* __restrict__ f, spec_jobs sj, uint32_t* __restrict__ tk, uint32_t* __restrict__ ok);
 __global__ void k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok, int nv,
@@ -259,12 +259,21 @@ struct fb_ws {
   g2_jac* rsig;
   g1_jac* rpk;
   uint8_t *gv0, *gv1;
+  // the committee stage (aggregate batches on the fused path; all null otherwise): slist n words,
+  // fex n_roots + 1 values, ftot = the batch check's Miller product before the final exponentiation
+  // (k_miller_final), nS / xtk: two words of the slot's ticket block (zero on entry, zeroed again
+  // by their consumers), xok one word
+  uint32_t *slist, *nS, *xtk, *xok;
+  fp12* fex;
+  const fp12* ftot;
 };
+// the jobs of an aggregate batch (share_off, t, ids), for the committee stage of the fallback
+struct fb_jobs { int n_jobs; const uint32_t* off; const uint32_t* tt; const uint64_t* ids; };
 int fallback_log2_branch();
 int fallback_levels(size_t n);
-void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, const uint32_t* flags,
+void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, const fp12* froot,
-                     const fb_ws& fw, uint8_t* verdict, bool fast_verdicts);
+                     const fb_ws& fw, uint8_t* verdict, bool fast_verdicts, const fb_jobs& jobs);
 // first use of a new queue: acquire its scratch for the largest slot kernel while the other queues
 // are idle (ssb_k_combine.hip); synchronous, 0 on success
 int prime_queue(hipStream_t st);

@@ -228,6 +228,15 @@ template <class GR> SSB_INL void f12_cyc_exp_x(GR& g, int r, int f) {
   f12_conj(g, r, r);
 }
 
+// slots d[0..11] = (a[0..5] as an Fp6)^-1 (the w-half zero), on one lane; out of line, so its
+// Fp6 temporaries live in its own frame, not in every kernel that runs a final exponentiation
+SSB_FN void fp6_inv_slots(const lfp* a, lfp* d) {
+  // the slots hold an fp6's fields in order (c0.c0, c0.c1, c1.c0, ..): invert in place through flat
+  // pointers, no copies in a frame
+  fp6_inv(*(fp6*)(d), *(const fp6*)(a));
+  for (int k = 6; k < 12; ++k) d[k] = fp_zero();
+}
+
 // final exponentiation of the Fp12 value at `f` (in place); 7 x 12 work slots at `tmp`.
 // Same chain as ssb::final_exponentiation.
 template <class GR> SSB_INL void f12_final_exp(GR& g, int f, int tmp) {
@@ -238,15 +247,7 @@ template <class GR> SSB_INL void f12_final_exp(GR& g, int f, int tmp) {
   // ~2 KB of private segment per lane, the largest on the batch streams).
   f12_mul(g, f, t0, t2);  // N: slots t2 .. t2+5 (the w-half is zero)
   LP_FOR(1) {
-    if (role == 0) {
-      fp6 x, xi;
-      fp2* v[3] = {&x.c0, &x.c1, &x.c2};
-      for (int k = 0; k < 3; ++k) { v[k]->c0 = g.s[t2 + 2 * k]; v[k]->c1 = g.s[t2 + 2 * k + 1]; }
-      fp6_inv(xi, x);
-      const fp2 w[3] = {xi.c0, xi.c1, xi.c2};
-      for (int k = 0; k < 3; ++k) { g.s[t1 + 2 * k] = w[k].c0; g.s[t1 + 2 * k + 1] = w[k].c1; }
-      for (int k = 6; k < 12; ++k) g.s[t1 + k] = fp_zero();
-    }
+    if (role == 0) fp6_inv_slots(g.s + t2, g.s + t1);
   }
   LP_SYNC();
   f12_mul(g, t1, t0, t1);  // f^-1

@@ -386,14 +386,18 @@ struct verify_ws {
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
   g2_jac* rsig; uint32_t* gst; uint8_t* gv0; uint8_t* gv1;                         // failed-batch group tests
   uint64_t* k64; g2_jac* fbX; uint32_t* rtk; uint32_t* nfail;                                     // (level 0 per root)
+  uint32_t* slist; uint32_t* xok; fp12* fex;                                       // committee stage
   size_t npairs;
 };
 // Miller values of the pairs plus the levels of the 8-ary product tree
 inline size_t fp12_slots(size_t np) {
   size_t tot = np;
   while (np > 8) { np = (np + 7) / 8; tot += np; }
-  return tot + 1;
+  return tot + 2;   // (+ k_miller_final's product before the final exponentiation)
 }
+// the ticket block of the fused path: [0, 4) sort / windows / clears, [4, 5 + ceil(np / 8))
+// k_miller_final's, then the fallback's committee stage: nS (suspects listed), xtk[2]
+inline uint32_t ntk_words(size_t np) { return 4 + 1 + (uint32_t)((np + 7) / 8) + 3; }
 
 size_t verify_ws_bytes(size_t n, size_t n_roots) {
   const msm_plan p = plan_size(n, n_roots);
@@ -407,7 +411,8 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
          3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(n * sizeof(g2_jac)) +
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
-         align_up(n * 8) + align_up(4 * n_roots * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4);
+         align_up(n * 8) + align_up(4 * n_roots * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4) +
+         align_up(n * 4) + align_up(4) + align_up((n_roots + 1) * sizeof(fp12)) + align_up(ntk_words(np) * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) {
@@ -420,7 +425,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.flags = c.take<uint32_t>(n); w.sflags = c.take<uint32_t>(n); w.pflags = c.take<uint32_t>(n);
   w.gflags = c.take<uint32_t>(n); w.gexc = c.take<uint32_t>(n);
   w.f = c.take<fp12>(fp12_slots(np)); w.ok = c.take<uint32_t>(1);
-  w.ntk = 4 + 1 + (uint32_t)((np + 7) / 8);
+  w.ntk = ntk_words(np);
   w.tickets = c.take<uint32_t>(w.ntk);
   w.hws = c.take<char>(launch::hash_ws_bytes(n_roots));
   w.cnt = c.take<uint32_t>(sz.K); w.start = c.take<uint32_t>(sz.K); w.cur = c.take<uint32_t>(sz.K);
@@ -435,6 +440,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
   w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
   w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(4 * n_roots); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
+  w.slist = c.take<uint32_t>(n); w.xok = c.take<uint32_t>(1); w.fex = c.take<fp12>(n_roots + 1);
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
@@ -621,9 +627,18 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
       hipLaunchKernelGGL(k_fallback_lane, dim3((unsigned)std::min<size_t>(n, 1024)), dim3(64), 0, fbs, (int)n, w.ok, w.flags,
                          d_share_root, w.H, w.sig_aff, w.pk_aff, d_verdict);
     else
+    {
+      // the committee stage (fused path of an aggregate batch: its jobs, and k_miller_final's product)
+      const bool cm = miller_final && sj && sj->n_jobs > 0 && !getenv("SSB_NO_COMMITTEE");
+      const uint32_t* ptk = w.tickets + w.ntk - 3;
+      launch::fb_ws fw{w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rtk, w.nfail, w.k64, w.fbX, w.rsig, w.rpk, w.gv0, w.gv1,
+                       cm ? w.slist : nullptr, cm ? (uint32_t*)ptk : nullptr, cm ? (uint32_t*)ptk + 1 : nullptr,
+                       cm ? w.xok : nullptr, cm ? w.fex : nullptr,
+                       cm ? w.f + w.npairs + (w.npairs + 7) / 8 : nullptr};
+      const launch::fb_jobs fj = cm ? launch::fb_jobs{sj->n_jobs, sj->off, sj->tt, sj->ids} : launch::fb_jobs{0, nullptr, nullptr, nullptr};
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, w.f,
-                              launch::fb_ws{w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rtk, w.nfail, w.k64, w.fbX, w.rsig, w.rpk,
-                                            w.gv0, w.gv1}, d_verdict, true);
+                              fw, d_verdict, true, fj);
+    }
   }
   if (!fb_tail && tail != st) {
     SSB_HIP(hipEventRecord(ctx->cur->ev_fin, st));

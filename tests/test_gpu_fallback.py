@@ -1,0 +1,87 @@
+"""GPU: exact verdicts of a FAILED batch on bench.py's timed path (one-stream slots, keys from the
+cache, the fused launches), through each stage of the fallback (csrc/ssb_k_bisect.hip):
+
+  committee stage  a job whose shares break their committee relation (sum_i c_i sig_i != O over t + 1
+                   shares) has its shares checked one by one, and the rest of the batch is decided by
+                   ONE exclusion check (the batch check without the suspects, from its own Miller
+                   product) -- one invalid share, 1% invalid shares, registry operator ids;
+  tree             what the committee stage cannot decide: a faulty operator in every committee (too
+                   many suspects), shares that are invalid but consistent (every share of a job signed
+                   over the wrong root: the exclusion check fails), jobs without redundancy (t = n).
+
+Every verdict, status, error field and combined signature == the plain-C oracle (oracle/bls_c.c) on
+the same bytes, and == the construction truth."""
+import numpy as np
+import pytest
+
+import bench
+from test_gpu_configs import _c_oracle, _cached_one_stream, _check_against_truth
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(engine, wl, V, t, n):
+    runs = _cached_one_stream(engine, wl, V, t, n)
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
+    for out, st, err, ver in runs:
+        assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
+        assert (st == o_st).all() and (err.astype(np.uint64) == o_err.astype(np.uint64)).all()
+        ok = st == 0
+        assert (out[ok] == o_out[ok]).all()
+        _check_against_truth(wl, V, t, n, out, st, err, ver)
+    return o_ver
+
+
+@pytest.mark.parametrize("ids", ["seq", "registry"])
+@pytest.mark.parametrize("case", ["one", "pct1"])
+def test_committee_stage_matches_c_oracle(engine, case, ids):
+    V, t, n, R = 4096, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=21, ids=ids, invalid_count=1 if case == "one" else 0,
+                             invalid_rate=0.01 if case == "pct1" else 0.0)
+    o_ver = _check(engine, wl, V, t, n)
+    assert int((o_ver[:V * n] == 0).sum()) == wl["n_bad"] and wl["n_bad"] >= 1
+
+
+@pytest.mark.parametrize("op", [1, 4])
+def test_bad_operator_matches_c_oracle(engine, op):
+    """Every share of operator `op` invalid in every committee (4,096 suspect jobs: the tree decides)."""
+    V, t, n, R = 4096, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=22, bad_operator=op)
+    o_ver = _check(engine, wl, V, t, n)
+    assert int((o_ver[:V * n] == 0).sum()) == V
+
+
+def test_consistent_invalid_jobs_fall_to_the_tree(engine):
+    """Jobs whose four shares are ALL signed over the wrong root are consistent (the relation holds)
+    yet invalid: the exclusion check fails and the tree decides them exactly; a job with one wrong share
+    beside them is a suspect."""
+    V, t, n, R = 1024, 3, 4, 16
+    wl = bench.make_workload(engine, V, t, n, R, rank=23)
+    # re-sign every share of jobs 5, 77, 900 over the next root, and share 2 of job 300
+    bad_jobs, N = [5, 77, 900], V * n
+    sigs = bytearray(wl["sigs"])
+    shares = []
+    for v in bad_jobs:
+        shares += [(v * n + i, (wl["job_root"][v] + 1) % R) for i in range(n)]
+    shares.append((300 * n + 2, (wl["job_root"][300] + 1) % R))
+    # the shares' secret keys are not kept by make_workload: derive the wrong-root signatures from a
+    # second workload with the same seed whose every share signs the next root
+    wl2 = bench.make_workload(engine, V, t, n, R, rank=23, invalid_rate=1.0)
+    for i, _ in shares:
+        sigs[96 * i:96 * (i + 1)] = wl2["sigs"][96 * i:96 * (i + 1)]
+    wl["sigs"] = bytes(sigs)
+    valid = np.ones(N, dtype=np.uint8)
+    for i, _ in shares:
+        valid[i] = 0
+    wl["valid"] = valid.tolist()
+    o_ver = _check(engine, wl, V, t, n)
+    assert int((o_ver[:N] == 0).sum()) == len(shares)
+
+
+def test_no_redundancy_jobs_fall_to_the_tree(engine):
+    """3-of-3 jobs (an operator offline: no relation to test) with invalid shares: every job is left to
+    the exclusion check, which fails; the tree decides."""
+    V, t, n, R = 2048, 3, 3, 32
+    wl = bench.make_workload(engine, V, t, n, R, rank=24, invalid_count=5)
+    o_ver = _check(engine, wl, V, t, n)
+    assert int((o_ver[:V * n] == 0).sum()) == 5
