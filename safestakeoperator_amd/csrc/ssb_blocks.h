@@ -288,7 +288,7 @@ SSB_INL void select_job(int j, uint32_t n_shares, const uint32_t* __restrict__ o
   if (cnt < t) { status[j] = SSB_DVF_INSUFFICIENT_VALID_SIGNATURES; err[2 * j] = cnt; err[2 * j + 1] = t; return; }
   status[j] = SSB_DVF_OK; err[2 * j] = 0; err[2 * j + 1] = 0;
 }
-SSB_INL void lagrange_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+SSB_FN void lagrange_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                           const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel, fr* __restrict__ lam) {
   const uint32_t b = off[j], t = tt[j];
   uint64_t x[SSB_MAX_T];
@@ -301,22 +301,28 @@ SSB_INL void lagrange_job(int j, const uint32_t* __restrict__ off, const uint32_
 // (hence order-r) point, so sum c_i sig_i with the integer c_i == lambda_i mod r is the reference's
 // combination.  fast[j] = 1 when the job was finished here; the 255-bit path skips those jobs.
 constexpr uint32_t FAST_T = 16;
-// fast[j] = 1 when the job was finished here
-SSB_INL uint32_t combine_fast_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
-                                  const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
-                                  const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
-                                  uint8_t* __restrict__ out96) {
+// The combine of job j after its selection: small-integer Lagrange coefficients (ids 1..n:
+// unit_lagrange_small) finish the job here (returns 1, out96 written); coefficients that are ratios
+// of small integers (registry ids: unit_lagrange_ratio) leave T and the digits of M^-1 in rj[j]
+// (returns 2; k_combine_terms_gls / k_combine_sum finish it); else 0 (the general 255-bit path).
+// One function for both, out of line: one set of per-lane arrays in its own frame.
+SSB_FN uint32_t combine_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                            const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
+                            const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
+                            uint8_t* __restrict__ out96, ratio_job* __restrict__ rj) {
   if (status[j] != SSB_DVF_OK || tt[j] > FAST_T) return 0u;
   const uint32_t t = tt[j], b = off[j];
   uint64_t x[FAST_T];
   int64_t c[FAST_T];
-  const g2_aff* pts[FAST_T];
-  for (uint32_t i = 0; i < t; ++i) { x[i] = ids[sel[b + i]]; pts[i] = &sig_aff[sel[b + i]]; }
-  if (!unit_lagrange_small(c, x, t)) return 0u;
-  uint8_t o[96];
-  unit_combine_small(o, pts, c, t);
-  for (int k = 0; k < 96; ++k) out96[96 * (size_t)j + k] = o[k];
-  return 1u;
+  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
+  if (unit_lagrange_small(c, x, t)) {
+    unit_combine_small_at(out96 + 96 * (size_t)j, sig_aff, sel + b, c, t);
+    return 1u;
+  }
+  uint64_t M;
+  if (!rj || !unit_lagrange_ratio(c, &M, x, t)) return 0u;
+  unit_combine_ratio_at(rj[j], sig_aff, sel + b, c, t, M);
+  return 2u;
 }
 }  // namespace k
 }  // namespace ssb

@@ -66,16 +66,23 @@ __global__ void SSB_LB(64) k_combine_terms_gls(int n, uint32_t n_jobs, const uin
                                               const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                               const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
                                               const uint32_t* __restrict__ skip_if_ok, const uint32_t* __restrict__ fast,
-                                              g2_jac* __restrict__ term) {
+                                              g2_jac* __restrict__ term, const ratio_job* __restrict__ rj) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= 4 * n) return;
   if (skip_if_ok && *skip_if_ok) return;
   const int s = g >> 2, q = g & 3;
   const uint32_t j = share_job[s];
   if (j >= n_jobs) return;   // outside every well-formed job (k_share_map's sentinel)
-  if (fast && fast[j]) return;
+  if (fast && fast[j] == 1u) return;
   const uint32_t k = (uint32_t)s - off[j];
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
+  if (fast && fast[j] == 2u) {   // registry ids: [M^-1] T, one digit per lane, on the job's first share
+    if (k != 0) return;
+    g2_jac r;
+    unit_gls_term(r, rj[j].T, rj[j].d[q], q);
+    term[4 * (size_t)s + q] = r;
+    return;
+  }
   const fr l = lam[s];
   g2_jac r;
   unit_combine_term_gls(r, sig_aff[sel[s]], l.l, q);
@@ -89,10 +96,12 @@ __global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict_
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
-  if (fast && fast[j]) return;
+  if (fast && fast[j] == 1u) return;
   uint8_t o[96];
   if (status[j] == SSB_DVF_OK) {
-    unit_combine_sum(o, term + (size_t)stride * off[j], (uint32_t)stride * tt[j]);  // infinity(t) start (blst.rs:74)
+    // (fast[j] == 2: the four digit terms of [M^-1] T on the job's first share)
+    const uint32_t cnt = (fast && fast[j] == 2u) ? 4u : (uint32_t)stride * tt[j];
+    unit_combine_sum(o, term + (size_t)stride * off[j], cnt);  // infinity(t) start (blst.rs:74)
   } else {
     for (int k = 0; k < 96; ++k) o[k] = 0;
   }
@@ -107,7 +116,7 @@ __global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
-  fast[j] = combine_fast_job(j, off, tt, status, sel, ids, sig_aff, out96);
+  fast[j] = combine_job(j, off, tt, status, sel, ids, sig_aff, out96, nullptr);
 }
 // k_select + k_combine_fast + k_lagrange of one job in one thread (one launch instead of three)
 __global__ void SSB_LB(64) k_select_combine(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off,
@@ -116,12 +125,12 @@ __global__ void SSB_LB(64) k_select_combine(int n_jobs, uint32_t n_shares, const
                                             const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ sel,
                                             int32_t* __restrict__ status, uint64_t* __restrict__ err,
                                             const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ fast,
-                                            uint8_t* __restrict__ out96, fr* __restrict__ lam) {
+                                            uint8_t* __restrict__ out96, fr* __restrict__ lam, ratio_job* __restrict__ rj) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
   select_job(j, n_shares, off, tt, ids, verdict, flags, sel, status, err);
-  const uint32_t f = combine_fast_job(j, off, tt, status, sel, ids, sig_aff, out96);
+  const uint32_t f = combine_job(j, off, tt, status, sel, ids, sig_aff, out96, rj);
   fast[j] = f;
   if (!f && status[j] == SSB_DVF_OK) lagrange_job(j, off, tt, ids, sel, lam);
 }

@@ -13,6 +13,16 @@
 namespace ssb {
 namespace k {
 
+// the speculative a-1 scan + combine of job j (candidate flags as verdicts), out of line: its
+// temporaries live in its own frame, not in the Miller blocks' (every kernel's private segment sets
+// the scratch each slot queue reserves)
+SSB_FN void spec_job(int j, const spec_jobs& sj) {
+  select_job(j, sj.n_shares, sj.off, sj.tt, sj.ids, (const uint8_t*)nullptr, sj.flags, sj.sel, sj.status, sj.err);
+  const uint32_t fj = combine_job(j, sj.off, sj.tt, sj.status, sj.sel, sj.ids, sj.sig_aff, sj.out96, sj.rj);
+  sj.fast[j] = fj;
+  if (!fj && sj.status[j] == SSB_DVF_OK) lagrange_job(j, sj.off, sj.tt, sj.ids, sj.sel, sj.lam);
+}
+
 // ---- lane-program versions (straight-line programs of gen_lane_progs.py, G = 64) ----
 constexpr int ML_S0 = lane::MILLER_ITER_SCRATCH > lane::MILLER_ADDSTEP_SCRATCH ? lane::MILLER_ITER_SCRATCH
                                                                                : lane::MILLER_ADDSTEP_SCRATCH;
@@ -29,10 +39,7 @@ __global__ void SSB_LB(64) k_miller_pairs(int npairs, const g1_aff* __restrict__
   if (p >= npairs) {   // the speculative a-1 scan + combine, 64 jobs per block (candidate flags as verdicts)
     const int j = (p - npairs) * 64 + lane_;
     if (j >= sj.n_jobs) return;
-    select_job(j, sj.n_shares, sj.off, sj.tt, sj.ids, (const uint8_t*)nullptr, sj.flags, sj.sel, sj.status, sj.err);
-    const uint32_t fj = combine_fast_job(j, sj.off, sj.tt, sj.status, sj.sel, sj.ids, sj.sig_aff, sj.out96);
-    sj.fast[j] = fj;
-    if (!fj && sj.status[j] == SSB_DVF_OK) lagrange_job(j, sj.off, sj.tt, sj.ids, sj.sel, sj.lam);
+    spec_job(j, sj);
     return;
   }
   const g1_aff P = Pa[p];
@@ -175,10 +182,7 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
   if (p >= npairs) {   // the speculative a-1 scan + combine, 64 jobs per block (candidate flags as verdicts)
     const int j = (p - npairs) * 64 + lane_;
     if (j >= sj.n_jobs) return;
-    select_job(j, sj.n_shares, sj.off, sj.tt, sj.ids, (const uint8_t*)nullptr, sj.flags, sj.sel, sj.status, sj.err);
-    const uint32_t fj = combine_fast_job(j, sj.off, sj.tt, sj.status, sj.sel, sj.ids, sj.sig_aff, sj.out96);
-    sj.fast[j] = fj;
-    if (!fj && sj.status[j] == SSB_DVF_OK) lagrange_job(j, sj.off, sj.tt, sj.ids, sj.sel, sj.lam);
+    spec_job(j, sj);
     return;
   }
   lp_init_consts(g);

@@ -48,6 +48,7 @@ struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
 struct spec_jobs {
   int n_jobs; uint32_t n_shares; const uint32_t* off; const uint32_t* tt; const uint64_t* ids; const uint32_t* flags;
   uint32_t* sel; int32_t* status; uint64_t* err; const g2_aff* sig_aff; uint32_t* fast; uint8_t* out96; fr* lam;
+  ratio_job* rj;   // registry ids: the ratio path's per-job T and digits (fast[j] == 2)
 };
 
 // share -> (job, root) of an aggregate batch (share_lookup, ssb_blocks.h)
@@ -147,7 +148,8 @@ __global__ void k_combine_terms_gls(int n, uint32_t n_jobs, const uint32_t* __re
                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                     const uint32_t* __restrict__ sel, const fr* __restrict__ lam,
                                     const g2_aff* __restrict__ sig_aff, const uint32_t* __restrict__ skip_if_ok,
-                                    const uint32_t* __restrict__ fast, g2_jac* __restrict__ term);
+                                    const uint32_t* __restrict__ fast, g2_jac* __restrict__ term,
+                                    const ratio_job* __restrict__ rj);
 __global__ void k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
@@ -158,7 +160,7 @@ __global__ void k_select_combine(int n_jobs, uint32_t n_shares, const uint32_t* 
                                  const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ sel,
                                  int32_t* __restrict__ status, uint64_t* __restrict__ err,
                                  const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ fast,
-                                 uint8_t* __restrict__ out96, fr* __restrict__ lam);
+                                 uint8_t* __restrict__ out96, fr* __restrict__ lam, ratio_job* __restrict__ rj);
 __global__ void k_combine_fast(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,

@@ -162,14 +162,17 @@ SSB_INL uint64_t gls_digit(const uint32_t* k8, int q) {
   }
   return rem;
 }
-SSB_FN void unit_combine_term_gls(g2_jac& r, const g2_aff& sig, const uint32_t* lam8, int q) {
+// [d] (+-psi^q(p)) -- digit q of a GLS split (sign as above); p in G2
+SSB_FN void unit_gls_term(g2_jac& r, const g2_aff& sig, uint64_t d, int q) {
   if (sig.inf) { jac_set_inf(r); return; }
-  const uint64_t d = gls_digit(lam8, q);
   g2_aff p = sig;
   for (int i = 0; i < q; ++i) g2_psi_aff(p, p);
   if (q & 1) fp2_neg(p.y, p.y);
   const uint32_t dw[2] = {(uint32_t)d, (uint32_t)(d >> 32)};
   jac_mul_aff(r, p, dw, 2);
+}
+SSB_FN void unit_combine_term_gls(g2_jac& r, const g2_aff& sig, const uint32_t* lam8, int q) {
+  unit_gls_term(r, sig, gls_digit(lam8, q), q);
 }
 
 // unit "combine_sum": sum of t terms, affine, compressed (src/crypto/impls/blst.rs:74-86)
@@ -277,6 +280,84 @@ SSB_FN void unit_combine_small(uint8_t* out96, const g2_aff* const* pts, const i
   }
   g2_aff a; jac_to_aff(a, acc);
   g2_compress(out96, a);
+}
+// the same, the points read as pts[idx[i]] (the device path: no array of point pointers in a frame)
+SSB_INL void combine_small_jac(g2_jac& acc, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
+                               const int64_t* c, uint32_t t) {
+  int nb = 0;
+  for (uint32_t i = 0; i < t; ++i) {
+    const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
+    const int b = m ? 64 - __builtin_clzll(m) : 0;
+    nb = b > nb ? b : nb;
+  }
+  jac_set_inf(acc);
+  for (int b = nb - 1; b >= 0; --b) {
+    jac_dbl_inl(acc, acc);
+    for (uint32_t i = 0; i < t; ++i) {
+      const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
+      if ((m >> b) & 1ull) {
+        g2_aff q = pts[idx[i]];
+        if (c[i] < 0) fp2_neg(q.y, q.y);
+        jac_add_aff_inl(acc, acc, q);
+      }
+    }
+  }
+}
+SSB_FN void unit_combine_small_at(uint8_t* out96, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
+                                  const int64_t* c, uint32_t t) {
+  g2_jac acc;
+  combine_small_jac(acc, pts, idx, c, t);
+  g2_aff a; jac_to_aff(a, acc);
+  g2_compress(out96, a);
+}
+
+// ---- registry-id Lagrange path ---------------------------------------------------------------
+// Operator ids from the registry contract (src/node/node.rs:470-474) are arbitrary u64 (small in
+// practice: < 2^16), so lambda_i is not an integer; it is a RATIO of small integers:
+//     lambda_i = N_i / D_i,  N_i = prod_{j != i} x_j,  D_i = prod_{j != i} (x_j - x_i)
+// (src/crypto/impls/blst.rs:19-39).  With M = lcm_i |D_i|: lambda_i = c_i / M, c_i = N_i (M / D_i),
+// and for points of order r
+//     sum_i lambda_i sig_i = [M^-1 mod r] (sum_i c_i sig_i)
+// -- t products with small scalars (ids < 2^16, t = 3: |c_i| < 2^48) and ONE 255-bit product per job
+// (its four GLS digits, unit_gls_term) instead of t of them.  Returns false when a value does not
+// fit 62 bits, or ids repeat (the general path then runs).
+SSB_FN bool unit_lagrange_ratio(int64_t* c, uint64_t* M, const uint64_t* x, uint32_t t) {
+  int64_t L = 1;
+  for (uint32_t i = 0; i < t; ++i) {
+    if (x[i] >= (1ull << 62)) return false;
+    int64_t d = 1;
+    for (uint32_t j = 0; j < t; ++j) {
+      if (j == i) continue;
+      const int64_t df = (int64_t)x[j] - (int64_t)x[i];
+      if (df == 0 || __builtin_mul_overflow(d, df, &d)) return false;
+    }
+    const int64_t a = d < 0 ? -d : d, g = i64_gcd(L, a);
+    if (__builtin_mul_overflow(L / g, a, &L) || L >= (1ll << 62)) return false;
+  }
+  for (uint32_t i = 0; i < t; ++i) {
+    int64_t d = 1, nn = 1;
+    for (uint32_t j = 0; j < t; ++j) {
+      if (j == i) continue;
+      d *= (int64_t)x[j] - (int64_t)x[i];   // (fits: checked above)
+      if (__builtin_mul_overflow(nn, (int64_t)x[j], &nn)) return false;
+    }
+    if (__builtin_mul_overflow(nn, L / d, &c[i]) || c[i] >= (1ll << 62) || c[i] <= -(1ll << 62)) return false;
+  }
+  *M = (uint64_t)L;
+  return true;
+}
+// the per-job result of the ratio path: T = sum c_i sig_i (affine) and the GLS digits of M^-1 mod r
+struct ratio_job { g2_aff T; uint64_t d[4]; };
+SSB_FN void unit_combine_ratio_at(ratio_job& out, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
+                                  const int64_t* c, uint32_t t, uint64_t M) {
+  g2_jac acc;
+  combine_small_jac(acc, pts, idx, c, t);
+  jac_to_aff(out.T, acc);
+  fr mi, mc;
+  fr_from_u64(mi, M);
+  fr_inv(mi, mi);
+  fr_from_mont(mc, mi);
+  for (int q = 0; q < 4; ++q) out.d[q] = gls_digit(mc.l, q);
 }
 
 }  // namespace ssb

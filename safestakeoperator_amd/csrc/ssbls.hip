@@ -966,7 +966,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   const size_t n = n_shares;
   size_t need = verify_ws_bytes(n, n_roots) + align_up(n * 4) * 3 + align_up(n) + align_up(n * sizeof(fr)) +
-                align_up(4 * n * sizeof(g2_jac)) + align_up(n_jobs * 4);
+                align_up(4 * n * sizeof(g2_jac)) + align_up(n_jobs * 4) + align_up(n_jobs * sizeof(ratio_job));
   if ((rc = ensure_ws(ctx, need, true))) return rc;
   hipStream_t user = (hipStream_t)stream;
   const bool on_slot = post_on_slot(ctx->cur);
@@ -986,6 +986,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
+  ratio_job* rjb = getenv("SSB_NO_RATIO") ? nullptr : c.take<ratio_job>(n_jobs);   // registry ids (unit_lagrange_ratio)
   // share -> (job, root): in the decode launch on the fused path, else a launch of its own
   const bool fmap = fused_sort_path(ctx->cur, n, n_roots, pre);
   const job_map jm{(int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root};
@@ -997,14 +998,14 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     { timed tm(ctx, "k_combine_fast", sc);   // select + small-integer combine + Lagrange, one launch
       hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, (uint32_t)n, share_off, t, ids,
                          (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err, w.sig_aff, fast,
-                         out_sig96, lam); }
-    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term); }
+                         out_sig96, lam, rjb); }
+    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term, (const ratio_job*)rjb); }
     { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
   // one-stream slots: the speculative pass rides in the window-sum launch (msm_both), no stream
   const spec_jobs sj{(int)n_jobs, (uint32_t)n, share_off, t, ids, w.flags, sel, out_status, out_err, w.sig_aff, fast,
-                     out_sig96, lam};
+                     out_sig96, lam, rjb};
   bool spec_in_window = false;
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict,
                        [&] { if (!on_slot) spec(); }, tl, on_slot ? &sj : nullptr, &spec_in_window, fmap ? &jm : nullptr)))
@@ -1019,15 +1020,15 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   if (on_slot) {
     timed tm(ctx, "k_combine_fast", st);
     hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids,
-                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam);
+                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam, rjb);
   } else {
     hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids,
-                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam);
+                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam, rjb);
   }
   // (after a speculative pass in the window launch the general combine of the jobs the small-
   // integer path did not finish still follows here, on whichever selection stands)
   const uint32_t* gate2 = spec_in_window ? nullptr : gate;
-  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term);
+  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term, (const ratio_job*)rjb);
   hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate2, (const uint32_t*)fast, out_sig96, 4);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));

@@ -85,3 +85,14 @@ def test_no_redundancy_jobs_fall_to_the_tree(engine):
     wl = bench.make_workload(engine, V, t, n, R, rank=24, invalid_count=5)
     o_ver = _check(engine, wl, V, t, n)
     assert int((o_ver[:V * n] == 0).sum()) == 5
+
+
+@pytest.mark.parametrize("t,n,V", [(3, 4, 4096), (5, 7, 1024)], ids=["3of4_full_c2", "5of7"])
+def test_registry_ids_match_c_oracle(engine, t, n, V):
+    """Registry operator ids (distinct pseudo-random ids in [1, 2^16) per committee, src/node/node.rs:470-474):
+    the Lagrange coefficients are ratios of small integers.  3-of-4: the ratio path (T = sum c_i sig_i,
+    [M^-1] T by four GLS digits); 5-of-7: coefficients past 62 bits, the general 255-bit path.  Every
+    status, verdict and combined signature == the C oracle."""
+    wl = bench.make_workload(engine, V, t, n, 64, rank=25, ids="registry")
+    assert len(set(wl["ids"][:n])) == n and max(wl["ids"]) > n
+    _check(engine, wl, V, t, n)
