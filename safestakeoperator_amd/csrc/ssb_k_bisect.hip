@@ -39,32 +39,55 @@ using launch::fb_jobs;
 constexpr uint32_t FB_SUSPECT_MAX = 2048;
 constexpr unsigned EX_SINGLE_BLOCKS = 512;
 
-// One workgroup (the last block of k_fb_rlc's grid): counting sort of the shares by root (cnt,
-// start, perm) and the group starts of every level (gst[l][r], n_roots + 1 words per level); it
-// also zeroes k_fb_root's per-root tickets.  Phases separated by workgroup barriers (global atomics
-// and stores of one workgroup are ordered by them).  (It used to be a launch of its own, k_fb_prep:
-// one more no-op launch on every passing batch's tail.)
+// One workgroup (the last block of k_fb_rlc's grid): counting sort of the shares by (root, operator-id
+// bucket) -- key = root * NB + bucket(id), NB = fb_nbuckets(n_roots) -- into perm, the per-key
+// segments (kcnt, kstart) and the per-root ones they nest in (cnt, start), and the group starts of
+// every tree level (gst[l][r], n_roots + 1 words per level); it also zeroes k_fb_root's per-root
+// tickets.  Inside a root the shares of one operator id are contiguous: the committee stage's group
+// tests (a faulty operator's shares fail together) and the tree's level groups (any order is valid
+// for them) use the same permutation.  Phases separated by workgroup barriers (global atomics and
+// stores of one workgroup are ordered by them).
 struct fb_prep_args { int n_roots, L, lb; const uint32_t* share_root; uint32_t* cnt; uint32_t* start; uint32_t* cursor;
-                      uint32_t* gst; uint32_t* perm; uint32_t* rtk; uint32_t* nfail; };
+                      uint32_t* gst; uint32_t* perm; uint32_t* rtk; uint32_t* nfail; const uint64_t* ids;
+                      uint32_t* kcnt; uint32_t* kstart; };
+SSB_INL uint32_t fb_bucket(uint64_t id, int nb) {
+  return nb > 1 ? (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> 60) & (uint32_t)(nb - 1) : 0u;
+}
 SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   const int t = threadIdx.x, NT = blockDim.x, n_roots = a.n_roots, L = a.L, lb = a.lb;
+  const int NB = a.ids && a.kcnt ? launch::fb_nbuckets(n_roots) : 1;
+  const int K = n_roots * NB;
   const uint32_t* __restrict__ share_root = a.share_root;
   uint32_t* __restrict__ cnt = a.cnt;
   uint32_t* __restrict__ start = a.start;
   uint32_t* __restrict__ cursor = a.cursor;
   uint32_t* __restrict__ gst = a.gst;
   uint32_t* __restrict__ perm = a.perm;
-  for (int r = t; r < n_roots; r += NT) { cnt[r] = 0u; a.rtk[r] = 0u; }
+  uint32_t* __restrict__ kc = NB > 1 ? a.kcnt : cnt;       // per-key counts (the roots' when NB == 1)
+  uint32_t* __restrict__ ks = NB > 1 ? a.kstart : start;
+  auto key = [&](int s) { return share_root[s] * (uint32_t)NB + (NB > 1 ? fb_bucket(a.ids[s], NB) : 0u); };
+  for (int k = t; k < K; k += NT) kc[k] = 0u;
+  for (int r = t; r < n_roots; r += NT) a.rtk[r] = 0u;
   if (t == 0) *a.nfail = 0u;
   __syncthreads();
   for (int s = t; s < n; s += NT)
-    if (share_root[s] < (uint32_t)n_roots) atomicAdd(&cnt[share_root[s]], 1u);
+    if (share_root[s] < (uint32_t)n_roots) atomicAdd(&kc[key(s)], 1u);
   __syncthreads();
   if (t == 0) {
     uint32_t acc = 0;
-    for (int r = 0; r < n_roots; ++r) { start[r] = acc; cursor[r] = acc; acc += cnt[r]; }
-  } else if (t <= L) {
-    const int l = t - 1;
+    for (int k = 0; k < K; ++k) { ks[k] = acc; cursor[k] = acc; acc += kc[k]; }
+  }
+  __syncthreads();
+  if (NB > 1)
+    for (int r = t; r < n_roots; r += NT) {
+      uint32_t c = 0;
+      for (int b = 0; b < NB; ++b) c += kc[r * NB + b];
+      cnt[r] = c;
+      start[r] = ks[r * NB];
+    }
+  __syncthreads();
+  if (t < L) {
+    const int l = t;
     const uint32_t lg = (uint32_t)(lb * (L - 1 - l));   // Gs_l = 2^lg
     uint32_t* g = gst + (size_t)l * (n_roots + 1);
     uint32_t acc = 0;
@@ -74,9 +97,8 @@ SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
     }
     g[n_roots] = acc;
   }
-  __syncthreads();
   for (int s = t; s < n; s += NT)
-    if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[share_root[s]], 1u)] = (uint32_t)s;
+    if (share_root[s] < (uint32_t)n_roots) perm[atomicAdd(&cursor[key(s)], 1u)] = (uint32_t)s;
 }
 // ---- committee stage (aggregate batches): consistency of each job's shares ------------------------
 // All valid shares of a job lie on one polynomial of degree t - 1 (generic_threshold.rs:59-80: the
@@ -156,6 +178,63 @@ SSB_INL void consist_job(int j, uint32_t n, const fb_jobs& jb, uint32_t* __restr
       const uint32_t k = atomicAdd(nS, 1u);
       if (k < FB_SUSPECT_MAX) slist[k] = s;
     }
+}
+
+// sum_i c_i P_i == O for the points P_i = pts[i < m - 1 ? base[i] : extra] (signed binary, shared
+// doublings) -- a committee relation over t + 1 shares, in G1 (public keys) or G2 (signatures)
+template <class F>
+SSB_INL bool rel_holds(const aff<F>* __restrict__ pts, const uint32_t* base, uint32_t extra, const int64_t* c, int m) {
+  uint64_t mx = 0;
+  for (int i = 0; i < m; ++i) { const uint64_t v = (uint64_t)(c[i] < 0 ? -c[i] : c[i]); mx = v > mx ? v : mx; }
+  const int nbits = mx ? 64 - __builtin_clzll(mx) : 0;
+  jac<F> acc;
+  jac_set_inf(acc);
+  for (int bit = nbits - 1; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    for (int i = 0; i < m; ++i) {
+      const uint64_t v = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
+      if ((v >> bit) & 1ull) {
+        aff<F> q = pts[i < m - 1 ? base[i] : extra];
+        if (c[i] < 0) f_neg(q.y, q.y);
+        jac_add_aff(acc, acc, q);
+      }
+    }
+  }
+  return jac_is_inf(acc);
+}
+// Group-test mode, after the group tests: job j's undecided candidates from the relations.  With t
+// shares of the job PROVEN valid (passing groups: sig_i = s_i H, pk_i = s_i g1) and the public-key
+// relation over them and share u holding (pk_u = s'_u g1 with s'_u the interpolated share), share u is
+// valid -- e(pk_u, H) == e(g1, sig_u) -- exactly when sig_u = s'_u H, i.e. when the signature relation
+// holds (c_u != 0 mod r: |c_u| < 2^62).  So the verdict of u follows without a pairing; a faulty
+// operator's share in every committee is decided this way.  Without t proven shares, or when the
+// key relation fails, u is left to its single check.
+SSB_FN void deduce_job(int j, uint32_t n, const fb_jobs& jb, uint32_t* __restrict__ flags, uint8_t* __restrict__ verdict,
+                       const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff) {
+  const uint32_t b = jb.off[j], e = jb.off[j + 1], t = jb.tt[j];
+  if (e < b || e > n || t == 0 || t > (uint32_t)REL_TMAX) return;
+  uint32_t base[REL_TMAX];
+  uint32_t nb = 0;
+  bool open = false;
+  for (uint32_t s = b; s < e; ++s) {
+    const uint32_t f = flags[s];
+    if (!(f & FLAG_CANDIDATE)) continue;
+    if (!(f & FLAG_DECIDED)) { open = true; continue; }
+    if (verdict[s] && nb < t) base[nb++] = s;
+  }
+  if (!open || nb < t) return;
+  uint64_t x[REL_TMAX + 1];
+  int64_t c[REL_TMAX + 1];
+  for (uint32_t i = 0; i < t; ++i) x[i] = jb.ids[base[i]];
+  for (uint32_t s = b; s < e; ++s) {
+    const uint32_t f = flags[s];
+    if (!(f & FLAG_CANDIDATE) || (f & FLAG_DECIDED)) continue;
+    x[t] = jb.ids[s];
+    if (!rel_coeffs(c, x, (int)t + 1)) continue;
+    if (!rel_holds<fp>(pk_aff, base, s, c, (int)t + 1)) continue;
+    verdict[s] = rel_holds<fp2>(sig_aff, base, s, c, (int)t + 1) ? 1 : 0;
+    atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
+  }
 }
 
 // Threads [0, n): the candidates' RLC scalars k64[s] (the main check's own, rlc_scalar_odd).  With
@@ -244,7 +323,7 @@ SSB_INL bool f12_slots_one(const lane::grp& g, int F) {
 
 // e(P, h) * e(-g1, Q) == 1 with the workgroup's lane programs (one two-pair loop when both pairs are
 // finite; e(O, .) = e(., O) = 1), then the final exponentiation.  Uniform per workgroup.
-SSB_INL bool pair_check(lane::grp& g, const g1_aff& P, const g2_aff& Q, const g2_aff& h, int F1, int B, int BP, int TMP) {
+SSB_FN bool pair_check(lane::grp& g, const g1_aff& P, const g2_aff& Q, const g2_aff& h, int F1, int B, int BP, int TMP) {
   using namespace ssb::lane;
   const int lane_ = threadIdx.x;
   const g1_aff ng = g1_neg_generator();
@@ -288,11 +367,12 @@ SSB_INL g2_jac shfl_down_g2(const g2_jac& p, int off) { return shfl_down_pt(p, o
 // the shares are sorted into 64 buckets (4 windows x 16 digits) in LDS, chunk by chunk; lane (w, d)
 // sums bucket d of window w; a 16-lane suffix scan and tree give W = sum_d d B_d; lanes 0, 16, 32, 48
 // shift and add.  Result in lane 0.  Shares without `need` in their flags are skipped.
-SSB_FN g2_jac quarter_sum(fr_bucket_lds& ub, const uint32_t* __restrict__ list, uint32_t nr,
-                           const uint32_t* __restrict__ flags, uint32_t need, const uint64_t* __restrict__ k64,
-                           const g2_aff* __restrict__ sig_aff, int q) {
+template <class F>
+SSB_FN jac<F> quarter_sum(fr_bucket_lds& ub, const uint32_t* __restrict__ list, uint32_t nr,
+                          const uint32_t* __restrict__ flags, uint32_t need, const uint64_t* __restrict__ k64,
+                          const aff<F>* __restrict__ pts, int q) {
   const int lane_ = threadIdx.x, wl = lane_ >> 4, d = lane_ & 15;
-  g2_jac acc;
+  jac<F> acc;
   jac_set_inf(acc);
   for (uint32_t c0 = 0; c0 < nr; c0 += FR_CHUNK) {
     const uint32_t m = nr - c0 < (uint32_t)FR_CHUNK ? nr - c0 : (uint32_t)FR_CHUNK;
@@ -321,28 +401,39 @@ SSB_FN g2_jac quarter_sum(fr_bucket_lds& ub, const uint32_t* __restrict__ list, 
     }
     __syncthreads();
     const uint32_t e = ub.off[lane_] + ub.cnt[lane_];
-    for (uint32_t i = ub.off[lane_]; i < e; ++i) { const g2_aff p = sig_aff[ub.list[i]]; jac_add_aff_inl(acc, acc, p); }
+    for (uint32_t i = ub.off[lane_]; i < e; ++i) { const aff<F> p = pts[ub.list[i]]; jac_add_aff_inl(acc, acc, p); }
     __syncthreads();
   }
   // W_w = sum_d d B_{w,d}: suffix sums S_d = sum_{d' >= d} B_{w,d'} over the window's 16 lanes (lane
   // d = 0 holds no bucket), then the sum of S_1 .. S_15
   for (int off = 1; off < 16; off <<= 1) {
-    const g2_jac o = shfl_down_g2(acc, off);
+    const jac<F> o = shfl_down_pt(acc, off);
     if (d + off < 16) jac_add_inl(acc, acc, o);
   }
   if (d == 0) jac_set_inf(acc);
   for (int h = 8; h >= 1; h >>= 1) {
-    const g2_jac o = shfl_down_g2(acc, h);
+    const jac<F> o = shfl_down_pt(acc, h);
     if (d < h) jac_add_inl(acc, acc, o);
   }
   // X_q = sum_w 2^(4w) W_{4q+w}  (lanes 0, 16, 32, 48)
   if (d == 0) for (int i = 0; i < 4 * wl; ++i) jac_dbl_inl(acc, acc);
   for (int h = 32; h >= 16; h >>= 1) {
-    const g2_jac o = shfl_down_g2(acc, h);
+    const jac<F> o = shfl_down_pt(acc, h);
     if (lane_ < h && d == 0) jac_add_inl(acc, acc, o);
   }
   return acc;
 }
+// S = 2^16 S + X (q < 3) or S + X (q == 3): the group tests' Horner step over the quarters, lane 0,
+// both points in LDS
+template <class F>
+SSB_FN void horner_step(jac<F>* __restrict__ S, const jac<F>* __restrict__ X, int q) {
+  jac<F> a = *S;
+  if (q < 3) for (int i = 0; i < 16; ++i) jac_dbl_inl(a, a);
+  const jac<F> x = *X;
+  jac_add_inl(a, a, x);
+  *S = a;
+}
+
 // sum_q 2^(16q) X[q] (q < 4), affine, in lane 0 (Q.inf on the other lanes)
 SSB_FN g2_aff combine_quarters(const g2_jac* __restrict__ X) {
   const int lane_ = threadIdx.x;
@@ -389,13 +480,20 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
                                      const g2_aff* __restrict__ sig_aff, const fp12* __restrict__ froot,
                                      g2_jac* __restrict__ X, uint32_t* __restrict__ rtk, uint8_t* __restrict__ gv0,
                                      uint32_t* __restrict__ nfail, uint8_t* __restrict__ verdict, int n,
-                                     const uint32_t* __restrict__ xok, uint32_t* __restrict__ nS) {
+                                     const uint32_t* __restrict__ xok, uint32_t* __restrict__ nS, fb_jobs jobs,
+                                     const g1_aff* __restrict__ pk_aff) {
   using namespace ssb::lane;
   if (*ok) return;   // uniform: the batch passed
   if (nS && blockIdx.x == 0 && threadIdx.x == 0) *nS = 0u;   // (k_fb_excl, the last reader, has finished)
-  if (xok && *xok) {   // the committee stage decided every candidate: the non-suspects passed
+  const uint32_t xv = xok ? *xok : 0u;
+  if (xv == 1u) {   // the exclusion check passed: the non-suspects are valid (the suspects were checked alone)
     for (int s = blockIdx.x * 64 + threadIdx.x; s < n; s += gridDim.x * 64)
       if ((flags[s] & (FLAG_CANDIDATE | FLAG_SUSPECT)) == FLAG_CANDIDATE) verdict[s] = 1;
+    return;
+  }
+  if (xv == 2u) {   // group-test mode: the undecided shares of every job from its relations
+    for (int j = blockIdx.x * 64 + threadIdx.x; j < jobs.n_jobs; j += gridDim.x * 64)
+      deduce_job(j, (uint32_t)n, jobs, (uint32_t*)flags, verdict, sig_aff, pk_aff);
     return;
   }
   const int r = blockIdx.x >> 2, q = blockIdx.x & 3;
@@ -405,7 +503,7 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
   __shared__ fr_lds u;
   __shared__ uint32_t flg, last;
   const int lane_ = threadIdx.x;
-  const g2_jac acc = quarter_sum(u.b, perm + sb, nr, flags, FLAG_CANDIDATE, k64, sig_aff, q);
+  const g2_jac acc = quarter_sum<fp2>(u.b, perm + sb, nr, flags, FLAG_CANDIDATE, k64, sig_aff, q);
   if (lane_ == 0) X[4 * r + q] = acc;
   __threadfence();
   __syncthreads();
@@ -476,72 +574,127 @@ SSB_FN g1_aff neg_suspect_sum(uint32_t sb, uint32_t nr, const uint32_t* __restri
 //     (blocks n_roots + 4 ..).
 // The pair blocks finish with completion tickets (xtk[0]: pairs, xtk[1]: X's quarters); the last
 // pair multiplies ftot by the n_roots + 1 Miller values and runs ONE final exponentiation.
-__global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nS,
-                                     const uint32_t* __restrict__ slist, const uint32_t* __restrict__ start,
-                                     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
-                                     const uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
-                                     const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
-                                     const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H,
-                                     const fp12* __restrict__ ftot, fp12* __restrict__ fex, g2_jac* __restrict__ X4,
-                                     uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict) {
+// (the roles of k_fb_excl are out of line: each role's temporaries live in its own frame, and the
+// kernel's private segment is the largest role's, not their sum)
+struct ex_lds { fr_lds u; uint32_t flg, last, ncand; g1_aff sP; g2_aff sQ; g2_jac S2, X2; g1_jac S1, X1; };
+SSB_FN void ex_groups(ex_lds& L, int n_roots, const uint32_t* __restrict__ perm, uint32_t* __restrict__ flags,
+                      const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
+                      const g2_aff* __restrict__ H, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ kcnt,
+                      const uint32_t* __restrict__ kstart) {
   using namespace ssb::lane;
-  if (*ok) return;   // uniform: the batch passed
-  const uint32_t ns = *nS;
-  const int blk = blockIdx.x, lane_ = threadIdx.x;
-  if (ns == 0 || ns > FB_SUSPECT_MAX) {   // nothing to exclude / too many suspects: the tree decides
-    if (blk == 0 && lane_ == 0) *xok = 0u;
-    return;
-  }
-  __shared__ fr_lds u;
-  __shared__ uint32_t flg, last;
-  grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  const int lane_ = threadIdx.x;
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
   const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
-  if (blk >= n_roots + 4) {   // the suspects, one pairing check each
-    bool init = false;
-    for (uint32_t x = (uint32_t)(blk - n_roots - 4); x < ns; x += gridDim.x - (unsigned)(n_roots + 4)) {
-      const uint32_t s = slist[x];
-      const uint32_t r = share_root[s];
-      if (!init) { lp_init_consts(g); init = true; }
-      const bool pass = pair_check(g, pk_aff[s], sig_aff[s], H[r], F1, B, BP, TMP);
-      if (lane_ == 0) verdict[s] = pass ? 1 : 0;
+  const int NB = launch::fb_nbuckets(n_roots);
+  const uint32_t K = (uint32_t)n_roots * (uint32_t)NB;
+  for (uint32_t key = blockIdx.x; key < K; key += gridDim.x) {
+    const uint32_t gn = kcnt[key];
+    if (!gn) continue;
+    const uint32_t* list = perm + kstart[key];
+    const int r = (int)(key / (uint32_t)NB);
+    if (lane_ == 0) L.ncand = 0u;
+    __syncthreads();
+    uint32_t nc = 0;
+    for (uint32_t x = lane_; x < gn; x += 64) nc += (flags[list[x]] & FLAG_CANDIDATE) ? 1u : 0u;
+    if (nc) atomicAdd(&L.ncand, nc);
+    __syncthreads();
+    const uint32_t m = L.ncand;
+    if (!m) continue;
+    // G2 then G1 sums, each the Horner combination of its four 16-bit quarters (lane 0; the points
+    // stay in LDS)
+    if (lane_ == 0) { jac_set_inf(L.S2); jac_set_inf(L.S1); }
+    for (int q = 3; q >= 0; --q) {
+      const g2_jac x2 = quarter_sum<fp2>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, sig_aff, q);
+      if (lane_ == 0) { L.X2 = x2; horner_step<fp2>(&L.S2, &L.X2, q); }
+      __syncthreads();
     }
-    return;
+    for (int q = 3; q >= 0; --q) {
+      const g1_jac x1 = quarter_sum<fp>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, pk_aff, q);
+      if (lane_ == 0) { L.X1 = x1; horner_step<fp>(&L.S1, &L.X1, q); }
+      __syncthreads();
+    }
+    if (lane_ == 0) { jac_to_aff(L.sQ, L.S2); jac_to_aff(L.sP, L.S1); }
+    __syncthreads();
+    lp_init_consts(g);
+    const bool pass = pair_check(g, L.sP, L.sQ, H[r], F1, B, BP, TMP);
+    if (pass || m == 1)
+      for (uint32_t x = lane_; x < gn; x += 64) {
+        const uint32_t s = list[x];
+        if (!(flags[s] & FLAG_CANDIDATE)) continue;
+        verdict[s] = pass ? 1 : 0;
+        atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
+      }
+    __syncthreads();
   }
-  int pair;   // the exclusion pair this block computes: root r, or n_roots for X
+}
+SSB_FN void ex_singles(ex_lds& L, int first, uint32_t ns, const uint32_t* __restrict__ slist,
+                       const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ sig_aff,
+                       const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H, uint8_t* __restrict__ verdict) {
+  using namespace ssb::lane;
+  const int lane_ = threadIdx.x;
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
+  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
+  bool init = false;
+  for (uint32_t x = (uint32_t)(blockIdx.x - first); x < ns; x += gridDim.x - (unsigned)first) {
+    const uint32_t s = slist[x];
+    if (!init) { lp_init_consts(g); init = true; }
+    const bool pass = pair_check(g, pk_aff[s], sig_aff[s], H[share_root[s]], F1, B, BP, TMP);
+    if (lane_ == 0) verdict[s] = pass ? 1 : 0;
+  }
+}
+// the exclusion pair of block `blk` (root r < n_roots: -E_r; n_roots .. +3: the quarters of X) into
+// fex[pair]; returns true in the block that must run the final product (tickets)
+SSB_FN bool ex_pair(ex_lds& L, int n_roots, uint32_t ns, const uint32_t* __restrict__ slist,
+                    const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
+                    const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
+                    const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H, fp12* __restrict__ fex,
+                    g2_jac* __restrict__ X4, uint32_t* __restrict__ xtk) {
+  using namespace ssb::lane;
+  const int blk = blockIdx.x, lane_ = threadIdx.x;
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
+  const int F1 = BS_S0, B = F1 + 24;
+  int pair;
   if (blk < n_roots) {
     const int r = blk;
     const g1_aff P = neg_suspect_sum(start[r], cnt[r], perm, flags, k64, pk_aff);   // -E_r (lane 0)
     __syncthreads();
     lp_init_consts(g);
-    miller_one(g, P, H[r], F1, B, flg);
+    miller_one(g, P, H[r], F1, B, L.flg);
     pair = r;
   } else {
     const int q = blk - n_roots;
-    const g2_jac acc = quarter_sum(u.b, slist, ns, flags, FLAG_SUSPECT, k64, sig_aff, q);
+    const g2_jac acc = quarter_sum<fp2>(L.u.b, slist, ns, flags, FLAG_SUSPECT, k64, sig_aff, q);
     if (lane_ == 0) X4[q] = acc;
     __threadfence();
     __syncthreads();
-    if (lane_ == 0) last = atomicAdd(&xtk[1], 1u) == 3u ? 1u : 0u;
+    if (lane_ == 0) L.last = atomicAdd(&xtk[1], 1u) == 3u ? 1u : 0u;
     __syncthreads();
-    if (!last) return;
+    if (!L.last) return false;
     __threadfence();
     const g2_aff Q = combine_quarters(X4);
     __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
     lp_init_consts(g);
     g1_aff G = g1_neg_generator();
     fp_neg(G.y, G.y);   // +g1
-    miller_one(g, G, Q, F1, B, flg);
+    miller_one(g, G, Q, F1, B, L.flg);
     if (lane_ == 0) xtk[1] = 0u;
     pair = n_roots;
   }
   if (lane_ < 12) ((fp*)&fex[pair])[lane_] = g.s[F1 + lane_];
   __threadfence();
   __syncthreads();
-  if (lane_ == 0) last = atomicAdd(&xtk[0], 1u) == (uint32_t)n_roots ? 1u : 0u;
+  if (lane_ == 0) L.last = atomicAdd(&xtk[0], 1u) == (uint32_t)n_roots ? 1u : 0u;
   __syncthreads();
-  if (!last) return;
+  return L.last != 0;
+}
+// ftot * prod of the n_roots + 1 exclusion values, ONE final exponentiation -> *xok
+SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, const fp12* __restrict__ fex,
+                     uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok) {
+  using namespace ssb::lane;
+  const int lane_ = threadIdx.x;
   __threadfence();
-  // ftot * prod of the n_roots + 1 exclusion values, ONE final exponentiation
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
+  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
   const int ACC = F1, IN = F1 + 12;
   if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)ftot)[lane_];
   __syncthreads();
@@ -553,6 +706,54 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
   f12_final_exp(g, ACC, TMP);
   const bool pass = f12_slots_one(g, ACC);
   if (lane_ == 0) { *xok = pass ? 1u : 0u; xtk[0] = 0u; }
+}
+
+// The committee stage's checks, after k_fb_rlc's consistency pass listed the suspects (nS of them):
+//   nS <= FB_SUSPECT_MAX -- the EXCLUSION check, the batch check without the suspects:
+//       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
+//       E_r = sum_{suspects of root r} k_i pk_i  (block r: products on the lanes, a lane tree),
+//       X   = sum_{suspects} k_i sig_i          (blocks n_roots .. +3: 4-bit-digit bucket sums),
+//     where ftot is the batch check's own Miller product (k_miller_final) -- by bilinearity this is
+//     the RLC check over every non-suspect candidate with the batch's own scalars (soundness 2^-63),
+//     at the cost of one Miller loop per root holding suspects: *xok = 1 decides them all valid;
+//     and every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's
+//     verify (blocks n_roots + 4 ..).  The pair blocks finish with completion tickets (xtk[0]: pairs,
+//     xtk[1]: X's quarters); the last pair runs the product and ONE final exponentiation;
+//   nS > FB_SUSPECT_MAX -- GROUP-TEST mode (e.g. a faulty operator in every committee): one RLC check
+//     per (root, operator-id bucket) group of candidates with the batch's own scalars (ex_groups), a
+//     passing group decides its candidates valid, a one-candidate group is exactly that share's verify;
+//     *xok = 2, and k_fb_root deduces the rest from the committee relations (deduce_job), k_fb_single
+//     checks what is left;
+//   nS == 0 (no relation broken: the invalid shares sit in jobs without redundancy) -- *xok = 0, the tree.
+__global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nS,
+                                     const uint32_t* __restrict__ slist, const uint32_t* __restrict__ start,
+                                     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
+                                     uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
+                                     const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
+                                     const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H,
+                                     const fp12* __restrict__ ftot, fp12* __restrict__ fex, g2_jac* __restrict__ X4,
+                                     uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict,
+                                     const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ kstart) {
+  if (*ok) return;   // uniform: the batch passed
+  const uint32_t ns = *nS;
+  const int blk = blockIdx.x, lane_ = threadIdx.x;
+  const bool gmode = ns > FB_SUSPECT_MAX && kcnt;
+  if (ns == 0 || (ns > FB_SUSPECT_MAX && !gmode)) {   // nothing to exclude / no group keys: the tree decides
+    if (blk == 0 && lane_ == 0) *xok = 0u;
+    return;
+  }
+  __shared__ ex_lds L;
+  if (gmode) {
+    if (blk == 0 && lane_ == 0) *xok = 2u;
+    ex_groups(L, n_roots, perm, flags, k64, sig_aff, pk_aff, H, verdict, kcnt, kstart);
+    return;
+  }
+  if (blk >= n_roots + 4) {   // the suspects, one pairing check each
+    ex_singles(L, n_roots + 4, ns, slist, share_root, sig_aff, pk_aff, H, verdict);
+    return;
+  }
+  if (ex_pair(L, n_roots, ns, slist, start, cnt, perm, flags, k64, sig_aff, pk_aff, H, fex, X4, xtk))
+    ex_final(L, n_roots, ftot, fex, xtk, xok);
 }
 
 // Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
@@ -567,7 +768,9 @@ __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__
                                       const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
                                       uint8_t* __restrict__ verdict, const uint32_t* __restrict__ xok) {
   using namespace ssb::lane;
-  if (*ok || *nfail > FB_SINGLE_MAX || (xok && *xok)) return;   // uniform
+  if (*ok) return;   // uniform
+  const uint32_t xv = xok ? *xok : 0u;
+  if (xv == 1u || (xv == 0u && *nfail > FB_SINGLE_MAX)) return;   // (xv == 2: group-test mode's leftovers)
   __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ uint32_t flg;
   const int lane_ = threadIdx.x;
@@ -578,7 +781,8 @@ __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__
   for (uint32_t x = blockIdx.x; x < total; x += gridDim.x) {
     const uint32_t s = perm[x];
     const uint32_t r = share_root[s];
-    if (!(flags[s] & FLAG_CANDIDATE) || gv0[gst0[r]]) continue;
+    if (!(flags[s] & FLAG_CANDIDATE)) continue;
+    if (xv == 2u ? (flags[s] & FLAG_DECIDED) != 0 : gv0[gst0[r]] != 0) continue;
     if (!init) { lp_init_consts(g); init = true; }
     const bool pass = pair_check(g, pk_aff[s], sig_aff[s], H[r], F1, B, BP, TMP);
     if (lane_ == 0) verdict[s] = pass ? 1 : 0;
@@ -708,21 +912,23 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   const int L = fallback_levels((size_t)n);
   const int lb = fallback_log2_branch();
   // the committee stage needs the jobs, the batch check's Miller product and the stage's workspace
-  const bool committee = jobs.n_jobs > 0 && fw.slist && fw.nS && fw.xtk && fw.xok && fw.fex && fw.ftot;
+  const bool committee = jobs.n_jobs > 0 && fw.slist && fw.nS && fw.xtk && fw.xok && fw.fex && fw.ftot && fw.kcnt &&
+                         fw.kstart;
   const fb_jobs cj = committee ? jobs : fb_jobs{0, nullptr, nullptr, nullptr};
   const uint32_t* xok = committee ? fw.xok : nullptr;
-  const fb_prep_args prep{n_roots, L, lb, share_root, fw.cnt, fw.start, fw.cursor, fw.gst, fw.perm, fw.rtk, fw.nfail};
+  const fb_prep_args prep{n_roots, L, lb, share_root, fw.cnt, fw.start, fw.cursor, fw.gst, fw.perm, fw.rtk, fw.nfail,
+                          committee ? jobs.ids : nullptr, committee ? fw.kcnt : nullptr, committee ? fw.kstart : nullptr};
   hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + nb((size_t)cj.n_jobs, 64) + 1), dim3(64), 0, st, n, key, ok, flags,
                      fw.k64, fast_verdicts ? verdict : (uint8_t*)nullptr, prep, cj, sig, fw.slist, fw.nS);
   if (committee)
     hipLaunchKernelGGL(k_fb_excl, dim3((unsigned)n_roots + 4 + EX_SINGLE_BLOCKS), dim3(64), 0, st, n_roots, ok,
                        (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
-                       (const uint32_t*)fw.perm, (const uint32_t*)flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
-                       fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict);
+                       (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
+                       fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
                      (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                      (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,
-                     committee ? fw.nS : (uint32_t*)nullptr);
+                     committee ? fw.nS : (uint32_t*)nullptr, cj, pk);
   if (L == 1) return;
   {
     const unsigned grid = (unsigned)(n < 2048 ? n : 2048);

@@ -268,11 +268,15 @@ struct fb_ws {
   uint32_t *slist, *nS, *xtk, *xok;
   fp12* fex;
   const fp12* ftot;
+  uint32_t *kcnt, *kstart;   // per (root, id bucket) key: fb_keys(n_roots) words each (cursor too)
 };
 // the jobs of an aggregate batch (share_off, t, ids), for the committee stage of the fallback
 struct fb_jobs { int n_jobs; const uint32_t* off; const uint32_t* tt; const uint64_t* ids; };
 int fallback_log2_branch();
 int fallback_levels(size_t n);
+// operator-id buckets per root of the failed-batch sort (fb_prep_block): 16 while the keys stay few
+SSB_INL int fb_nbuckets(int n_roots) { return n_roots <= 1024 ? 16 : 1; }
+inline size_t fb_keys(size_t n_roots) { return n_roots * (size_t)fb_nbuckets((int)n_roots); }
 void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, const uint32_t* ok, uint32_t* flags,
                      const uint32_t* share_root, const g2_aff* H, const g2_aff* sig, const g1_aff* pk, const fp12* froot,
                      const fb_ws& fw, uint8_t* verdict, bool fast_verdicts, const fb_jobs& jobs);

@@ -10,7 +10,8 @@ namespace ssb {
 
 // FLAG_SUSPECT (failed batches only, ssb_k_bisect.hip): the share's job failed its committee
 // consistency relation, so the share is checked on its own and left out of the exclusion check
-enum : uint32_t { FLAG_CANDIDATE = 1u << 16, FLAG_SUSPECT = 1u << 17 };
+// FLAG_DECIDED (failed batches, group-test mode): the share's verdict is final
+enum : uint32_t { FLAG_CANDIDATE = 1u << 16, FLAG_SUSPECT = 1u << 17, FLAG_DECIDED = 1u << 18 };
 
 // ---- random-linear-combination scalars -------------------------------------------------------
 // lighthouse's verify_signature_sets draws one fresh non-zero 64-bit scalar per signature set from

@@ -386,7 +386,7 @@ struct verify_ws {
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
   g2_jac* rsig; uint32_t* gst; uint8_t* gv0; uint8_t* gv1;                         // failed-batch group tests
   uint64_t* k64; g2_jac* fbX; uint32_t* rtk; uint32_t* nfail;                                     // (level 0 per root)
-  uint32_t* slist; uint32_t* xok; fp12* fex;                                       // committee stage
+  uint32_t* slist; uint32_t* xok; fp12* fex; uint32_t* kcnt; uint32_t* kstart;      // committee stage
   size_t npairs;
 };
 // Miller values of the pairs plus the levels of the 8-ary product tree
@@ -412,7 +412,8 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(n * sizeof(g2_jac)) +
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
          align_up(n * 8) + align_up(4 * n_roots * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4) +
-         align_up(n * 4) + align_up(4) + align_up((n_roots + 1) * sizeof(fp12)) + align_up(ntk_words(np) * 4);
+         align_up(n * 4) + align_up(4) + align_up((n_roots + 1) * sizeof(fp12)) + align_up(ntk_words(np) * 4) +
+         3 * align_up(launch::fb_keys(n_roots) * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) {
@@ -434,13 +435,14 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.b1 = c.take<g1_jac>((size_t)sz.g1.ngroups * sz.g1.W << sz.g1.c);   // >= the merged layout's ngroups << 4
   w.w1 = c.take<g1_jac>((size_t)sz.g1.ngroups * sz.g1.W);
   w.rpk = c.take<g1_jac>(n);
-  w.rcnt = c.take<uint32_t>(n_roots); w.rstart = c.take<uint32_t>(n_roots); w.rcur = c.take<uint32_t>(n_roots);
+  w.rcnt = c.take<uint32_t>(n_roots); w.rstart = c.take<uint32_t>(n_roots); w.rcur = c.take<uint32_t>(launch::fb_keys(n_roots));
   w.perm = c.take<uint32_t>(n);
   w.rsig = c.take<g2_jac>(n);
   w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
   w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
   w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(4 * n_roots); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
   w.slist = c.take<uint32_t>(n); w.xok = c.take<uint32_t>(1); w.fex = c.take<fp12>(n_roots + 1);
+  w.kcnt = c.take<uint32_t>(launch::fb_keys(n_roots)); w.kstart = c.take<uint32_t>(launch::fb_keys(n_roots));
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
@@ -634,7 +636,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
       launch::fb_ws fw{w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rtk, w.nfail, w.k64, w.fbX, w.rsig, w.rpk, w.gv0, w.gv1,
                        cm ? w.slist : nullptr, cm ? (uint32_t*)ptk : nullptr, cm ? (uint32_t*)ptk + 1 : nullptr,
                        cm ? w.xok : nullptr, cm ? w.fex : nullptr,
-                       cm ? w.f + w.npairs + (w.npairs + 7) / 8 : nullptr};
+                       cm ? w.f + w.npairs + (w.npairs + 7) / 8 : nullptr, cm ? w.kcnt : nullptr, cm ? w.kstart : nullptr};
       const launch::fb_jobs fj = cm ? launch::fb_jobs{sj->n_jobs, sj->off, sj->tt, sj->ids} : launch::fb_jobs{0, nullptr, nullptr, nullptr};
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, w.f,
                               fw, d_verdict, true, fj);
