@@ -96,3 +96,13 @@ def test_registry_ids_match_c_oracle(engine, t, n, V):
     wl = bench.make_workload(engine, V, t, n, 64, rank=25, ids="registry")
     assert len(set(wl["ids"][:n])) == n and max(wl["ids"]) > n
     _check(engine, wl, V, t, n)
+
+
+def test_knobs_tree_only_and_no_ratio(engine, monkeypatch):
+    """SSB_NO_COMMITTEE (a failed batch goes straight to the tree) and SSB_NO_RATIO (registry-id jobs
+    through the general 255-bit combine): the same exact results."""
+    monkeypatch.setenv("SSB_NO_COMMITTEE", "1")
+    monkeypatch.setenv("SSB_NO_RATIO", "1")
+    V, t, n, R = 1024, 3, 4, 16
+    wl = bench.make_workload(engine, V, t, n, R, rank=26, ids="registry", invalid_rate=0.01)
+    _check(engine, wl, V, t, n)
