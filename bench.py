@@ -440,6 +440,11 @@ def main():
     d_jr = torch.tensor(wl["job_root"], dtype=torch.int32, device=dev)
     d_roots = dt8(b"".join(wl["roots"]))
     S = max(1, args.pipeline)
+    if args.dist_backend == "gloo" and world > 1:
+        # rehearsal with ranks sharing GPUs: the GPU's slot queues are split between its ranks (each
+        # slot is a hardware queue with its own scratch reservation; 24 on one GPU exhausted it)
+        per_gpu = -(-world // max(1, torch.cuda.device_count()))
+        S = max(1, S // per_gpu)
     outs = [dict(out=torch.empty((V, 96), dtype=torch.uint8, device=dev), st=torch.empty((V,), dtype=torch.int32, device=dev),
                  err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev),
                  fv=torch.empty((V,), dtype=torch.uint8, device=dev))

@@ -577,29 +577,39 @@ def test_dev_malformed_job_shapes(engine):
 
 def test_host_submit_wait_pipelined(engine):
     """ssb_threshold_aggregate_batch_submit / ssb_batch_wait (zero-copy staging over PCIe): seven
-    batches submitted onto three slots before any wait -- every slot is reused while its previous
-    batch is pending, which must deliver that batch first -- then waited in reverse order; each
-    delivers exactly the fixture's statuses, combines and share verdicts.  The same with the public
-    keys from the decoded-key cache (the _cached_submit variant)."""
+    batches, each with its OWN job order (the golden cases rotated by the batch index), submitted onto
+    three slots before any wait -- every slot is reused while its previous batch is pending, which
+    must deliver that batch first into ITS caller's buffers -- then waited in reverse order; each
+    delivers exactly its own statuses, combines and share verdicts (a delivery into the wrong caller's
+    buffers, or a stale read of the reused staging buffer, would show as a rotation mismatch).  The
+    same with the public keys from the decoded-key cache (the _cached_submit variant).  A batch whose
+    PendingBatch is dropped without a wait is still delivered safely (the engine keeps its arrays)."""
     cases = _load("threshold_cases.json")["cases"]
-    roots, t, offs, sigs, pks, ids, jr = _golden_batch(cases, 3)
     lib = engine._lib
     assert lib.ssb_set_slot_streams(engine.handle, 1) == 0
     assert lib.ssb_set_pipeline_depth(engine.handle, 3) == 0
     try:
         for cached in (False, True):
-            kw = {}
+            pend, orders = [], []
+            uniq = sorted({p for c in cases for p in c["pks"]})
             if cached:
-                uniq = sorted(set(pks))
-                table = np.frombuffer(b"".join(uniq), dtype=np.uint8)
+                table = np.frombuffer(b"".join(bytes.fromhex(p) for p in uniq), dtype=np.uint8)
                 from safestakeoperator_amd import _lib
                 assert lib.ssb_pk_cache_set(engine.handle, len(uniq), table.ctypes.data_as(_lib._u8p)) == 0
-                kw["pk_index"] = [uniq.index(p) for p in pks]
-            pend = [engine.submit_batch_raw(t, offs, b"".join(sigs), b"".join(pks), ids, jr, roots, **kw) for _ in range(7)]
-            for pb in reversed(pend):
+            for b in range(7):
+                rot = cases[b % len(cases):] + cases[:b % len(cases)]
+                roots, t, offs, sigs, pks, ids, jr = _golden_batch(rot, 3)
+                kw = {"pk_index": [uniq.index(p.hex()) for p in pks]} if cached else {}
+                pend.append(engine.submit_batch_raw(t, offs, b"".join(sigs), b"".join(pks), ids, jr, roots, **kw))
+                orders.append((rot, offs, t))
+            # one more whose PendingBatch is dropped at once: delivered later into arrays the engine keeps
+            roots, t, offs, sigs, pks, ids, jr = _golden_batch(cases, 1)
+            kw = {"pk_index": [uniq.index(p.hex()) for p in pks]} if cached else {}
+            engine.submit_batch_raw(t, offs, b"".join(sigs), b"".join(pks), ids, jr, roots, **kw)
+            for pb, (rot, offs, t) in reversed(list(zip(pend, orders))):
                 out, st, err, ver = pb.wait()
                 for k in range(len(t)):
-                    c = cases[k % len(cases)]
+                    c = rot[k % len(rot)]
                     assert int(st[k]) == c["expected_status"], c["name"]
                     if c["expected_status"] == 0:
                         assert out[k].tobytes().hex() == c["expected_sig"], c["name"]
