@@ -354,6 +354,25 @@ int main() {
       int same = -1;
       if (elig) { unit_combine_small(b, pp.data(), c.data(), (uint32_t)t); same = memcmp(a, b, 96) == 0; }
       printf("%d %d\n", elig ? 1 : 0, same);
+    } else if (cmd == "lagratio") {  // lagratio t id1 .. idt : registry ratio path vs 255-bit path
+      int t; is >> t; std::vector<uint64_t> ids(t); for (int i = 0; i < t; ++i) is >> ids[i];
+      std::vector<g2_aff> P(t); std::vector<uint32_t> idx(t);
+      for (int i = 0; i < t; ++i) { uint8_t m[32] = {0}; m[0] = (uint8_t)i; m[1] = 0x5a; hash_to_g2(P[i], m, (const uint8_t*)DST, (int)strlen(DST)); idx[i] = (uint32_t)i; }
+      std::vector<int64_t> c(t); std::vector<fr> lam(t); uint64_t M = 0;
+      const bool elig = unit_lagrange_ratio(c.data(), &M, ids.data(), (uint32_t)t);
+      unit_lagrange(lam.data(), ids.data(), (uint32_t)t);
+      std::vector<g2_jac> terms(t);
+      for (int i = 0; i < t; ++i) unit_combine_term(terms[i], P[i], lam[i].l);
+      uint8_t a[96], b[96]; unit_combine_sum(a, terms.data(), (uint32_t)t);
+      int same = -1;
+      if (elig) {
+        ratio_job rj; unit_combine_ratio_at(rj, P.data(), idx.data(), c.data(), (uint32_t)t, M);
+        g2_jac q4[4];
+        for (int q = 0; q < 4; ++q) unit_gls_term(q4[q], rj.T, rj.d[q], q);
+        unit_combine_sum(b, q4, 4);
+        same = memcmp(a, b, 96) == 0;
+      }
+      printf("%d %d %llu\n", elig ? 1 : 0, same, (unsigned long long)M);
     } else if (cmd == "lafin") {  // lafin <trials>: accumulator engine vs repeated modular add/sub
       int trials; is >> trials;
       uint64_t st = 0x9E3779B97F4A7C15ull;

@@ -125,6 +125,33 @@ def test_small_lagrange_fast_path(host_exe):
             assert same == 1, ids
 
 
+def test_registry_ratio_path(host_exe):
+    """Registry ids (arbitrary, < 2^16): T = sum c_i sig_i and [M^-1 mod r] T by its four GLS digits
+    (unit_lagrange_ratio / unit_combine_ratio_at / unit_gls_term) == the 255-bit lambda_i path, with
+    M = lcm |prod_{j!=i}(x_j - x_i)|; repeated ids and values past 62 bits are not eligible."""
+    import random
+    rnd = random.Random(7)
+    cases = [(5, 9, 100), (1, 2, 4), (65535, 1, 40000), (17, 3, 60001, 2), (1, 2, 3)]
+    cases += [tuple(rnd.sample(range(1, 1 << 16), t)) for t in (3, 3, 3, 4, 4, 5)]
+    lines = ["lagratio %d %s" % (len(k), " ".join(map(str, k))) for k in cases]
+    lines += ["lagratio 3 1 1 2", "lagratio 3 %d 2 3" % (1 << 62)]
+    out = _run(host_exe, lines)
+    from math import lcm, prod
+    n_elig = 0
+    for ids, line in zip(cases, out):
+        e, same, M = map(int, line.split())
+        D = [prod(x - y for x in ids if x != y) for y in ids]
+        L = lcm(*[abs(d) for d in D])
+        c = [prod(x for x in ids if x != y) * (L // d) for y, d in zip(ids, D)]
+        want = L < 2**62 and all(abs(v) < 2**62 for v in c)   # t = 3 always; wider committees rarely
+        assert e == int(want), (ids, line)
+        if e:
+            n_elig += 1
+            assert same == 1 and M == L, (ids, line)
+    assert n_elig >= 8
+    assert [l.split()[0] for l in out[len(cases):]] == ["0", "0"]
+
+
 def test_accumulator_engine_reduction(host_exe):
     """la_fin (sum of scaled +-terms, one Barrett-style step) equals the modular sum, including the
     edge values 0 and p-1 and coefficients up to 300 per term."""
