@@ -82,6 +82,44 @@ SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, uint32_t* __restrict__ cnt,
 #endif
 // (blocks [3 nbd, 3 nbd + nbu): the hash's first stage, one lane per root, when the slot's counts
 // and tickets are already clean -- then no prep launch stands in front of the decode)
+// the roles out of line: each gets its own register allocation (inlined, the hash's and the decode's
+// demands were merged into one allocation for every lane of the launch, and all of them spilled)
+SSB_ROLE void dc_hash_role(int i, const uint8_t* __restrict__ roots, const dst_arg& dst, fp2* __restrict__ u) {
+  uint8_t m[32];
+  for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
+  fp2 u0, u1;
+  h2c_field(u0, u1, m, dst.b, dst.len, 32);
+  u[2 * i] = u0;
+  u[2 * i + 1] = u1;
+}
+SSB_ROLE void dc_count_role(int s, const job_map& jm, const uint32_t* __restrict__ share_root, const rlc_key& key,
+                          const msm_cfg& c2, const msm_cfg& c1, uint32_t* __restrict__ cnt) {
+  uint32_t g;
+  if (jm.n_jobs) { uint32_t j; share_lookup((uint32_t)s, jm, j, g); }   // (the decode blocks store it)
+  else g = share_root[s];
+  msm_sort_lane_root<false>(s, g, key, c2, c1, cnt, (uint32_t*)nullptr);
+}
+SSB_ROLE void dc_sig_role(int s, const uint8_t* __restrict__ sig96, g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ sflags,
+                        const job_map& jm) {
+  if (jm.n_jobs) {   // share -> (job, root) for the later launches (k_share_map's work)
+    uint32_t j, r;
+    share_lookup((uint32_t)s, jm, j, r);
+    jm.share_job[s] = j;
+    jm.share_root[s] = r;
+  }
+  uint8_t b[96];
+  for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
+  g2_aff sig;
+  sflags[s] = unit_decode_sig(sig, b);
+  sig_aff[s] = sig;
+}
+SSB_ROLE void dc_pk_role(int s, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ pflags) {
+  uint8_t b[48];
+  for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
+  g1_aff pk;
+  pflags[s] = unit_decode_pk(pk, b);
+  pk_aff[s] = pk;
+}
 template <bool CACHED>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_DC_WAVES))) k_decode_count(int n, uint32_t nbd, const uint8_t* __restrict__ sig96,
                                            const uint8_t* __restrict__ pk48, const uint32_t* __restrict__ pk_index,
@@ -97,25 +135,14 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
   const uint32_t part = blockIdx.x / nbd;
   if (part >= 3) {
     const int i = (int)(blockIdx.x - 3 * nbd) * 64 + threadIdx.x;
-    if (i >= n_roots) return;
-    uint8_t m[32];
-    for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
-    fp2 u0, u1;
-    h2c_field(u0, u1, m, dst.b, dst.len, 32);
-    u[2 * i] = u0;
-    u[2 * i + 1] = u1;
+    if (i < n_roots) dc_hash_role(i, roots, dst, u);
     return;
   }
   const int s = (blockIdx.x - part * nbd) * 64 + threadIdx.x;
   if (part == 2) {   // count pass; the last count block to finish runs the scans
     __shared__ uint32_t sh[64 + 512];
     __shared__ uint32_t last;
-    if (s < n) {
-      uint32_t g;
-      if (jm.n_jobs) { uint32_t j; share_lookup((uint32_t)s, jm, j, g); }   // (the decode blocks store it)
-      else g = share_root[s];
-      msm_sort_lane_root<false>(s, g, key, c2, c1, cnt, (uint32_t*)nullptr);
-    }
+    if (s < n) dc_count_role(s, jm, share_root, key, c2, c1, cnt);
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence();
@@ -131,28 +158,14 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
   }
   if (s >= n) return;
   if (part == 0) {
-    if (jm.n_jobs) {   // share -> (job, root) for the later launches (k_share_map's work)
-      uint32_t j, r;
-      share_lookup((uint32_t)s, jm, j, r);
-      jm.share_job[s] = j;
-      jm.share_root[s] = r;
-    }
-    uint8_t b[96];
-    for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
-    g2_aff sig;
-    sflags[s] = unit_decode_sig(sig, b);
-    sig_aff[s] = sig;
+    dc_sig_role(s, sig96, sig_aff, sflags, jm);
   } else if (part == 1) {
     if (CACHED) {
       const uint32_t i = pk_index[s];
       if (i < n_cache) { pk_aff[s] = cache_aff[i]; pflags[s] = cache_flags[i]; }
       else pflags[s] = 0u;   // out-of-range index: the share cannot verify
     } else {
-      uint8_t b[48];
-      for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
-      g1_aff pk;
-      pflags[s] = unit_decode_pk(pk, b);
-      pk_aff[s] = pk;
+      dc_pk_role(s, pk48, pk_aff, pflags);
     }
   }
 }

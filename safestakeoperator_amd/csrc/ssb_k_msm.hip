@@ -296,15 +296,21 @@ __global__ void SSB_LB2(64) k_subgroup_fix(int n, const uint32_t* __restrict__ s
 // a subgroup lane also writes the share's combined flags (k_flags) when sc.flags is given
 struct sort_scatter { int n; rlc_key key; const uint32_t* share_root; msm_cfg c2, c1; uint32_t* cur; uint32_t* ent;
                       const uint32_t* pflags; uint32_t n_roots; uint32_t* flags; };
+// the riding roles out of line: inlined, their register demand set the whole kernel's allocation and
+// the subgroup lanes spilled (32 scratch stores in the kernel body against 5 in k_subgroup)
+SSB_ROLE void sg_map_role(uint32_t b, h2c_cand* cs, const h2c_fuse& h) { h2c_map_block(b, cs, h.n, h.u, h.q); }
+SSB_ROLE void sg_scatter_role(int i, const sort_scatter& sc) {
+  msm_sort_lane<true>(i, sc.key, sc.share_root, sc.c2, sc.c1, sc.cur, sc.ent);
+}
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_SG_WAVES))) k_subgroup_map(int n, uint32_t nbs, const uint32_t* __restrict__ sflags,
                                            const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags, h2c_fuse h,
                                            uint32_t nbm, sort_scatter sc) {
   __shared__ h2c_cand cs[64];
   if (blockIdx.x >= nbs) {
     const uint32_t b = blockIdx.x - nbs;
-    if (b < nbm) { h2c_map_block(b, cs, h.n, h.u, h.q); return; }
+    if (b < nbm) { sg_map_role(b, cs, h); return; }
     const int i = (b - nbm) * 64 + threadIdx.x;
-    if (i < sc.n) msm_sort_lane<true>(i, sc.key, sc.share_root, sc.c2, sc.c1, sc.cur, sc.ent);
+    if (i < sc.n) sg_scatter_role(i, sc);
     return;
   }
   const int s = blockIdx.x * blockDim.x + threadIdx.x;

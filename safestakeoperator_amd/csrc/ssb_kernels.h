@@ -5,6 +5,16 @@
 #include "ssb_units.h"
 #include "../../include/ssbls.h"
 
+// The roles of a fused launch (its block ranges running different stages) are out-of-line functions:
+// each role gets its own register allocation instead of one allocation -- and one set of spills --
+// shared by every lane of the launch.  SSB_VARIANT_DEFS=-DSSB_ROLES_INLINE builds the inlined form
+// for A/B runs.
+#ifdef SSB_ROLES_INLINE
+#define SSB_ROLE SSB_INL
+#else
+#define SSB_ROLE SSB_FN
+#endif
+
 // Experiment builds only (SSB_VARIANT_DEFS=-DSSB_TRACE_TAIL, bench_tools/trace_tail.py): the tail
 // kernels record per-block start / end wall-clock stamps (100 MHz) in a device buffer of their
 // translation unit (read back by ssb_debug_trace_<tu>), so the critical path inside a fused launch
