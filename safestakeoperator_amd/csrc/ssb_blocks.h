@@ -72,12 +72,12 @@ SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t ba
     if (pow) {
       for (uint32_t x = s + j; x < e; x += J) {
         const uint32_t en = ent[x], i = en >> 4;
-        if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pow[(size_t)pidx[i] * PKPOW_W + (en & 15u)]; jac_add_aff_inl(acc, acc, q); }
+        if (flags[i] & FLAG_CANDIDATE) jac_madd_at(acc, pow + ((size_t)pidx[i] * PKPOW_W + (en & 15u)));
       }
     } else {
       for (uint32_t x = s + j; x < e; x += J) {
         const uint32_t i = ent[x];
-        if (flags[i] & FLAG_CANDIDATE) { const aff<F> q = pts[i]; jac_add_aff_inl(acc, acc, q); }
+        if (flags[i] & FLAG_CANDIDATE) jac_madd_at(acc, pts + i);
       }
     }
   }

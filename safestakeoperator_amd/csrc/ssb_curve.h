@@ -101,6 +101,37 @@ template <class F> SSB_INL void jac_add_aff_inl(jac<F>& r, const jac<F>& p, cons
   r.x = x3; r.y = y3; r.z = z3;
 }
 template <class F> SSB_FN void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) { jac_add_aff_inl(r, p, q); }
+// a += *qp in place, the same formula and special cases as jac_add_aff_inl, written for the bucket
+// loops at two waves per SIMD (256 registers): q's coordinates are loaded where they are consumed,
+// temporaries die early (at most six Fp2 values live besides a product's operands), and the rare
+// doubling branch is inlined -- a call there made the loop save its live registers around it.
+// Static spill census of a G2 bucket loop (bench_tools/isa_scratch.py): 83 scratch stores and 71
+// loads on the addition's path with jac_add_aff_inl, 27 / 27 with this form.
+template <class F> SSB_INL void jac_madd_at(jac<F>& a, const aff<F>* __restrict__ qp) {
+  if (qp->inf) return;
+  if (jac_is_inf(a)) { jac_from_aff(a, *qp); return; }
+  F Z1Z1, r, H;
+  f_sqr(Z1Z1, a.z);
+  { F S2; const F y2 = qp->y; f_mul(S2, y2, a.z); f_mul(S2, S2, Z1Z1); f_sub(r, S2, a.y); }   // S2 - Y1
+  { F U2; const F x2 = qp->x; f_mul(U2, x2, Z1Z1); f_sub(H, U2, a.x); }                       // U2 - X1
+  if (f_is_zero(H)) {
+    if (f_is_zero(r)) { jac<F> d; jac_from_aff(d, *qp); jac_dbl_inl(a, d); } else jac_set_inf(a);
+    return;
+  }
+  f_dbl(r, r);
+  F I;
+  {
+    F HH, t;
+    f_sqr(HH, H);
+    f_add(t, a.z, H); f_sqr(t, t); f_sub(t, t, Z1Z1); f_sub(a.z, t, HH);   // Z3 = (Z1 + H)^2 - Z1Z1 - HH
+    f_dbl(I, HH); f_dbl(I, I);
+  }
+  F V; f_mul(V, a.x, I);
+  F J; f_mul(J, H, I);
+  F t; f_mul(t, a.y, J);
+  f_sqr(a.x, r); f_sub(a.x, a.x, J); f_dbl(J, V); f_sub(a.x, a.x, J);     // X3 = r^2 - J - 2V
+  f_sub(V, V, a.x); f_mul(a.y, r, V); f_dbl(t, t); f_sub(a.y, a.y, t);    // Y3 = r (V - X3) - 2 Y1 J
+}
 
 // add-2007-bl: general Jacobian addition with the special cases.
 template <class F> SSB_INL void jac_add_inl(jac<F>& r, const jac<F>& p, const jac<F>& q) {

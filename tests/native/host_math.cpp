@@ -373,6 +373,37 @@ int main() {
         same = memcmp(a, b, 96) == 0;
       }
       printf("%d %d %llu\n", elig ? 1 : 0, same, (unsigned long long)M);
+    } else if (cmd == "madd") {  // madd <trials>: jac_madd_at (bucket loops) vs jac_add_aff_inl, incl. special cases
+      int trials; is >> trials;
+      int bad = 0, n = 0;
+      auto same = [](const auto& a, const auto& b) { return memcmp(&a, &b, sizeof(a)) == 0; };
+      for (int tr = 0; tr < trials; ++tr) {
+        uint8_t m[32] = {0}; m[0] = (uint8_t)tr; m[1] = (uint8_t)(tr >> 8); m[2] = 0x3c;
+        g2_aff P, Q; hash_to_g2(P, m, (const uint8_t*)DST, (int)strlen(DST));
+        m[3] = 1; hash_to_g2(Q, m, (const uint8_t*)DST, (int)strlen(DST));
+        g2_jac A; jac_from_aff(A, P); jac_dbl(A, A); jac_add_aff(A, A, Q);    // Z != 1
+        g2_aff Aa; jac_to_aff(Aa, A);
+        g2_aff nAa = Aa; fp2_neg(nAa.y, nAa.y);
+        g2_aff inf = Q; inf.inf = 1;
+        g2_jac I; jac_set_inf(I);
+        const g2_jac accs[4] = {A, A, A, I};
+        const g2_aff qs[4] = {Q, Aa, nAa, Q};
+        for (int c = 0; c < 5; ++c) {
+          const g2_jac a0 = c < 4 ? accs[c] : A;
+          const g2_aff q = c < 4 ? qs[c] : inf;
+          g2_jac want; jac_add_aff_inl(want, a0, q);
+          g2_jac got = a0; jac_madd_at(got, &q);
+          ++n; if (!same(want, got)) ++bad;
+        }
+        // G1 (the cached keys' bases): the same over Fp
+        g1_aff g = g1_neg_generator(); fp_neg(g.y, g.y);
+        g1_jac B; jac_from_aff(B, g); for (int k = 0; k <= tr % 7; ++k) jac_dbl(B, B);
+        g1_aff Ba; jac_to_aff(Ba, B);
+        g1_jac w1; jac_add_aff_inl(w1, B, g); g1_jac g1v = B; jac_madd_at(g1v, &g);
+        g1_jac w2; jac_add_aff_inl(w2, B, Ba); g1_jac g2v = B; jac_madd_at(g2v, &Ba);
+        n += 2; bad += !same(w1, g1v); bad += !same(w2, g2v);
+      }
+      printf("%d %d\n", n - bad, n);
     } else if (cmd == "lafin") {  // lafin <trials>: accumulator engine vs repeated modular add/sub
       int trials; is >> trials;
       uint64_t st = 0x9E3779B97F4A7C15ull;

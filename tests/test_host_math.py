@@ -152,6 +152,13 @@ def test_registry_ratio_path(host_exe):
     assert [l.split()[0] for l in out[len(cases):]] == ["0", "0"]
 
 
+def test_bucket_madd_matches_generic(host_exe):
+    """jac_madd_at (the MSM bucket loops' in-place mixed addition) == jac_add_aff_inl coordinate for
+    coordinate, on G2 and G1, including infinity on either side, doubling and opposite points."""
+    ok, n = _run(host_exe, ["madd 12"])[0].split()
+    assert ok == n and int(n) == 12 * 7
+
+
 def test_accumulator_engine_reduction(host_exe):
     """la_fin (sum of scaled +-terms, one Barrett-style step) equals the modular sum, including the
     edge values 0 and p-1 and coefficients up to 300 per term."""
