@@ -423,28 +423,18 @@ SSB_FN jac<F> quarter_sum(fr_bucket_lds& ub, const uint32_t* __restrict__ list, 
   }
   return acc;
 }
-// S = 2^16 S + X (q < 3) or S + X (q == 3): the group tests' Horner step over the quarters, lane 0,
-// both points in LDS
+// sum_q 2^(16q) X[q] (q < 4), affine, in lane 0 (infinity on the other lanes)
 template <class F>
-SSB_FN void horner_step(jac<F>* __restrict__ S, const jac<F>* __restrict__ X, int q) {
-  jac<F> a = *S;
-  if (q < 3) for (int i = 0; i < 16; ++i) jac_dbl_inl(a, a);
-  const jac<F> x = *X;
-  jac_add_inl(a, a, x);
-  *S = a;
-}
-
-// sum_q 2^(16q) X[q] (q < 4), affine, in lane 0 (Q.inf on the other lanes)
-SSB_FN g2_aff combine_quarters(const g2_jac* __restrict__ X) {
+SSB_FN aff<F> combine_quarters(const jac<F>* __restrict__ X) {
   const int lane_ = threadIdx.x;
-  g2_jac t;
+  jac<F> t;
   jac_set_inf(t);
   if (lane_ < 4) { t = X[lane_]; for (int i = 0; i < 16 * lane_; ++i) jac_dbl_inl(t, t); }
   for (int h = 2; h >= 1; h >>= 1) {
-    const g2_jac o = shfl_down_g2(t, h);
+    const jac<F> o = shfl_down_pt(t, h);
     if (lane_ < h) jac_add_inl(t, t, o);
   }
-  g2_aff Q;
+  aff<F> Q;
   Q.inf = true;
   if (lane_ == 0) jac_to_aff(Q, t);
   return Q;
@@ -512,7 +502,7 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
   if (!last) return;
   __threadfence();
   // S_r = sum_q 2^(16q) X_q, then the root's check FE(f[r] * e(-g1, S_r)) == 1
-  const g2_aff Q = combine_quarters(X + 4 * r);
+  const g2_aff Q = combine_quarters<fp2>(X + 4 * r);
   __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
   grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
   lp_init_consts(g);
@@ -576,57 +566,7 @@ SSB_FN g1_aff neg_suspect_sum(uint32_t sb, uint32_t nr, const uint32_t* __restri
 // pair multiplies ftot by the n_roots + 1 Miller values and runs ONE final exponentiation.
 // (the roles of k_fb_excl are out of line: each role's temporaries live in its own frame, and the
 // kernel's private segment is the largest role's, not their sum)
-struct ex_lds { fr_lds u; uint32_t flg, last, ncand; g1_aff sP; g2_aff sQ; g2_jac S2, X2; g1_jac S1, X1; };
-SSB_FN void ex_groups(ex_lds& L, int n_roots, const uint32_t* __restrict__ perm, uint32_t* __restrict__ flags,
-                      const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
-                      const g2_aff* __restrict__ H, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ kcnt,
-                      const uint32_t* __restrict__ kstart) {
-  using namespace ssb::lane;
-  const int lane_ = threadIdx.x;
-  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
-  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
-  const int NB = launch::fb_nbuckets(n_roots);
-  const uint32_t K = (uint32_t)n_roots * (uint32_t)NB;
-  for (uint32_t key = blockIdx.x; key < K; key += gridDim.x) {
-    const uint32_t gn = kcnt[key];
-    if (!gn) continue;
-    const uint32_t* list = perm + kstart[key];
-    const int r = (int)(key / (uint32_t)NB);
-    if (lane_ == 0) L.ncand = 0u;
-    __syncthreads();
-    uint32_t nc = 0;
-    for (uint32_t x = lane_; x < gn; x += 64) nc += (flags[list[x]] & FLAG_CANDIDATE) ? 1u : 0u;
-    if (nc) atomicAdd(&L.ncand, nc);
-    __syncthreads();
-    const uint32_t m = L.ncand;
-    if (!m) continue;
-    // G2 then G1 sums, each the Horner combination of its four 16-bit quarters (lane 0; the points
-    // stay in LDS)
-    if (lane_ == 0) { jac_set_inf(L.S2); jac_set_inf(L.S1); }
-    for (int q = 3; q >= 0; --q) {
-      const g2_jac x2 = quarter_sum<fp2>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, sig_aff, q);
-      if (lane_ == 0) { L.X2 = x2; horner_step<fp2>(&L.S2, &L.X2, q); }
-      __syncthreads();
-    }
-    for (int q = 3; q >= 0; --q) {
-      const g1_jac x1 = quarter_sum<fp>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, pk_aff, q);
-      if (lane_ == 0) { L.X1 = x1; horner_step<fp>(&L.S1, &L.X1, q); }
-      __syncthreads();
-    }
-    if (lane_ == 0) { jac_to_aff(L.sQ, L.S2); jac_to_aff(L.sP, L.S1); }
-    __syncthreads();
-    lp_init_consts(g);
-    const bool pass = pair_check(g, L.sP, L.sQ, H[r], F1, B, BP, TMP);
-    if (pass || m == 1)
-      for (uint32_t x = lane_; x < gn; x += 64) {
-        const uint32_t s = list[x];
-        if (!(flags[s] & FLAG_CANDIDATE)) continue;
-        verdict[s] = pass ? 1 : 0;
-        atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
-      }
-    __syncthreads();
-  }
-}
+struct ex_lds { fr_lds u; uint32_t flg, last; };
 SSB_FN void ex_singles(ex_lds& L, int first, uint32_t ns, const uint32_t* __restrict__ slist,
                        const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ sig_aff,
                        const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H, uint8_t* __restrict__ verdict) {
@@ -671,7 +611,7 @@ SSB_FN bool ex_pair(ex_lds& L, int n_roots, uint32_t ns, const uint32_t* __restr
     __syncthreads();
     if (!L.last) return false;
     __threadfence();
-    const g2_aff Q = combine_quarters(X4);
+    const g2_aff Q = combine_quarters<fp2>(X4);
     __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
     lp_init_consts(g);
     g1_aff G = g1_neg_generator();
@@ -719,11 +659,9 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
 //     and every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's
 //     verify (blocks n_roots + 4 ..).  The pair blocks finish with completion tickets (xtk[0]: pairs,
 //     xtk[1]: X's quarters); the last pair runs the product and ONE final exponentiation;
-//   nS > FB_SUSPECT_MAX -- GROUP-TEST mode (e.g. a faulty operator in every committee): one RLC check
-//     per (root, operator-id bucket) group of candidates with the batch's own scalars (ex_groups), a
-//     passing group decides its candidates valid, a one-candidate group is exactly that share's verify;
-//     *xok = 2, and k_fb_root deduces the rest from the committee relations (deduce_job), k_fb_single
-//     checks what is left;
+//   nS > FB_SUSPECT_MAX -- GROUP-TEST mode (e.g. a faulty operator in every committee): *xok = 2, and
+//     k_fb_group runs one RLC check per (root, operator-id bucket) group of candidates, k_fb_root
+//     deduces the rest from the committee relations (deduce_job), k_fb_single checks what is left;
 //   nS == 0 (no relation broken: the invalid shares sit in jobs without redundancy) -- *xok = 0, the tree.
 __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nS,
                                      const uint32_t* __restrict__ slist, const uint32_t* __restrict__ start,
@@ -743,9 +681,8 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
     return;
   }
   __shared__ ex_lds L;
-  if (gmode) {
+  if (gmode) {   // the group tests follow in k_fb_group
     if (blk == 0 && lane_ == 0) *xok = 2u;
-    ex_groups(L, n_roots, perm, flags, k64, sig_aff, pk_aff, H, verdict, kcnt, kstart);
     return;
   }
   if (blk >= n_roots + 4) {   // the suspects, one pairing check each
@@ -754,6 +691,85 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
   }
   if (ex_pair(L, n_roots, ns, slist, start, cnt, perm, flags, k64, sig_aff, pk_aff, H, fex, X4, xtk))
     ex_final(L, n_roots, ftot, fex, xtk, xok);
+}
+
+// GROUP-TEST mode of the committee stage (k_fb_excl set *xok = 2: more suspects than FB_SUSPECT_MAX,
+// e.g. a faulty operator in every committee): one RLC check per (root, operator-id bucket) group of
+// candidates with the batch's own scalars,
+//     e(S1, H(r)) * e(-g1, S2) == 1,   S1 = sum k_i pk_i,   S2 = sum k_i sig_i  over the group,
+// a passing group decides its candidates valid (soundness 2^-63), a one-candidate group is exactly that
+// share's verify.  Blocks (key, q), the layout of k_fb_root: block q sums quarter q of the scalars
+// (bits 16q .. 16q+15) of both sums into gX2 / gX1 (the tree's per-share product buffers, unused in
+// this mode: sized for 4 fb_keys entries); the last of the key's four blocks -- ticket: the scatter's
+// cursor, which fb_prep_block left at kstart + kcnt -- combines the quarters and runs the check.
+// k_fb_root then deduces the rest of every job from its committee relations (deduce_job) and
+// k_fb_single checks what is left.
+// (k_fb_group's roles out of line: the quarter sums' and the combines' point temporaries live in
+// their own frames, not in the kernel's beside the pairing check's)
+SSB_FN void group_quarters(fr_bucket_lds& ub, const uint32_t* __restrict__ list, uint32_t gn, const uint32_t* __restrict__ flags,
+                           const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
+                           const g1_aff* __restrict__ pk_aff, int q, g2_jac* __restrict__ o2, g1_jac* __restrict__ o1) {
+  const g2_jac a2 = quarter_sum<fp2>(ub, list, gn, flags, FLAG_CANDIDATE, k64, sig_aff, q);
+  if (threadIdx.x == 0) *o2 = a2;
+  const g1_jac a1 = quarter_sum<fp>(ub, list, gn, flags, FLAG_CANDIDATE, k64, pk_aff, q);
+  if (threadIdx.x == 0) *o1 = a1;
+}
+SSB_FN void group_combine(const g2_jac* __restrict__ X2, const g1_jac* __restrict__ X1, g2_aff* sQ, g1_aff* sP) {
+  const g2_aff Q = combine_quarters<fp2>(X2);
+  if (threadIdx.x == 0) *sQ = Q;
+  const g1_aff P = combine_quarters<fp>(X1);
+  if (threadIdx.x == 0) *sP = P;
+}
+__global__ void SSB_LB2(64) k_fb_group(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ xok,
+                                      const uint32_t* __restrict__ perm, uint32_t* __restrict__ flags,
+                                      const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
+                                      const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H,
+                                      uint8_t* __restrict__ verdict, const uint32_t* __restrict__ kcnt,
+                                      const uint32_t* __restrict__ kstart, uint32_t* __restrict__ cursor,
+                                      g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1) {
+  using namespace ssb::lane;
+  if (*ok || *xok != 2u) return;   // uniform: the batch passed / not the group-test mode
+  const uint32_t NB = (uint32_t)launch::fb_nbuckets(n_roots);
+  const uint32_t key = blockIdx.x >> 2, q = blockIdx.x & 3;
+  if (key >= (uint32_t)n_roots * NB) return;
+  const uint32_t gn = kcnt[key];
+  if (!gn) return;   // (the four blocks of an empty key all leave here: no ticket)
+  const uint32_t* list = perm + kstart[key];
+  __shared__ fr_lds u;
+  __shared__ uint32_t flg, last, ncand;
+  __shared__ g1_aff sP;
+  __shared__ g2_aff sQ;
+  const int lane_ = threadIdx.x;
+  group_quarters(u.b, list, gn, flags, k64, sig_aff, pk_aff, (int)q, gX2 + 4 * key + q, gX1 + 4 * key + q);
+  __threadfence();
+  __syncthreads();
+  if (lane_ == 0) last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (lane_ == 0) ncand = 0u;
+  __syncthreads();
+  uint32_t nc = 0;
+  for (uint32_t x = lane_; x < gn; x += 64) nc += (flags[list[x]] & FLAG_CANDIDATE) ? 1u : 0u;
+  if (nc) atomicAdd(&ncand, nc);
+  __syncthreads();
+  const uint32_t m = ncand;
+  if (!m) return;   // uniform
+  group_combine(gX2 + 4 * key, gX1 + 4 * key, &sQ, &sP);
+  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+  grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  lp_init_consts(g);
+  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
+  const g1_aff Pu = sP;
+  const g2_aff Qu = sQ;
+  const bool pass = pair_check(g, Pu, Qu, H[key / NB], F1, B, BP, TMP);
+  if (pass || m == 1)
+    for (uint32_t x = lane_; x < gn; x += 64) {
+      const uint32_t s = list[x];
+      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      verdict[s] = pass ? 1 : 0;
+      atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
+    }
 }
 
 // Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
@@ -925,6 +941,10 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
                        (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
                        (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
                        fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart);
+  if (committee)
+    hipLaunchKernelGGL(k_fb_group, dim3(4 * (unsigned)fb_keys((size_t)n_roots)), dim3(64), 0, st, n_roots, ok,
+                       (const uint32_t*)fw.xok, (const uint32_t*)fw.perm, flags, (const uint64_t*)fw.k64, sig, pk, H, verdict,
+                       (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart, fw.cursor, fw.rsig, fw.rpk);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
                      (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                      (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,

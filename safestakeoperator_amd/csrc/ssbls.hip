@@ -399,6 +399,9 @@ inline size_t fp12_slots(size_t np) {
 // k_miller_final's, then the fallback's committee stage: nS (suspects listed), xtk[2]
 inline uint32_t ntk_words(size_t np) { return 4 + 1 + (uint32_t)((np + 7) / 8) + 3; }
 
+// the tree's per-share products rsig / rpk; the committee stage's group-test mode (k_fb_group) keeps
+// its four quarter sums per (root, id bucket) key in the same buffers
+inline size_t fb_prod_slots(size_t n, size_t n_roots) { return std::max(n, 4 * launch::fb_keys(n_roots)); }
 size_t verify_ws_bytes(size_t n, size_t n_roots) {
   const msm_plan p = plan_size(n, n_roots);
   const size_t np = n_roots + MSM_WMAX;
@@ -408,8 +411,8 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up(launch::hash_ws_bytes(n_roots)) + 4 * align_up((size_t)p.K * 4) + align_up(1024 * 4) +
          align_up(p.n_ent * 4) + align_up(((size_t)p.g2.W << p.g2.c) * sizeof(g2_jac)) +
          align_up(((size_t)p.g1.ngroups * p.g1.W << p.g1.c) * sizeof(g1_jac)) +
-         align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(n * sizeof(g1_jac)) +
-         3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(n * sizeof(g2_jac)) +
+         align_up((size_t)p.g1.ngroups * p.g1.W * sizeof(g1_jac)) + align_up(fb_prod_slots(n, n_roots) * sizeof(g1_jac)) +
+         3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(fb_prod_slots(n, n_roots) * sizeof(g2_jac)) +
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
          align_up(n * 8) + align_up(4 * n_roots * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4) +
          align_up(n * 4) + align_up(4) + align_up((n_roots + 1) * sizeof(fp12)) + align_up(ntk_words(np) * 4) +
@@ -434,10 +437,10 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.b2 = c.take<g2_jac>((size_t)sz.g2.W << sz.g2.c);
   w.b1 = c.take<g1_jac>((size_t)sz.g1.ngroups * sz.g1.W << sz.g1.c);   // >= the merged layout's ngroups << 4
   w.w1 = c.take<g1_jac>((size_t)sz.g1.ngroups * sz.g1.W);
-  w.rpk = c.take<g1_jac>(n);
+  w.rpk = c.take<g1_jac>(fb_prod_slots(n, n_roots));
   w.rcnt = c.take<uint32_t>(n_roots); w.rstart = c.take<uint32_t>(n_roots); w.rcur = c.take<uint32_t>(launch::fb_keys(n_roots));
   w.perm = c.take<uint32_t>(n);
-  w.rsig = c.take<g2_jac>(n);
+  w.rsig = c.take<g2_jac>(fb_prod_slots(n, n_roots));
   w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
   w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
   w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(4 * n_roots); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
