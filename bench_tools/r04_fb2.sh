@@ -14,5 +14,5 @@ for v in "valid:" "one:--invalid-count 1" "pct1:--invalid-rate 0.01" "badop:--ba
   python -c "import json,sys; d=json.load(open('$OUT/$name.json')); print('$name', d['value'], d['ms_per_step'], d['results_ok'], d['invalid_shares_per_batch'])"
 done
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_pct1 -o run -- python -u bench.py $X --invalid-rate 0.01 > $OUT/prof_pct1.json 2> $OUT/prof_pct1.err || { echo "prof failed"; tail -5 $OUT/prof_pct1.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_pct1 -o run -- python -u bench.py $X --invalid-rate 0.01 > $OUT/prof_pct1.json 2> $OUT/prof_pct1.err || { echo "prof failed"; tail -5 $OUT/prof_pct1.err; exit 1; }
 f=$(find $OUT/prof_pct1 -name "*kernel_stats.csv" | head -1); cp $f $OUT/pct1_kernel_stats.csv; head -16 $OUT/pct1_kernel_stats.csv | cut -c1-160

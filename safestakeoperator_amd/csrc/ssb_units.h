@@ -163,14 +163,36 @@ SSB_INL uint64_t gls_digit(const uint32_t* k8, int q) {
   }
   return rem;
 }
+// NAF masks of m < 2^62: m = sum_i 2^i (pos_i - neg_i), no two adjacent digits nonzero (with h = 3m:
+// digit i is nonzero where bits i + 1 of h and m differ, +1 where h has the bit) -- a third of the
+// positions nonzero against half for the binary digits
+SSB_INL void naf_masks(uint64_t m, uint64_t& pos, uint64_t& neg) {
+  const uint64_t h = 3 * m;
+  pos = (h & ~m) >> 1;
+  neg = (m & ~h) >> 1;
+}
+// [d] p for a 64-bit d by NAF digits (d < 2^64: h = 3d in 128 bits, 65 digit positions)
+template <class F> SSB_FN void jac_mul_naf_aff(jac<F>& r, const aff<F>& p, uint64_t d) {
+  const unsigned __int128 h = (unsigned __int128)d * 3u;
+  const unsigned __int128 pos = (h & ~(unsigned __int128)d) >> 1, neg = ((unsigned __int128)d & ~h) >> 1;
+  aff<F> np = p;
+  f_neg(np.y, np.y);
+  jac<F> acc;
+  jac_set_inf(acc);
+  for (int i = 64; i >= 0; --i) {
+    jac_dbl_inl(acc, acc);
+    if ((uint64_t)(pos >> i) & 1u) jac_madd_at(acc, &p);
+    else if ((uint64_t)(neg >> i) & 1u) jac_madd_at(acc, &np);
+  }
+  r = acc;
+}
 // [d] (+-psi^q(p)) -- digit q of a GLS split (sign as above); p in G2
 SSB_FN void unit_gls_term(g2_jac& r, const g2_aff& sig, uint64_t d, int q) {
   if (sig.inf) { jac_set_inf(r); return; }
   g2_aff p = sig;
   for (int i = 0; i < q; ++i) g2_psi_aff(p, p);
   if (q & 1) fp2_neg(p.y, p.y);
-  const uint32_t dw[2] = {(uint32_t)d, (uint32_t)(d >> 32)};
-  jac_mul_aff(r, p, dw, 2);
+  jac_mul_naf_aff(r, p, d);
 }
 SSB_FN void unit_combine_term_gls(g2_jac& r, const g2_aff& sig, const uint32_t* lam8, int q) {
   unit_gls_term(r, sig, gls_digit(lam8, q), q);
@@ -283,22 +305,27 @@ SSB_FN void unit_combine_small(uint8_t* out96, const g2_aff* const* pts, const i
   g2_compress(out96, a);
 }
 // the same, the points read as pts[idx[i]] (the device path: no array of point pointers in a frame)
+// (NAF digits of each |c_i| -- |c_i| < 2^62 -- shared doublings: the registry ids' 48-bit
+// coefficients cost ~16 additions per term instead of ~24)
 SSB_INL void combine_small_jac(g2_jac& acc, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
                                const int64_t* c, uint32_t t) {
-  int nb = 0;
+  uint64_t any = 0;
   for (uint32_t i = 0; i < t; ++i) {
-    const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
-    const int b = m ? 64 - __builtin_clzll(m) : 0;
-    nb = b > nb ? b : nb;
+    uint64_t ps, ng;
+    naf_masks((uint64_t)(c[i] < 0 ? -c[i] : c[i]), ps, ng);
+    any |= ps | ng;
   }
+  const int nb = any ? 64 - __builtin_clzll(any) : 0;
   jac_set_inf(acc);
   for (int b = nb - 1; b >= 0; --b) {
     jac_dbl_inl(acc, acc);
     for (uint32_t i = 0; i < t; ++i) {
-      const uint64_t m = (uint64_t)(c[i] < 0 ? -c[i] : c[i]);
-      if ((m >> b) & 1ull) {
+      uint64_t ps, ng;
+      naf_masks((uint64_t)(c[i] < 0 ? -c[i] : c[i]), ps, ng);
+      const bool p1 = (ps >> b) & 1ull, n1 = (ng >> b) & 1ull;
+      if (p1 || n1) {
         g2_aff q = pts[idx[i]];
-        if (c[i] < 0) fp2_neg(q.y, q.y);
+        if ((c[i] < 0) != n1) fp2_neg(q.y, q.y);
         jac_add_aff_inl(acc, acc, q);
       }
     }
@@ -347,6 +374,66 @@ SSB_FN bool unit_lagrange_ratio(int64_t* c, uint64_t* M, const uint64_t* x, uint
   *M = (uint64_t)L;
   return true;
 }
+// (hi:lo) / d for hi < d: quotient, *rem the remainder (shift-subtract; no 128-bit divide on the device)
+SSB_INL uint64_t udiv128_64(uint64_t hi, uint64_t lo, uint64_t d, uint64_t* rem) {
+  uint64_t q = 0;
+  for (int i = 0; i < 64; ++i) {
+    const uint64_t top = hi >> 63;
+    hi = (hi << 1) | (lo >> 63);
+    lo <<= 1;
+    q <<= 1;
+    if (top || hi >= d) { hi -= d; q |= 1ull; }
+  }
+  *rem = hi;
+  return q;
+}
+// w (n little-endian 64-bit limbs) /= d, returns w mod d
+SSB_INL uint64_t divmod_limbs(uint64_t* w, int n, uint64_t d) {
+  uint64_t rem = 0;
+  for (int i = n - 1; i >= 0; --i) w[i] = udiv128_64(rem, w[i], d, &rem);
+  return rem;
+}
+// y = M^-1 mod r (canonical, 4 limbs) for 1 <= M < 2^62 -- without an Fr exponentiation: with
+// a = r mod M and b = a^-1 mod M (extended Euclid on 64-bit integers), r b == 1 (mod M), so
+// y' = (r b - 1) / M is an integer with M y' == -1 (mod r), and y = r - y'  (y' < r since b < M).
+SSB_INL void inv_small_mod_r(uint64_t* y, uint64_t M) {
+  uint64_t rl[4];
+  for (int i = 0; i < 4; ++i) rl[i] = (uint64_t)R_LIMBS[2 * i] | ((uint64_t)R_LIMBS[2 * i + 1] << 32);
+  if (M == 1) { y[0] = 1; y[1] = y[2] = y[3] = 0; return; }
+  uint64_t w[4] = {rl[0], rl[1], rl[2], rl[3]};
+  const uint64_t a = divmod_limbs(w, 4, M);
+  int64_t t0 = 0, t1 = 1;                        // Bezout coefficients of a modulo M
+  uint64_t r0 = M, r1 = a;
+  while (r1) {
+    const uint64_t qq = r0 / r1;
+    const uint64_t r2 = r0 - qq * r1; r0 = r1; r1 = r2;
+    const int64_t t2 = t0 - (int64_t)qq * t1; t0 = t1; t1 = t2;
+  }
+  const uint64_t b = t0 < 0 ? (uint64_t)(t0 + (int64_t)M) : (uint64_t)t0;   // (r0 == 1: r is prime, M < r)
+  uint64_t v[5];                                 // r b - 1, five limbs
+  uint64_t carry = 0;
+  for (int i = 0; i < 4; ++i) {
+    const unsigned __int128 pr = (unsigned __int128)rl[i] * b;
+    const uint64_t lo = (uint64_t)pr, hi = (uint64_t)(pr >> 64);
+    v[i] = lo + carry;
+    carry = hi + (v[i] < lo ? 1ull : 0ull);
+  }
+  v[4] = carry;
+  for (int i = 0; i < 5; ++i) { const bool bw = v[i] == 0; v[i] -= 1ull; if (!bw) break; }
+  divmod_limbs(v, 5, M);                         // exact: y' in v[0..3]
+  uint64_t br = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t d = rl[i] - v[i] - br;
+    br = (rl[i] < v[i] || (rl[i] == v[i] && br)) ? 1ull : 0ull;
+    y[i] = d;
+  }
+}
+// the four base-u digits of k < r (the GLS split, gls_digit) in one pass: three divisions by u
+SSB_INL void gls_digits4(uint64_t* d, const uint64_t* k) {
+  uint64_t w[4] = {k[0], k[1], k[2], k[3]};
+  for (int q = 0; q < 3; ++q) d[q] = divmod_limbs(w, 4, GLS_U);
+  d[3] = w[0];   // (k < r < u^4)
+}
 // the per-job result of the ratio path: T = sum c_i sig_i (affine) and the GLS digits of M^-1 mod r
 struct ratio_job { g2_aff T; uint64_t d[4]; };
 SSB_FN void unit_combine_ratio_at(ratio_job& out, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
@@ -354,11 +441,9 @@ SSB_FN void unit_combine_ratio_at(ratio_job& out, const g2_aff* __restrict__ pts
   g2_jac acc;
   combine_small_jac(acc, pts, idx, c, t);
   jac_to_aff(out.T, acc);
-  fr mi, mc;
-  fr_from_u64(mi, M);
-  fr_inv(mi, mi);
-  fr_from_mont(mc, mi);
-  for (int q = 0; q < 4; ++q) out.d[q] = gls_digit(mc.l, q);
+  uint64_t y[4];
+  inv_small_mod_r(y, M);
+  gls_digits4(out.d, y);
 }
 
 }  // namespace ssb

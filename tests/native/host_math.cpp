@@ -373,6 +373,15 @@ int main() {
         same = memcmp(a, b, 96) == 0;
       }
       printf("%d %d %llu\n", elig ? 1 : 0, same, (unsigned long long)M);
+    } else if (cmd == "invsmall") {  // invsmall M: M^-1 mod r (4 limbs hex, most significant first) and its GLS digits
+      std::string a; is >> a;
+      const uint64_t M = std::stoull(a, nullptr, 0);
+      uint64_t y[4], d[4];
+      inv_small_mod_r(y, M);
+      gls_digits4(d, y);
+      printf("%016llx%016llx%016llx%016llx %llu %llu %llu %llu\n", (unsigned long long)y[3], (unsigned long long)y[2],
+             (unsigned long long)y[1], (unsigned long long)y[0], (unsigned long long)d[0], (unsigned long long)d[1],
+             (unsigned long long)d[2], (unsigned long long)d[3]);
     } else if (cmd == "madd") {  // madd <trials>: jac_madd_at (bucket loops) vs jac_add_aff_inl, incl. special cases
       int trials; is >> trials;
       int bad = 0, n = 0;

@@ -152,6 +152,22 @@ def test_registry_ratio_path(host_exe):
     assert [l.split()[0] for l in out[len(cases):]] == ["0", "0"]
 
 
+def test_small_inverse_and_gls_digits(host_exe):
+    """inv_small_mod_r (extended Euclid on 64-bit integers + one exact division) == pow(M, -1, r), and
+    gls_digits4 (three divisions by u) are the base-u digits, for edge and pseudo-random M < 2^62."""
+    import random
+    r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    u = 0xd201000000010000
+    rnd = random.Random(5)
+    Ms = [1, 2, 3, 7, 2**32, 2**32 + 1, 2**61 - 1, 2**62 - 1, 65535 * 65534, 6] + [rnd.randrange(1, 2**62) for _ in range(40)]
+    out = _run(host_exe, ["invsmall %d" % M for M in Ms])
+    for M, line in zip(Ms, out):
+        y, *d = line.split()
+        y, d = int(y, 16), list(map(int, d))
+        assert y == pow(M, -1, r), M
+        assert all(0 <= x < u for x in d[:3]) and sum(x * u ** q for q, x in enumerate(d)) == y, M
+
+
 def test_bucket_madd_matches_generic(host_exe):
     """jac_madd_at (the MSM bucket loops' in-place mixed addition) == jac_add_aff_inl coordinate for
     coordinate, on G2 and G1, including infinity on either side, doubling and opposite points."""
