@@ -171,28 +171,14 @@ SSB_INL void naf_masks(uint64_t m, uint64_t& pos, uint64_t& neg) {
   pos = (h & ~m) >> 1;
   neg = (m & ~h) >> 1;
 }
-// [d] p for a 64-bit d by NAF digits (d < 2^64: h = 3d in 128 bits, 65 digit positions)
-template <class F> SSB_FN void jac_mul_naf_aff(jac<F>& r, const aff<F>& p, uint64_t d) {
-  const unsigned __int128 h = (unsigned __int128)d * 3u;
-  const unsigned __int128 pos = (h & ~(unsigned __int128)d) >> 1, neg = ((unsigned __int128)d & ~h) >> 1;
-  aff<F> np = p;
-  f_neg(np.y, np.y);
-  jac<F> acc;
-  jac_set_inf(acc);
-  for (int i = 64; i >= 0; --i) {
-    jac_dbl_inl(acc, acc);
-    if ((uint64_t)(pos >> i) & 1u) jac_madd_at(acc, &p);
-    else if ((uint64_t)(neg >> i) & 1u) jac_madd_at(acc, &np);
-  }
-  r = acc;
-}
 // [d] (+-psi^q(p)) -- digit q of a GLS split (sign as above); p in G2
 SSB_FN void unit_gls_term(g2_jac& r, const g2_aff& sig, uint64_t d, int q) {
   if (sig.inf) { jac_set_inf(r); return; }
   g2_aff p = sig;
   for (int i = 0; i < q; ++i) g2_psi_aff(p, p);
   if (q & 1) fp2_neg(p.y, p.y);
-  jac_mul_naf_aff(r, p, d);
+  const uint32_t dw[2] = {(uint32_t)d, (uint32_t)(d >> 32)};
+  jac_mul_aff(r, p, dw, 2);
 }
 SSB_FN void unit_combine_term_gls(g2_jac& r, const g2_aff& sig, const uint32_t* lam8, int q) {
   unit_gls_term(r, sig, gls_digit(lam8, q), q);
@@ -374,6 +360,13 @@ SSB_FN bool unit_lagrange_ratio(int64_t* c, uint64_t* M, const uint64_t* x, uint
   *M = (uint64_t)L;
   return true;
 }
+// high 64 bits of a 64 x 64-bit product (32-bit halves)
+SSB_INL uint64_t mulhi64(uint64_t a, uint64_t b) {
+  const uint64_t a0 = (uint32_t)a, a1 = a >> 32, b0 = (uint32_t)b, b1 = b >> 32;
+  const uint64_t p00 = a0 * b0, p01 = a0 * b1, p10 = a1 * b0, p11 = a1 * b1;
+  const uint64_t mid = (p00 >> 32) + (uint32_t)p01 + (uint32_t)p10;
+  return p11 + (p01 >> 32) + (p10 >> 32) + (mid >> 32);
+}
 // (hi:lo) / d for hi < d: quotient, *rem the remainder (shift-subtract; no 128-bit divide on the device)
 SSB_INL uint64_t udiv128_64(uint64_t hi, uint64_t lo, uint64_t d, uint64_t* rem) {
   uint64_t q = 0;
@@ -413,8 +406,7 @@ SSB_INL void inv_small_mod_r(uint64_t* y, uint64_t M) {
   uint64_t v[5];                                 // r b - 1, five limbs
   uint64_t carry = 0;
   for (int i = 0; i < 4; ++i) {
-    const unsigned __int128 pr = (unsigned __int128)rl[i] * b;
-    const uint64_t lo = (uint64_t)pr, hi = (uint64_t)(pr >> 64);
+    const uint64_t lo = rl[i] * b, hi = mulhi64(rl[i], b);
     v[i] = lo + carry;
     carry = hi + (v[i] < lo ? 1ull : 0ull);
   }
