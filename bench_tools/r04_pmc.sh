@@ -2,7 +2,7 @@
 # round 4: HBM traffic of the per-share launches, attributed.  FETCH_SIZE and WRITE_SIZE passes (one
 # counter per rocprofv3 run, never combined with tracing) over a short bench run -- its roofline batch
 # (8 x C2, fused launches) and the C2 batches -- for the product library ("base": the fused launches'
-# roles out of line) and the inlined-roles build ("inl", SSB_VARIANT=inl SSB_VARIANT_DEFS=-DSSB_ROLES_INLINE),
+# roles inlined) and the out-of-line-roles build ("outl", SSB_VARIANT=outl SSB_VARIANT_DEFS=-DSSB_ROLES_OUTLINE),
 # and once on three-stream slots, where the subgroup checks, the sort's scatter and its count are
 # launches of their own (k_subgroup, k_msm_sort, k_decode_sig).
 #   bench_tools/r04_pmc.sh TAG
@@ -20,11 +20,11 @@ run() {   # name, variant, extra bench args
   rm -rf $OUT/$name
 }
 run base "" || exit 1
-run inl inl || exit 1
+run outl outl || exit 1
 run split "" --pipeline 1 --slot-streams 3 || exit 1
 python3 - <<EOF
 import json
-for name in ("base", "inl", "split"):
+for name in ("base", "outl", "split"):
     d = json.load(open("$OUT/%s.summary.json" % name))
     for k, v in sorted(d.items()):
         if any(x in k for x in ("subgroup", "decode", "msm_sort", "bucket2")):

@@ -5,14 +5,15 @@
 #include "ssb_units.h"
 #include "../../include/ssbls.h"
 
-// The roles of a fused launch (its block ranges running different stages) are out-of-line functions:
-// each role gets its own register allocation instead of one allocation -- and one set of spills --
-// shared by every lane of the launch.  SSB_VARIANT_DEFS=-DSSB_ROLES_INLINE builds the inlined form
-// for A/B runs.
-#ifdef SSB_ROLES_INLINE
-#define SSB_ROLE SSB_INL
-#else
+// The roles of a fused launch (its block ranges running different stages) stay inlined: out of line
+// (SSB_VARIANT_DEFS=-DSSB_ROLES_OUTLINE, an experiment build) each role has its own register
+// allocation and the subgroup lanes' loop spills drop, but the roles' argument structs go through
+// scratch at every call and the measured HBM writes grew (round 4 PMC, profiles/r04_pmc_*.json:
+// k_subgroup_map 155 -> 212 MB, k_decode_count 552 -> 635 MB per roofline launch).
+#ifdef SSB_ROLES_OUTLINE
 #define SSB_ROLE SSB_FN
+#else
+#define SSB_ROLE SSB_INL
 #endif
 
 // Experiment builds only (SSB_VARIANT_DEFS=-DSSB_TRACE_TAIL, bench_tools/trace_tail.py): the tail
