@@ -300,7 +300,13 @@ def launch_ranks(n, argv):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    return subprocess.call(launch_command(n, argv, port))
+    # the ranks' stdout through a pipe: rank 0's JSON line stays on stdout, anything else the launcher
+    # or a backend prints there (gloo's "[Gloo] Rank ... connected" lines) goes to stderr
+    p = subprocess.Popen(launch_command(n, argv, port), stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def main():

@@ -25,3 +25,13 @@ def test_world_size_mismatch_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
                        text=True, timeout=60)
     assert r.returncode == 2 and "WORLD_SIZE=3 but --gpus 2" in r.stderr
+
+
+def test_launch_ranks_keeps_only_the_json_line_on_stdout(monkeypatch, capsys):
+    """The self-launch forwards the ranks' stdout: the JSON line stays on stdout, a backend's chatter
+    ("[Gloo] Rank 0 is connected ...") goes to stderr; the launcher's exit status is returned."""
+    child = "print('[Gloo] Rank 0 is connected to 1 peer ranks'); print('{\"value\": 1}'); raise SystemExit(3)"
+    monkeypatch.setattr(bench, "launch_command", lambda n, argv, port: [sys.executable, "-c", child])
+    rc = bench.launch_ranks(2, [])
+    out, err = capsys.readouterr()
+    assert rc == 3 and out.strip() == '{"value": 1}' and "[Gloo]" in err
