@@ -38,6 +38,11 @@ using launch::fb_jobs;
 // committee stage: at most this many suspect shares are checked one by one (beyond it the tree decides)
 constexpr uint32_t FB_SUSPECT_MAX = 2048;
 constexpr unsigned EX_SINGLE_BLOCKS = 512;
+// grid of the fallback launches that stride over their work (k_fb_group, k_fb_single, k_fb_level):
+// most failed batches leave them at their first test, and a grid of thousands of blocks waited
+// milliseconds for free slots behind the other pipeline slots' waves (round 4 profile of the 1e-2
+// workload: k_fb_single 6.0 ms, k_fb_group 2.9 ms per launch while doing nothing)
+constexpr unsigned FB_GRID_MAX = 512;
 
 // One workgroup (the last block of k_fb_rlc's grid): counting sort of the shares by (root, operator-id
 // bucket) -- key = root * NB + bucket(id), NB = fb_nbuckets(n_roots) -- into perm, the per-key
@@ -698,9 +703,9 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
 // candidates with the batch's own scalars,
 //     e(S1, H(r)) * e(-g1, S2) == 1,   S1 = sum k_i pk_i,   S2 = sum k_i sig_i  over the group,
 // a passing group decides its candidates valid (soundness 2^-63), a one-candidate group is exactly that
-// share's verify.  Blocks (key, q), the layout of k_fb_root: block q sums quarter q of the scalars
+// share's verify.  Items (key, q), the layout of k_fb_root: item q sums quarter q of the scalars
 // (bits 16q .. 16q+15) of both sums into gX2 / gX1 (the tree's per-share product buffers, unused in
-// this mode: sized for 4 fb_keys entries); the last of the key's four blocks -- ticket: the scatter's
+// this mode: sized for 4 fb_keys entries); the last of the key's four items -- ticket: the scatter's
 // cursor, which fb_prep_block left at kstart + kcnt -- combines the quarters and runs the check.
 // k_fb_root then deduces the rest of every job from its committee relations (deduce_job) and
 // k_fb_single checks what is left.
@@ -730,46 +735,52 @@ __global__ void SSB_LB2(64) k_fb_group(int n_roots, const uint32_t* __restrict__
   using namespace ssb::lane;
   if (*ok || *xok != 2u) return;   // uniform: the batch passed / not the group-test mode
   const uint32_t NB = (uint32_t)launch::fb_nbuckets(n_roots);
-  const uint32_t key = blockIdx.x >> 2, q = blockIdx.x & 3;
-  if (key >= (uint32_t)n_roots * NB) return;
-  const uint32_t gn = kcnt[key];
-  if (!gn) return;   // (the four blocks of an empty key all leave here: no ticket)
-  const uint32_t* list = perm + kstart[key];
+  const uint32_t items = 4u * (uint32_t)n_roots * NB;
   __shared__ fr_lds u;
   __shared__ uint32_t flg, last, ncand;
   __shared__ g1_aff sP;
   __shared__ g2_aff sQ;
   const int lane_ = threadIdx.x;
-  group_quarters(u.b, list, gn, flags, k64, sig_aff, pk_aff, (int)q, gX2 + 4 * key + q, gX1 + 4 * key + q);
-  __threadfence();
-  __syncthreads();
-  if (lane_ == 0) last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (lane_ == 0) ncand = 0u;
-  __syncthreads();
-  uint32_t nc = 0;
-  for (uint32_t x = lane_; x < gn; x += 64) nc += (flags[list[x]] & FLAG_CANDIDATE) ? 1u : 0u;
-  if (nc) atomicAdd(&ncand, nc);
-  __syncthreads();
-  const uint32_t m = ncand;
-  if (!m) return;   // uniform
-  group_combine(gX2 + 4 * key, gX1 + 4 * key, &sQ, &sP);
-  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
-  grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
-  lp_init_consts(g);
-  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
-  const g1_aff Pu = sP;
-  const g2_aff Qu = sQ;
-  const bool pass = pair_check(g, Pu, Qu, H[key / NB], F1, B, BP, TMP);
-  if (pass || m == 1)
-    for (uint32_t x = lane_; x < gn; x += 64) {
-      const uint32_t s = list[x];
-      if (!(flags[s] & FLAG_CANDIDATE)) continue;
-      verdict[s] = pass ? 1 : 0;
-      atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
-    }
+  // blocks stride over the (key, quarter) items: a launch of a few hundred blocks, not 4 per key --
+  // on batches that do not take this mode every block leaves at once, and a launch of thousands of
+  // blocks spent milliseconds waiting for free slots behind the other pipeline slots' waves
+  for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const uint32_t key = it >> 2, q = it & 3;
+    const uint32_t gn = kcnt[key];
+    if (!gn) continue;   // (uniform: the four items of an empty key all skip: no ticket)
+    const uint32_t* list = perm + kstart[key];
+    group_quarters(u.b, list, gn, flags, k64, sig_aff, pk_aff, (int)q, gX2 + 4 * key + q, gX1 + 4 * key + q);
+    __threadfence();
+    __syncthreads();
+    if (lane_ == 0) last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
+    __syncthreads();
+    if (!last) continue;
+    __threadfence();
+    if (lane_ == 0) ncand = 0u;
+    __syncthreads();
+    uint32_t nc = 0;
+    for (uint32_t x = lane_; x < gn; x += 64) nc += (flags[list[x]] & FLAG_CANDIDATE) ? 1u : 0u;
+    if (nc) atomicAdd(&ncand, nc);
+    __syncthreads();
+    const uint32_t m = ncand;
+    if (!m) continue;   // uniform
+    group_combine(gX2 + 4 * key, gX1 + 4 * key, &sQ, &sP);
+    __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+    grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+    lp_init_consts(g);
+    const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
+    const g1_aff Pu = sP;
+    const g2_aff Qu = sQ;
+    const bool pass = pair_check(g, Pu, Qu, H[key / NB], F1, B, BP, TMP);
+    if (pass || m == 1)
+      for (uint32_t x = lane_; x < gn; x += 64) {
+        const uint32_t s = list[x];
+        if (!(flags[s] & FLAG_CANDIDATE)) continue;
+        verdict[s] = pass ? 1 : 0;
+        atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
+      }
+    __syncthreads();
+  }
 }
 
 // Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
@@ -942,7 +953,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
                        (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
                        fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart);
   if (committee)
-    hipLaunchKernelGGL(k_fb_group, dim3(4 * (unsigned)fb_keys((size_t)n_roots)), dim3(64), 0, st, n_roots, ok,
+    hipLaunchKernelGGL(k_fb_group, dim3(std::min(4 * (unsigned)fb_keys((size_t)n_roots), FB_GRID_MAX)), dim3(64), 0, st, n_roots, ok,
                        (const uint32_t*)fw.xok, (const uint32_t*)fw.perm, flags, (const uint64_t*)fw.k64, sig, pk, H, verdict,
                        (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart, fw.cursor, fw.rsig, fw.rpk);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
@@ -951,7 +962,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
                      committee ? fw.nS : (uint32_t*)nullptr, cj, pk);
   if (L == 1) return;
   {
-    const unsigned grid = (unsigned)(n < 2048 ? n : 2048);
+    const unsigned grid = std::min((unsigned)n, FB_GRID_MAX);
     hipLaunchKernelGGL(k_fb_single, dim3(grid), dim3(64), 0, st, n_roots, ok, (const uint32_t*)fw.nfail,
                        (const uint32_t*)fw.start, (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst,
                        (const uint8_t*)fw.gv0, (const uint32_t*)flags, share_root, H, sig, pk, verdict, xok);
@@ -962,7 +973,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   for (int l = 1; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;
-    const unsigned grid = (unsigned)(bound < 2048 ? bound : 2048);
+    const unsigned grid = (unsigned)std::min(bound, (uint64_t)FB_GRID_MAX);
     uint8_t* cur = (l & 1) ? fw.gv1 : fw.gv0;
     const uint8_t* prev = (l & 1) ? fw.gv0 : fw.gv1;
     hipLaunchKernelGGL(k_fb_level, dim3(grid), dim3(LV_THREADS), 0, st, l, L, lb, n_roots, ok, (const uint32_t*)fw.start,
