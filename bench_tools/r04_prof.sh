@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=$1; shift; mkdir -p $OUT
 export TMPDIR=/tmp
-X="--steps 20 --warmup 2 --no-cpu-baseline --no-host-buffers --collector-windows 0 --sustained-steps 0"
+X="${PROF_X:---steps 20 --warmup 2} --no-cpu-baseline --no-host-buffers --collector-windows 0 --sustained-steps 0"
 for v in "$@"; do
   name=${v%%:*}; a=${v#*:}
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$name -o run -- python3 -u bench.py $X $a > $OUT/prof_$name.json 2> $OUT/prof_$name.err || { echo "prof $name failed"; tail -5 $OUT/prof_$name.err; exit 1; }
