@@ -15,12 +15,14 @@
 // reference's verify (k_i != 0 mod r), so it gets verdict 0.  Children of a passing group are not
 // tested; a group whose share range equals its failed parent's inherits the failure untested.
 // Launches (all on the slot's stream, each a uniform no-op when the batch passed):
-//   k_fb_rlc     verdicts the batch check decides, the candidates' scalars k_i, counting sort by root
-//   k_fb_root    level 0, one check per root: S_r = sum k_i sig_i as a 4-bit-digit bucket sum (no
+//   k_fb_rlc     verdicts the batch check decides, the candidates' scalars k_i, counting sort by root,
+//                the committee relations (suspect jobs)
+//   k_fb_excl    the committee stage: exclusion check + suspects alone, or the group-test mode
+//   k_fb_root    level 0, one check per root (or the committee stage's verdicts / deductions): S_r = sum k_i sig_i as a 4-bit-digit bucket sum (no
 //                per-share products); e(PK_r, H(r)) is the batch check's own Miller value
 //   k_fb_single  <= FB_SINGLE_MAX shares in failing roots: each checked alone (no products, one
 //                pairing check deep) -- one invalid share per C2 batch: 256 single checks
-//   k_fb_sparse  otherwise: k_i sig_i, k_i pk_i for the failing roots' candidates, then
+//                otherwise (same launch): k_i sig_i, k_i pk_i for the failing roots' candidates, then
 //   k_fb_level l the 16-ary levels below the root (work at 1% invalid shares, C2: ~3.5k group checks
 //                instead of 16,384 per-share checks)
 // lane-program kernels at two waves per SIMD (256 registers, the rest spilled within the queue
@@ -38,10 +40,10 @@ using launch::fb_jobs;
 // committee stage: at most this many suspect shares are checked one by one (beyond it the tree decides)
 constexpr uint32_t FB_SUSPECT_MAX = 2048;
 constexpr unsigned EX_SINGLE_BLOCKS = 512;
-// grid of the fallback launches that stride over their work (k_fb_group, k_fb_single, k_fb_level):
+// grid of the fallback launches that stride over their work (k_fb_single, k_fb_level):
 // most failed batches leave them at their first test, and a grid of thousands of blocks waited
 // milliseconds for free slots behind the other pipeline slots' waves (round 4 profile of the 1e-2
-// workload: k_fb_single 6.0 ms, k_fb_group 2.9 ms per launch while doing nothing)
+// workload: k_fb_single 6.0 ms, the former k_fb_group 2.9 ms per launch while doing nothing)
 constexpr unsigned FB_GRID_MAX = 512;
 
 // One workgroup (the last block of k_fb_rlc's grid): counting sort of the shares by (root, operator-id
@@ -282,7 +284,8 @@ __global__ void SSB_LB(64) k_fb_rlc(int n, rlc_key key, const uint32_t* __restri
 // X_q = sum_w 2^(4w) W_{4q+w}.  The last of the root's four blocks (completion ticket rtk[r], zeroed
 // by fb_prep_block) forms S_r = sum_q 2^(16q) X_q and runs the check: one lane-program Miller loop
 // e(-g1, S_r), times f[r], final exponentiation.  gv0[group of r] and, on a pass, the verdicts of
-// the root's candidates.  Product-free: the failing roots' per-share products follow in k_fb_sparse.
+// the root's candidates.  Product-free: the failing roots' per-share products follow in k_fb_single's
+// launch (sparse_product).
 constexpr int FR_CHUNK = 512;
 // at most this many shares in failing roots after level 0: k_fb_single checks them one by one
 constexpr uint32_t FB_SINGLE_MAX = 384;
@@ -294,18 +297,14 @@ constexpr int BS_S0 = bs_max(bs_max(bs_max(lane::MILLER_ITER_SCRATCH, lane::MILL
 constexpr int BS_SLOTS = BS_S0 + 24 + 12 + 4 + 84;
 
 // The per-share products the levels below 0 sum, for the candidates of the roots whose level-0
-// check failed only: threads [0, n) rsig[s] = k_s sig_s, [n, 2n) rpk[s] = k_s pk_s.
+// check failed only: items [0, n) rsig[s] = k_s sig_s, [n, 2n) rpk[s] = k_s pk_s (run by
+// k_fb_single's blocks when the failing roots hold more than FB_SINGLE_MAX shares).
 // Binary double-and-add (no window table): the private segment stays small -- every slot queue
 // reserves scratch for the largest kernel it has run, and this one is launched on every batch.
-__global__ void SSB_LB2(64) k_fb_sparse(int n, int n_roots, const uint32_t* __restrict__ ok,
-                                      const uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
-                                      const uint32_t* __restrict__ gst0, const uint8_t* __restrict__ gv0,
-                                      const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
-                                      const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
-                                      g1_jac* __restrict__ rpk, const uint32_t* __restrict__ nfail,
-                                      const uint32_t* __restrict__ xok) {
-  if (*ok || *nfail <= FB_SINGLE_MAX || (xok && *xok)) return;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+SSB_FN void sparse_product(int g, int n, int n_roots, const uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
+                           const uint32_t* __restrict__ gst0, const uint8_t* __restrict__ gv0, const uint64_t* __restrict__ k64,
+                           const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff, g2_jac* __restrict__ rsig,
+                           g1_jac* __restrict__ rpk) {
   const int s = g < n ? g : g - n;
   if (s >= n || !(flags[s] & FLAG_CANDIDATE)) return;
   const uint32_t r = share_root[s];
@@ -571,7 +570,7 @@ SSB_FN g1_aff neg_suspect_sum(uint32_t sb, uint32_t nr, const uint32_t* __restri
 // pair multiplies ftot by the n_roots + 1 Miller values and runs ONE final exponentiation.
 // (the roles of k_fb_excl are out of line: each role's temporaries live in its own frame, and the
 // kernel's private segment is the largest role's, not their sum)
-struct ex_lds { fr_lds u; uint32_t flg, last; };
+struct ex_lds { fr_lds u; uint32_t flg, last, ncand; g1_aff sP; g2_aff sQ; };
 SSB_FN void ex_singles(ex_lds& L, int first, uint32_t ns, const uint32_t* __restrict__ slist,
                        const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ sig_aff,
                        const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H, uint8_t* __restrict__ verdict) {
@@ -653,52 +652,7 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
   if (lane_ == 0) { *xok = pass ? 1u : 0u; xtk[0] = 0u; }
 }
 
-// The committee stage's checks, after k_fb_rlc's consistency pass listed the suspects (nS of them):
-//   nS <= FB_SUSPECT_MAX -- the EXCLUSION check, the batch check without the suspects:
-//       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
-//       E_r = sum_{suspects of root r} k_i pk_i  (block r: products on the lanes, a lane tree),
-//       X   = sum_{suspects} k_i sig_i          (blocks n_roots .. +3: 4-bit-digit bucket sums),
-//     where ftot is the batch check's own Miller product (k_miller_final) -- by bilinearity this is
-//     the RLC check over every non-suspect candidate with the batch's own scalars (soundness 2^-63),
-//     at the cost of one Miller loop per root holding suspects: *xok = 1 decides them all valid;
-//     and every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's
-//     verify (blocks n_roots + 4 ..).  The pair blocks finish with completion tickets (xtk[0]: pairs,
-//     xtk[1]: X's quarters); the last pair runs the product and ONE final exponentiation;
-//   nS > FB_SUSPECT_MAX -- GROUP-TEST mode (e.g. a faulty operator in every committee): *xok = 2, and
-//     k_fb_group runs one RLC check per (root, operator-id bucket) group of candidates, k_fb_root
-//     deduces the rest from the committee relations (deduce_job), k_fb_single checks what is left;
-//   nS == 0 (no relation broken: the invalid shares sit in jobs without redundancy) -- *xok = 0, the tree.
-__global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nS,
-                                     const uint32_t* __restrict__ slist, const uint32_t* __restrict__ start,
-                                     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
-                                     uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
-                                     const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
-                                     const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H,
-                                     const fp12* __restrict__ ftot, fp12* __restrict__ fex, g2_jac* __restrict__ X4,
-                                     uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict,
-                                     const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ kstart) {
-  if (*ok) return;   // uniform: the batch passed
-  const uint32_t ns = *nS;
-  const int blk = blockIdx.x, lane_ = threadIdx.x;
-  const bool gmode = ns > FB_SUSPECT_MAX && kcnt;
-  if (ns == 0 || (ns > FB_SUSPECT_MAX && !gmode)) {   // nothing to exclude / no group keys: the tree decides
-    if (blk == 0 && lane_ == 0) *xok = 0u;
-    return;
-  }
-  __shared__ ex_lds L;
-  if (gmode) {   // the group tests follow in k_fb_group
-    if (blk == 0 && lane_ == 0) *xok = 2u;
-    return;
-  }
-  if (blk >= n_roots + 4) {   // the suspects, one pairing check each
-    ex_singles(L, n_roots + 4, ns, slist, share_root, sig_aff, pk_aff, H, verdict);
-    return;
-  }
-  if (ex_pair(L, n_roots, ns, slist, start, cnt, perm, flags, k64, sig_aff, pk_aff, H, fex, X4, xtk))
-    ex_final(L, n_roots, ftot, fex, xtk, xok);
-}
-
-// GROUP-TEST mode of the committee stage (k_fb_excl set *xok = 2: more suspects than FB_SUSPECT_MAX,
+// GROUP-TEST mode of the committee stage (more suspects than FB_SUSPECT_MAX,
 // e.g. a faulty operator in every committee): one RLC check per (root, operator-id bucket) group of
 // candidates with the batch's own scalars,
 //     e(S1, H(r)) * e(-g1, S2) == 1,   S1 = sum k_i pk_i,   S2 = sum k_i sig_i  over the group,
@@ -708,8 +662,10 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
 // this mode: sized for 4 fb_keys entries); the last of the key's four items -- ticket: the scatter's
 // cursor, which fb_prep_block left at kstart + kcnt -- combines the quarters and runs the check.
 // k_fb_root then deduces the rest of every job from its committee relations (deduce_job) and
-// k_fb_single checks what is left.
-// (k_fb_group's roles out of line: the quarter sums' and the combines' point temporaries live in
+// k_fb_single checks what is left.  (Run by k_fb_excl's blocks in that mode: one launch less in
+// every failed batch's chain -- a launch that leaves at once still waits for a free wave slot
+// behind the other pipeline slots' waves.)
+// (the group tests' roles out of line: the quarter sums' and the combines' point temporaries live in
 // their own frames, not in the kernel's beside the pairing check's)
 SSB_FN void group_quarters(fr_bucket_lds& ub, const uint32_t* __restrict__ list, uint32_t gn, const uint32_t* __restrict__ flags,
                            const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
@@ -725,67 +681,103 @@ SSB_FN void group_combine(const g2_jac* __restrict__ X2, const g1_jac* __restric
   const g1_aff P = combine_quarters<fp>(X1);
   if (threadIdx.x == 0) *sP = P;
 }
-__global__ void SSB_LB2(64) k_fb_group(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ xok,
-                                      const uint32_t* __restrict__ perm, uint32_t* __restrict__ flags,
-                                      const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
-                                      const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H,
-                                      uint8_t* __restrict__ verdict, const uint32_t* __restrict__ kcnt,
-                                      const uint32_t* __restrict__ kstart, uint32_t* __restrict__ cursor,
-                                      g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1) {
+// the last item of a group: combine the quarters, ONE RLC check, the candidates' verdicts on a pass
+// (or for a one-candidate group); out of line, so its temporaries stay out of k_fb_excl's frame
+SSB_FN void ex_group_check(ex_lds& L, const uint32_t* __restrict__ list, uint32_t gn, uint32_t m,
+                           uint32_t* __restrict__ flags, const g2_jac* __restrict__ X2, const g1_jac* __restrict__ X1,
+                           const g2_aff& h, uint8_t* __restrict__ verdict) {
   using namespace ssb::lane;
-  if (*ok || *xok != 2u) return;   // uniform: the batch passed / not the group-test mode
-  const uint32_t NB = (uint32_t)launch::fb_nbuckets(n_roots);
-  const uint32_t items = 4u * (uint32_t)n_roots * NB;
-  __shared__ fr_lds u;
-  __shared__ uint32_t flg, last, ncand;
-  __shared__ g1_aff sP;
-  __shared__ g2_aff sQ;
   const int lane_ = threadIdx.x;
-  // blocks stride over the (key, quarter) items: a launch of a few hundred blocks, not 4 per key --
-  // on batches that do not take this mode every block leaves at once, and a launch of thousands of
-  // blocks spent milliseconds waiting for free slots behind the other pipeline slots' waves
-  for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
-    const uint32_t key = it >> 2, q = it & 3;
-    const uint32_t gn = kcnt[key];
-    if (!gn) continue;   // (uniform: the four items of an empty key all skip: no ticket)
-    const uint32_t* list = perm + kstart[key];
-    group_quarters(u.b, list, gn, flags, k64, sig_aff, pk_aff, (int)q, gX2 + 4 * key + q, gX1 + 4 * key + q);
-    __threadfence();
-    __syncthreads();
-    if (lane_ == 0) last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
-    __syncthreads();
-    if (!last) continue;
-    __threadfence();
-    if (lane_ == 0) ncand = 0u;
-    __syncthreads();
-    uint32_t nc = 0;
-    for (uint32_t x = lane_; x < gn; x += 64) nc += (flags[list[x]] & FLAG_CANDIDATE) ? 1u : 0u;
-    if (nc) atomicAdd(&ncand, nc);
-    __syncthreads();
-    const uint32_t m = ncand;
-    if (!m) continue;   // uniform
-    group_combine(gX2 + 4 * key, gX1 + 4 * key, &sQ, &sP);
-    __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
-    grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
-    lp_init_consts(g);
-    const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
-    const g1_aff Pu = sP;
-    const g2_aff Qu = sQ;
-    const bool pass = pair_check(g, Pu, Qu, H[key / NB], F1, B, BP, TMP);
-    if (pass || m == 1)
-      for (uint32_t x = lane_; x < gn; x += 64) {
-        const uint32_t s = list[x];
-        if (!(flags[s] & FLAG_CANDIDATE)) continue;
-        verdict[s] = pass ? 1 : 0;
-        atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
-      }
-    __syncthreads();
+  group_combine(X2, X1, &L.sQ, &L.sP);
+  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
+  lp_init_consts(g);
+  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
+  const g1_aff Pu = L.sP;
+  const g2_aff Qu = L.sQ;
+  const bool pass = pair_check(g, Pu, Qu, h, F1, B, BP, TMP);
+  if (pass || m == 1)
+    for (uint32_t x = lane_; x < gn; x += 64) {
+      const uint32_t s = list[x];
+      if (!(flags[s] & FLAG_CANDIDATE)) continue;
+      verdict[s] = pass ? 1 : 0;
+      atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
+    }
+  __syncthreads();
+}
+// The committee stage's checks, after k_fb_rlc's consistency pass listed the suspects (nS of them):
+//   nS <= FB_SUSPECT_MAX -- the EXCLUSION check, the batch check without the suspects:
+//       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
+//       E_r = sum_{suspects of root r} k_i pk_i  (block r: products on the lanes, a lane tree),
+//       X   = sum_{suspects} k_i sig_i          (blocks n_roots .. +3: 4-bit-digit bucket sums),
+//     where ftot is the batch check's own Miller product (k_miller_final) -- by bilinearity this is
+//     the RLC check over every non-suspect candidate with the batch's own scalars (soundness 2^-63),
+//     at the cost of one Miller loop per root holding suspects: *xok = 1 decides them all valid;
+//     and every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's
+//     verify (blocks n_roots + 4 ..).  The pair blocks finish with completion tickets (xtk[0]: pairs,
+//     xtk[1]: X's quarters); the last pair runs the product and ONE final exponentiation;
+//   nS > FB_SUSPECT_MAX -- GROUP-TEST mode (e.g. a faulty operator in every committee): *xok = 2, and
+//     the blocks run one RLC check per (root, operator-id bucket) group of candidates, k_fb_root
+//     deduces the rest from the committee relations (deduce_job), k_fb_single checks what is left;
+//   nS == 0 (no relation broken: the invalid shares sit in jobs without redundancy) -- *xok = 0, the tree.
+__global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nS,
+                                     const uint32_t* __restrict__ slist, const uint32_t* __restrict__ start,
+                                     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
+                                     uint32_t* __restrict__ flags, const uint32_t* __restrict__ share_root,
+                                     const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
+                                     const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H,
+                                     const fp12* __restrict__ ftot, fp12* __restrict__ fex, g2_jac* __restrict__ X4,
+                                     uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict,
+                                     const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ kstart,
+                                     uint32_t* __restrict__ cursor, g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1) {
+  if (*ok) return;   // uniform: the batch passed
+  const uint32_t ns = *nS;
+  const int blk = blockIdx.x, lane_ = threadIdx.x;
+  const bool gmode = ns > FB_SUSPECT_MAX && kcnt;
+  if (ns == 0 || (ns > FB_SUSPECT_MAX && !gmode)) {   // nothing to exclude / no group keys: the tree decides
+    if (blk == 0 && lane_ == 0) *xok = 0u;
+    return;
   }
+  __shared__ ex_lds L;
+  if (gmode) {   // group-test mode: blocks stride over the (key, quarter) items
+    if (blk == 0 && lane_ == 0) *xok = 2u;
+    const uint32_t NB = (uint32_t)launch::fb_nbuckets(n_roots);
+    const uint32_t items = 4u * (uint32_t)n_roots * NB;
+    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+      const uint32_t key = it >> 2, q = it & 3;
+      const uint32_t gn = kcnt[key];
+      if (!gn) continue;   // (uniform: the four items of an empty key all skip: no ticket)
+      const uint32_t* list = perm + kstart[key];
+      group_quarters(L.u.b, list, gn, flags, k64, sig_aff, pk_aff, (int)q, gX2 + 4 * key + q, gX1 + 4 * key + q);
+      __threadfence();
+      __syncthreads();
+      if (lane_ == 0) L.last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
+      __syncthreads();
+      if (!L.last) continue;
+      __threadfence();
+      if (lane_ == 0) L.ncand = 0u;
+      __syncthreads();
+      uint32_t nc = 0;
+      for (uint32_t x = lane_; x < gn; x += 64) nc += (flags[list[x]] & FLAG_CANDIDATE) ? 1u : 0u;
+      if (nc) atomicAdd(&L.ncand, nc);
+      __syncthreads();
+      const uint32_t m = L.ncand;
+      if (!m) continue;   // uniform
+      ex_group_check(L, list, gn, m, flags, gX2 + 4 * key, gX1 + 4 * key, H[key / NB], verdict);
+    }
+    return;
+  }
+  if (blk >= n_roots + 4) {   // the suspects, one pairing check each
+    ex_singles(L, n_roots + 4, ns, slist, share_root, sig_aff, pk_aff, H, verdict);
+    return;
+  }
+  if (ex_pair(L, n_roots, ns, slist, start, cnt, perm, flags, k64, sig_aff, pk_aff, H, fex, X4, xtk))
+    ex_final(L, n_roots, ftot, fex, xtk, xok);
 }
 
 // Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
 // e(pk_s, H(r)) * e(-g1, sig_s) == 1 -- exactly the reference's verify, no RLC scalar, no per-share
-// products, one pairing check deep instead of k_fb_sparse + the levels below the root.  Blocks
+// products, one pairing check deep instead of the products + the levels below the root.  Blocks
 // stride over the root-sorted order (a failing root's shares are contiguous there: one per block).
 __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ nfail,
                                       const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
@@ -793,11 +785,18 @@ __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__
                                       const uint8_t* __restrict__ gv0, const uint32_t* __restrict__ flags,
                                       const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ H,
                                       const g2_aff* __restrict__ sig_aff, const g1_aff* __restrict__ pk_aff,
-                                      uint8_t* __restrict__ verdict, const uint32_t* __restrict__ xok) {
+                                      uint8_t* __restrict__ verdict, const uint32_t* __restrict__ xok, int n,
+                                      const uint64_t* __restrict__ k64, g2_jac* __restrict__ rsig, g1_jac* __restrict__ rpk) {
   using namespace ssb::lane;
   if (*ok) return;   // uniform
   const uint32_t xv = xok ? *xok : 0u;
-  if (xv == 1u || (xv == 0u && *nfail > FB_SINGLE_MAX)) return;   // (xv == 2: group-test mode's leftovers)
+  if (xv == 1u) return;   // the exclusion check decided the batch
+  if (xv == 0u && *nfail > FB_SINGLE_MAX) {   // the tree's per-share products instead (one launch for both)
+    for (int g = (int)(blockIdx.x * 64 + threadIdx.x); g < 2 * n; g += (int)(gridDim.x * 64))
+      sparse_product(g, n, n_roots, flags, share_root, gst0, gv0, k64, sig_aff, pk_aff, rsig, rpk);
+    return;
+  }
+  // (xv == 2: group-test mode's leftovers)
   __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ uint32_t flg;
   const int lane_ = threadIdx.x;
@@ -951,11 +950,8 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
     hipLaunchKernelGGL(k_fb_excl, dim3((unsigned)n_roots + 4 + EX_SINGLE_BLOCKS), dim3(64), 0, st, n_roots, ok,
                        (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
                        (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
-                       fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart);
-  if (committee)
-    hipLaunchKernelGGL(k_fb_group, dim3(std::min(4 * (unsigned)fb_keys((size_t)n_roots), FB_GRID_MAX)), dim3(64), 0, st, n_roots, ok,
-                       (const uint32_t*)fw.xok, (const uint32_t*)fw.perm, flags, (const uint64_t*)fw.k64, sig, pk, H, verdict,
-                       (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart, fw.cursor, fw.rsig, fw.rpk);
+                       fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart,
+                       fw.cursor, fw.rsig, fw.rpk);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
                      (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                      (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,
@@ -965,11 +961,9 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
     const unsigned grid = std::min((unsigned)n, FB_GRID_MAX);
     hipLaunchKernelGGL(k_fb_single, dim3(grid), dim3(64), 0, st, n_roots, ok, (const uint32_t*)fw.nfail,
                        (const uint32_t*)fw.start, (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst,
-                       (const uint8_t*)fw.gv0, (const uint32_t*)flags, share_root, H, sig, pk, verdict, xok);
+                       (const uint8_t*)fw.gv0, (const uint32_t*)flags, share_root, H, sig, pk, verdict, xok, n,
+                       (const uint64_t*)fw.k64, fw.rsig, fw.rpk);
   }
-  hipLaunchKernelGGL(k_fb_sparse, dim3(nb(2 * (size_t)n, 64)), dim3(64), 0, st, n, n_roots, ok, (const uint32_t*)flags,
-                     share_root, (const uint32_t*)fw.gst, (const uint8_t*)fw.gv0, (const uint64_t*)fw.k64, sig, pk, fw.rsig,
-                     fw.rpk, (const uint32_t*)fw.nfail, xok);
   for (int l = 1; l < L; ++l) {
     const uint64_t gs = 1ull << (lb * (L - 1 - l));
     const uint64_t bound = (uint64_t)n_roots + ((uint64_t)n + gs - 1) / gs;

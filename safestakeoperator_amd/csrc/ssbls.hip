@@ -399,7 +399,7 @@ inline size_t fp12_slots(size_t np) {
 // k_miller_final's, then the fallback's committee stage: nS (suspects listed), xtk[2]
 inline uint32_t ntk_words(size_t np) { return 4 + 1 + (uint32_t)((np + 7) / 8) + 3; }
 
-// the tree's per-share products rsig / rpk; the committee stage's group-test mode (k_fb_group) keeps
+// the tree's per-share products rsig / rpk; the committee stage's group-test mode (k_fb_excl) keeps
 // its four quarter sums per (root, id bucket) key in the same buffers
 inline size_t fb_prod_slots(size_t n, size_t n_roots) { return std::max(n, 4 * launch::fb_keys(n_roots)); }
 size_t verify_ws_bytes(size_t n, size_t n_roots) {

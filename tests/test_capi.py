@@ -108,6 +108,6 @@ def test_batch_kernels_fit_the_queue_primer():
     res = b.check_private_segments(objs)
     limit = b._prime_bytes()
     for k in ("k_decode_count", "k_subgroup_map", "k_msm_bucket2", "k_msm_window2", "k_miller_pairs", "k_miller_final",
-              "k_fp12_prod8", "k_final_lane", "k_fb_rlc", "k_fb_root", "k_fb_single", "k_fb_sparse", "k_fb_level", "k_select_combine", "k_combine_terms_gls",
+              "k_fp12_prod8", "k_final_lane", "k_fb_rlc", "k_fb_excl", "k_fb_root", "k_fb_single", "k_fb_level", "k_select_combine", "k_combine_terms_gls",
               "k_combine_sum", "k_share_map"):
         assert k in res and res[k]["private"] <= limit, (k, res.get(k))
