@@ -312,7 +312,10 @@ def launch_ranks(n, argv):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=48)
+    # (200 steps by default: with 20 batches in flight a short run is dominated by the pipeline's
+    # drain -- the last batch's whole latency inside the timed region; 48 steps measured 12.0-12.8 M
+    # where 200 measured 14.2-14.6 M on the same build, round 4)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
                     help="BASELINE.json workload per GPU (the headline is C2; the others are reported under profiles/); "
@@ -348,7 +351,7 @@ def main():
     ap.add_argument("--ids", default="seq", choices=("seq", "registry"),
                     help="operator ids: 1..n per committee (seq), or distinct pseudo-random registry ids in [1, 2^16) "
                          "per committee (registry, src/node/node.rs:470-474)")
-    ap.add_argument("--sustained-steps", type=int, default=200,
+    ap.add_argument("--sustained-steps", type=int, default=1000,
                     help="length of the sustained-rate run reported as value_sustained (0: skip)")
     ap.add_argument("--collector-windows", type=int, default=200,
                     help="4,096-job windows pushed through the native per-slot collector for value_collector (0: skip)")
