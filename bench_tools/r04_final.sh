@@ -11,6 +11,10 @@ python -c "
 import json; d=json.load(open('$OUT/bench.json'))
 print({k: d.get(k) for k in ('value', 'ms_per_step', 'value_sustained', 'value_collector', 'batch_latency_ms', 'value_host_buffers', 'results_ok')})
 print('roofline', {k: d['roofline'].get(k) for k in ('achieved', 'frac', 'traffic', 'avg_launch_ms')})"
+timeout -k 10 500 python -u bench.py --gpus 2 --dist-backend gloo > $OUT/gloo2.json 2> $OUT/gloo2.err || { echo "gloo2 failed"; tail -20 $OUT/gloo2.err; exit 1; }
+python -c "
+import json; d=json.load(open('$OUT/gloo2.json'))
+print('gloo2', {k: d.get(k) for k in ('n_gpus', 'value', 'ms_per_step', 'value_sustained', 'value_collector', 'results_ok')})"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 -u bench.py > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { echo "prof failed"; tail -5 $OUT/prof_bench.err; exit 1; }
 f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); cp $f $OUT/final_kernel_stats.csv
