@@ -293,7 +293,7 @@ SSB_FN void lagrange_job(int j, const uint32_t* __restrict__ off, const uint32_t
   const uint32_t b = off[j], t = tt[j];
   uint64_t x[SSB_MAX_T];
   for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
-  unit_lagrange(lam + b, x, t);
+  unit_lagrange_fast(lam + b, x, t);
 }
 // Small-integer Lagrange fast path (unit_lagrange_small), for t <= FAST_T (larger thresholds take
 // the 255-bit path; the per-lane arrays stay small -- this kernel's private segment sets the

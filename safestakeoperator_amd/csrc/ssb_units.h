@@ -426,6 +426,33 @@ SSB_INL void gls_digits4(uint64_t* d, const uint64_t* k) {
   for (int q = 0; q < 3; ++q) d[q] = divmod_limbs(w, 4, GLS_U);
   d[3] = w[0];   // (k < r < u^4)
 }
+// lambda_i mod r (canonical, unit_lagrange's output) by the ratio form when the ids allow it
+// (unit_lagrange_ratio: lambda_i = c_i / M, |c_i|, M < 2^62 -- registry ids of committees up to t = 3
+// and most of t = 4): M^-1 mod r by inv_small_mod_r (64-bit extended Euclid) and one Montgomery
+// product per share (c_i R * M^-1 * R^-1 = c_i M^-1), instead of unit_lagrange's Fr exponentiation.
+// Anything else (repeated ids, wider committees, values past 62 bits) takes unit_lagrange.
+SSB_FN void unit_lagrange_fast(fr* lam, const uint64_t* x, uint32_t t) {
+  constexpr uint32_t TMAX = 16;
+  if (t <= TMAX) {
+    int64_t c[TMAX];
+    uint64_t M;
+    if (unit_lagrange_ratio(c, &M, x, t)) {
+      uint64_t y[4];
+      inv_small_mod_r(y, M);
+      fr yc;
+      for (int i = 0; i < 4; ++i) { yc.l[2 * i] = (uint32_t)y[i]; yc.l[2 * i + 1] = (uint32_t)(y[i] >> 32); }
+      for (uint32_t i = 0; i < t; ++i) {
+        fr cm, l;
+        fr_from_u64(cm, (uint64_t)(c[i] < 0 ? -c[i] : c[i]));
+        fr_mul(l, cm, yc);
+        if (c[i] < 0 && !fr_is_zero(l)) fr_sub(l, fr_zero(), l);
+        lam[i] = l;
+      }
+      return;
+    }
+  }
+  unit_lagrange(lam, x, t);
+}
 // the per-job result of the ratio path: T = sum c_i sig_i (affine) and the GLS digits of M^-1 mod r
 struct ratio_job { g2_aff T; uint64_t d[4]; };
 SSB_FN void unit_combine_ratio_at(ratio_job& out, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,

@@ -991,7 +991,10 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
-  ratio_job* rjb = getenv("SSB_NO_RATIO") ? nullptr : c.take<ratio_job>(n_jobs);   // registry ids (unit_lagrange_ratio)
+  // registry ids: by default the general combine with the ratio form's cheap lambda_i
+  // (unit_lagrange_fast) and four GLS lanes per share, which fills the chip; SSB_RATIO=1 takes
+  // [M^-1](sum c_i sig_i) instead (one lane per job for the sum: 3.11 vs 3.32 M partial sigs/s, round 4)
+  ratio_job* rjb = getenv("SSB_RATIO") ? c.take<ratio_job>(n_jobs) : nullptr;
   // share -> (job, root): in the decode launch on the fused path, else a launch of its own
   const bool fmap = fused_sort_path(ctx->cur, n, n_roots, pre);
   const job_map jm{(int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root};

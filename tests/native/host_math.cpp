@@ -373,6 +373,17 @@ int main() {
         same = memcmp(a, b, 96) == 0;
       }
       printf("%d %d %llu\n", elig ? 1 : 0, same, (unsigned long long)M);
+    } else if (cmd == "lagfast") {  // lagfast t id1 .. idt : unit_lagrange_fast's lambda_i (canonical hex, one per share)
+      int t; is >> t; std::vector<uint64_t> ids(t); for (int i = 0; i < t; ++i) is >> ids[i];
+      std::vector<fr> lam(t);
+      unit_lagrange_fast(lam.data(), ids.data(), (uint32_t)t);
+      std::string o;
+      for (int i = 0; i < t; ++i) {
+        char buf[72];
+        for (int k = 7; k >= 0; --k) snprintf(buf + 8 * (7 - k), 9, "%08x", lam[i].l[k]);
+        o += (i ? " " : ""); o += buf;
+      }
+      printf("%s\n", o.c_str());
     } else if (cmd == "invsmall") {  // invsmall M: M^-1 mod r (4 limbs hex, most significant first) and its GLS digits
       std::string a; is >> a;
       const uint64_t M = std::stoull(a, nullptr, 0);

@@ -168,6 +168,27 @@ def test_small_inverse_and_gls_digits(host_exe):
         assert all(0 <= x < u for x in d[:3]) and sum(x * u ** q for q, x in enumerate(d)) == y, M
 
 
+def test_lagrange_fast_matches_definition(host_exe):
+    """unit_lagrange_fast (ratio form: 64-bit Euclid inverse of M + one Montgomery product per share;
+    otherwise unit_lagrange) == prod_{j!=i} x_j / (x_j - x_i) mod r, blst's inverse(0) = 0 for repeated
+    ids, for sequential, registry-like and wide id sets."""
+    import random
+    r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    rnd = random.Random(11)
+    cases = [(1, 2, 3), (1, 2, 4), (2, 3, 4), (5, 9, 100), (65535, 1, 40000), (1, 1, 2), (7,), (2**40, 3, 5)]
+    cases += [tuple(rnd.sample(range(1, 1 << 16), t)) for t in (3, 3, 4, 4, 5, 7, 10)]
+    out = _run(host_exe, ["lagfast %d %s" % (len(k), " ".join(map(str, k))) for k in cases])
+    for ids, line in zip(cases, out):
+        want = []
+        for i, xi in enumerate(ids):
+            num, den = 1, 1
+            for j, xj in enumerate(ids):
+                if j != i:
+                    num, den = num * xj % r, den * (xj - xi) % r
+            want.append(num * (pow(den, -1, r) if den else 0) % r)
+        assert [int(h, 16) for h in line.split()] == want, ids
+
+
 def test_bucket_madd_matches_generic(host_exe):
     """jac_madd_at (the MSM bucket loops' in-place mixed addition) == jac_add_aff_inl coordinate for
     coordinate, on G2 and G1, including infinity on either side, doubling and opposite points."""
