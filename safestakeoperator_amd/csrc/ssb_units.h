@@ -171,38 +171,14 @@ SSB_INL void naf_masks(uint64_t m, uint64_t& pos, uint64_t& neg) {
   pos = (h & ~m) >> 1;
   neg = (m & ~h) >> 1;
 }
-// [d] p for a 64-bit d by NAF digits (65 positions: h = 3d has 66 bits, kept as h_hi:h_lo): a third
-// of the positions nonzero against half for binary digits; the same out-of-line mixed addition as
-// jac_mul_aff, the point or its negation passed by value
-template <class F> SSB_FN void jac_mul_naf_aff(jac<F>& r, const aff<F>& p, uint64_t d) {
-  const uint64_t t2 = d << 1, h_lo = t2 + d;
-  const uint64_t h_hi = (d >> 63) + (h_lo < t2 ? 1ull : 0ull);
-  const uint64_t pos = ((h_lo & ~d) >> 1) | (h_hi << 63), pos64 = h_hi >> 1;   // digit 64: pos64 & 1
-  const uint64_t neg = (d & ~h_lo) >> 1;
-  aff<F> np = p;
-  f_neg(np.y, np.y);
-  jac<F> acc;
-  jac_set_inf(acc);
-  if (pos64 & 1ull) jac_add_aff(acc, acc, p);
-  for (int i = 63; i >= 0; --i) {
-    jac_dbl_inl(acc, acc);
-    if ((pos >> i) & 1ull) jac_add_aff(acc, acc, p);
-    else if ((neg >> i) & 1ull) jac_add_aff(acc, acc, np);
-  }
-  r = acc;
-}
 // [d] (+-psi^q(p)) -- digit q of a GLS split (sign as above); p in G2
 SSB_FN void unit_gls_term(g2_jac& r, const g2_aff& sig, uint64_t d, int q) {
   if (sig.inf) { jac_set_inf(r); return; }
   g2_aff p = sig;
   for (int i = 0; i < q; ++i) g2_psi_aff(p, p);
   if (q & 1) fp2_neg(p.y, p.y);
-#ifdef SSB_GLS_NAF   // experiment build: NAF digit chains (jac_mul_naf_aff)
-  jac_mul_naf_aff(r, p, d);
-#else
   const uint32_t dw[2] = {(uint32_t)d, (uint32_t)(d >> 32)};
   jac_mul_aff(r, p, dw, 2);
-#endif
 }
 SSB_FN void unit_combine_term_gls(g2_jac& r, const g2_aff& sig, const uint32_t* lam8, int q) {
   unit_gls_term(r, sig, gls_digit(lam8, q), q);

@@ -384,27 +384,6 @@ int main() {
         o += (i ? " " : ""); o += buf;
       }
       printf("%s\n", o.c_str());
-    } else if (cmd == "nafmul") {  // nafmul <trials>: jac_mul_naf_aff vs jac_mul_aff on G2, edge and pseudo-random d
-      int trials; is >> trials;
-      uint64_t st = 0x243F6A8885A308D3ull;
-      auto rnd = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
-      const uint64_t edge[] = {0ull, 1ull, 2ull, 3ull, ~0ull, 0xAAAAAAAAAAAAAAAAull, 0x5555555555555555ull, 1ull << 63,
-                               (1ull << 63) + 1, 0xd201000000010000ull, 0xFFFFFFFF00000000ull};
-      int ok = 0, n = 0;
-      uint8_t m[32] = {0}; m[0] = 0x42;
-      g2_aff P; hash_to_g2(P, m, (const uint8_t*)DST, (int)strlen(DST));
-      const int ne = (int)(sizeof(edge) / sizeof(edge[0]));
-      for (int k = 0; k < ne + trials; ++k) {
-        const uint64_t d = k < ne ? edge[k] : rnd();
-        g2_jac a, b;
-        jac_mul_naf_aff(a, P, d);
-        const uint32_t dw[2] = {(uint32_t)d, (uint32_t)(d >> 32)};
-        jac_mul_aff(b, P, dw, 2);
-        g2_aff x, y; jac_to_aff(x, a); jac_to_aff(y, b);
-        uint8_t cx[96], cy[96]; g2_compress(cx, x); g2_compress(cy, y);
-        ok += memcmp(cx, cy, 96) == 0; ++n;
-      }
-      printf("%d %d\n", ok, n);
     } else if (cmd == "invsmall") {  // invsmall M: M^-1 mod r (4 limbs hex, most significant first) and its GLS digits
       std::string a; is >> a;
       const uint64_t M = std::stoull(a, nullptr, 0);

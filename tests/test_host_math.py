@@ -189,13 +189,6 @@ def test_lagrange_fast_matches_definition(host_exe):
         assert [int(h, 16) for h in line.split()] == want, ids
 
 
-def test_naf_chain_matches_binary(host_exe):
-    """jac_mul_naf_aff (NAF digits, the experiment build's GLS digit chains) == the binary chain,
-    as group elements, for edge digits (0, 1, all ones, alternating bits, 2^63, |x|) and random ones."""
-    ok, n = _run(host_exe, ["nafmul 40"])[0].split()
-    assert ok == n and int(n) == 51
-
-
 def test_bucket_madd_matches_generic(host_exe):
     """jac_madd_at (the MSM bucket loops' in-place mixed addition) == jac_add_aff_inl coordinate for
     coordinate, on G2 and G1, including infinity on either side, doubling and opposite points."""
