@@ -351,6 +351,9 @@ def main():
     ap.add_argument("--ids", default="seq", choices=("seq", "registry"),
                     help="operator ids: 1..n per committee (seq), or distinct pseudo-random registry ids in [1, 2^16) "
                          "per committee (registry, src/node/node.rs:470-474)")
+    ap.add_argument("--no-registry", dest="registry_leg", action="store_false",
+                    help="skip the registry-operator-id leg (value_registry: the same path and --steps, ids from "
+                         "the registry contract instead of 1..n)")
     ap.add_argument("--sustained-steps", type=int, default=1000,
                     help="length of the sustained-rate run reported as value_sustained (0: skip)")
     ap.add_argument("--collector-windows", type=int, default=200,
@@ -498,7 +501,7 @@ def main():
         s = streams[k]
         fn = lib.ssb_threshold_aggregate_batch_cached_dev if use_cache[0] else lib.ssb_threshold_aggregate_batch_dev
         pk_arg = d_pkidx if use_cache[0] else d_pk
-        src = dict(d_sig=d_sig, d_ids=d_ids, d_jr=d_jr, d_roots=d_roots)
+        src = inputs
         if use_host[0]:   # (world == 1 only; the library picks slot k round robin like the _dev calls)
             host_io[k] = eng.submit_batch_raw(h_in["t"], h_in["off"], h_in["sig"], h_in["pk"], h_in["ids"], h_in["jr"],
                                               h_in["roots"], seed=(seed_base + i) & (2 ** 64 - 1),
@@ -513,7 +516,7 @@ def main():
                     w.wait()
         # (the argument tuple of slot k is built once: the timed loop's host time per submit is the
         # library's, not Python's -- the last batch of a round starts that much later)
-        key = (k, use_cache[0], s.cuda_stream)
+        key = (k, use_cache[0], s.cuda_stream, inputs["gen"])
         a = call_args.get(key)
         if a is None:
             a = call_args[key] = (
@@ -539,7 +542,8 @@ def main():
         if len(group) >= S:
             exchange_group()
 
-    call_args = {}  # per (slot, key variant): the submit call's fixed arguments
+    call_args = {}  # per (slot, key variant, input generation): the submit call's fixed arguments
+    inputs = dict(d_sig=d_sig, d_ids=d_ids, d_jr=d_jr, d_roots=d_roots, gen=0)   # the batch step() submits
     group = []      # slots whose results are not exchanged yet
     xchg = BatchExchange(strong, sizes=sizes, device=cdev) if dist is not None else None
 
@@ -650,6 +654,7 @@ def main():
     # (tests/test_generic_threshold.rs:35), checked for every slot's batch, untimed
     msig = eng.sign_batch(wl["master"], wl["job_root"], wl["roots"])
     msig_arr = np.frombuffer(b"".join(msig), dtype=np.uint8).reshape(V, 96)
+    truth = dict(job_ok=job_ok, valid=valid, msig=msig_arr)
     primed = []
 
     def check_slots(host=False):
@@ -661,11 +666,12 @@ def main():
                 out_host, st_host, _, ver_host = host_io[k].wait()
             else:
                 st_host, ver_host, out_host = o["st"].cpu().numpy(), o["ver"].cpu().numpy(), o["out"].cpu().numpy()
-            ok = ok and bool(((st_host == 0) == job_ok).all()) and bool((ver_host == valid).all())
-            ok = ok and bool((out_host[job_ok] == msig_arr[job_ok]).all())
+            jo = truth["job_ok"]
+            ok = ok and bool(((st_host == 0) == jo).all()) and bool((ver_host == truth["valid"]).all())
+            ok = ok and bool((out_host[jo] == truth["msig"][jo]).all())
             if args.final_verify and not host:
                 fv = o["fv"].cpu().numpy()
-                ok = ok and bool(((fv == 1) == job_ok).all())
+                ok = ok and bool(((fv == 1) == jo).all())
         return ok
 
     def warm_and_check():
@@ -760,30 +766,65 @@ def main():
     # decoded-key table (ssb_pk_cache_add), timed from the first submit to the last result
     coll = None
     if args.collector_windows > 0 and not strong:
-        from safestakeoperator_amd.collector import NativeCollector, collbench_run
+        from safestakeoperator_amd.collector import NativeCollector, collbench_run, wire_records
+
+        def collector_leg(wire):
+            """(seconds, results, windows, profile) of n_jobs jobs through a collector; wire: the jobs'
+            shares as the records operators send (bincode(bls::Signature), encoded before the run),
+            through ssb_collector_submit_wire and the device's record decode"""
+            torch.cuda.synchronize(dev)
+            streams.clear()
+            col = NativeCollector(eng, max_jobs=V, max_shares=V * n, window_s=0.005, in_flight=S, wire=wire)
+            rec = wire_records(wl["sigs"]) if wire else None
+            try:
+                rows = col.rows(wl["share_pks"])
+                collbench_run(col, wl, V, n, t, rows, S * V, threads=args.collector_threads, wire=rec)  # warm-up
+                n_jobs = args.collector_windows * V
+                if dist is not None:
+                    dist.barrier()
+                c_sec, c_res = collbench_run(col, wl, V, n, t, rows, n_jobs, threads=args.collector_threads, wire=rec)
+                return c_sec, c_res, n_jobs, col.stats(), col.profile()
+            finally:
+                col.close()
+
+        def collector_ok(c_res, n_jobs):
+            vv = np.arange(n_jobs) % V
+            vbits = (valid.reshape(V, n).astype(np.uint64) << np.arange(n, dtype=np.uint64)).sum(axis=1)
+            return (bool((c_res["done"] == 1).all()) and bool((c_res["rc"] == 0).all())
+                    and bool(((c_res["status"] == 0) == job_ok[vv]).all()) and bool((c_res["verdicts"] == vbits[vv]).all())
+                    and bool((c_res["absent"] == 0).all())
+                    and bool((c_res["sig96"][job_ok[vv]] == msig_arr[vv[job_ok[vv]]]).all()))
+
+        c_sec, c_res, n_jobs, cw, cprof = collector_leg(False)
+        coll = dict(seconds=c_sec, jobs=n_jobs, windows=cw[0], ok=collector_ok(c_res, n_jobs), profile=cprof)
+        w_sec, w_res, _, ww, _ = collector_leg(True)
+        coll.update(wire_seconds=w_sec, wire_windows=ww[0], wire_ok=collector_ok(w_res, n_jobs))
+    # the same path and the same --steps on committees with REGISTRY operator ids (distinct pseudo-random
+    # ids in [1, 2^16) per committee, src/node/node.rs:470-474): the Lagrange coefficients are ratios of
+    # small integers, so the combine is [M^-1](sum c_i sig_i) per job (k_combine_ratio) where ids 1..n
+    # combine with small integers.  New keys, so the key table is replaced (after every other leg).
+    reg = None
+    if args.registry_leg and args.ids == "seq" and not strong and not args.final_verify and not wl["n_bad"]:
         torch.cuda.synchronize(dev)
+        wl_r = make_workload(eng, V, t, n, n_roots, rank, ids="registry")
+        if lib.ssb_pk_cache_set(eng.handle, N, np.frombuffer(wl_r["pks"], dtype=np.uint8).ctypes.data_as(_lib._u8p)) != 0:
+            raise RuntimeError("ssb_pk_cache_set: %s" % lib.ssb_last_error(eng.handle))
+        inputs.update(d_sig=dt8(wl_r["sigs"]), d_ids=torch.tensor(wl_r["ids"], dtype=torch.int64, device=dev), gen=1)
+        msig_r = eng.sign_batch(wl_r["master"], wl_r["job_root"], wl_r["roots"])
+        truth.update(msig=np.frombuffer(b"".join(msig_r), dtype=np.uint8).reshape(V, 96),
+                     job_ok=np.ones(V, dtype=bool), valid=np.ones(N, dtype=np.uint8))
+        use_cache[0] = True
         streams.clear()
-        col = NativeCollector(eng, max_jobs=V, max_shares=V * n, window_s=0.005, in_flight=S)
-        try:
-            rows = col.rows(wl["share_pks"])
-            collbench_run(col, wl, V, n, t, rows, S * V, threads=args.collector_threads)          # warm-up
-            n_jobs = args.collector_windows * V
-            if dist is not None:
-                dist.barrier()
-            c_sec, c_res = collbench_run(col, wl, V, n, t, rows, n_jobs, threads=args.collector_threads)
-            cw = col.stats()
-            cprof = col.profile()
-        finally:
-            col.close()
-        vv = np.arange(n_jobs) % V
-        vbits = (valid.reshape(V, n).astype(np.uint64) << np.arange(n, dtype=np.uint64)).sum(axis=1)
-        c_ok = (bool((c_res["done"] == 1).all()) and bool((c_res["rc"] == 0).all())
-                and bool(((c_res["status"] == 0) == job_ok[vv]).all()) and bool((c_res["verdicts"] == vbits[vv]).all())
-                and bool((c_res["sig96"][job_ok[vv]] == msig_arr[vv[job_ok[vv]]]).all()))
-        coll = dict(seconds=c_sec, jobs=n_jobs, windows=cw[0], ok=c_ok, profile=cprof)
-    ok_st = ok_comb = ok_head and ok_other and ok_timed and ok_x and ok_host and ok_sus and (coll is None or coll["ok"])
+        ok_r = warm_and_check()
+        elapsed_reg = timed_run()
+        ok_r = ok_r and check_slots()
+        reg = dict(seconds=elapsed_reg, ok=ok_r)
+    ok_st = ok_comb = ok_head and ok_other and ok_timed and ok_x and ok_host and ok_sus and (
+        coll is None or (coll["ok"] and coll["wire_ok"]))
+    ok_st = ok_st and (reg is None or reg["ok"])
     if dist is not None:
-        tt = torch.tensor([elapsed, elapsed_other, elapsed_sus or 0.0, coll["seconds"] if coll else 0.0],
+        tt = torch.tensor([elapsed, elapsed_other, elapsed_sus or 0.0, coll["seconds"] if coll else 0.0,
+                           reg["seconds"] if reg else 0.0, coll["wire_seconds"] if coll else 0.0],
                           dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, elapsed_other = float(tt[0].item()), float(tt[1].item())
@@ -791,6 +832,10 @@ def main():
             elapsed_sus = float(tt[2].item())
         if coll:
             coll["seconds"] = float(tt[3].item())
+        if reg:
+            reg["seconds"] = float(tt[4].item())
+        if coll:
+            coll["wire_seconds"] = float(tt[5].item())
         okt = torch.tensor([1 if (ok_st and ok_comb) else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_all = bool(okt.item())
@@ -884,6 +929,7 @@ def main():
             "sustained": ("the headline path for %d batches (%d in flight), results of every slot's last batch checked"
                           % (args.sustained_steps, S)) if elapsed_sus else None,
             "value_collector": (round(coll["jobs"] * n * world / coll["seconds"], 1) if coll else None),
+            "value_collector_wire": (round(coll["jobs"] * n * world / coll["wire_seconds"], 1) if coll else None),
             "collector": (dict(jobs_per_gpu=coll["jobs"], windows=coll["windows"], window_jobs=V, in_flight=S,
                                submitter_threads=args.collector_threads, seconds=round(coll["seconds"], 4),
                                combined_sigs_per_s=round(coll["jobs"] * world / coll["seconds"], 1),
@@ -892,10 +938,25 @@ def main():
                                                         (V_glob * n * args.sustained_steps / elapsed_sus), 3)
                                                   if elapsed_sus else None),
                                worker_profile_incl_warmup=coll["profile"],
+                               wire=dict(seconds=round(coll["wire_seconds"], 4), windows=coll["wire_windows"],
+                                         frac_of_value=round(coll["jobs"] * n * world / coll["wire_seconds"] / value, 3),
+                                         path="the same jobs with every share as the record an operator sends "
+                                              "(bincode(bls::Signature), 202 B) through ssb_collector_submit_wire: "
+                                              "a SSB_COLLECTOR_WIRE collector, records decoded and decompressed on "
+                                              "the device (ssb_threshold_aggregate_batch_wire_cached_dev) -- the "
+                                              "receive path of RemoteOperator::sign without the CPU deserialize"),
                                path="ssb_collector_submit per job from native threads (bench_tools/collbench.cpp) -> "
                                     "4,096-job windows -> ssb_threshold_aggregate_batch_cached_dev on %d one-stream "
                                     "slots; timed first submit -> last result; every job's status, verdicts and "
                                     "combined signature checked" % S) if coll else None),
+            "value_registry": (round(V_glob * n * args.steps / reg["seconds"], 1) if reg else None),
+            "registry": (dict(ms_per_step=round(reg["seconds"] / args.steps * 1e3, 3), steps=args.steps,
+                              combined_sigs_per_s=round(V_glob * args.steps / reg["seconds"], 1),
+                              frac_of_value=round(elapsed / reg["seconds"], 3), results_ok=reg["ok"],
+                              path="the headline path (same slots, steps, key cache) on committees with registry "
+                                   "operator ids: distinct pseudo-random ids in [1, 2^16) per committee "
+                                   "(src/node/node.rs:470-474); lambda_i = c_i / M, combined as [M^-1](sum c_i sig_i), "
+                                   "one lane per job (k_combine_ratio)") if reg else None),
             "host_buffers": "every batch's inputs start in, and its results end in, ordinary host memory: "
                             "ssb_threshold_aggregate_batch%s_submit copies them into the slot's pinned device-mapped "
                             "staging buffer, the kernels read / write it in place over PCIe, ssb_batch_wait delivers "

@@ -52,8 +52,12 @@
  *     over PCIe -- and a hipStream_t (as void*), enqueue everything on that stream and return
  *     without synchronising.
  *   - Return value of every function: SSB_OK or a negative SSB_E* code (ssb_last_error() has
- *     the message).  No C++ exception crosses this ABI.  A context must not be used by two
- *     threads at once (one context per thread, or an external mutex).
+ *     the message).  No C++ exception crosses this ABI.  A context is thread-safe: every entry
+ *     point holds the context's lock for its whole call, so the threads of a process can share ONE
+ *     context (the collector's worker, direct callers, key registration); their calls are
+ *     serialised.  ssb_last_error is the message of the context's last failed call (read it on the
+ *     thread that got the error before another call on the context fails).  ssb_destroy must not
+ *     race with other calls on the context.
  */
 #ifndef SSBLS_H
 #define SSBLS_H
@@ -107,7 +111,16 @@ const char* ssb_last_error(const ssb_ctx* ctx);
  * SSB_EINVAL otherwise.  No GPU needed; ssb_set_pipeline_depth / ssb_set_slot_streams refuse what
  * this refuses. */
 int ssb_check_pipeline_config(int depth, int streams);
-/* Number of pipeline slots (1..20, default 1).  Each slot owns its streams and workspace; calls of
+/* Hardware queues the HIP runtime gives this process: GPU_MAX_HW_QUEUES from the environment (HIP
+ * reads it when it initialises, so the process must set it BEFORE its first HIP call; at most 32),
+ * else HIP's default, 4.  Every stream of a pipeline slot needs a queue of its own, or independent
+ * batches serialise on shared queues: ssb_set_pipeline_depth / ssb_set_slot_streams refuse a
+ * configuration of more than (budget - 1) slot streams (SSB_EINVAL, the reason in ssb_last_error),
+ * and ssb_collector_create lowers its in_flight to fit (with a warning on stderr).  Read at
+ * ssb_create. */
+int ssb_hw_queue_budget(void);
+/* Number of pipeline slots (1..20, default 1; depth x streams per slot at most ssb_hw_queue_budget() - 1).
+ * Each slot owns its streams and workspace; calls of
  * ssb_threshold_aggregate_batch_dev go to the slots round robin, so up to `depth` independent
  * batches are in flight and overlap on the device (e.g. the duties of consecutive slots).  Each
  * call's outputs are ready when the caller's `stream` reaches them. */
@@ -255,8 +268,10 @@ int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket);
  * launches it on the next of `in_flight` one-stream pipeline slots with the public keys from the key
  * table (ssb_pk_cache_add).  Up to `in_flight` windows run on the device while the next one fills;
  * every job's result is exactly threshold_aggregate's for that job alone (generic_threshold.rs:132-175).
- * The collector takes the context over (one-stream slots, pipeline depth in_flight): while it
- * exists, use the context only through ssb_collector_* calls. */
+ * The collector sets the context to one-stream slots at pipeline depth in_flight (and leaves it so
+ * after ssb_collector_destroy).  The context stays usable by other threads while the collector
+ * exists -- every entry point takes the context's lock -- so ONE context per process serves the
+ * collector, direct calls (unsafe_aggregate, signing, key validation) and key registration. */
 typedef struct ssb_collector ssb_collector;
 typedef struct ssb_job_result {
   uint8_t sig96[96];     /* the combined signature (status SSB_DVF_OK) */
@@ -266,6 +281,8 @@ typedef struct ssb_job_result {
   int32_t rc;            /* SSB_OK, or the negative SSB_E* code of the job's batch */
   uint32_t n_shares;
   uint32_t done;         /* 0 while pending; 1 (written last, release) when the fields are final */
+  uint64_t absent;       /* wire collectors: bit i set when share i's record did not deserialize -- the
+                            share was dropped from the job as the reference drops it (verdict 0) */
 } ssb_job_result;
 /* Called on the collector's worker thread when a job's result is final (after `done` is set); must
  * not block or call ssb_collector_* functions (e.g. complete a future / send on a channel and
@@ -278,6 +295,17 @@ typedef void (*ssb_job_done_fn)(void* user, const ssb_job_result* result);
  * window waits for company. */
 int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, uint32_t window_us, int in_flight,
                          ssb_collector** out);
+/* Flags of ssb_collector_create2.  SSB_COLLECTOR_WIRE: the windows hold every share as a wire record
+ * (bincode(bls::Signature), 202 bytes), and ssb_collector_submit_wire takes the bytes a remote
+ * operator sent -- no CPU deserialization on the receive path (src/validation/operator.rs:108); the
+ * window runs as one ssb_threshold_aggregate_batch_wire_cached_dev batch, so a record that does not
+ * deserialize makes its share absent (ssb_job_result.absent), exactly the reference's drop.  A
+ * compressed share submitted with ssb_collector_submit is stored as its record (bincode::serialize).
+ * max_jobs <= 2^20, max_shares <= 2^26.  in_flight above ssb_hw_queue_budget() - 1 is lowered to it
+ * (with a warning on stderr). */
+#define SSB_COLLECTOR_WIRE 1u
+int ssb_collector_create2(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, uint32_t window_us, int in_flight,
+                          uint32_t flags, ssb_collector** out);
 /* Drains: every submitted job is delivered before it returns.  The context stays usable. */
 void ssb_collector_destroy(ssb_collector* col);
 /* ssb_pk_cache_add through the collector (serialised with its launches). */
@@ -290,6 +318,12 @@ int ssb_collector_register_keys(ssb_collector* col, size_t n, const uint8_t* pk4
 int ssb_collector_submit(ssb_collector* col, uint32_t t, uint32_t n, const uint8_t* sig96, const uint32_t* pk_index,
                          const uint64_t* ids, const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb,
                          void* user);
+/* A job whose shares are the wire records as received (a SSB_COLLECTOR_WIRE collector): share i is
+ * wire[i] (wire_len[i] bytes; a record of another length than 202, or a NULL one, never deserializes:
+ * the share is absent).  Otherwise as ssb_collector_submit; the bytes are copied before it returns. */
+int ssb_collector_submit_wire(ssb_collector* col, uint32_t t, uint32_t n, const uint8_t* const* wire,
+                              const size_t* wire_len, const uint32_t* pk_index, const uint64_t* ids,
+                              const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb, void* user);
 /* Block until result->done (the job must have been submitted to this collector). */
 int ssb_collector_wait(ssb_collector* col, const ssb_job_result* result);
 /* Close the open window now and wait until every job submitted before the call is delivered. */
@@ -335,6 +369,23 @@ int ssb_threshold_aggregate_batch_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t
                                              const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
                                              uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
                                              uint64_t* out_err, uint8_t* share_verdicts, void* stream);
+
+/* The same with the partial signatures as WIRE RECORDS, the bytes a remote operator sends: record i at
+ * wire + i * stride (stride >= 202) is bincode(bls::Signature) (ssb_decode_wire_sigs), decoded and
+ * decompressed on the device -- the CPU never deserializes the share (RemoteOperator::sign,
+ * src/validation/operator.rs:108).  A record that does not deserialize (share_wire_status[i]: 1 length,
+ * 2 prefix, 3 hex digit, 4 not a curve point; 0 ok) makes its share ABSENT, as the reference drops it
+ * before threshold_aggregate (operator.rs:108-131, the `.flatten()` of hotstuff.rs:150-155): it does not
+ * count towards the job's share count -- InsufficientSignatures{got: present shares, expected: t} --
+ * and the scan never meets it (verdict 0).  share_wire_status: n_shares int32, device. */
+int ssb_threshold_aggregate_batch_wire_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares,
+                                                  const uint32_t* share_off, const uint32_t* t,
+                                                  const uint8_t* wire, size_t stride, const uint32_t* pk_index,
+                                                  const uint64_t* ids, const uint32_t* job_root, size_t n_roots,
+                                                  const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                                  uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
+                                                  uint64_t* out_err, uint8_t* share_verdicts,
+                                                  int32_t* share_wire_status, void* stream);
 
 /* Batched unsafe_aggregate: job j combines ALL its shares [share_off[j], share_off[j+1]) with
  * Lagrange coefficients of its ids (t = share count), starting from infinity. */

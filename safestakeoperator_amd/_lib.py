@@ -22,6 +22,7 @@ SIGNATURES = {
     "ssb_destroy": (None, [_ctx]),
     "ssb_last_error": (ctypes.c_char_p, [_ctx]),
     "ssb_check_pipeline_config": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "ssb_hw_queue_budget": (ctypes.c_int, []),
     "ssb_set_pipeline_depth": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_set_slot_streams": (ctypes.c_int, [_ctx, ctypes.c_int]),
     "ssb_slot_stream": (ctypes.c_void_p, [_ctx, ctypes.c_int]),
@@ -51,7 +52,12 @@ SIGNATURES = {
     "ssb_pk_cache_add": (ctypes.c_int, [_ctx, _sz, _u8p, _u32p]),
     "ssb_collector_create": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "ssb_collector_create2": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                             ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     "ssb_collector_destroy": (None, [ctypes.c_void_p]),
+    "ssb_collector_submit_wire": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "ssb_collector_register_keys": (ctypes.c_int, [ctypes.c_void_p, _sz, _u8p, _u32p]),
     "ssb_collector_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -72,6 +78,12 @@ SIGNATURES = {
                                                                 ctypes.c_void_p, _sz, ctypes.c_void_p, _u8p, _sz,
                                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_threshold_aggregate_batch_wire_cached_dev": (ctypes.c_int, [_ctx, _sz, _sz, ctypes.c_void_p, ctypes.c_void_p,
+                                                                     ctypes.c_void_p, _sz, ctypes.c_void_p,
+                                                                     ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p,
+                                                                     _u8p, _sz, ctypes.c_uint64, ctypes.c_void_p,
+                                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                                     ctypes.c_void_p, ctypes.c_void_p]),
     "ssb_unsafe_aggregate_batch": (ctypes.c_int, [_ctx, _sz, _u32p, _u8p, _u64p, _u8p, _i32p]),
     "ssb_sign_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u32p, _sz, _u8p, _u8p, _sz, _u8p]),
     "ssb_sk_to_pk_batch": (ctypes.c_int, [_ctx, _sz, _u8p, _u8p]),
@@ -89,7 +101,7 @@ class JobResult(ctypes.Structure):
     """ssb_job_result (include/ssbls.h): one collector job's outcome."""
     _fields_ = [("sig96", ctypes.c_uint8 * 96), ("err", ctypes.c_uint64 * 2), ("verdicts", ctypes.c_uint64),
                 ("status", ctypes.c_int32), ("rc", ctypes.c_int32), ("n_shares", ctypes.c_uint32),
-                ("done", ctypes.c_uint32)]
+                ("done", ctypes.c_uint32), ("absent", ctypes.c_uint64)]
 
 
 # ssb_job_done_fn: void (*)(void* user, const ssb_job_result* result)

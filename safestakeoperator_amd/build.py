@@ -119,6 +119,48 @@ def check_private_segments(objs, out_json=None):
     return res
 
 
+def _code_object(obj, td):
+    """The gfx950 code object embedded in a compiled object (None for a host-only TU)."""
+    fb, co = os.path.join(td, "fatbin"), os.path.join(td, "co")
+    if subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", ".hip_fatbin=" + fb, obj],
+                      capture_output=True).returncode != 0:
+        return None
+    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--" + ARCH, "--input=" + fb, "--output=" + co], check=True)
+    return co
+
+
+def long_branch_clobbers(objs):
+    """{function: count} of callable (non-kernel) device functions whose long branches go through
+    s[30:31], the return address.  The compiler relaxes a branch past +-128 KB into
+    s_getpc / s_add / s_setpc on a scratch SGPR pair; when the pre-RA size estimate said no long
+    branch was coming (amdgpu-long-branch-factor) no pair is reserved and relaxation takes
+    s[30:31] without saving it -- the function then "returns" to its own branch target and spins
+    forever (the round-4 and round-5 stalls: out-of-line ex_groups, the NAF chains, rc_k_chain).
+    FLAGS reserve the pair in every function; this guard fails the build if one slips through."""
+    import re
+    import tempfile
+    bad = {}
+    with tempfile.TemporaryDirectory() as td:
+        for obj in objs:
+            co = _code_object(obj, td)
+            if co is None:
+                continue
+            notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True,
+                                   capture_output=True, text=True).stdout
+            kernels = set(re.findall(r"\.name:\s+(\S+)", notes))
+            p = subprocess.Popen([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co],
+                                 stdout=subprocess.PIPE, text=True)
+            cur = None
+            for line in p.stdout:
+                if line.endswith(">:\n"):
+                    cur = line[line.index("<") + 1:-3]
+                elif "s_getpc_b64 s[30:31]" in line and cur not in kernels:
+                    bad[cur] = bad.get(cur, 0) + 1
+            p.wait()
+    return bad
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     want = _source_hash()
     if not force and os.path.exists(LIB) and os.path.exists(STAMP) and open(STAMP).read().strip() == want:
@@ -152,6 +194,11 @@ def build(force: bool = False, verbose: bool = True) -> str:
             if not VARIANT:
                 raise
             print("[ssbls] variant %s: %s" % (VARIANT, e), flush=True)   # experiment builds: reported only
+        clob = long_branch_clobbers(objs)
+        if clob:
+            raise RuntimeError("callable device functions whose long branches overwrite the return address "
+                               "s[30:31] (they would never return; split them into smaller out-of-line steps): %s"
+                               % clob)
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
     if verbose:
         print("[ssbls] linking:", " ".join(cmd), flush=True)

@@ -38,18 +38,27 @@ from .threshold import (MAX_T, DifferentLength, DvfError, Engine, ThresholdJob, 
 MAX_JOB_SHARES = 64   # ssb_collector_submit: shares per job
 
 
+SSB_COLLECTOR_WIRE = 1   # ssb_collector_create2 flag (include/ssbls.h)
+WIRE_RECORD = 202        # bincode(bls::Signature)
+
+
 class NativeCollector:
     """ssb_collector (include/ssbls.h): lock-free submission into pinned windows, one worker thread in
-    the library, `in_flight` windows on the device.  Takes the engine's context over while it lives."""
+    the library, `in_flight` windows on the device.  It sets the engine's context to one-stream slots
+    at depth `in_flight`; the context stays usable by other threads (every library call takes the
+    context's lock), so one engine serves the collector and direct calls.  wire=True: the windows
+    hold wire records (submit_wire takes the bytes an operator sent; a record that does not
+    deserialize makes its share absent, as the reference drops it)."""
 
     def __init__(self, engine: Engine, max_jobs: int = 4096, max_shares: Optional[int] = None, window_s: float = 0.005,
-                 in_flight: int = 20):
+                 in_flight: int = 20, wire: bool = False):
         self.engine = engine
         self._lib = engine._lib
+        self.wire = bool(wire)
         h = ctypes.c_void_p()
         ms = int(max_shares) if max_shares is not None else max(64, 16 * int(max_jobs))
-        rc = self._lib.ssb_collector_create(engine.handle, int(max_jobs), ms, int(round(window_s * 1e6)),
-                                            int(in_flight), ctypes.byref(h))
+        rc = self._lib.ssb_collector_create2(engine.handle, int(max_jobs), ms, int(round(window_s * 1e6)),
+                                             int(in_flight), SSB_COLLECTOR_WIRE if wire else 0, ctypes.byref(h))
         if rc != 0:
             raise RuntimeError("ssb_collector_create failed (%d): %s" % (rc, self._lib.ssb_last_error(engine.handle)))
         self._h = h
@@ -84,6 +93,21 @@ class NativeCollector:
                                             root, ctypes.addressof(result), cb, ctypes.c_void_p(user))
         if rc != 0:
             raise RuntimeError("ssb_collector_submit failed (%d)" % rc)
+
+    def submit_wire(self, t: int, records: Sequence[bytes], rows: np.ndarray, ids: np.ndarray, root: bytes,
+                    result: "_lib.JobResult", cb=None, user: int = 0) -> None:
+        """One job whose shares are wire records as received (a wire collector); the records are copied
+        before this returns."""
+        n = len(ids)
+        bufs = [bytes(r) for r in records]
+        ptrs = (ctypes.c_char_p * max(1, n))(*bufs) if n else (ctypes.c_char_p * 1)()
+        lens = (ctypes.c_size_t * max(1, n))(*[len(b) for b in bufs])
+        rc = self._lib.ssb_collector_submit_wire(self._h, int(t), n, ctypes.cast(ptrs, ctypes.c_void_p),
+                                                 ctypes.cast(lens, ctypes.c_void_p), rows.ctypes.data if n else None,
+                                                 ids.ctypes.data if n else None, root, ctypes.addressof(result), cb,
+                                                 ctypes.c_void_p(user))
+        if rc != 0:
+            raise RuntimeError("ssb_collector_submit_wire failed (%d)" % rc)
 
     def wait(self, result: "_lib.JobResult") -> None:
         self._lib.ssb_collector_wait(self._h, ctypes.addressof(result))
@@ -189,7 +213,19 @@ class SlotCollector:
         if len(job.sigs) != len(job.ids):
             return self._fail(fut, DifferentLength(len(job.sigs), len(job.ids)))
         if len(job.sigs) > MAX_JOB_SHARES:
-            return self._fail(fut, ValueError("more than %d shares in one job" % MAX_JOB_SHARES))
+            # beyond the collector's per-job limit: the engine's own batched call for this job alone, as
+            # slot_collector.rs falls back to the per-job call (the reference returns a result here too)
+            fut.set_running_or_notify_cancel()
+            try:
+                r = ThresholdSignature(t, self._native.engine).threshold_aggregate_batch([job])[0]
+            except BaseException as e:
+                fut.set_exception(e)
+                return fut
+            if isinstance(r, (DvfError, ValueError)):
+                fut.set_exception(r)
+            else:
+                fut.set_result(r)
+            return fut
         if self._closed:
             raise RuntimeError("collector closed")
         n = len(job.sigs)
@@ -308,23 +344,39 @@ class SlotCollector:
 
 # numpy view of ssb_job_result (include/ssbls.h), for arrays of results filled by native code
 JOB_RESULT_DTYPE = np.dtype([("sig96", np.uint8, 96), ("err", "<u8", 2), ("verdicts", "<u8"), ("status", "<i4"),
-                             ("rc", "<i4"), ("n_shares", "<u4"), ("done", "<u4")], align=True)
+                             ("rc", "<i4"), ("n_shares", "<u4"), ("done", "<u4"), ("absent", "<u8")], align=True)
 assert JOB_RESULT_DTYPE.itemsize == ctypes.sizeof(_lib.JobResult)
 
 
+def wire_records(sigs: bytes) -> bytes:
+    """bincode(bls::Signature) of each 96-byte compressed signature: u64 LE length 194, "0x", 192
+    lowercase hex digits -- the bytes an operator sends (src/node/dvfcore.rs:245-251)."""
+    n = len(sigs) // 96
+    a = np.frombuffer(sigs, dtype=np.uint8).reshape(n, 96)
+    hx = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
+    out = np.empty((n, WIRE_RECORD), dtype=np.uint8)
+    out[:, :8] = np.frombuffer((194).to_bytes(8, "little"), dtype=np.uint8)
+    out[:, 8], out[:, 9] = ord("0"), ord("x")
+    out[:, 10::2] = hx[a >> 4]
+    out[:, 11::2] = hx[a & 15]
+    return out.tobytes()
+
+
 def collbench_run(col: NativeCollector, wl: dict, V: int, n: int, t: int, rows: np.ndarray, n_jobs: int,
-                  threads: int = 8) -> Tuple[float, np.ndarray]:
+                  threads: int = 8, wire: Optional[bytes] = None) -> Tuple[float, np.ndarray]:
     """bench_tools/libcollbench.so: `threads` native submitters push n_jobs jobs (job k = validator
-    k % V of the workload) through the collector; (seconds first submit -> last result, results)."""
+    k % V of the workload) through the collector; (seconds first submit -> last result, results).
+    wire: the workload's shares as wire records (wire_records), submitted with
+    ssb_collector_submit_wire to a wire collector."""
     import os
     from .build import build_collbench
     lib = ctypes.CDLL(build_collbench(verbose=False))
-    fn = lib.ssb_collbench_run
+    fn = lib.ssb_collbench_run_wire if wire is not None else lib.ssb_collbench_run
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                    ctypes.POINTER(ctypes.c_double)]
-    sig = np.frombuffer(wl["sigs"], dtype=np.uint8)
+    sig = np.frombuffer(wire if wire is not None else wl["sigs"], dtype=np.uint8)
     ids = np.asarray(wl["ids"], dtype=np.uint64)
     roots = np.frombuffer(b"".join(wl["roots"]), dtype=np.uint8)
     jr = np.asarray(wl["job_root"], dtype=np.uint32)

@@ -264,16 +264,30 @@ SSB_INL void share_lookup(uint32_t s, const job_map& jm, uint32_t& job, uint32_t
   job = in ? (uint32_t)lo : 0xffffffffu;
   root = in ? (jm.job_root ? jm.job_root[lo] : 0u) : 0xffffffffu;
 }
+// wst != nullptr (the wire-record path, ssb_threshold_aggregate_batch_wire_cached_dev): a share whose
+// record did not deserialize -- a format error (wst[s] 1..3) or bytes that do not decompress (DEC_OK
+// clear; wst[s] := 4 here) -- is ABSENT, as the reference drops it before the call
+// (RemoteOperator::sign, operator.rs:108-131, then `.flatten()` in HotstuffOperatorCommittee::sign,
+// hotstuff.rs:150-155): it does not count towards sigs.len() (InsufficientSignatures{got: present,
+// expected: t}) and the scan never meets it.
 SSB_INL void select_job(int j, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                         const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
                         const uint32_t* __restrict__ flags, uint32_t* __restrict__ sel, int32_t* __restrict__ status,
-                        uint64_t* __restrict__ err) {
+                        uint64_t* __restrict__ err, int32_t* __restrict__ wst = nullptr) {
   const uint32_t b = off[j], e = off[j + 1], t = tt[j];
   if (!job_ok(b, e, t, n_shares)) { status[j] = SSB_DVF_INVALID_JOB; err[2 * j] = t; err[2 * j + 1] = e - b; return; }
-  const uint32_t n = e - b;
+  uint32_t n = e - b;
+  if (wst) {
+    for (uint32_t s = b; s < e; ++s)
+      if (!(flags[s] & DEC_OK)) {
+        if (wst[s] == 0) wst[s] = 4;
+        --n;
+      }
+  }
   if (n < t) { status[j] = SSB_DVF_INSUFFICIENT_SIGNATURES; err[2 * j] = n; err[2 * j + 1] = t; return; }
   uint32_t cnt = 0;
   for (uint32_t s = b; s < e; ++s) {
+    if (wst && !(flags[s] & DEC_OK)) continue;   // absent
     const uint64_t id = ids[s];
     if (id == 0) { status[j] = SSB_DVF_INVALID_OPERATOR_ID; err[2 * j] = 0; err[2 * j + 1] = 0; return; }
     bool dup = false;
@@ -303,13 +317,14 @@ SSB_FN void lagrange_job(int j, const uint32_t* __restrict__ off, const uint32_t
 constexpr uint32_t FAST_T = 16;
 // The combine of job j after its selection: small-integer Lagrange coefficients (ids 1..n:
 // unit_lagrange_small) finish the job here (returns 1, out96 written); coefficients that are ratios
-// of small integers (registry ids: unit_lagrange_ratio) leave T and the digits of M^-1 in rj[j]
-// (returns 2; k_combine_terms_gls / k_combine_sum finish it); else 0 (the general 255-bit path).
+// of small integers (registry ids, and ids 1..n with a share skipped: unit_lagrange_ratio) return 2
+// -- k_combine_ratio finishes the job, one lane each (unit_combine_ratio_w4); else 0 (the general
+// path: lambda_i, k_combine_terms_gls, k_combine_sum).  `ratio` = 0 (SSB_NO_RATIO): never 2.
 // One function for both, out of line: one set of per-lane arrays in its own frame.
 SSB_FN uint32_t combine_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                             const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                             const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
-                            uint8_t* __restrict__ out96, ratio_job* __restrict__ rj) {
+                            uint8_t* __restrict__ out96, uint32_t ratio) {
   if (status[j] != SSB_DVF_OK || tt[j] > FAST_T) return 0u;
   const uint32_t t = tt[j], b = off[j];
   uint64_t x[FAST_T];
@@ -320,9 +335,16 @@ SSB_FN uint32_t combine_job(int j, const uint32_t* __restrict__ off, const uint3
     return 1u;
   }
   uint64_t M;
-  if (!rj || !unit_lagrange_ratio(c, &M, x, t)) return 0u;
-  unit_combine_ratio_at(rj[j], sig_aff, sel + b, c, t, M);
-  return 2u;
+  return ratio && unit_lagrange_ratio(c, &M, x, t) ? 2u : 0u;
+}
+// the ratio coefficients of a job combine_job marked 2 (recomputed: a few 64-bit operations)
+SSB_INL void ratio_coeffs(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                          const uint32_t* __restrict__ sel, const uint64_t* __restrict__ ids, int64_t* c,
+                          uint64_t* M) {
+  const uint32_t t = tt[j], b = off[j];
+  uint64_t x[FAST_T];
+  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
+  unit_lagrange_ratio(c, M, x, t);
 }
 }  // namespace k
 }  // namespace ssb

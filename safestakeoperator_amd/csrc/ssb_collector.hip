@@ -7,14 +7,19 @@
 // handful of shares.  Here those calls become ssb_collector_submit: the job's bytes go straight into
 // the open window's pinned, device-mapped buffer, and the window runs as one engine batch.
 //
-// Concurrency.  Submitters reserve (job, share range) in the open window with ONE atomic fetch_add on
-// a packed word (bit 63 closed | jobs << 32 | shares): jobs and shares are handed out in order, so
-// the jobs that fit form a prefix and their share ranges are contiguous (share_off is written by the
-// submitters themselves).  A reservation past the capacity asks the worker to close the window and
-// retries in the next one.  The worker closes a window with fetch_or(closed): the reservations made
-// before it are exactly `jobs` of the returned word; it waits until all of them have settled
-// (copied, or given up as overflow), deduplicates the signing roots (hash_to_G2 runs once per
-// distinct root), and launches the window on the next one-stream pipeline slot.  Up to `in_flight`
+// Concurrency.  Submitters reserve (job, share range) in the open window with a compare-and-swap on a
+// packed word (bit 63 closed | 15-bit incarnation tag | jobs << 27 | shares): jobs and shares are
+// handed out in order, so the jobs form a prefix and their share ranges are contiguous (share_off is
+// written by the submitters themselves).  The tag is the window's incarnation (window objects are
+// reused): a submitter that loaded `open` and was preempted while that window was closed, delivered
+// and reopened fails its CAS instead of reserving in the wrong incarnation, and it waits for the
+// incarnation to change, not the pointer (with a plain fetch_add the add could land inside
+// reset() -- a lost job -- or on the closed word of a window that then reopened -- a caller blocked
+// forever).  A window without room asks the worker to close it and retries in the next one.  The
+// worker closes a window with fetch_or(closed): the reservations made before it are exactly `jobs` of
+// the returned word; it waits until all of them have been copied, deduplicates the signing roots
+// (hash_to_G2 runs once per distinct root), and launches the window on the next one-stream pipeline
+// slot.  Up to `in_flight`
 // windows run on the device while the next fills; a window's buffer is reused only after its event
 // completes, and results are delivered in launch order -- by a second thread, so that delivering a
 // window's results (copies + callbacks, tens of microseconds per window) never delays closing and
@@ -24,6 +29,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -32,12 +38,23 @@
 
 #include "../../include/ssbls.h"
 
-namespace ssb { int ctx_device(const ssb_ctx* ctx); }
+namespace ssb {
+int ctx_device(const ssb_ctx* ctx);
+std::recursive_mutex& ctx_mutex(ssb_ctx* ctx);
+}
 
 namespace {
 
+// the reservation word: bit 63 closed | tag (bits 48..62) | jobs (bits 27..47) | shares (bits 0..26)
 constexpr uint64_t CLOSED = 1ull << 63;
+constexpr int JOB_SHIFT = 27, TAG_SHIFT = 48;
+constexpr uint64_t SHARE_MASK = (1ull << JOB_SHIFT) - 1, JOB_MASK = (1ull << (TAG_SHIFT - JOB_SHIFT)) - 1;
+constexpr uint64_t TAG_FIELD = 0x7fffull << TAG_SHIFT;
+constexpr uint32_t MAX_WINDOW_JOBS = 1u << 20, MAX_WINDOW_SHARES = 1u << 26;
+inline uint64_t tag_of(uint64_t gen) { return (gen & 0x7fffull) << TAG_SHIFT; }
+inline uint32_t jobs_of(uint64_t r) { return (uint32_t)((r >> JOB_SHIFT) & JOB_MASK); }
 constexpr uint32_t MAX_JOB_SHARES = 64;
+constexpr size_t WIRE_REC = 202;   // bincode(bls::Signature): u64 length 194, "0x", 192 hex digits
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -47,8 +64,10 @@ inline void cpu_relax() { __builtin_ia32_pause(); }
 struct window {
   uint8_t* h = nullptr;   // pinned host buffer (inputs, then the engine's outputs)
   uint8_t* d = nullptr;   // its device address
-  size_t i_sig = 0, i_pk = 0, i_ids = 0, i_off = 0, i_t = 0, i_jr = 0, i_roots = 0, o_sig = 0, o_st = 0, o_err = 0, o_ver = 0;
-  std::atomic<uint64_t> resv{0};
+  size_t i_sig = 0, i_pk = 0, i_ids = 0, i_off = 0, i_t = 0, i_jr = 0, i_roots = 0, o_sig = 0, o_st = 0, o_err = 0, o_ver = 0,
+         o_wst = 0;   // (wire collectors: i_sig holds 202-byte records; o_wst their statuses)
+  std::atomic<uint64_t> resv{CLOSED};
+  std::atomic<uint64_t> gen{0};   // the incarnation (== seq while open), tagged into resv
   std::atomic<uint32_t> settled{0};
   std::atomic<uint32_t> committed{0};
   std::atomic<int64_t> t_first{0};
@@ -57,6 +76,7 @@ struct window {
   std::vector<void*> user;
   std::vector<uint8_t> root_in;   // per job, the 32-byte root as submitted
   hipEvent_t ev = nullptr;
+  bool ev_ok = false;     // ev was recorded after the window's launches (sync on it before reuse)
   uint64_t seq = 0;
   uint32_t nj = 0, ns = 0;
   int rc = SSB_OK;
@@ -69,6 +89,7 @@ struct ssb_collector {
   ssb_ctx* ctx = nullptr;
   int device = 0;
   uint32_t J = 0, N = 0, in_flight = 1;
+  bool wire = false;               // SSB_COLLECTOR_WIRE: shares held as wire records
   int64_t window_ns = 0;
   std::vector<window*> all;
   std::atomic<window*> open{nullptr};
@@ -76,7 +97,6 @@ struct ssb_collector {
   std::mutex mu;                   // worker state, the queues, the condition variables
   std::condition_variable cv_worker, cv_submit, cv_done, cv_deliver, cv_free;
   bool sealing_done = false;       // the worker has closed its last window (destroy)
-  std::mutex ctx_mu;               // the engine context: launches and key registration
   uint64_t seal_upto = 0;          // a submitter found window seq <= this full: close it
   uint32_t max_windows = 1;        // windows on the device: two per slot (one running, one queued)
   std::atomic<bool> stopping{false};
@@ -89,15 +109,19 @@ struct ssb_collector {
   std::thread worker, deliverer;
   std::vector<uint32_t> rtab;      // worker-only: root dedup table (index + 1)
 
+  // a new incarnation of a free window: every counter first, the reservation word LAST (release),
+  // so a submitter whose CAS succeeds on the new tag sees the zeroed counters
   void reset(window* w) {
-    w->resv.store(0, std::memory_order_relaxed);
     w->settled.store(0, std::memory_order_relaxed);
     w->committed.store(0, std::memory_order_relaxed);
     w->t_first.store(0, std::memory_order_relaxed);
     w->off()[0] = 0;
     w->nj = w->ns = 0;
     w->rc = SSB_OK;
+    w->ev_ok = false;
     w->seq = seq_next++;
+    w->gen.store(w->seq, std::memory_order_release);
+    w->resv.store(tag_of(w->seq), std::memory_order_release);
   }
   void seal(window* w);
   void deliver(window* w);
@@ -107,10 +131,13 @@ struct ssb_collector {
 
 namespace {
 
-void wait_new_window(ssb_collector* c, window* w) {
+// until the open window is another one or another incarnation of w (a window object is reused)
+void wait_new_window(ssb_collector* c, window* w, uint64_t gen) {
   c->n_full_waits.fetch_add(1, std::memory_order_relaxed);
   std::unique_lock<std::mutex> lk(c->mu);
-  c->cv_submit.wait(lk, [&] { return c->open.load(std::memory_order_acquire) != w || c->stopping; });
+  c->cv_submit.wait(lk, [&] {
+    return c->open.load(std::memory_order_acquire) != w || w->gen.load(std::memory_order_acquire) != gen || c->stopping;
+  });
 }
 
 }  // namespace
@@ -143,15 +170,30 @@ void ssb_collector::seal(window* w) {
     }
   }
   static const uint8_t dst[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";   // src/crypto/impls/blst.rs:11
-  std::lock_guard<std::mutex> g(ctx_mu);
+  std::lock_guard<std::recursive_mutex> g(ssb::ctx_mutex(ctx));   // the slot's stream and the launches, atomically
   const int k = (int)(slot_rr++ % in_flight);
   void* st = ssb_slot_stream(ctx, k);
   uint8_t* d = w->d;
-  w->rc = ssb_threshold_aggregate_batch_cached_dev(
-      ctx, nj, w->ns, (const uint32_t*)(d + w->i_off), (const uint32_t*)(d + w->i_t), d + w->i_sig,
-      (const uint32_t*)(d + w->i_pk), (const uint64_t*)(d + w->i_ids), (const uint32_t*)(d + w->i_jr), nr, d + w->i_roots,
-      dst, sizeof(dst) - 1, 0, d + w->o_sig, (int32_t*)(d + w->o_st), (uint64_t*)(d + w->o_err), d + w->o_ver, st);
-  if (w->rc == SSB_OK && hipEventRecord(w->ev, (hipStream_t)st) != hipSuccess) w->rc = SSB_EHIP;
+  if (wire)
+    w->rc = ssb_threshold_aggregate_batch_wire_cached_dev(
+        ctx, nj, w->ns, (const uint32_t*)(d + w->i_off), (const uint32_t*)(d + w->i_t), d + w->i_sig, WIRE_REC,
+        (const uint32_t*)(d + w->i_pk), (const uint64_t*)(d + w->i_ids), (const uint32_t*)(d + w->i_jr), nr, d + w->i_roots,
+        dst, sizeof(dst) - 1, 0, d + w->o_sig, (int32_t*)(d + w->o_st), (uint64_t*)(d + w->o_err), d + w->o_ver,
+        (int32_t*)(d + w->o_wst), st);
+  else
+    w->rc = ssb_threshold_aggregate_batch_cached_dev(
+        ctx, nj, w->ns, (const uint32_t*)(d + w->i_off), (const uint32_t*)(d + w->i_t), d + w->i_sig,
+        (const uint32_t*)(d + w->i_pk), (const uint64_t*)(d + w->i_ids), (const uint32_t*)(d + w->i_jr), nr, d + w->i_roots,
+        dst, sizeof(dst) - 1, 0, d + w->o_sig, (int32_t*)(d + w->o_st), (uint64_t*)(d + w->o_err), d + w->o_ver, st);
+  // the event follows whatever the call enqueued, a failed call's partial launches included: the
+  // deliverer waits on it before the window's buffer is refilled; if it cannot be
+  // recorded, the stream is drained here instead
+  w->ev_ok = st && hipEventRecord(w->ev, (hipStream_t)st) == hipSuccess;
+  if (!w->ev_ok) {
+    if (st) (void)hipStreamSynchronize((hipStream_t)st);
+    (void)hipGetLastError();
+    if (w->rc == SSB_OK) w->rc = SSB_EHIP;
+  }
   n_windows.fetch_add(1, std::memory_order_relaxed);
 }
 
@@ -171,15 +213,21 @@ void ssb_collector::deliver(window* w) {
       r->status = st[j];
       r->err[0] = er[2 * (size_t)j];
       r->err[1] = er[2 * (size_t)j + 1];
-      uint64_t bits = 0;
+      uint64_t bits = 0, absent = 0;
       for (uint32_t i = 0; i < n && i < 64; ++i) bits |= (uint64_t)(vr[b + i] != 0) << i;
+      if (wire) {
+        const int32_t* ws = (const int32_t*)(w->h + w->o_wst);
+        for (uint32_t i = 0; i < n && i < 64; ++i) absent |= (uint64_t)(ws[b + i] != 0) << i;
+      }
       r->verdicts = bits;
+      r->absent = absent;
     } else {
       memset(r->sig96, 0, 96);
       r->status = SSB_DVF_ENGINE_ERROR;
       r->err[0] = (uint64_t)(int64_t)w->rc;
       r->err[1] = 0;
       r->verdicts = 0;
+      r->absent = 0;
     }
     __atomic_store_n(&r->done, 1u, __ATOMIC_RELEASE);
     if (w->cb[j]) w->cb[j](w->user[j], r);
@@ -194,7 +242,7 @@ void ssb_collector::run() {
   for (;;) {
     window* w = open.load(std::memory_order_relaxed);
     const uint64_t r = w->resv.load(std::memory_order_acquire);
-    const uint32_t nres = (uint32_t)(r >> 32) & 0x7fffffffu;
+    const uint32_t nres = jobs_of(r);
     const int64_t t0 = w->t_first.load(std::memory_order_relaxed);
     const int64_t now = now_ns();
     const bool due = nres > 0 && (seal_upto >= w->seq || stopping || flush_upto >= w->seq || nres >= J ||
@@ -213,7 +261,7 @@ void ssb_collector::run() {
       cv_submit.notify_all();
       lk.unlock();
       const int64_t s0 = now_ns();
-      const uint32_t pre = (uint32_t)(w->resv.fetch_or(CLOSED, std::memory_order_acq_rel) >> 32) & 0x7fffffffu;
+      const uint32_t pre = jobs_of(w->resv.fetch_or(CLOSED, std::memory_order_acq_rel));
       while (w->settled.load(std::memory_order_acquire) < pre) cpu_relax();   // submitters mid-copy
       seal(w);
       ns_seal.fetch_add((uint64_t)(now_ns() - s0), std::memory_order_relaxed);
@@ -241,7 +289,7 @@ void ssb_collector::deliver_loop() {
     if (inflight.empty()) break;   // (sealing_done: nothing more will be launched)
     window* f = inflight.front();  // stays queued while it runs: FIFO delivery, and the worker counts it
     lk.unlock();
-    if (f->rc == SSB_OK && hipEventSynchronize(f->ev) != hipSuccess) f->rc = SSB_EHIP;
+    if (f->ev_ok && hipEventSynchronize(f->ev) != hipSuccess && f->rc == SSB_OK) f->rc = SSB_EHIP;
     const int64_t d0 = now_ns();
     deliver(f);
     ns_deliver.fetch_add((uint64_t)(now_ns() - d0), std::memory_order_relaxed);
@@ -266,27 +314,50 @@ void free_windows(ssb_collector* c) {
 }
 // wake the worker about a change of a window's reservation word (which it reads outside `mu`):
 // taking `mu` first means the worker is either before its check or already waiting (no lost wakeup)
-void poke_worker(ssb_collector* c, const window* full) {
+// (full_gen: the incarnation found without room -- closing is asked for THAT incarnation only, so a
+// late request never closes its successor; 0: just a wake-up)
+void poke_worker(ssb_collector* c, uint64_t full_gen) {
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    // per window: a late overflow on an already closed window must not close its successor
-    if (full && full->seq > c->seal_upto) c->seal_upto = full->seq;
+    if (full_gen > c->seal_upto) c->seal_upto = full_gen;
   }
   c->cv_worker.notify_one();
+}
+// lowercase hex of a 96-byte compressed signature into a wire record (a compressed share submitted
+// to a wire collector): exactly bincode::serialize(&sig), which the device decodes back
+void to_wire(uint8_t* rec, const uint8_t* sig96) {
+  static const char* hx = "0123456789abcdef";
+  const uint64_t len = 194;
+  memcpy(rec, &len, 8);
+  rec[8] = '0'; rec[9] = 'x';
+  for (int b = 0; b < 96; ++b) { rec[10 + 2 * b] = (uint8_t)hx[sig96[b] >> 4]; rec[11 + 2 * b] = (uint8_t)hx[sig96[b] & 15]; }
 }
 }  // namespace
 
 extern "C" {
 
-int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, uint32_t window_us, int in_flight,
-                         ssb_collector** out) {
+int ssb_collector_create2(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, uint32_t window_us, int in_flight,
+                          uint32_t flags, ssb_collector** out) {
   if (!out) return SSB_EINVAL;
   *out = nullptr;
-  if (!ctx || max_jobs == 0 || max_jobs > (1u << 24) || max_shares < MAX_JOB_SHARES || max_shares > (1u << 28) ||
-      in_flight < 1 || ssb_check_pipeline_config(in_flight, 1) != SSB_OK)
+  if (!ctx || max_jobs == 0 || max_jobs > MAX_WINDOW_JOBS || max_shares < MAX_JOB_SHARES || max_shares > MAX_WINDOW_SHARES ||
+      in_flight < 1 || (flags & ~(uint32_t)SSB_COLLECTOR_WIRE) || ssb_check_pipeline_config(in_flight, 1) != SSB_OK)
     return SSB_EINVAL;
+  // one hardware queue per slot stream, one left for the process (ssb_hw_queue_budget): a larger
+  // in_flight would put independent windows on shared queues, where they serialise
+  const int budget = ssb_hw_queue_budget();
+  if (in_flight > budget - 1) {
+    const int cap = budget - 1 > 1 ? budget - 1 : 1;
+    fprintf(stderr, "ssb_collector_create: in_flight %d lowered to %d -- the process has GPU_MAX_HW_QUEUES=%d hardware "
+                    "queues (set GPU_MAX_HW_QUEUES >= in_flight + 1, at most 32, before the first HIP call)\n",
+            in_flight, cap, budget);
+    in_flight = cap;
+  }
   int rc;
-  if ((rc = ssb_set_slot_streams(ctx, 1)) || (rc = ssb_set_pipeline_depth(ctx, in_flight))) return rc;
+  {
+    std::lock_guard<std::recursive_mutex> g(ssb::ctx_mutex(ctx));
+    if ((rc = ssb_set_slot_streams(ctx, 1)) || (rc = ssb_set_pipeline_depth(ctx, in_flight))) return rc;
+  }
   ssb_collector* c = new (std::nothrow) ssb_collector();
   if (!c) return SSB_ENOMEM;
   c->ctx = ctx;
@@ -294,6 +365,7 @@ int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, u
   c->J = max_jobs;
   c->N = max_shares;
   c->in_flight = (uint32_t)in_flight;
+  c->wire = (flags & SSB_COLLECTOR_WIRE) != 0;
   c->max_windows = 2u * (uint32_t)in_flight;
   c->window_ns = (int64_t)window_us * 1000;
   uint32_t rt = 1;
@@ -307,9 +379,10 @@ int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, u
     c->all.push_back(w);
     size_t o = 0;
     auto at = [&](size_t bytes) { const size_t r = o; o += al(bytes); return r; };
-    w->i_sig = at(N * 96); w->i_pk = at(N * 4); w->i_ids = at(N * 8); w->i_off = at((J + 1) * 4); w->i_t = at(J * 4);
-    w->i_jr = at(J * 4); w->i_roots = at(J * 32); w->o_sig = at(J * 96); w->o_st = at(J * 4); w->o_err = at(J * 16);
-    w->o_ver = at(N);
+    w->i_sig = at(N * (c->wire ? WIRE_REC : 96)); w->i_pk = at(N * 4); w->i_ids = at(N * 8); w->i_off = at((J + 1) * 4);
+    w->i_t = at(J * 4); w->i_jr = at(J * 4); w->i_roots = at(J * 32); w->o_sig = at(J * 96); w->o_st = at(J * 4);
+    w->o_err = at(J * 16); w->o_ver = at(N);
+    if (c->wire) w->o_wst = at(N * 4);
     if (hipHostMalloc((void**)&w->h, o, hipHostMallocMapped | hipHostMallocNonCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&w->d, w->h, 0) != hipSuccess ||
         hipEventCreateWithFlags(&w->ev, hipEventDisableTiming) != hipSuccess) {
@@ -335,6 +408,11 @@ int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, u
   return SSB_OK;
 }
 
+int ssb_collector_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, uint32_t window_us, int in_flight,
+                         ssb_collector** out) {
+  return ssb_collector_create2(ctx, max_jobs, max_shares, window_us, in_flight, 0u, out);
+}
+
 void ssb_collector_destroy(ssb_collector* c) {
   if (!c) return;
   {
@@ -351,36 +429,41 @@ void ssb_collector_destroy(ssb_collector* c) {
 
 int ssb_collector_register_keys(ssb_collector* c, size_t n, const uint8_t* pk48, uint32_t* out_index) {
   if (!c) return SSB_EINVAL;
-  std::lock_guard<std::mutex> g(c->ctx_mu);
-  return ssb_pk_cache_add(c->ctx, n, pk48, out_index);
+  return ssb_pk_cache_add(c->ctx, n, pk48, out_index);   // (the context's lock serialises it with the launches)
 }
 
-int ssb_collector_submit(ssb_collector* c, uint32_t t, uint32_t n, const uint8_t* sig96, const uint32_t* pk_index,
-                         const uint64_t* ids, const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb,
-                         void* user) {
-  if (!c || !result || !root32 || t == 0 || t > SSB_MAX_T || n > MAX_JOB_SHARES || (n && (!sig96 || !pk_index || !ids)))
-    return SSB_EINVAL;
+}  // extern "C"
+namespace {
+// one job into the open window: a CAS reservation on the incarnation's tagged word, then the copy;
+// `put` writes share i's signature bytes at `dst` (96 bytes, or a wire record in a wire collector)
+template <class Put>
+int submit_job(ssb_collector* c, uint32_t t, uint32_t n, Put put, const uint32_t* pk_index, const uint64_t* ids,
+               const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb, void* user) {
   __atomic_store_n(&result->done, 0u, __ATOMIC_RELAXED);
   for (;;) {
     if (c->stopping.load(std::memory_order_acquire)) return SSB_EINVAL;   // (a submit must not race destroy)
     window* w = c->open.load(std::memory_order_acquire);
-    const uint64_t old = w->resv.fetch_add((1ull << 32) | n, std::memory_order_acq_rel);
-    if (old & CLOSED) {   // the worker closed this window after we loaded it: retry in the next one
-      if (c->stopping) return SSB_EINVAL;
-      wait_new_window(c, w);
-      continue;
+    const uint64_t g = w->gen.load(std::memory_order_acquire);
+    uint64_t r = w->resv.load(std::memory_order_acquire);
+    bool placed = false, full = false;
+    uint32_t j = 0, s = 0;
+    while (!(r & CLOSED) && (r & TAG_FIELD) == tag_of(g)) {
+      j = jobs_of(r);
+      s = (uint32_t)(r & SHARE_MASK);
+      if (j >= c->J || (uint64_t)s + n > c->N) { full = true; break; }
+      if (w->resv.compare_exchange_weak(r, r + (1ull << JOB_SHIFT) + n, std::memory_order_acq_rel,
+                                        std::memory_order_acquire)) { placed = true; break; }
     }
-    const uint32_t j = (uint32_t)(old >> 32) & 0x7fffffffu, s = (uint32_t)old;
-    if (j >= c->J || (uint64_t)s + n > c->N) {   // full: have it closed, retry in the next window
-      w->settled.fetch_add(1, std::memory_order_release);
-      poke_worker(c, w);
+    if (!placed) {   // closed, another incarnation, or no room: have it closed, retry in the next window
+      if (full) poke_worker(c, g);
       if (c->stopping) return SSB_EINVAL;
-      wait_new_window(c, w);
+      wait_new_window(c, w, g);
       continue;
     }
     if (j == 0) w->t_first.store(now_ns(), std::memory_order_relaxed);
     uint8_t* h = w->h;
-    memcpy(h + w->i_sig + 96 * (size_t)s, sig96, 96 * (size_t)n);
+    const size_t rec = c->wire ? WIRE_REC : 96;
+    for (uint32_t i = 0; i < n; ++i) put(h + w->i_sig + rec * ((size_t)s + i), i);
     memcpy(h + w->i_pk + 4 * (size_t)s, pk_index, 4 * (size_t)n);
     memcpy(h + w->i_ids + 8 * (size_t)s, ids, 8 * (size_t)n);
     w->off()[j + 1] = s + n;
@@ -391,9 +474,39 @@ int ssb_collector_submit(ssb_collector* c, uint32_t t, uint32_t n, const uint8_t
     w->user[j] = user;
     w->committed.fetch_add(1, std::memory_order_release);
     w->settled.fetch_add(1, std::memory_order_release);
-    if (j == 0 || j + 1 == c->J) poke_worker(c, nullptr);   // a window starts (its timer) / is full
+    if (j == 0 || j + 1 == c->J) poke_worker(c, 0);   // a window starts (its timer) / is full
     return SSB_OK;
   }
+}
+}  // namespace
+extern "C" {
+
+int ssb_collector_submit(ssb_collector* c, uint32_t t, uint32_t n, const uint8_t* sig96, const uint32_t* pk_index,
+                         const uint64_t* ids, const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb,
+                         void* user) {
+  if (!c || !result || !root32 || t == 0 || t > SSB_MAX_T || n > MAX_JOB_SHARES || (n && (!sig96 || !pk_index || !ids)))
+    return SSB_EINVAL;
+  if (c->wire)
+    return submit_job(c, t, n, [&](uint8_t* d, uint32_t i) { to_wire(d, sig96 + 96 * (size_t)i); }, pk_index, ids, root32,
+                      result, cb, user);
+  return submit_job(c, t, n, [&](uint8_t* d, uint32_t i) { memcpy(d, sig96 + 96 * (size_t)i, 96); }, pk_index, ids, root32,
+                    result, cb, user);
+}
+
+int ssb_collector_submit_wire(ssb_collector* c, uint32_t t, uint32_t n, const uint8_t* const* wire, const size_t* wire_len,
+                              const uint32_t* pk_index, const uint64_t* ids, const uint8_t* root32, ssb_job_result* result,
+                              ssb_job_done_fn cb, void* user) {
+  if (!c || !c->wire || !result || !root32 || t == 0 || t > SSB_MAX_T || n > MAX_JOB_SHARES ||
+      (n && (!wire || !wire_len || !pk_index || !ids)))
+    return SSB_EINVAL;
+  // a record of any other length than 202 bytes cannot be a bincode Signature: its length field or
+  // its digits fail on the device (the record is copied as received, truncated or zero-padded)
+  return submit_job(c, t, n, [&](uint8_t* d, uint32_t i) {
+    const size_t l = wire[i] ? (wire_len[i] < WIRE_REC ? wire_len[i] : WIRE_REC) : 0;
+    if (l) memcpy(d, wire[i], l);
+    if (l < WIRE_REC) memset(d + l, 0, WIRE_REC - l);
+    if (wire[i] && wire_len[i] != WIRE_REC) { const uint64_t bad = ~0ull; memcpy(d, &bad, 8); }   // never parses
+  }, pk_index, ids, root32, result, cb, user);
 }
 
 int ssb_collector_wait(ssb_collector* c, const ssb_job_result* r) {
@@ -408,7 +521,7 @@ int ssb_collector_flush(ssb_collector* c) {
   if (!c) return SSB_EINVAL;
   std::unique_lock<std::mutex> lk(c->mu);
   window* w = c->open.load(std::memory_order_acquire);
-  const bool empty = ((w->resv.load(std::memory_order_acquire) >> 32) & 0x7fffffffu) == 0;
+  const bool empty = jobs_of(w->resv.load(std::memory_order_acquire)) == 0;
   const uint64_t target = empty ? w->seq - 1 : w->seq;
   if (target > c->flush_upto) c->flush_upto = target;
   c->cv_worker.notify_one();

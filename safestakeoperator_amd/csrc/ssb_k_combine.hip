@@ -65,49 +65,68 @@ __global__ void SSB_LB(64) k_combine_terms(int n, uint32_t n_jobs, const uint32_
   unit_combine_term(r, sig_aff[sel[s]], l.l);  // blst_p2_mult(.., 255 bits)
   term[s] = r;
 }
-// verified candidates only: four lanes per share, one base-u digit each (unit_combine_term_gls);
-// term[4 s + q]
+// The general combine's terms and phase T of the ratio combine, in one launch.
+// Blocks [0, nbt): verified candidates only, four lanes per share, one base-u digit each
+// (unit_combine_term_gls); term[4 s + q].  Jobs combine_job finished (fast 1) or left to the ratio
+// combine (fast 2) are skipped.
+// Blocks [nbt, ..): one lane per job of the ratio combine (fast 2: lambda_i = c_i / M), phase T --
+// T = sum c_i sig_i, lane-uniform joint windows (unit_ratio_T), into rT[j]; tables in the job's
+// RC_TAB_BYTES region of `tabs`.  Every lane of the wave takes part in the window count's maximum
+// before any returns, so the doubling chain is the wave's.
 __global__ void SSB_LB(64) k_combine_terms_gls(int n, uint32_t n_jobs, const uint32_t* __restrict__ share_job,
                                               const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                               const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                               const fr* __restrict__ lam, const g2_aff* __restrict__ sig_aff,
                                               const uint32_t* __restrict__ skip_if_ok, const uint32_t* __restrict__ fast,
-                                              g2_jac* __restrict__ term, const ratio_job* __restrict__ rj) {
+                                              g2_jac* __restrict__ term, ratio_args ra) {
+  if (blockIdx.x >= ra.nbt) {
+    const int j = (blockIdx.x - ra.nbt) * blockDim.x + threadIdx.x;
+    const bool act = (uint32_t)j < n_jobs && !(skip_if_ok && *skip_if_ok) && fast && fast[j] == 2u;
+    int64_t c[FAST_T];
+    uint64_t M = 1;
+    int W = 1;
+    if (act) {
+      ratio_coeffs(j, off, tt, sel, ra.ids, c, &M);
+      W = rc_windows(c, tt[j]);
+    }
+    for (int o = 32; o >= 1; o >>= 1) { const int x = __shfl_xor(W, o, 64); W = x > W ? x : W; }
+    W = __builtin_amdgcn_readfirstlane(W);
+    if (!act) return;
+    unit_ratio_T(ra.rT + j, ra.rk + 4 * (size_t)j, sig_aff, sel + off[j], c, tt[j], M, W, ra.tabs + (size_t)j * RC_TAB_BYTES);
+    return;
+  }
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= 4 * n) return;
   if (skip_if_ok && *skip_if_ok) return;
   const int s = g >> 2, q = g & 3;
   const uint32_t j = share_job[s];
   if (j >= n_jobs) return;   // outside every well-formed job (k_share_map's sentinel)
-  if (fast && fast[j] == 1u) return;
+  if (fast && fast[j]) return;
   const uint32_t k = (uint32_t)s - off[j];
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
-  if (fast && fast[j] == 2u) {   // registry ids: [M^-1] T, one digit per lane, on the job's first share
-    if (k != 0) return;
-    g2_jac r;
-    unit_gls_term(r, rj[j].T, rj[j].d[q], q);
-    term[4 * (size_t)s + q] = r;
-    return;
-  }
   const fr l = lam[s];
   g2_jac r;
   unit_combine_term_gls(r, sig_aff[sel[s]], l.l, q);
   term[4 * (size_t)s + q] = r;
 }
-// stride: terms per share (1: k_combine_terms, 4: k_combine_terms_gls)
+// stride: terms per share (1: k_combine_terms, 4: k_combine_terms_gls).  Jobs of the ratio combine
+// (fast 2; ra.rT != nullptr) run its phase K here: [M^-1] T from rT[j], compressed (unit_ratio_K).
 __global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
-                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride) {
+                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride,
+                                                    const uint32_t* __restrict__ sel, ratio_args ra) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
-  if (fast && fast[j] == 1u) return;
+  if (fast && fast[j] == 2u && ra.rT) {
+    unit_ratio_K(out96 + 96 * (size_t)j, ra.rT + j, ra.rk + 4 * (size_t)j, ra.tabs + (size_t)j * RC_TAB_BYTES);
+    return;
+  }
+  if (fast && fast[j]) return;   // finished by combine_job (1)
   uint8_t o[96];
   if (status[j] == SSB_DVF_OK) {
-    // (fast[j] == 2: the four digit terms of [M^-1] T on the job's first share)
-    const uint32_t cnt = (fast && fast[j] == 2u) ? 4u : (uint32_t)stride * tt[j];
-    unit_combine_sum(o, term + (size_t)stride * off[j], cnt);  // infinity(t) start (blst.rs:74)
+    unit_combine_sum(o, term + (size_t)stride * off[j], (uint32_t)stride * tt[j]);  // infinity(t) start (blst.rs:74)
   } else {
     for (int k = 0; k < 96; ++k) o[k] = 0;
   }
@@ -122,7 +141,7 @@ __global__ void SSB_LB(64) k_combine_fast(int n_jobs, const uint32_t* __restrict
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
-  fast[j] = combine_job(j, off, tt, status, sel, ids, sig_aff, out96, nullptr);
+  fast[j] = combine_job(j, off, tt, status, sel, ids, sig_aff, out96, 0u);
 }
 // k_select + k_combine_fast + k_lagrange of one job in one thread (one launch instead of three)
 __global__ void SSB_LB(64) k_select_combine(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off,
@@ -131,12 +150,13 @@ __global__ void SSB_LB(64) k_select_combine(int n_jobs, uint32_t n_shares, const
                                             const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ sel,
                                             int32_t* __restrict__ status, uint64_t* __restrict__ err,
                                             const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ fast,
-                                            uint8_t* __restrict__ out96, fr* __restrict__ lam, ratio_job* __restrict__ rj) {
+                                            uint8_t* __restrict__ out96, fr* __restrict__ lam, uint32_t ratio,
+                                            int32_t* __restrict__ wst) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
-  select_job(j, n_shares, off, tt, ids, verdict, flags, sel, status, err);
-  const uint32_t f = combine_job(j, off, tt, status, sel, ids, sig_aff, out96, rj);
+  select_job(j, n_shares, off, tt, ids, verdict, flags, sel, status, err, wst);
+  const uint32_t f = combine_job(j, off, tt, status, sel, ids, sig_aff, out96, ratio);
   fast[j] = f;
   if (!f && status[j] == SSB_DVF_OK) lagrange_job(j, off, tt, ids, sel, lam);
 }

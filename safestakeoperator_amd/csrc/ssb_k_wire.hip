@@ -23,7 +23,7 @@ __device__ __forceinline__ int hexval(uint32_t c) {
 }
 
 __global__ void SSB_LB(64) k_wire_sig(int n, const uint8_t* __restrict__ wire, size_t stride, uint8_t* __restrict__ out96,
-                           int32_t* __restrict__ status) {
+                           int32_t* __restrict__ status, int check_point) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* r = wire + (size_t)i * stride;
@@ -38,10 +38,12 @@ __global__ void SSB_LB(64) k_wire_sig(int n, const uint8_t* __restrict__ wire, s
     if ((hi | lo) < 0) st = st ? st : 3;
     o[b] = (uint8_t)(((hi & 15) << 4) | (lo & 15));
   }
+  if (st)   // a record that did not parse leaves zeros (no compression flag: never decodes downstream)
+    for (int b = 0; b < 96; ++b) o[b] = 0;
   // bincode::deserialize::<Signature> also decompresses the point (blst uncompress: flags, x < p,
   // on the curve; infinity is a valid Signature) -- a record that fails is dropped by the reference
   // (operator.rs:108-113), so it is reported here instead of failing later as an invalid share
-  if (!st) {
+  if (!st && check_point) {
     uint8_t b[96];
     for (int k = 0; k < 96; ++k) b[k] = o[k];
     g2_aff pt;
@@ -53,8 +55,9 @@ __global__ void SSB_LB(64) k_wire_sig(int n, const uint8_t* __restrict__ wire, s
 }  // namespace k
 
 namespace launch {
-void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status) {
-  if (n > 0) hipLaunchKernelGGL(k::k_wire_sig, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, wire, stride, out96, status);
+void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status, int check_point) {
+  if (n > 0) hipLaunchKernelGGL(k::k_wire_sig, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, wire, stride, out96, status,
+                                check_point);
 }
 }  // namespace launch
 }  // namespace ssb

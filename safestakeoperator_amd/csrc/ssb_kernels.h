@@ -59,8 +59,13 @@ struct dst_arg { uint8_t b[SSB_MAX_DST + 1]; int len; };
 struct spec_jobs {
   int n_jobs; uint32_t n_shares; const uint32_t* off; const uint32_t* tt; const uint64_t* ids; const uint32_t* flags;
   uint32_t* sel; int32_t* status; uint64_t* err; const g2_aff* sig_aff; uint32_t* fast; uint8_t* out96; fr* lam;
-  ratio_job* rj;   // registry ids: the ratio path's per-job T and digits (fast[j] == 2)
+  uint32_t ratio;  // 1: jobs whose lambda_i are ratios of small integers are marked for k_combine_ratio (fast 2)
+  int32_t* wst;    // the wire-record path: per-share record status, undecodable shares absent (select_job)
 };
+
+// the ratio combine's arguments riding in k_combine_terms_gls (phase T, blocks past nbt) and
+// k_combine_sum (phase K): the jobs' ids, the per-job table regions, the per-job T
+struct ratio_args { const uint64_t* ids; uint8_t* tabs; g2_jac* rT; uint64_t* rk; uint32_t nbt; };
 
 // share -> (job, root) of an aggregate batch (share_lookup, ssb_blocks.h)
 struct job_map {
@@ -159,19 +164,20 @@ __global__ void k_combine_terms_gls(int n, uint32_t n_jobs, const uint32_t* __re
                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                     const uint32_t* __restrict__ sel, const fr* __restrict__ lam,
                                     const g2_aff* __restrict__ sig_aff, const uint32_t* __restrict__ skip_if_ok,
-                                    const uint32_t* __restrict__ fast, g2_jac* __restrict__ term,
-                                    const ratio_job* __restrict__ rj);
+                                    const uint32_t* __restrict__ fast, g2_jac* __restrict__ term, ratio_args ra);
 __global__ void k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
-                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride);
+                                                    const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride,
+                                                    const uint32_t* __restrict__ sel, ratio_args ra);
 __global__ void k_select_combine(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off,
                                  const uint32_t* __restrict__ tt, const uint64_t* __restrict__ ids,
                                  const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ flags,
                                  const uint32_t* __restrict__ skip_if_ok, uint32_t* __restrict__ sel,
                                  int32_t* __restrict__ status, uint64_t* __restrict__ err,
                                  const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ fast,
-                                 uint8_t* __restrict__ out96, fr* __restrict__ lam, ratio_job* __restrict__ rj);
+                                 uint8_t* __restrict__ out96, fr* __restrict__ lam, uint32_t ratio,
+                                 int32_t* __restrict__ wst);
 __global__ void k_combine_fast(int n_jobs, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                                const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                                const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
@@ -296,7 +302,10 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
 int prime_queue(hipStream_t st);
 // wire-format records bincode(bls::Signature) -> 96-byte compressed signatures (ssb_k_wire.hip)
 constexpr size_t WIRE_SIG_BYTES = 202;
-void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status);
+// check_point: status 4 for bytes that do not decompress (ssb_decode_wire_sigs); 0: format and hex
+// only (the aggregate's wire path, whose decode stage decompresses anyway -- select_job marks 4)
+void wire_sig(hipStream_t st, int n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status,
+              int check_point = 1);
 // DKG share verification (ssb_k_dkg.hip): verdict[i] = ([s_i]h == sum_k [x_i^k] C_{i,k})
 void feldman_share(hipStream_t st, int n, int t, const uint8_t* comm48, const uint64_t* x, const uint8_t* s32le,
                    const g1_aff* h, const uint32_t* hflags, uint8_t* verdict);

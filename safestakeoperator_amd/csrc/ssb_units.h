@@ -453,16 +453,277 @@ SSB_FN void unit_lagrange_fast(fr* lam, const uint64_t* x, uint32_t t) {
   }
   unit_lagrange(lam, x, t);
 }
-// the per-job result of the ratio path: T = sum c_i sig_i (affine) and the GLS digits of M^-1 mod r
-struct ratio_job { g2_aff T; uint64_t d[4]; };
-SSB_FN void unit_combine_ratio_at(ratio_job& out, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
-                                  const int64_t* c, uint32_t t, uint64_t M) {
-  g2_jac acc;
-  combine_small_jac(acc, pts, idx, c, t);
-  jac_to_aff(out.T, acc);
-  uint64_t y[4];
+// ---- the ratio combine, lane-uniform (round 5) -------------------------------------------------
+// sigma = [M^-1 mod r] T, T = sum_i c_i sig_i, for a job whose lambda_i = c_i / M (unit_lagrange_ratio),
+// one lane per job, every lane of a wave on the same schedule (a 64-lane wave runs an addition
+// wherever ANY lane needs one, so per-lane binary / NAF chains cost an addition at nearly every bit):
+//   T      -- regular signed 4-bit windows (Joye-Tunstall: every digit odd, in [-15, 15], so every
+//             window adds a table entry) over the t coefficients JOINTLY: one doubling chain for all
+//             bases, tables of the odd multiples P, 3P, .., 15P of every base;
+//   [k] T  -- k = M^-1 mod r as four base-u GLS digits (psi acts as [x] = [-u] on G2), the same
+//             windows over the four digits jointly, one table of T's odd multiples normalised to
+//             affine (one inversion) and its psi images: 60 doublings + 64 mixed additions for a
+//             255-bit product, where four separate 64-bit binary chains cost 256 + 256.
+// Per 3-of-4 registry job ~6.6k Fp products on ONE lane; the round-4 general combine ran twelve
+// 64-bit binary chains (4 GLS lanes x 3 shares, ~2.9k each) on 16 lanes.  Same group element as
+// blst_p2_mult(sig_i, lambda_i, 255) summed (src/crypto/impls/blst.rs:67-87): compressed bytes equal.
+// Tables live in the caller's memory (device: a per-job region of the slot's workspace, read back
+// with 16-byte loads; they do not fit the registers or a wave's share of LDS): RC_TAB_BYTES per job.
+struct alignas(16) g2_xy { fp2 x, y; };     // affine table entry (a table entry is never infinity)
+constexpr int RC_GROUP = 4;                 // bases per joint pass of T (tables 4 x 8 affine points)
+// the per-job region: 32 affine entries (xy; X, Y of the Jacobian multiples until rc_normalize) | their
+// Z | prefix products of the Z (2P parked there while a table is built)
+constexpr size_t RC_XY_OFF = 0, RC_Z_OFF = 32 * sizeof(g2_xy), RC_PR_OFF = RC_Z_OFF + 32 * sizeof(fp2);
+constexpr size_t RC_TAB_BYTES = RC_PR_OFF + 32 * sizeof(fp2);   // 12,288 B
+static_assert(sizeof(g2_jac) <= 32 * sizeof(fp2), "2P fits the prefix area");
+
+// digit j (0 = least significant) of the regular signed 4-bit recoding of an odd k < 2^(4W), read in
+// any order without storing the recoding: with k_0 = k and k_{j+1} = (k_j - d_j) / 16 = 2 floor(k_j / 32) + 1,
+// the low five bits of k_j are bits 4j+1 .. 4j+4 of k with bit 0 set, d_j = (k_j mod 32) - 16, and the
+// top digit is k_{W-1} itself (odd, <= 15)
+SSB_INL int sw4_digit(uint64_t k, int j, int W) {
+  const uint64_t s = k >> (4 * j);
+  return j == W - 1 ? (int)(s | 1ull) : (int)((s & 30ull) | 1ull) - 16;
+}
+// windows needed for an odd k: the smallest W with k < 2^(4W)
+SSB_INL int sw4_windows(uint64_t k) { return k ? (64 - __builtin_clzll(k) + 3) / 4 : 1; }
+// a += (+-) *qp in place (add-2007-bl, q Jacobian, read from memory where consumed; neg: -q), every
+// special case (either side infinity, doubling, opposite points), few temporaries live
+SSB_INL void jac_add_at(g2_jac& a, const g2_jac* __restrict__ qp, bool neg) {
+  if (fp2_is_zero(qp->z)) return;
+  if (jac_is_inf(a)) { a = *qp; if (neg) fp2_neg(a.y, a.y); return; }
+  fp2 Z1Z1, Z2Z2, U1, S1, H, r;
+  fp2_sqr(Z1Z1, a.z);
+  { const fp2 z2 = qp->z; fp2_sqr(Z2Z2, z2); fp2_mul(S1, a.y, z2); }
+  fp2_mul(S1, S1, Z2Z2);                                                        // Y1 Z2^3
+  fp2_mul(U1, a.x, Z2Z2);                                                       // X1 Z2^2
+  { const fp2 x2 = qp->x; fp2_mul(H, x2, Z1Z1); fp2_sub(H, H, U1); }            // U2 - U1
+  { fp2 y2 = qp->y; if (neg) fp2_neg(y2, y2); fp2_mul(r, y2, a.z); fp2_mul(r, r, Z1Z1); fp2_sub(r, r, S1); }   // S2 - S1
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(r)) jac_dbl(a, a); else jac_set_inf(a);
+    return;
+  }
+  { const fp2 z2 = qp->z; fp2 t; fp2_add(t, a.z, z2); fp2_sqr(t, t); fp2_sub(t, t, Z1Z1); fp2_sub(t, t, Z2Z2); fp2_mul(a.z, t, H); }
+  fp2_dbl(r, r);
+  fp2 I; fp2_dbl(I, H); fp2_sqr(I, I);
+  fp2 J; fp2_mul(J, H, I);
+  fp2 V; fp2_mul(V, U1, I);
+  fp2_sqr(a.x, r); fp2_sub(a.x, a.x, J); { fp2 t; fp2_dbl(t, V); fp2_sub(a.x, a.x, t); }       // r^2 - J - 2V
+  fp2_sub(V, V, a.x); fp2_mul(a.y, r, V); fp2_mul(J, S1, J); fp2_dbl(J, J); fp2_sub(a.y, a.y, J);   // r (V - X3) - 2 S1 J
+}
+// a += (+-) *qp, q affine (madd-2007-bl, the special cases of jac_madd_at)
+SSB_INL void jac_madd_xy(g2_jac& a, const g2_xy* __restrict__ qp, bool neg) {
+  if (jac_is_inf(a)) { a.x = qp->x; a.y = qp->y; if (neg) fp2_neg(a.y, a.y); a.z = fp2_one(); return; }
+  fp2 Z1Z1, r, H;
+  fp2_sqr(Z1Z1, a.z);
+  { fp2 S2, y2 = qp->y; if (neg) fp2_neg(y2, y2); fp2_mul(S2, y2, a.z); fp2_mul(S2, S2, Z1Z1); fp2_sub(r, S2, a.y); }
+  { fp2 U2; const fp2 x2 = qp->x; fp2_mul(U2, x2, Z1Z1); fp2_sub(H, U2, a.x); }
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(r)) jac_dbl(a, a); else jac_set_inf(a);
+    return;
+  }
+  fp2_dbl(r, r);
+  fp2 I;
+  {
+    fp2 HH, t;
+    fp2_sqr(HH, H);
+    fp2_add(t, a.z, H); fp2_sqr(t, t); fp2_sub(t, t, Z1Z1); fp2_sub(a.z, t, HH);
+    fp2_dbl(I, HH); fp2_dbl(I, I);
+  }
+  fp2 V; fp2_mul(V, a.x, I);
+  fp2 J; fp2_mul(J, H, I);
+  fp2 t; fp2_mul(t, a.y, J);
+  fp2_sqr(a.x, r); fp2_sub(a.x, a.x, J); fp2_dbl(J, V); fp2_sub(a.x, a.x, J);
+  fp2_sub(V, V, a.x); fp2_mul(a.y, r, V); fp2_dbl(t, t); fp2_sub(a.y, a.y, t);
+}
+// The chains' group steps, each its own callable function (round 5).  A callable function whose
+// body outgrows the +-128 KB reach of a short branch gets long branches (s_getpc / s_add / s_setpc
+// through a scratch SGPR pair), and this compiler has been seen to take s[30:31] -- the return
+// address -- for them without saving it: the function then "returns" into its own loop and the
+// wave never finishes (rc_k_chain with inlined steps, 608 KB; build.py long_branch_clobbers fails
+// the build on it).  Small out-of-line steps keep every chain loop far inside that reach, and the
+// chains re-run one copy of each step's code instead of streaming megabytes of inlined copies
+// through the instruction cache.
+SSB_FN void rc_madd(g2_jac& a, const g2_xy* __restrict__ qp, bool neg) { jac_madd_xy(a, qp, neg); }
+SSB_FN void rc_add(g2_jac& a, const g2_jac* __restrict__ qp, bool neg) { jac_add_at(a, qp, neg); }
+SSB_FN void rc_dbl4(g2_jac& a) {
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) jac_dbl(a, a);
+}
+// the odd multiples (2e + 1) P, e < 8, of an affine P (not infinity): X, Y into xy[e], Z into zs[e]
+// (Jacobian until rc_normalize; entry 0 is P itself, Z = 1); 2P parked at *p2
+SSB_INL void rc_odd_multiples(g2_xy* __restrict__ xy, fp2* __restrict__ zs, g2_jac* __restrict__ p2, const g2_aff& P) {
+  xy[0].x = P.x; xy[0].y = P.y; zs[0] = fp2_one();
+  g2_jac e;
+  jac_from_aff(e, P);
+  jac_dbl(*p2, e);
+  jac_add_aff(e, *p2, P);                   // 3P
+#pragma unroll 1
+  for (int i = 1; i < 8; ++i) {
+    if (i > 1) rc_add(e, p2, false);
+    xy[i].x = e.x; xy[i].y = e.y; zs[i] = e.z;
+  }
+}
+// entries [0, K) to affine with ONE inversion (Montgomery's trick over their Z)
+SSB_INL void rc_normalize(g2_xy* __restrict__ xy, const fp2* __restrict__ zs, fp2* __restrict__ pr, int K) {
+  {
+    fp2 p = zs[0];
+    pr[0] = p;
+#pragma unroll 1
+    for (int k = 1; k < K; ++k) { const fp2 z = zs[k]; fp2_mul(p, p, z); pr[k] = p; }
+  }
+  fp2 inv; { const fp2 p = pr[K - 1]; fp2_inv(inv, p); }
+#pragma unroll 1
+  for (int k = K - 1; k >= 0; --k) {
+    fp2 zi;
+    if (k > 0) { const fp2 p = pr[k - 1]; fp2_mul(zi, inv, p); const fp2 z = zs[k]; fp2_mul(inv, inv, z); } else zi = inv;
+    fp2 z2, z3;
+    fp2_sqr(z2, zi); fp2_mul(z3, z2, zi);
+    { fp2 x = xy[k].x; fp2_mul(x, x, z2); xy[k].x = x; }
+    { fp2 y = xy[k].y; fp2_mul(y, y, z3); xy[k].y = y; }
+  }
+}
+
+// sum_i [c_i] P_i, P_i = pts[idx[i]] (verified G2 points), |c_i| < 2^62, c_i != 0; W = a window count
+// with every (|c_i| rounded up to odd) < 2^(4W) -- wave-uniform on the device (the caller takes the
+// wave's maximum), so every lane runs the same doublings
+// (T in memory: with more than RC_GROUP bases the groups' sums meet there, not in registers that
+// would stay live across the joint loop)
+SSB_INL void rc_joint_sum(g2_jac* __restrict__ T, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
+                          const int64_t* c, uint32_t t, int W, uint8_t* __restrict__ region) {
+  g2_xy* xy = (g2_xy*)(region + RC_XY_OFF);
+  fp2* zs = (fp2*)(region + RC_Z_OFF);
+  fp2* pr = (fp2*)(region + RC_PR_OFF);
+#pragma unroll 1
+  for (uint32_t g0 = 0; g0 < t; g0 += RC_GROUP) {
+    const uint32_t nb = t - g0 < (uint32_t)RC_GROUP ? t - g0 : (uint32_t)RC_GROUP;
+#pragma unroll 1
+    for (uint32_t b = 0; b < nb; ++b) rc_odd_multiples(xy + 8 * b, zs + 8 * b, (g2_jac*)pr, pts[idx[g0 + b]]);
+    rc_normalize(xy, zs, pr, 8 * (int)nb);
+    g2_jac acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (int j = W - 1; j >= 0; --j) {
+      if (j != W - 1) rc_dbl4(acc);
+#pragma unroll 1
+      for (uint32_t b = 0; b < nb; ++b) {
+        const int64_t cb = c[g0 + b];
+        const uint64_t m = (uint64_t)(cb < 0 ? -cb : cb) | 1ull;   // even |c|: [|c| + 1] P, and P subtracted below
+        const int d = sw4_digit(m, j, W);
+        const int ad = d < 0 ? -d : d;
+        rc_madd(acc, xy + 8 * b + ((ad - 1) >> 1), (d < 0) != (cb < 0));
+      }
+    }
+#pragma unroll 1
+    for (uint32_t b = 0; b < nb; ++b) {     // the even coefficients' correction: - sign(c) P
+      const int64_t cb = c[g0 + b];
+      if (!(((uint64_t)(cb < 0 ? -cb : cb)) & 1ull)) rc_madd(acc, xy + 8 * b, cb > 0);
+    }
+    if (g0) rc_add(acc, T, false);
+    *T = acc;
+  }
+}
+
+// [k] T for k = M^-1 mod r (1 <= M < 2^62, inv_small_mod_r), T in G2 (not infinity): four base-u
+// digits, one table of T's odd multiples (affine) and its signed psi images (digit q's base is
+// (-1)^q psi^q(T), as in unit_gls_term), 16 windows of every digit jointly.  Two steps, out of line,
+// each with its own private frame (one function held both frames' spills at once: 2.3 KB):
+//   rc_k_table: the table (the digits come from rc_digits, run in phase T);
+//   rc_k_chain: the joint chain from the region.
+// the four base-u digits of M^-1 mod r (1 <= M < 2^62)
+SSB_FN void rc_digits(uint64_t* __restrict__ kk, uint64_t M) {
+  uint64_t y[4], d[4];
   inv_small_mod_r(y, M);
-  gls_digits4(out.d, y);
+  gls_digits4(d, y);
+  for (int q = 0; q < 4; ++q) kk[q] = d[q];
+}
+SSB_FN void rc_k_table(const g2_jac* __restrict__ T, uint8_t* __restrict__ region) {
+  g2_xy* xy = (g2_xy*)(region + RC_XY_OFF);
+  fp2* zs = (fp2*)(region + RC_Z_OFF);
+  fp2* pr = (fp2*)(region + RC_PR_OFF);
+  {
+    g2_aff Ta;
+    { const g2_jac Tv = *T; jac_to_aff(Ta, Tv); }
+    rc_odd_multiples(xy, zs, (g2_jac*)pr, Ta);
+  }
+  rc_normalize(xy, zs, pr, 8);
+  // psi images: xy[8 q + i] = (-1)^q psi^q((2i + 1) T)
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    g2_aff p; p.x = xy[i].x; p.y = xy[i].y; p.inf = 0;
+#pragma unroll 1
+    for (int q = 1; q < 4; ++q) {
+      g2_psi_aff(p, p);
+      g2_xy o; o.x = p.x; o.y = p.y;
+      if (q & 1) fp2_neg(o.y, o.y);
+      xy[8 * q + i] = o;
+    }
+  }
+}
+SSB_FN void rc_k_chain(g2_jac& R, const uint8_t* __restrict__ region, const uint64_t* __restrict__ kd) {
+  const g2_xy* xy = (const g2_xy*)(region + RC_XY_OFF);
+  uint64_t kk[4];
+  for (int q = 0; q < 4; ++q) kk[q] = kd[q];
+  g2_jac acc;
+  jac_set_inf(acc);
+#pragma unroll 1
+  for (int j = 15; j >= 0; --j) {
+    if (j != 15) rc_dbl4(acc);
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+      const int d = sw4_digit(kk[q] | 1ull, j, 16);   // an even digit: d + 1, and the base subtracted below
+      const int ad = d < 0 ? -d : d;
+      rc_madd(acc, xy + 8 * q + ((ad - 1) >> 1), d < 0);
+    }
+  }
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q)
+    if (!(kk[q] & 1ull)) rc_madd(acc, xy + 8 * q, true);
+  R = acc;
+}
+
+// The ratio combine in two phases, one per launch (k_combine_terms_gls' extra blocks run phase T,
+// k_combine_sum's lanes of fast-2 jobs phase K), every step out of line so that no kernel holds two
+// steps' private frames at once.  Phase T: T = sum c_i sig_i into *T and the digits of M^-1 into kk.
+// Phase K: [M^-1] T, compressed into out96 (infinity when T is).
+SSB_FN void unit_ratio_T(g2_jac* __restrict__ T, uint64_t* __restrict__ kk, const g2_aff* __restrict__ pts,
+                         const uint32_t* __restrict__ idx, const int64_t* c, uint32_t t, uint64_t M, int W,
+                         uint8_t* __restrict__ region) {
+  rc_joint_sum(T, pts, idx, c, t, W, region);
+  rc_digits(kk, M);
+}
+SSB_FN void rc_k_finish(uint8_t* out96, const uint8_t* __restrict__ region, const uint64_t* __restrict__ kk) {
+  g2_jac R;
+  rc_k_chain(R, region, kk);
+  g2_aff a; jac_to_aff(a, R);
+  g2_compress(out96, a);
+}
+SSB_INL void unit_ratio_K(uint8_t* out96, const g2_jac* __restrict__ T, const uint64_t* __restrict__ kk,
+                          uint8_t* __restrict__ region) {
+  if (fp2_is_zero(T->z)) {   // T = O (e.g. a zero master key): the combination is infinity
+    out96[0] = 0xc0;
+    for (int i = 1; i < 96; ++i) out96[i] = 0;
+    return;
+  }
+  rc_k_table(T, region);
+  rc_k_finish(out96, region, kk);
+}
+// the whole ratio combine of one job into out96 (host tests; the device runs the two phases)
+SSB_INL void unit_combine_ratio_w4(uint8_t* out96, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
+                                   const int64_t* c, uint32_t t, uint64_t M, int W, uint8_t* __restrict__ region) {
+  g2_jac T;
+  uint64_t kk[4];
+  unit_ratio_T(&T, kk, pts, idx, c, t, M, W, region);
+  unit_ratio_K(out96, &T, kk, region);
+}
+// the window count T's coefficients need (before the wave-wide maximum)
+SSB_INL int rc_windows(const int64_t* c, uint32_t t) {
+  int W = 1;
+  for (uint32_t i = 0; i < t; ++i) {
+    const int w = sw4_windows((uint64_t)(c[i] < 0 ? -c[i] : c[i]) | 1ull);
+    W = w > W ? w : W;
+  }
+  return W;
 }
 
 }  // namespace ssb

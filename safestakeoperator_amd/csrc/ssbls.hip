@@ -80,7 +80,14 @@ struct ssb_slot {
 constexpr int SSB_MAX_SLOTS = 24;
 
 struct ssb_ctx {
+  // Every entry point holds this for its whole call (SSB_LOCK): one context may be shared by the
+  // threads of a process -- the collector's worker, a ThresholdSignature caller, registration --
+  // and their calls are serialised (recursive: entry points call entry points)
+  std::recursive_mutex mu;
   int device = 0;
+  // hardware queues the HIP runtime gives this process (GPU_MAX_HW_QUEUES, read by HIP when it
+  // initialises; HIP's default is 4): ssb_set_pipeline_depth refuses more slot streams than fit
+  int hw_queues = 4;
   ssb_slot sl[SSB_MAX_SLOTS];
   int nslots = 1, next = 0, slot_streams = 3;
   ssb_slot* cur = &sl[0];           // the slot the current call runs on
@@ -100,6 +107,9 @@ struct ssb_ctx {
   // (the kernels with the largest private segments stay off the slots' queues).  One-stream slots
   // run every stage on the slot's own stream and leave both idle.
   hipStream_t spec = nullptr, tail = nullptr;
+  // key registration (pkc_fill): its own stream, so registering a key waits for the key's decode
+  // only, not for the batches queued on a slot
+  hipStream_t reg = nullptr;
   // decoded public keys (ssb_pk_cache_set / ssb_pk_cache_add): affine points + DEC_* flags, indexed
   // by the caller; rows [0, pkc_n) are live, the arrays hold pkc_cap rows
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0, pkc_cap = 0;
@@ -126,6 +136,8 @@ namespace {
       return SSB_EHIP;                                                                \
     }                                                                                 \
   } while (0)
+
+#define SSB_LOCK(ctx) std::lock_guard<std::recursive_mutex> ssb_lock_((ctx)->mu)
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 const fp12 FP12_ONE_HOST = fp12_one();
@@ -657,6 +669,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
 
 namespace ssb {
 int ctx_device(const ssb_ctx* ctx) { return ctx->device; }   // (ssb_collector.hip)
+std::recursive_mutex& ctx_mutex(ssb_ctx* ctx) { return ctx->mu; }
 }
 
 extern "C" {
@@ -671,9 +684,11 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   ssb_ctx* ctx = new (std::nothrow) ssb_ctx();
   if (!ctx) return SSB_ENOMEM;
   ctx->device = device_ordinal;
+  ctx->hw_queues = ssb_hw_queue_budget();
   if (init_slot(ctx->sl[0], ctx->slot_streams) != SSB_OK) { delete ctx; return SSB_EHIP; }
   if (hipStreamCreateWithFlags(&ctx->spec, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
+      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->reg, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
@@ -700,7 +715,7 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
   if (ctx->pkc_pow) hipFree(ctx->pkc_pow);
   if (ctx->pkc_stage) hipFree(ctx->pkc_stage);
-  for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
+  for (hipStream_t x : {ctx->spec, ctx->tail, ctx->reg}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx, ctx->sl[i]);
   delete ctx;
 }
@@ -714,12 +729,34 @@ int ssb_check_pipeline_config(int depth, int streams) {
   return SSB_OK;
 }
 
+int ssb_hw_queue_budget(void) {
+  const char* v = getenv("GPU_MAX_HW_QUEUES");
+  const int q = v ? atoi(v) : 0;
+  return q > 0 ? q : 4;   // HIP's default
+}
+
+namespace {
+// slot streams beyond the process's hardware queues share queues: independent batches then
+// serialise behind each other (round 2: 21 active queues on 20 measured 6.5 M against 9.3 M), so
+// such a configuration is refused with the reason instead of running silently slower
+int check_queue_budget(ssb_ctx* ctx, int depth, int streams) {
+  if (depth * streams <= ctx->hw_queues - 1) return SSB_OK;   // one queue left for the caller's stream
+  ctx->err = "pipeline depth " + std::to_string(depth) + " x " + std::to_string(streams) +
+             " streams per slot needs " + std::to_string(depth * streams + 1) +
+             " hardware queues, but this process has GPU_MAX_HW_QUEUES=" + std::to_string(ctx->hw_queues) +
+             " (HIP's default is 4; set GPU_MAX_HW_QUEUES, at most 32, in the environment before the first HIP call)";
+  return SSB_EINVAL;
+}
+}  // namespace
+
 int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (ssb_check_pipeline_config(depth, ctx->slot_streams) != SSB_OK) {
     ctx->err = "pipeline depth x streams per slot outside the supported range (one-stream slots: depth 1..20; three-stream slots: depth 1..5)";
     return SSB_EINVAL;
   }
+  if (int rc = check_queue_budget(ctx, depth, ctx->slot_streams)) return rc;
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = ctx->nslots; i < depth; ++i) {
     if (init_slot(ctx->sl[i], ctx->slot_streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
@@ -735,10 +772,12 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
 
 int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (ssb_check_pipeline_config(ctx->nslots, streams) != SSB_OK) {
     ctx->err = "streams per slot must be 1 or 3, and three-stream slots at most 5 (lower the depth first)";
     return SSB_EINVAL;
   }
+  if (int rc = check_queue_budget(ctx, ctx->nslots, streams)) return rc;
   if (streams == ctx->slot_streams) return SSB_OK;
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = 0; i < ctx->nslots; ++i) { sync_slot(ctx, ctx->sl[i]); free_slot(ctx, ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
@@ -752,6 +791,7 @@ int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
 
 int ssb_set_rlc_deterministic(ssb_ctx* ctx, int on) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   ctx->rlc_deterministic = on != 0;
   return SSB_OK;
 }
@@ -763,7 +803,9 @@ int ssb_debug_hold(void* stream, const uint32_t* flag, uint32_t max_us) {
 }
 
 void* ssb_slot_stream(ssb_ctx* ctx, int slot) {
-  if (!ctx || slot < 0 || slot >= ctx->nslots) return nullptr;
+  if (!ctx) return nullptr;
+  SSB_LOCK(ctx);
+  if (slot < 0 || slot >= ctx->nslots) return nullptr;
   return (void*)ctx->sl[slot].stream;
 }
 
@@ -772,6 +814,7 @@ const char* ssb_last_error(const ssb_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int ssb_last_kernel_ms(const ssb_ctx* ctx_c, const char* name, float* ms) {
   ssb_ctx* ctx = const_cast<ssb_ctx*>(ctx_c);
   if (!ctx || !name || !ms) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   auto it = ctx->timers.find(name);
   if (it == ctx->timers.end() || !it->second.used) { ctx->err = "no timing for kernel"; return SSB_EINVAL; }
   SSB_HIP(hipEventSynchronize(it->second.b));
@@ -781,6 +824,7 @@ int ssb_last_kernel_ms(const ssb_ctx* ctx_c, const char* name, float* ms) {
 
 int ssb_kernel_timing(ssb_ctx* ctx, int on) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   for (int i = 0; i < ctx->nslots; ++i) sync_slot(ctx, ctx->sl[i]);
   for (auto& kv : ctx->history) for (auto& p : kv.second) ctx->pool.push_back(p);
   ctx->history.clear();
@@ -791,6 +835,7 @@ int ssb_kernel_timing(ssb_ctx* ctx, int on) {
 
 int ssb_kernel_time(ssb_ctx* ctx, const char* name, float* total_ms, int* launches) {
   if (!ctx || !name || !total_ms || !launches) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   *total_ms = 0.f; *launches = 0;
   auto it = ctx->history.find(name);
   if (it == ctx->history.end()) return SSB_OK;
@@ -807,6 +852,7 @@ namespace {
 int hash_to_g2_impl(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* lens, const uint8_t* dst, size_t dst_len,
                     uint8_t* out192) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!msgs32 || !out192) { ctx->err = "null pointer"; return SSB_EINVAL; }
   if (lens)
@@ -843,6 +889,7 @@ int ssb_hash_to_g2_msgs(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uin
 int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* commitments48, const uint64_t* ids,
                              const uint8_t* shares32, const uint8_t* h48, uint8_t* verdicts) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!commitments48 || !ids || !shares32 || !h48 || !verdicts || t == 0 || t > 1024 || n > (size_t)INT32_MAX) {
     ctx->err = "null pointer, t not in [1, 1024] or n too large"; return SSB_EINVAL;
@@ -871,6 +918,7 @@ int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* co
 int ssb_dleq_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* points48, const uint8_t* c32, const uint8_t* r32,
                           uint8_t* verdicts) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!points48 || !c32 || !r32 || !verdicts || n > (size_t)INT32_MAX) { ctx->err = "null pointer or n too large"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
@@ -893,6 +941,7 @@ int ssb_dleq_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* points48, const
 int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status,
                              void* stream) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!wire || !out96 || !status || stride < launch::WIRE_SIG_BYTES || n > (size_t)INT32_MAX) {
     ctx->err = "null pointer, stride < 202 or n too large"; return SSB_EINVAL;
@@ -905,6 +954,7 @@ int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t
 
 int ssb_decode_wire_sigs(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!wire || !out96 || !status || stride < launch::WIRE_SIG_BYTES || n > (size_t)INT32_MAX) {
     ctx->err = "null pointer, stride < 202 or n too large"; return SSB_EINVAL;
@@ -928,6 +978,7 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
                      size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
                      uint8_t* verdicts) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!pk48 || !sig96 || !root_idx || !roots32 || !verdicts || n_roots == 0) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
   for (size_t i = 0; i < n; ++i) if (root_idx[i] >= n_roots) { ctx->err = "root_idx out of range"; return SSB_EINVAL; }
@@ -956,22 +1007,31 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
 
 namespace {
 // the body of the _dev entry points: public keys compressed (pk48) or from the cache (pk_index)
+// (wire != nullptr: the shares arrive as wire records -- record i at wire + i * stride -- and sig96 is
+// unused; wire_status receives each record's status, and a share whose record does not deserialize
+// is absent from its job, as the reference drops it: select_job)
 int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* share_off,
                   const uint32_t* t, const uint8_t* sig96, const uint8_t* pk48, const uint32_t* pk_index,
                   const uint64_t* ids, const uint32_t* job_root, size_t n_roots, const uint8_t* roots32,
                   const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
-                  int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, void* stream) {
+                  int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, void* stream,
+                  const uint8_t* wire = nullptr, size_t stride = 0, int32_t* wire_status = nullptr) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n_jobs == 0) return SSB_OK;
   if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0 ||
-      (n_shares && (!sig96 || !(pk48 || pk_index) || !ids))) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
+      (n_shares && (!(sig96 || wire) || !(pk48 || pk_index) || !ids))) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
+  if (wire && (!wire_status || stride < launch::WIRE_SIG_BYTES || n_shares > (size_t)INT32_MAX)) {
+    ctx->err = "wire records: null status, stride < 202 or too many shares"; return SSB_EINVAL;
+  }
   if (pk_index && !ctx->pkc_aff) { ctx->err = "no public-key cache (ssb_pk_cache_set)"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
   pick_slot(ctx, stream);           // pipeline slot: batches on different slots overlap
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   const size_t n = n_shares;
   size_t need = verify_ws_bytes(n, n_roots) + align_up(n * 4) * 3 + align_up(n) + align_up(n * sizeof(fr)) +
-                align_up(4 * n * sizeof(g2_jac)) + align_up(n_jobs * 4) + align_up(n_jobs * sizeof(ratio_job));
+                align_up(4 * n * sizeof(g2_jac)) + align_up(n_jobs * 4) + align_up(n_jobs * RC_TAB_BYTES) + align_up(n_jobs * sizeof(g2_jac)) + align_up(32 * n_jobs) +
+                (wire ? align_up(n * 96) : 0);
   if ((rc = ensure_ws(ctx, need, true))) return rc;
   hipStream_t user = (hipStream_t)stream;
   const bool on_slot = post_on_slot(ctx->cur);
@@ -991,10 +1051,21 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   fr* lam = c.take<fr>(n);
   g2_jac* term = c.take<g2_jac>(4 * n);     // k_combine_terms_gls: four digit terms per share
   uint32_t* fast = c.take<uint32_t>(n_jobs);
-  // registry ids: by default the general combine with the ratio form's cheap lambda_i
-  // (unit_lagrange_fast) and four GLS lanes per share, which fills the chip; SSB_RATIO=1 takes
-  // [M^-1](sum c_i sig_i) instead (one lane per job for the sum: 3.11 vs 3.32 M partial sigs/s, round 4)
-  ratio_job* rjb = getenv("SSB_RATIO") ? c.take<ratio_job>(n_jobs) : nullptr;
+  // jobs whose lambda_i are ratios of small integers (registry ids; ids 1..n with a share skipped):
+  // [M^-1](sum c_i sig_i) on one lane per job, lane-uniform windows (k_combine_ratio); SSB_NO_RATIO=1
+  // sends them to the general combine (lambda_i by unit_lagrange_fast, four GLS lanes per share)
+  const uint32_t ratio = getenv("SSB_NO_RATIO") ? 0u : 1u;
+  uint8_t* rtab = c.take<uint8_t>(n_jobs * RC_TAB_BYTES);
+  g2_jac* rT = c.take<g2_jac>(n_jobs);
+  uint64_t* rk = c.take<uint64_t>(4 * n_jobs);
+  // the ratio combine rides in the terms launch (phase T: its blocks past nbt) and the sum launch (phase K)
+  const unsigned nbt = nblk(4 * n, 64), nbr = nblk(n_jobs, 64);
+  const ratio_args ra{ids, rtab, ratio ? rT : nullptr, rk, nbt};
+  if (wire && n) {   // the records' hex -> the 96-byte compressed form, first on the slot's stream
+    uint8_t* sig_ws = c.take<uint8_t>(n * 96);
+    { timed tm(ctx, "k_wire_sig", st); launch::wire_sig(st, (int)n, wire, stride, sig_ws, wire_status, 0); }
+    sig96 = sig_ws;
+  }
   // share -> (job, root): in the decode launch on the fused path, else a launch of its own
   const bool fmap = fused_sort_path(ctx->cur, n, n_roots, pre);
   const job_map jm{(int)n_jobs, (uint32_t)n, share_off, t, job_root, share_job, share_root};
@@ -1006,14 +1077,14 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     { timed tm(ctx, "k_combine_fast", sc);   // select + small-integer combine + Lagrange, one launch
       hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, (uint32_t)n, share_off, t, ids,
                          (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err, w.sig_aff, fast,
-                         out_sig96, lam, rjb); }
-    if (n) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, sc, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term, (const ratio_job*)rjb); }
-    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4); }
+                         out_sig96, lam, ratio, wire ? wire_status : (int32_t*)nullptr); }
+    if (nbt + (ratio ? nbr : 0)) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nbt + (ratio ? nbr : 0)), dim3(64), 0, sc, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term, ra); }
+    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4, (const uint32_t*)sel, ra); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
   // one-stream slots: the speculative pass rides in the window-sum launch (msm_both), no stream
   const spec_jobs sj{(int)n_jobs, (uint32_t)n, share_off, t, ids, w.flags, sel, out_status, out_err, w.sig_aff, fast,
-                     out_sig96, lam, rjb};
+                     out_sig96, lam, ratio, wire ? wire_status : nullptr};
   bool spec_in_window = false;
   if ((rc = run_verify(ctx, w, n, n_roots, sig96, pk48, pk_index, share_root, roots32, d, rlc_seed, verdict,
                        [&] { if (!on_slot) spec(); }, tl, on_slot ? &sj : nullptr, &spec_in_window, fmap ? &jm : nullptr)))
@@ -1028,16 +1099,22 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   if (on_slot) {
     timed tm(ctx, "k_combine_fast", st);
     hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids,
-                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam, rjb);
+                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam, ratio,
+                       wire ? wire_status : (int32_t*)nullptr);
   } else {
     hipLaunchKernelGGL(k_select_combine, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, (uint32_t)n, share_off, t, ids,
-                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam, rjb);
+                       (const uint8_t*)verdict, w.flags, gate, sel, out_status, out_err, w.sig_aff, fast, out_sig96, lam, ratio,
+                       wire ? wire_status : (int32_t*)nullptr);
   }
   // (after a speculative pass in the window launch the general combine of the jobs the small-
   // integer path did not finish still follows here, on whichever selection stands)
   const uint32_t* gate2 = spec_in_window ? nullptr : gate;
-  if (n) hipLaunchKernelGGL(k_combine_terms_gls, dim3(nblk(4 * n, 64)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term, (const ratio_job*)rjb);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate2, (const uint32_t*)fast, out_sig96, 4);
+  if (nbt + (ratio ? nbr : 0)) {
+    timed tm(ctx, "k_combine_terms", st);
+    hipLaunchKernelGGL(k_combine_terms_gls, dim3(nbt + (ratio ? nbr : 0)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term, ra);
+  }
+  { timed tm(ctx, "k_combine_sum", st);
+    hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate2, (const uint32_t*)fast, out_sig96, 4, (const uint32_t*)sel, ra); }
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
   ctx->cur->out_pending = true;
@@ -1052,6 +1129,7 @@ int verify_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint32_t* pk_i
                const uint32_t* root_idx, size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
                uint64_t rlc_seed, uint8_t* verdicts, void* stream) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!(pk48 || pk_index) || !sig96 || !root_idx || !roots32 || !verdicts || n_roots == 0) {
     ctx->err = "null pointer or no roots"; return SSB_EINVAL;
@@ -1103,6 +1181,18 @@ int ssb_threshold_aggregate_batch_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t
   return aggregate_dev(ctx, n_jobs, n_shares, share_off, t, sig96, nullptr, pk_index, ids, job_root, n_roots, roots32, dst,
                        dst_len, rlc_seed, out_sig96, out_status, out_err, share_verdicts, stream);
 }
+int ssb_threshold_aggregate_batch_wire_cached_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* share_off,
+                                                  const uint32_t* t, const uint8_t* wire, size_t stride,
+                                                  const uint32_t* pk_index, const uint64_t* ids, const uint32_t* job_root,
+                                                  size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len,
+                                                  uint64_t rlc_seed, uint8_t* out_sig96, int32_t* out_status,
+                                                  uint64_t* out_err, uint8_t* share_verdicts, int32_t* share_wire_status,
+                                                  void* stream) {
+  if (ctx && n_shares && (!pk_index || !wire)) { ctx->err = "null pk_index or wire"; return SSB_EINVAL; }
+  return aggregate_dev(ctx, n_jobs, n_shares, share_off, t, nullptr, nullptr, pk_index, ids, job_root, n_roots, roots32, dst,
+                       dst_len, rlc_seed, out_sig96, out_status, out_err, share_verdicts, stream, wire, stride,
+                       share_wire_status);
+}
 
 int ssb_verify_batch_dev(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t* sig96, const uint32_t* root_idx,
                          size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
@@ -1149,7 +1239,7 @@ int pkc_reserve(ssb_ctx* ctx, size_t need) {
   // the precomputed bases of the batch path's merged G1 MSM (plan_msm g1_pre): registration-time
   // work, like the decompression; without them (allocation failed) batches use the windowed G1 MSM
   if (hipMalloc(&p, cap * PKPOW_W * sizeof(g1_aff)) != hipSuccess) { p = nullptr; (void)hipGetLastError(); }
-  hipStream_t st = ctx->sl[0].stream;
+  hipStream_t st = ctx->reg;
   const size_t n = ctx->pkc_n;
   if (n) {
     SSB_HIP(hipMemcpyAsync(a, ctx->pkc_aff, n * sizeof(g1_aff), hipMemcpyDeviceToDevice, st));
@@ -1176,7 +1266,7 @@ int pkc_fill(ssb_ctx* ctx, size_t row, size_t n, const uint8_t* pk48) {
     if (hipMalloc(&ctx->pkc_stage, want) != hipSuccess) { ctx->pkc_stage = nullptr; ctx->err = "hipMalloc key staging failed"; return SSB_ENOMEM; }
     ctx->pkc_stage_bytes = want;
   }
-  hipStream_t st = ctx->sl[0].stream;
+  hipStream_t st = ctx->reg;
   SSB_HIP(hipMemcpyAsync(ctx->pkc_stage, pk48, n * 48, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_decode_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const uint8_t*)ctx->pkc_stage,
                      ctx->pkc_aff + row, ctx->pkc_flags + row);
@@ -1192,6 +1282,7 @@ extern "C" {
 
 int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n && !pk48) { ctx->err = "null pk48"; return SSB_EINVAL; }
   if (n > (size_t)UINT32_MAX) { ctx->err = "too many keys"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
@@ -1213,6 +1304,7 @@ int ssb_pk_cache_set(ssb_ctx* ctx, size_t n, const uint8_t* pk48) {
 
 int ssb_pk_cache_add(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint32_t* out_index) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!pk48 || !out_index) { ctx->err = "null pointer"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
@@ -1257,6 +1349,7 @@ int submit_impl(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const ui
                 const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed, uint8_t* out_sig96,
                 int32_t* out_status, uint64_t* out_err, uint8_t* share_verdicts, uint64_t* ticket) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (ticket) *ticket = 0;
   if (n_jobs == 0) return SSB_OK;
   if (!share_off || !t || !job_root || !roots32 || !out_sig96 || !out_status || !out_err || n_roots == 0 || !ticket) {
@@ -1340,6 +1433,7 @@ int ssb_threshold_aggregate_batch_cached_submit(ssb_ctx* ctx, size_t n_jobs, con
 
 int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (ticket == 0) return SSB_OK;
   const int k = (int)(ticket & 0xff);
   // only generations never issued are unknown; any issued ticket that no live slot holds was
@@ -1372,6 +1466,7 @@ int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* s
 int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint8_t* sig96,
                                const uint64_t* ids, uint8_t* out_sig96, int32_t* out_status) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n_jobs == 0) return SSB_OK;
   if (!share_off || !out_sig96 || !out_status) { ctx->err = "null pointer"; return SSB_EINVAL; }
   if (share_off[0] != 0) { ctx->err = "share_off[0] must be 0"; return SSB_EINVAL; }
@@ -1407,7 +1502,7 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   // unsafe_aggregate does not subgroup-check its inputs (blst.rs:77-84): always the exact 255-bit path
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, (const uint32_t*)nullptr, (const uint32_t*)nullptr, lam);
   if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, (const uint32_t*)nullptr, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out, 1);
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out, 1, (const uint32_t*)nullptr, ratio_args{nullptr, nullptr, nullptr, nullptr, 0u});
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
@@ -1418,6 +1513,7 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
 int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t* root_idx, size_t n_roots,
                    const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint8_t* out_sig96) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!sk32le || !root_idx || !roots32 || !out_sig96 || n_roots == 0) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
   for (size_t i = 0; i < n; ++i) if (root_idx[i] >= n_roots) { ctx->err = "root_idx out of range"; return SSB_EINVAL; }
@@ -1444,6 +1540,7 @@ int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t
 
 int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* out_pk48) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!sk32le || !out_pk48) { ctx->err = "null pointer"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
@@ -1463,6 +1560,7 @@ int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* o
 
 int ssb_pk_validate_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint8_t* out_valid, uint8_t* out_pk48) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!pk48 || !out_valid || !out_pk48 || n > (size_t)INT32_MAX) { ctx->err = "null pointer or n too large"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
@@ -1482,6 +1580,7 @@ int ssb_pk_validate_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint8_t* 
 
 int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* out32) {
   if (!ctx) return SSB_EINVAL;
+  SSB_LOCK(ctx);
   if (t == 0) return SSB_OK;
   if (!ids || !out32 || t > SSB_MAX_T) { ctx->err = "bad arguments"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));

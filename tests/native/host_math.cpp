@@ -366,13 +366,30 @@ int main() {
       uint8_t a[96], b[96]; unit_combine_sum(a, terms.data(), (uint32_t)t);
       int same = -1;
       if (elig) {
-        ratio_job rj; unit_combine_ratio_at(rj, P.data(), idx.data(), c.data(), (uint32_t)t, M);
-        g2_jac q4[4];
-        for (int q = 0; q < 4; ++q) unit_gls_term(q4[q], rj.T, rj.d[q], q);
-        unit_combine_sum(b, q4, 4);
+        // the lane-uniform windowed combine (k_combine_ratio), at the job's own window count and at a
+        // wider one (the wave's maximum on the device), with the table region in host memory
+        std::vector<uint8_t> region(RC_TAB_BYTES);
+        const int W = rc_windows(c.data(), (uint32_t)t);
+        unit_combine_ratio_w4(b, P.data(), idx.data(), c.data(), (uint32_t)t, M, W, region.data());
         same = memcmp(a, b, 96) == 0;
+        unit_combine_ratio_w4(b, P.data(), idx.data(), c.data(), (uint32_t)t, M, 16, region.data());
+        same = same && memcmp(a, b, 96) == 0;
       }
       printf("%d %d %llu\n", elig ? 1 : 0, same, (unsigned long long)M);
+    } else if (cmd == "ratiozero") {  // ratiozero t id1 .. idt: P_i = [x_i] P, so T = sum c_i x_i P = O -> infinity
+      int t; is >> t; std::vector<uint64_t> ids(t); for (int i = 0; i < t; ++i) is >> ids[i];
+      g2_aff H; { uint8_t m[32] = {0}; m[0] = 0x33; hash_to_g2(H, m, (const uint8_t*)DST, (int)strlen(DST)); }
+      std::vector<g2_aff> P(t); std::vector<uint32_t> idx(t);
+      for (int i = 0; i < t; ++i) {
+        const uint32_t kw[2] = {(uint32_t)ids[i], (uint32_t)(ids[i] >> 32)};
+        g2_jac r; jac_mul_aff(r, H, kw, 2); jac_to_aff(P[i], r); idx[i] = (uint32_t)i;
+      }
+      std::vector<int64_t> c(t); uint64_t M = 0;
+      const bool elig = unit_lagrange_ratio(c.data(), &M, ids.data(), (uint32_t)t);
+      uint8_t b[96] = {0};
+      std::vector<uint8_t> region(RC_TAB_BYTES);
+      if (elig) unit_combine_ratio_w4(b, P.data(), idx.data(), c.data(), (uint32_t)t, M, rc_windows(c.data(), (uint32_t)t), region.data());
+      printf("%d %s\n", elig ? 1 : 0, hex(b, 96).c_str());
     } else if (cmd == "lagfast") {  // lagfast t id1 .. idt : unit_lagrange_fast's lambda_i (canonical hex, one per share)
       int t; is >> t; std::vector<uint64_t> ids(t); for (int i = 0; i < t; ++i) is >> ids[i];
       std::vector<fr> lam(t);

@@ -134,3 +134,136 @@ def test_slot_collector_native_golden_concurrent(eng):
             pl = c["expected_payload"]
             assert r == _error_from(c["expected_status"], pl[0], pl[1] if len(pl) > 1 else 0), c["name"]
     assert len(out) == 16 * len(cases)
+
+
+def _wire_case(eng):
+    """A 3-of-4 batch whose shares travel as wire records (bincode(bls::Signature)), with records that
+    do not deserialize -- the reference drops such a share before threshold_aggregate
+    (RemoteOperator::sign, src/validation/operator.rs:108-131, and `.flatten()`, hotstuff.rs:150-155).
+    Returns the workload, the records, their per-share lengths, and the expected (present) shares."""
+    from safestakeoperator_amd.collector import wire_records
+    V, t, n, R = 1024, 3, 4, 16
+    wl = bench.make_workload(eng, V, t, n, R, rank=31)
+    wl2 = bench.make_workload(eng, V, t, n, R, rank=31, invalid_rate=1.0)   # every share over the next root
+    rec = bytearray(wire_records(wl["sigs"]))
+    lens = [202] * (V * n)
+    absent = set()
+
+    def put(s, b):
+        rec[202 * s:202 * s + 202] = b
+
+    def r(s):
+        return bytes(rec[202 * s:202 * s + 202])
+    put(3 * n + 1, (195).to_bytes(8, "little") + r(3 * n + 1)[8:]); absent.add(3 * n + 1)          # length field
+    put(5 * n + 0, r(5 * n)[:8] + b"1x" + r(5 * n)[10:]); absent.add(5 * n)                          # prefix
+    put(5 * n + 2, r(5 * n + 2)[:40] + b"zz" + r(5 * n + 2)[42:]); absent.add(5 * n + 2)             # hex digit
+    put(7 * n + 1, r(7 * n + 1)[:10] + b"9f" + b"ff" * 47 + r(7 * n + 1)[106:]); absent.add(7 * n + 1)   # x.c1 >= p
+    put(9 * n + 0, r(9 * n)[:10] + b"00" + r(9 * n)[12:]); absent.add(9 * n)                         # no compression flag
+    sigs = bytearray(wl["sigs"])
+    sigs[96 * (9 * n + 1):96 * (9 * n + 2)] = wl2["sigs"][96 * (9 * n + 1):96 * (9 * n + 2)]       # present, invalid
+    put(9 * n + 1, wire_records(bytes(sigs[96 * (9 * n + 1):96 * (9 * n + 2)])))
+    lens[11 * n + 3] = 150; absent.add(11 * n + 3)                                                  # truncated record
+    inf = b"\xc0" + b"\x00" * 95
+    sigs[96 * (13 * n + 2):96 * (13 * n + 3)] = inf                                                 # infinity: present, invalid
+    put(13 * n + 2, wire_records(inf))
+    up = r(15 * n + 1)
+    put(15 * n + 1, up[:10] + up[10:].upper())                                                      # upper-case hex parses
+    for k in range(40, 1024, 97):                                                                   # scattered drops
+        s = k * n + (k % n)
+        put(s, (0).to_bytes(8, "little") + r(s)[8:]); absent.add(s)
+    wl["sigs"] = bytes(sigs)
+    # the reference's view: each job's PRESENT shares, in order
+    off, sg, pk, ids = [0], b"", b"", []
+    for v in range(V):
+        for i in range(n):
+            s = v * n + i
+            if s in absent:
+                continue
+            sg += wl["sigs"][96 * s:96 * s + 96]; pk += wl["pks"][48 * s:48 * s + 48]; ids.append(wl["ids"][s])
+        off.append(len(ids))
+    o_out, o_st, o_err, o_ver = bls_c.threshold_batch(off, [t] * V, sg, pk, ids, wl["job_root"], wl["roots"], 16,
+                                                      verify_all=True)
+    ver = np.zeros(V * n, dtype=np.uint8)
+    keep = [s for s in range(V * n) if s not in absent]
+    ver[keep] = o_ver[:len(keep)]
+    assert o_st[5] == 2 and tuple(o_err[5]) == (2, 3)          # InsufficientSignatures{got: 2, expected: 3}
+    assert o_st[9] == 4 and tuple(o_err[9]) == (2, 3)          # InsufficientValidSignatures{got: 2, expected: 3}
+    return wl, bytes(rec), lens, absent, (o_out, o_st, o_err, ver), (V, t, n, R)
+
+
+def test_wire_collector_drops_undecodable_shares(eng):
+    """A wire collector (ssb_collector_create2(.., SSB_COLLECTOR_WIRE)): jobs submitted as the records
+    operators send (ssb_collector_submit_wire), decoded on the device.  A record that does not
+    deserialize -- bad length field, prefix, hex digit, x >= p, no compression flag, truncated -- makes
+    its share ABSENT: two absent shares of a 3-of-4 job give the reference's InsufficientSignatures
+    {got: 2, expected: 3}, not an invalid-share error; the absent bits say which.  Every status, error
+    field, verdict and combined signature == the C oracle on each job's present shares."""
+    from safestakeoperator_amd import _lib
+    wl, rec, lens, absent, (o_out, o_st, o_err, o_ver), (V, t, n, R) = _wire_case(eng)
+    col = NativeCollector(eng, max_jobs=256, window_s=0.002, in_flight=3, wire=True)
+    try:
+        rows = col.rows(wl["share_pks"])
+        res = [_lib.JobResult() for _ in range(V)]
+        keep = []
+        for v in range(V):
+            recs = [rec[202 * (v * n + i):202 * (v * n + i) + lens[v * n + i]] for i in range(n)]
+            r_ = np.ascontiguousarray(rows[v * n:(v + 1) * n], dtype=np.uint32)
+            ids = np.asarray(wl["ids"][v * n:(v + 1) * n], dtype=np.uint64)
+            keep.append((r_, ids))
+            col.submit_wire(t, recs, r_, ids, wl["roots"][wl["job_root"][v]], res[v])
+        col.flush()
+    finally:
+        col.close()
+    for v in range(V):
+        r = res[v]
+        assert r.done == 1 and r.rc == 0
+        assert r.status == o_st[v] and (r.err[0], r.err[1]) == (o_err[v][0], o_err[v][1]), v
+        if r.status == 0:
+            assert bytes(r.sig96) == o_out[v].tobytes(), v
+        want_abs = sum(1 << i for i in range(n) if v * n + i in absent)
+        assert r.absent == want_abs, v
+        want_ver = sum(int(o_ver[v * n + i]) << i for i in range(n))
+        assert r.verdicts == want_ver, v
+
+
+def test_wire_aggregate_entry_point(eng):
+    """ssb_threshold_aggregate_batch_wire_cached_dev (one batch, device buffers): the same records,
+    statuses per share (1 length, 2 prefix, 3 hex, 4 not a point), the same results as the oracle."""
+    import torch
+    from safestakeoperator_amd import DST, _lib
+    wl, rec, lens, absent, (o_out, o_st, o_err, o_ver), (V, t, n, R) = _wire_case(eng)
+    rec = bytearray(rec)
+    for s, l in enumerate(lens):
+        if l != 202:
+            rec[202 * s:202 * s + 8] = (0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")   # what the collector stores
+    N = V * n
+    eng.pk_cache_set(wl["share_pks"])
+    dev = torch.device("cuda", 0)
+    d = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_rec, d_roots = d(bytes(rec)), d(b"".join(wl["roots"]))
+    d_off = torch.arange(0, N + 1, n, dtype=torch.int32, device=dev)
+    d_t = torch.full((V,), t, dtype=torch.int32, device=dev)
+    d_pk = torch.arange(0, N, dtype=torch.int32, device=dev)
+    d_ids = torch.tensor(wl["ids"], dtype=torch.int64, device=dev)
+    d_jr = torch.tensor(wl["job_root"], dtype=torch.int32, device=dev)
+    out = torch.zeros((V, 96), dtype=torch.uint8, device=dev)
+    st = torch.zeros((V,), dtype=torch.int32, device=dev)
+    err = torch.zeros((V, 2), dtype=torch.int64, device=dev)
+    ver = torch.zeros((N,), dtype=torch.uint8, device=dev)
+    wst = torch.full((N,), -1, dtype=torch.int32, device=dev)
+    lib = eng._lib
+    dst = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
+    rc = lib.ssb_threshold_aggregate_batch_wire_cached_dev(
+        eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_rec.data_ptr(), 202, d_pk.data_ptr(), d_ids.data_ptr(),
+        d_jr.data_ptr(), R, d_roots.data_ptr(), ctypes.cast(dst, _lib._u8p), len(DST), 7, out.data_ptr(), st.data_ptr(),
+        err.data_ptr(), ver.data_ptr(), wst.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    assert rc == 0, lib.ssb_last_error(eng.handle)
+    torch.cuda.synchronize(dev)
+    st, err, out, ver, wst = st.cpu().numpy(), err.cpu().numpy(), out.cpu().numpy(), ver.cpu().numpy(), wst.cpu().numpy()
+    assert (st == o_st).all() and (err.astype(np.uint64) == o_err.astype(np.uint64)).all()
+    ok = st == 0
+    assert (out[ok] == o_out[ok]).all()
+    assert (ver == o_ver).all()
+    assert sorted(np.nonzero(wst)[0].tolist()) == sorted(absent)
+    assert wst[3 * n + 1] == 1 and wst[5 * n] == 2 and wst[5 * n + 2] == 3 and wst[7 * n + 1] == 4 and wst[9 * n] == 4
+    assert wst[11 * n + 3] == 1 and wst[13 * n + 2] == 0 and wst[15 * n + 1] == 0

@@ -90,19 +90,21 @@ def test_no_redundancy_jobs_fall_to_the_tree(engine):
 @pytest.mark.parametrize("t,n,V", [(3, 4, 4096), (5, 7, 1024)], ids=["3of4_full_c2", "5of7"])
 def test_registry_ids_match_c_oracle(engine, t, n, V):
     """Registry operator ids (distinct pseudo-random ids in [1, 2^16) per committee, src/node/node.rs:470-474):
-    the Lagrange coefficients are ratios of small integers.  3-of-4: lambda_i = c_i M^-1 by the 64-bit
-    Euclid inverse (unit_lagrange_fast), then the general GLS combine; 5-of-7: coefficients past 62
-    bits, the Fr-exponentiation lambda_i.  Every status, verdict and combined signature == the C oracle."""
+    the Lagrange coefficients are ratios of small integers.  3-of-4: [M^-1](sum c_i sig_i) on one lane
+    per job, lane-uniform windows (k_combine_ratio, unit_combine_ratio_w4); 5-of-7: coefficients past 62
+    bits, the general GLS combine with the Fr-exponentiation lambda_i.  Every status, verdict and
+    combined signature == the C oracle."""
     wl = bench.make_workload(engine, V, t, n, 64, rank=25, ids="registry")
     assert len(set(wl["ids"][:n])) == n and max(wl["ids"]) > n
     _check(engine, wl, V, t, n)
 
 
-def test_knobs_tree_only_and_ratio(engine, monkeypatch):
-    """SSB_NO_COMMITTEE (a failed batch goes straight to the tree) and SSB_RATIO (registry-id jobs
-    through [M^-1](sum c_i sig_i) instead of the general combine): the same exact results."""
+def test_knobs_tree_only_and_no_ratio(engine, monkeypatch):
+    """SSB_NO_COMMITTEE (a failed batch goes straight to the tree) and SSB_NO_RATIO (registry-id jobs
+    through the general combine -- lambda_i, four GLS lanes per share -- instead of k_combine_ratio):
+    the same exact results."""
     monkeypatch.setenv("SSB_NO_COMMITTEE", "1")
-    monkeypatch.setenv("SSB_RATIO", "1")
+    monkeypatch.setenv("SSB_NO_RATIO", "1")
     V, t, n, R = 1024, 3, 4, 16
     wl = bench.make_workload(engine, V, t, n, R, rank=26, ids="registry", invalid_rate=0.01)
     _check(engine, wl, V, t, n)

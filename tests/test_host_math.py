@@ -127,7 +127,7 @@ def test_small_lagrange_fast_path(host_exe):
 
 def test_registry_ratio_path(host_exe):
     """Registry ids (arbitrary, < 2^16): T = sum c_i sig_i and [M^-1 mod r] T by its four GLS digits
-    (unit_lagrange_ratio / unit_combine_ratio_at / unit_gls_term) == the 255-bit lambda_i path, with
+    (unit_lagrange_ratio / unit_combine_ratio_w4: lane-uniform joint windows) == the 255-bit lambda_i path, with
     M = lcm |prod_{j!=i}(x_j - x_i)|; repeated ids and values past 62 bits are not eligible."""
     import random
     rnd = random.Random(7)
@@ -150,6 +150,16 @@ def test_registry_ratio_path(host_exe):
             assert same == 1 and M == L, (ids, line)
     assert n_elig >= 8
     assert [l.split()[0] for l in out[len(cases):]] == ["0", "0"]
+
+
+def test_ratio_combine_infinity(host_exe):
+    """The windowed ratio combine (unit_combine_ratio_w4) when T = sum c_i sig_i is the point at
+    infinity: shares [x_i] P make T = M (sum lambda_i x_i) P = O, and the output is INFINITY_SIGNATURE
+    (0xc0 || 0^95), as blst's sum of the 255-bit terms."""
+    out = _run(host_exe, ["ratiozero 3 5 9 100", "ratiozero 3 1 2 4", "ratiozero 4 1 2 4 5"])
+    for line in out:
+        e, sig = line.split()
+        assert e == "1" and sig == "c0" + "00" * 95
 
 
 def test_small_inverse_and_gls_digits(host_exe):

@@ -35,7 +35,12 @@ def test_patches_apply_in_order(tmp_path):
         assert r.returncode == 0, f"{os.path.basename(p)}: {r.stderr}"
         subprocess.run(["git", "apply", p], cwd=tmp_path, check=True, capture_output=True)
     hot = (tmp_path / "src/validation/impls/hotstuff.rs").read_text()
-    assert "slot_collector::threshold_aggregate" in hot and 'cfg(not(feature = "hip"))' in hot
+    assert "slot_collector::threshold_aggregate_wire" in hot and 'cfg(not(feature = "hip"))' in hot
+    assert "operator.sign_wire(msg)" in hot   # the shares stay wire records on the receive path
+    op = (tmp_path / "src/validation/operator.rs").read_text()
+    assert "async fn sign_wire" in op and "pub struct WireSignature" in op and "fn wire_record_ok" in op
+    # without the feature the reference's own deserializing sign() is untouched
+    assert "bincode::deserialize::<Signature>(&data)" in op
     oc = (tmp_path / "src/validation/operator_committees.rs").read_text()
     assert "register_committee_keys(&def.operator_public_keys)" in oc
     gt = (tmp_path / "src/crypto/generic_threshold.rs").read_text()
