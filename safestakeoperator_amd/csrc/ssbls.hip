@@ -107,9 +107,6 @@ struct ssb_ctx {
   // (the kernels with the largest private segments stay off the slots' queues).  One-stream slots
   // run every stage on the slot's own stream and leave both idle.
   hipStream_t spec = nullptr, tail = nullptr;
-  // key registration (pkc_fill): its own stream, so registering a key waits for the key's decode
-  // only, not for the batches queued on a slot
-  hipStream_t reg = nullptr;
   // decoded public keys (ssb_pk_cache_set / ssb_pk_cache_add): affine points + DEC_* flags, indexed
   // by the caller; rows [0, pkc_n) are live, the arrays hold pkc_cap rows
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0, pkc_cap = 0;
@@ -687,8 +684,7 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   ctx->hw_queues = ssb_hw_queue_budget();
   if (init_slot(ctx->sl[0], ctx->slot_streams) != SSB_OK) { delete ctx; return SSB_EHIP; }
   if (hipStreamCreateWithFlags(&ctx->spec, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->reg, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
+      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
@@ -715,7 +711,7 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
   if (ctx->pkc_pow) hipFree(ctx->pkc_pow);
   if (ctx->pkc_stage) hipFree(ctx->pkc_stage);
-  for (hipStream_t x : {ctx->spec, ctx->tail, ctx->reg}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
+  for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx, ctx->sl[i]);
   delete ctx;
 }
@@ -1223,6 +1219,21 @@ int pkc_quiesce(ssb_ctx* ctx) {
   for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) SSB_HIP(hipStreamSynchronize(x));
   return SSB_OK;
 }
+// Key registration (pkc_reserve / pkc_fill) runs on a stream created for the call and destroyed
+// after it: registering a key waits for that key's decode only, not for the batches queued on a
+// slot, and holds no hardware queue between registrations.  (A context-lifetime stream
+// took one of the process's GPU_MAX_HW_QUEUES from the slots: two slots then shared a queue and
+// the pipelined rate fell from 12.8 M to 9.6 M partial sigs/s, round 5.)
+struct reg_stream {
+  hipStream_t s = nullptr;
+  int open(ssb_ctx* ctx) {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) return SSB_OK;
+    s = nullptr;
+    ctx->err = "hipStreamCreate (key registration) failed";
+    return SSB_EHIP;
+  }
+  ~reg_stream() { if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); } }
+};
 // room for `need` rows; growing (capacity doubles) moves the live rows to the new arrays after every
 // in-flight batch has finished -- registration-time work, amortised over the doublings
 int pkc_reserve(ssb_ctx* ctx, size_t need) {
@@ -1239,9 +1250,11 @@ int pkc_reserve(ssb_ctx* ctx, size_t need) {
   // the precomputed bases of the batch path's merged G1 MSM (plan_msm g1_pre): registration-time
   // work, like the decompression; without them (allocation failed) batches use the windowed G1 MSM
   if (hipMalloc(&p, cap * PKPOW_W * sizeof(g1_aff)) != hipSuccess) { p = nullptr; (void)hipGetLastError(); }
-  hipStream_t st = ctx->reg;
   const size_t n = ctx->pkc_n;
   if (n) {
+    reg_stream rs;
+    if (int rc = rs.open(ctx)) return rc;
+    hipStream_t st = rs.s;
     SSB_HIP(hipMemcpyAsync(a, ctx->pkc_aff, n * sizeof(g1_aff), hipMemcpyDeviceToDevice, st));
     SSB_HIP(hipMemcpyAsync(f, ctx->pkc_flags, n * 4, hipMemcpyDeviceToDevice, st));
     if (p && ctx->pkc_pow)
@@ -1257,7 +1270,7 @@ int pkc_reserve(ssb_ctx* ctx, size_t need) {
   return SSB_OK;
 }
 // decode n compressed keys into rows [row, row + n) (+ their precomputed bases); synchronous.  Runs
-// on slot 0's stream: rows below `row` -- the only ones an in-flight batch can index -- are untouched.
+// on a registration stream (reg_stream): rows below `row` -- the only ones an in-flight batch can index -- are untouched.
 int pkc_fill(ssb_ctx* ctx, size_t row, size_t n, const uint8_t* pk48) {
   if (!n) return SSB_OK;
   if (n * 48 > ctx->pkc_stage_bytes) {
@@ -1266,7 +1279,9 @@ int pkc_fill(ssb_ctx* ctx, size_t row, size_t n, const uint8_t* pk48) {
     if (hipMalloc(&ctx->pkc_stage, want) != hipSuccess) { ctx->pkc_stage = nullptr; ctx->err = "hipMalloc key staging failed"; return SSB_ENOMEM; }
     ctx->pkc_stage_bytes = want;
   }
-  hipStream_t st = ctx->reg;
+  reg_stream rs;
+  if (int rc = rs.open(ctx)) return rc;
+  hipStream_t st = rs.s;
   SSB_HIP(hipMemcpyAsync(ctx->pkc_stage, pk48, n * 48, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_decode_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (const uint8_t*)ctx->pkc_stage,
                      ctx->pkc_aff + row, ctx->pkc_flags + row);
