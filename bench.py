@@ -35,6 +35,8 @@ def set_hw_queues(n):
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < n:
         os.environ["GPU_MAX_HW_QUEUES"] = str(n)
 
+DIST_QUEUES = 0   # hardware queues added for the process group's streams (RCCL) beside the slots (see main)
+
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 METRIC = "verified partial sigs/sec + combined threshold sigs/sec, 1 and 8 MI355X"
 MAD_PEAK_MEASURED = 3.8235e13  # v_mad_u64_u32/s, profiles/r01_madpeak.json (16 chains, 4096 WGs)
@@ -359,6 +361,9 @@ def main():
     ap.add_argument("--collector-windows", type=int, default=200,
                     help="4,096-job windows pushed through the native per-slot collector for value_collector (0: skip)")
     ap.add_argument("--collector-threads", type=int, default=8, help="native submitter threads of value_collector")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (default: pipeline x slot streams + 3, + %d with "
+                         "torch.distributed; at most 32)" % DIST_QUEUES)
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the process group even at one rank (rehearses RCCL's stream beside the slot "
                          "queues on one GPU: torchrun --nproc-per-node 1 ... --force-dist)")
@@ -387,8 +392,11 @@ def main():
     # issued once per pipeline round (exchange_group), after the round's batches, so that stream is
     # not active beside the 20 slot queues.
     # slot streams + the context's speculative-combine and tail streams (idle with one-stream slots,
-    # which run every stage on the slot's stream) + one for torch
-    set_hw_queues(args.pipeline * args.slot_streams + 3)
+    # which run every stage on the slot's stream) + one for torch; with torch.distributed, room for
+    # the process group's streams too (RCCL at N = 1 with no room: two slots shared a queue, 9.36 M
+    # against 12.27 M without the process group, round 5)
+    dist_run = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.force_dist
+    set_hw_queues(args.hw_queues or (args.pipeline * args.slot_streams + 3 + (DIST_QUEUES if dist_run else 0)))
 
     import numpy as np
     import torch
@@ -399,30 +407,41 @@ def main():
     # --dist-backend gloo: rehearsal of the N > 1 path on fewer GPUs than ranks (ranks share
     # devices round robin, the collectives run on host copies); the measured path is RCCL.
     gpu = local % max(1, torch.cuda.device_count()) if args.dist_backend == "gloo" else local
-    if world > 1 or args.force_dist:
-        import torch.distributed as dist
-        torch.cuda.set_device(gpu)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group("gloo")
-    else:
-        torch.cuda.set_device(gpu)
+    torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")   # where collectives run
     local = gpu
 
+    # the library (a no-op when the in-tree build is current); ranks of one node take turns
+    import fcntl
     from safestakeoperator_amd.build import build
-    if rank == 0 or world == 1:
+    with open(os.path.join(ROOT, ".bench_build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
         build(verbose=False)
-    if dist is not None:
-        dist.barrier()
     from safestakeoperator_amd import Engine, DST
     from safestakeoperator_amd import _lib
 
     V, t, n, n_roots = args.validators, args.threshold, args.operators, args.roots
     V_glob = V * (1 if strong else world)             # validators of the whole job (all ranks)
+    S = max(1, args.pipeline)
+    if args.dist_backend == "gloo" and world > 1:
+        # rehearsal with ranks sharing GPUs: the GPU's slot queues are split between its ranks (each
+        # slot is a hardware queue with its own scratch reservation; 24 on one GPU exhausted it)
+        per_gpu = -(-world // max(1, torch.cuda.device_count()))
+        S = max(1, S // per_gpu)
     eng = Engine(local)
+    # the S slots' streams exist BEFORE the process group: each holds a hardware queue of its own and
+    # the engine reuses them whatever the slot configuration (ssb_ctx::streams_all); the process
+    # group's streams, created after, take the queues left.  (Process group first: recreated slot
+    # streams landed two to a queue -- RCCL at N = 1 9.15 M against 12.4 M, round 5.)
+    if eng._lib.ssb_set_slot_streams(eng.handle, 1) != 0 or eng._lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
+        raise RuntimeError("ssb_set_pipeline_depth: %s" % eng._lib.ssb_last_error(eng.handle))
+    if world > 1 or args.force_dist:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
     from safestakeoperator_amd.shard import BatchExchange, shard_jobs, shard_sizes
     sizes = None
     if strong:
@@ -451,12 +470,6 @@ def main():
     d_t = torch.full((V,), t, dtype=torch.int32, device=dev)
     d_jr = torch.tensor(wl["job_root"], dtype=torch.int32, device=dev)
     d_roots = dt8(b"".join(wl["roots"]))
-    S = max(1, args.pipeline)
-    if args.dist_backend == "gloo" and world > 1:
-        # rehearsal with ranks sharing GPUs: the GPU's slot queues are split between its ranks (each
-        # slot is a hardware queue with its own scratch reservation; 24 on one GPU exhausted it)
-        per_gpu = -(-world // max(1, torch.cuda.device_count()))
-        S = max(1, S // per_gpu)
     outs = [dict(out=torch.empty((V, 96), dtype=torch.uint8, device=dev), st=torch.empty((V,), dtype=torch.int32, device=dev),
                  err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev),
                  fv=torch.empty((V,), dtype=torch.uint8, device=dev))

@@ -107,6 +107,13 @@ struct ssb_ctx {
   // (the kernels with the largest private segments stay off the slots' queues).  One-stream slots
   // run every stage on the slot's own stream and leave both idle.
   hipStream_t spec = nullptr, tail = nullptr;
+  // Every stream the context creates stays alive until ssb_destroy and is reused: a slot or
+  // context stream that is released returns here (FIFO), and a new one is taken from here first.
+  // Each holds a hardware queue of its own from its creation, so reconfiguring the slots (depth 1
+  // <-> 20, one <-> three streams) never hands a slot a queue that a stream created later -- the
+  // process group's, the caller's -- has been given meanwhile (round 5: after torch.distributed
+  // started, recreated slot streams landed two to a queue and the rate fell by a quarter).
+  std::vector<hipStream_t> streams_all, streams_free;
   // decoded public keys (ssb_pk_cache_set / ssb_pk_cache_add): affine points + DEC_* flags, indexed
   // by the caller; rows [0, pkc_n) are live, the arrays hold pkc_cap rows
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0, pkc_cap = 0;
@@ -179,6 +186,18 @@ void pick_slot(ssb_ctx* ctx, void* stream) {
 
 hipStream_t slot_tail(ssb_ctx* ctx) { return ctx->tail; }
 
+// The context-wide spec / tail streams are taken only while the slots are three-stream: one-stream
+// slots run every stage on the slot's stream, and the two streams then serve as slots' streams.
+int take_stream(ssb_ctx* ctx, hipStream_t* s);
+void give_stream(ssb_ctx* ctx, hipStream_t& s);
+int ctx_streams(ssb_ctx* ctx, bool on) {
+  for (hipStream_t* x : {&ctx->spec, &ctx->tail}) {
+    if (on && !*x && take_stream(ctx, x)) return SSB_EHIP;
+    if (!on && *x) { hipStreamSynchronize(*x); give_stream(ctx, *x); }
+  }
+  return SSB_OK;
+}
+
 int ensure_io(ssb_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->io_bytes) return SSB_OK;
   if (ctx->io) { hipFree(ctx->io); ctx->io = nullptr; ctx->io_bytes = 0; }
@@ -193,19 +212,37 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 // streams = 3: main chain + hash_to_G2 + G1 side, overlapping inside the batch (lowest latency);
 // streams = 1: the whole batch in order on one stream (side[] alias it) -- one hardware queue per
 // slot, so many more slots fit the runtime's per-queue scratch reservations (highest throughput).
-int init_slot(ssb_slot& S, int streams) {
-  if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
+// a stream from the context's pool (ssb_ctx::streams_free), created if the pool is empty; a new
+// stream's queue acquires its scratch at once, alone (streams are taken one after the other)
+int take_stream(ssb_ctx* ctx, hipStream_t* s) {
+  if (!ctx->streams_free.empty()) {
+    *s = ctx->streams_free.front();
+    ctx->streams_free.erase(ctx->streams_free.begin());
+    return SSB_OK;
+  }
+  if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) { *s = nullptr; return SSB_EHIP; }
+  ctx->streams_all.push_back(*s);
+  return launch::prime_queue(*s) ? SSB_EHIP : SSB_OK;
+}
+void give_stream(ssb_ctx* ctx, hipStream_t& s) {
+  if (s) ctx->streams_free.push_back(s);
+  s = nullptr;
+}
+void destroy_streams(ssb_ctx* ctx) {
+  for (hipStream_t x : ctx->streams_all) { hipStreamSynchronize(x); hipStreamDestroy(x); }
+  ctx->streams_all.clear();
+  ctx->streams_free.clear();
+}
+int init_slot(ssb_ctx* ctx, ssb_slot& S, int streams) {
+  if (take_stream(ctx, &S.stream)) return SSB_EHIP;
   S.shared = streams == 1;
   for (int i = 0; i < 2; ++i) {
     if (S.shared) S.side[i] = S.stream;
-    else if (hipStreamCreateWithFlags(&S.side[i], hipStreamNonBlocking) != hipSuccess) return SSB_EHIP;
+    else if (take_stream(ctx, &S.side[i])) return SSB_EHIP;
   }
   for (hipEvent_t* e : {&S.ev_in, &S.ev_hash, &S.ev_dec, &S.ev_comb, &S.ev_out, &S.ev_sdec, &S.ev_r2, &S.ev_r1, &S.ev_user, &S.ev_fin,
                         &S.ev_host})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return SSB_EHIP;
-  // each new queue acquires its scratch now, alone (slots are created one after the other)
-  if (launch::prime_queue(S.stream)) return SSB_EHIP;
-  if (!S.shared) for (hipStream_t sd : S.side) if (launch::prime_queue(sd)) return SSB_EHIP;
   return SSB_OK;
 }
 // the pending host-buffer batch of the slot: wait for it, copy its outputs to the caller's pointers.
@@ -242,11 +279,11 @@ void free_slot(ssb_ctx* ctx, ssb_slot& S) {
   deliver_host(ctx, S);
   if (S.ws) hipFree(S.ws);
   if (S.hst) hipHostFree(S.hst);
-  if (!S.shared) for (hipStream_t sd : S.side) if (sd) hipStreamDestroy(sd);
+  if (!S.shared) for (hipStream_t& sd : S.side) give_stream(ctx, sd);
   for (hipEvent_t e : {S.ev_in, S.ev_hash, S.ev_dec, S.ev_comb, S.ev_out, S.ev_sdec, S.ev_r2, S.ev_r1, S.ev_user, S.ev_fin,
                        S.ev_host})
     if (e) hipEventDestroy(e);
-  if (S.stream) hipStreamDestroy(S.stream);
+  give_stream(ctx, S.stream);
 }
 
 // hipEvent pair around one kernel launch on the engine's stream (the stream the kernel runs on)
@@ -682,16 +719,15 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   if (!ctx) return SSB_ENOMEM;
   ctx->device = device_ordinal;
   ctx->hw_queues = ssb_hw_queue_budget();
-  if (init_slot(ctx->sl[0], ctx->slot_streams) != SSB_OK) { delete ctx; return SSB_EHIP; }
-  if (hipStreamCreateWithFlags(&ctx->spec, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->tail, hipStreamNonBlocking) != hipSuccess) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
+  if (init_slot(ctx, ctx->sl[0], ctx->slot_streams) != SSB_OK) { free_slot(ctx, ctx->sl[0]); destroy_streams(ctx); delete ctx; return SSB_EHIP; }
+  if (ctx_streams(ctx, ctx->slot_streams == 3) != SSB_OK) { free_slot(ctx, ctx->sl[0]); destroy_streams(ctx); delete ctx; return SSB_EHIP; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
     for (int i = 0; i < 64; ++i) { jac_to_aff(h[i], p); jac_dbl(p, p); }
     if (hipMalloc(&ctx->negg1_pow, sizeof(h)) != hipSuccess ||
         hipMemcpy(ctx->negg1_pow, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
-      free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP;
+      free_slot(ctx, ctx->sl[0]); ctx_streams(ctx, false); destroy_streams(ctx); delete ctx; return SSB_EHIP;
     }
   }
   *out = ctx;
@@ -711,8 +747,9 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->pkc_flags) hipFree(ctx->pkc_flags);
   if (ctx->pkc_pow) hipFree(ctx->pkc_pow);
   if (ctx->pkc_stage) hipFree(ctx->pkc_stage);
-  for (hipStream_t x : {ctx->spec, ctx->tail}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
+  ctx_streams(ctx, false);
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx, ctx->sl[i]);
+  destroy_streams(ctx);
   delete ctx;
 }
 
@@ -755,7 +792,7 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
   if (int rc = check_queue_budget(ctx, depth, ctx->slot_streams)) return rc;
   SSB_HIP(hipSetDevice(ctx->device));
   for (int i = ctx->nslots; i < depth; ++i) {
-    if (init_slot(ctx->sl[i], ctx->slot_streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
+    if (init_slot(ctx, ctx->sl[i], ctx->slot_streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
     ctx->nslots = i + 1;
   }
   for (int i = depth; i < ctx->nslots; ++i) { sync_slot(ctx, ctx->sl[i]); free_slot(ctx, ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
@@ -779,7 +816,8 @@ int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
   for (int i = 0; i < ctx->nslots; ++i) { sync_slot(ctx, ctx->sl[i]); free_slot(ctx, ctx->sl[i]); ctx->sl[i] = ssb_slot(); }
   ctx->slot_streams = streams;
   for (int i = 0; i < ctx->nslots; ++i)
-    if (init_slot(ctx->sl[i], streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
+    if (init_slot(ctx, ctx->sl[i], streams) != SSB_OK) { ctx->err = "stream/event creation failed"; return SSB_EHIP; }
+  if (ctx_streams(ctx, streams == 3) != SSB_OK) { ctx->err = "stream creation failed"; return SSB_EHIP; }
   ctx->next = 0;
   ctx->cur = &ctx->sl[0];
   return SSB_OK;
