@@ -321,21 +321,39 @@ constexpr uint32_t FAST_T = 16;
 // -- k_combine_ratio finishes the job, one lane each (unit_combine_ratio_w4); else 0 (the general
 // path: lambda_i, k_combine_terms_gls, k_combine_sum).  `ratio` = 0 (SSB_NO_RATIO): never 2.
 // One function for both, out of line: one set of per-lane arrays in its own frame.
+// The coefficients' kind, a leaf (no calls: a function that calls out keeps its values in the
+// callee-saved VGPRs and saves ~110 of them in its frame -- combine_job did, 736 B, round 5):
+// 1 with c[] the small-integer coefficients, 2 (ratio != 0) ratio coefficients, else 0.
+SSB_FN uint32_t lagrange_kind(int64_t* __restrict__ c, const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel,
+                              uint32_t t, uint32_t ratio) {
+  uint64_t x[FAST_T];
+  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[i]];
+  if (unit_lagrange_small(c, x, t)) return 1u;
+  uint64_t M;
+  return ratio && unit_lagrange_ratio(c, &M, x, t) ? 2u : 0u;
+}
+// the small-integer combine of a job lagrange_kind classed 1 (its coefficients recomputed here, so
+// no array of them lives in combine_job's frame across a call)
+SSB_FN void combine_small_job(uint8_t* __restrict__ out96, const g2_aff* __restrict__ sig_aff,
+                              const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel, uint32_t t) {
+  int64_t c[FAST_T];
+  lagrange_kind(c, ids, sel, t, 0u);
+  unit_combine_small_at(out96, sig_aff, sel, c, t);
+}
+SSB_FN uint32_t lagrange_class(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ sel, uint32_t t,
+                               uint32_t ratio) {
+  int64_t c[FAST_T];
+  return lagrange_kind(c, ids, sel, t, ratio);
+}
 SSB_FN uint32_t combine_job(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                             const int32_t* __restrict__ status, const uint32_t* __restrict__ sel,
                             const uint64_t* __restrict__ ids, const g2_aff* __restrict__ sig_aff,
                             uint8_t* __restrict__ out96, uint32_t ratio) {
   if (status[j] != SSB_DVF_OK || tt[j] > FAST_T) return 0u;
   const uint32_t t = tt[j], b = off[j];
-  uint64_t x[FAST_T];
-  int64_t c[FAST_T];
-  for (uint32_t i = 0; i < t; ++i) x[i] = ids[sel[b + i]];
-  if (unit_lagrange_small(c, x, t)) {
-    unit_combine_small_at(out96 + 96 * (size_t)j, sig_aff, sel + b, c, t);
-    return 1u;
-  }
-  uint64_t M;
-  return ratio && unit_lagrange_ratio(c, &M, x, t) ? 2u : 0u;
+  const uint32_t kind = lagrange_class(ids, sel + b, t, ratio);
+  if (kind == 1u) combine_small_job(out96 + 96 * (size_t)j, sig_aff, ids, sel + b, t);
+  return kind;
 }
 // the ratio coefficients of a job combine_job marked 2 (recomputed: a few 64-bit operations)
 SSB_INL void ratio_coeffs(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,

@@ -427,6 +427,15 @@ SSB_FN jac<F> quarter_sum(fr_bucket_lds& ub, const uint32_t* __restrict__ list, 
   }
   return acc;
 }
+// quarter_sum stored by lane 0 at *out: one call per group sum, from the kernel (a function that held
+// both group sums' results held both in its frame)
+template <class F>
+SSB_FN void quarter_sum_to(fr_bucket_lds& ub, const uint32_t* __restrict__ list, uint32_t nr,
+                           const uint32_t* __restrict__ flags, uint32_t need, const uint64_t* __restrict__ k64,
+                           const aff<F>* __restrict__ pts, int q, jac<F>* __restrict__ out) {
+  const jac<F> a = quarter_sum<F>(ub, list, nr, flags, need, k64, pts, q);
+  if (threadIdx.x == 0) *out = a;
+}
 // sum_q 2^(16q) X[q] (q < 4), affine, in lane 0 (infinity on the other lanes)
 template <class F>
 SSB_FN aff<F> combine_quarters(const jac<F>* __restrict__ X) {
@@ -587,44 +596,55 @@ SSB_FN void ex_singles(ex_lds& L, int first, uint32_t ns, const uint32_t* __rest
   }
 }
 // the exclusion pair of block `blk` (root r < n_roots: -E_r; n_roots .. +3: the quarters of X) into
-// fex[pair]; returns true in the block that must run the final product (tickets)
-SSB_FN bool ex_pair(ex_lds& L, int n_roots, uint32_t ns, const uint32_t* __restrict__ slist,
-                    const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ perm,
-                    const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
-                    const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H, fp12* __restrict__ fex,
-                    g2_jac* __restrict__ X4, uint32_t* __restrict__ xtk) {
+// fex[pair]; returns true in the block that must run the final product (tickets).  The two roles are
+// separate functions (each frame holds one role's temporaries; the deepest call chain of k_fb_excl
+// runs through the X role: quarter_sum's frame under this one).
+SSB_FN void ex_pair_root(ex_lds& L, int r, const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                         const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
+                         const uint64_t* __restrict__ k64, const g1_aff* __restrict__ pk_aff,
+                         const g2_aff* __restrict__ H) {
   using namespace ssb::lane;
-  const int blk = blockIdx.x, lane_ = threadIdx.x;
-  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, (int)threadIdx.x};
   const int F1 = BS_S0, B = F1 + 24;
-  int pair;
-  if (blk < n_roots) {
-    const int r = blk;
-    const g1_aff P = neg_suspect_sum(start[r], cnt[r], perm, flags, k64, pk_aff);   // -E_r (lane 0)
-    __syncthreads();
-    lp_init_consts(g);
-    miller_one(g, P, H[r], F1, B, L.flg);
-    pair = r;
-  } else {
-    const int q = blk - n_roots;
+  const g1_aff P = neg_suspect_sum(start[r], cnt[r], perm, flags, k64, pk_aff);   // -E_r (lane 0)
+  __syncthreads();
+  lp_init_consts(g);
+  miller_one(g, P, H[r], F1, B, L.flg);
+}
+// X's quarter q; returns false in the blocks that are not the last of the four (they are done)
+SSB_FN bool ex_pair_x(ex_lds& L, int q, uint32_t ns, const uint32_t* __restrict__ slist,
+                      const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64,
+                      const g2_aff* __restrict__ sig_aff, g2_jac* __restrict__ X4, uint32_t* __restrict__ xtk) {
+  using namespace ssb::lane;
+  const int lane_ = threadIdx.x;
+  {
     const g2_jac acc = quarter_sum<fp2>(L.u.b, slist, ns, flags, FLAG_SUSPECT, k64, sig_aff, q);
     if (lane_ == 0) X4[q] = acc;
-    __threadfence();
-    __syncthreads();
-    if (lane_ == 0) L.last = atomicAdd(&xtk[1], 1u) == 3u ? 1u : 0u;
-    __syncthreads();
-    if (!L.last) return false;
-    __threadfence();
-    const g2_aff Q = combine_quarters<fp2>(X4);
-    __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
-    lp_init_consts(g);
-    g1_aff G = g1_neg_generator();
-    fp_neg(G.y, G.y);   // +g1
-    miller_one(g, G, Q, F1, B, L.flg);
-    if (lane_ == 0) xtk[1] = 0u;
-    pair = n_roots;
   }
-  if (lane_ < 12) ((fp*)&fex[pair])[lane_] = g.s[F1 + lane_];
+  __threadfence();
+  __syncthreads();
+  if (lane_ == 0) L.last = atomicAdd(&xtk[1], 1u) == 3u ? 1u : 0u;
+  __syncthreads();
+  if (!L.last) return false;
+  __threadfence();
+  {
+    const g2_aff Q = combine_quarters<fp2>(X4);
+    if (lane_ == 0) L.sQ = Q;
+  }
+  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
+  const int F1 = BS_S0, B = F1 + 24;
+  lp_init_consts(g);
+  if (lane_ == 0) { L.sP = g1_neg_generator(); fp_neg(L.sP.y, L.sP.y); }   // +g1
+  __syncthreads();
+  miller_one(g, L.sP, L.sQ, F1, B, L.flg);
+  if (lane_ == 0) xtk[1] = 0u;
+  return true;
+}
+// the pair's Miller value into fex[pair], then the pairs' ticket: true in the block that runs the product
+SSB_INL bool ex_pair_ticket(ex_lds& L, int n_roots, int pair, fp12* __restrict__ fex, uint32_t* __restrict__ xtk) {
+  const int lane_ = threadIdx.x;
+  if (lane_ < 12) ((fp*)&fex[pair])[lane_] = L.u.s[lane::LP_NCODE_CONST + BS_S0 + lane_];   // (g.s + F1 of the roles)
   __threadfence();
   __syncthreads();
   if (lane_ == 0) L.last = atomicAdd(&xtk[0], 1u) == (uint32_t)n_roots ? 1u : 0u;
@@ -667,35 +687,29 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
 // behind the other pipeline slots' waves.)
 // (the group tests' roles out of line: the quarter sums' and the combines' point temporaries live in
 // their own frames, not in the kernel's beside the pairing check's)
-SSB_FN void group_quarters(fr_bucket_lds& ub, const uint32_t* __restrict__ list, uint32_t gn, const uint32_t* __restrict__ flags,
-                           const uint64_t* __restrict__ k64, const g2_aff* __restrict__ sig_aff,
-                           const g1_aff* __restrict__ pk_aff, int q, g2_jac* __restrict__ o2, g1_jac* __restrict__ o1) {
-  const g2_jac a2 = quarter_sum<fp2>(ub, list, gn, flags, FLAG_CANDIDATE, k64, sig_aff, q);
-  if (threadIdx.x == 0) *o2 = a2;
-  const g1_jac a1 = quarter_sum<fp>(ub, list, gn, flags, FLAG_CANDIDATE, k64, pk_aff, q);
-  if (threadIdx.x == 0) *o1 = a1;
+// the last item of a group: its quarters combined into L.sQ / L.sP (lane 0), then (ex_group_check)
+// ONE RLC check and the candidates' verdicts on a pass (or for a one-candidate group).  Two functions
+// called one after the other from the kernel: the combines' frame and the pairing check's frame are
+// never on the call chain together (private segment: the deeper of the two, not their sum).
+SSB_FN void group_combine(ex_lds& L, const g2_jac* __restrict__ X2, const g1_jac* __restrict__ X1) {
+  const int lane_ = threadIdx.x;
+  {
+    const g2_aff Q = combine_quarters<fp2>(X2);
+    if (lane_ == 0) L.sQ = Q;
+  }
+  {
+    const g1_aff P = combine_quarters<fp>(X1);
+    if (lane_ == 0) L.sP = P;
+  }
 }
-SSB_FN void group_combine(const g2_jac* __restrict__ X2, const g1_jac* __restrict__ X1, g2_aff* sQ, g1_aff* sP) {
-  const g2_aff Q = combine_quarters<fp2>(X2);
-  if (threadIdx.x == 0) *sQ = Q;
-  const g1_aff P = combine_quarters<fp>(X1);
-  if (threadIdx.x == 0) *sP = P;
-}
-// the last item of a group: combine the quarters, ONE RLC check, the candidates' verdicts on a pass
-// (or for a one-candidate group); out of line, so its temporaries stay out of k_fb_excl's frame
 SSB_FN void ex_group_check(ex_lds& L, const uint32_t* __restrict__ list, uint32_t gn, uint32_t m,
-                           uint32_t* __restrict__ flags, const g2_jac* __restrict__ X2, const g1_jac* __restrict__ X1,
-                           const g2_aff& h, uint8_t* __restrict__ verdict) {
+                           uint32_t* __restrict__ flags, const g2_aff& h, uint8_t* __restrict__ verdict) {
   using namespace ssb::lane;
   const int lane_ = threadIdx.x;
-  group_combine(X2, X1, &L.sQ, &L.sP);
-  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
   grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
   lp_init_consts(g);
   const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
-  const g1_aff Pu = L.sP;
-  const g2_aff Qu = L.sQ;
-  const bool pass = pair_check(g, Pu, Qu, h, F1, B, BP, TMP);
+  const bool pass = pair_check(g, L.sP, L.sQ, h, F1, B, BP, TMP);   // (the points read from LDS)
   if (pass || m == 1)
     for (uint32_t x = lane_; x < gn; x += 64) {
       const uint32_t s = list[x];
@@ -748,7 +762,8 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
       const uint32_t gn = kcnt[key];
       if (!gn) continue;   // (uniform: the four items of an empty key all skip: no ticket)
       const uint32_t* list = perm + kstart[key];
-      group_quarters(L.u.b, list, gn, flags, k64, sig_aff, pk_aff, (int)q, gX2 + 4 * key + q, gX1 + 4 * key + q);
+      quarter_sum_to<fp2>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, sig_aff, (int)q, gX2 + 4 * key + q);
+      quarter_sum_to<fp>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, pk_aff, (int)q, gX1 + 4 * key + q);
       __threadfence();
       __syncthreads();
       if (lane_ == 0) L.last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
@@ -763,7 +778,9 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
       __syncthreads();
       const uint32_t m = L.ncand;
       if (!m) continue;   // uniform
-      ex_group_check(L, list, gn, m, flags, gX2 + 4 * key, gX1 + 4 * key, H[key / NB], verdict);
+      group_combine(L, gX2 + 4 * key, gX1 + 4 * key);
+      __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+      ex_group_check(L, list, gn, m, flags, H[key / NB], verdict);
     }
     return;
   }
@@ -771,7 +788,12 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
     ex_singles(L, n_roots + 4, ns, slist, share_root, sig_aff, pk_aff, H, verdict);
     return;
   }
-  if (ex_pair(L, n_roots, ns, slist, start, cnt, perm, flags, k64, sig_aff, pk_aff, H, fex, X4, xtk))
+  if (blk < n_roots) {
+    ex_pair_root(L, blk, start, cnt, perm, flags, k64, pk_aff, H);
+  } else if (!ex_pair_x(L, blk - n_roots, ns, slist, flags, k64, sig_aff, X4, xtk)) {
+    return;
+  }
+  if (ex_pair_ticket(L, n_roots, blk < n_roots ? blk : n_roots, fex, xtk))
     ex_final(L, n_roots, ftot, fex, xtk, xok);
 }
 

@@ -247,7 +247,7 @@ SSB_INL int64_t i64_gcd(int64_t a, int64_t b) {
   while (b) { const int64_t t = a % b; a = b; b = t; }
   return a;
 }
-SSB_FN bool unit_lagrange_small(int64_t* c, const uint64_t* x, uint32_t t) {
+SSB_INL bool unit_lagrange_small(int64_t* c, const uint64_t* x, uint32_t t) {
   for (uint32_t i = 0; i < t; ++i) {
     int64_t num = 1, den = 1;
     for (uint32_t k = 0; k < t; ++k) {
@@ -292,7 +292,8 @@ SSB_FN void unit_combine_small(uint8_t* out96, const g2_aff* const* pts, const i
 }
 // the same, the points read as pts[idx[i]] (the device path: no array of point pointers in a frame)
 // (NAF digits of each |c_i| -- |c_i| < 2^62 -- shared doublings: the registry ids' 48-bit
-// coefficients cost ~16 additions per term instead of ~24)
+// coefficients cost ~16 additions per term instead of ~24; the group steps out of line, so the
+// frame of the combine kernels holds no inlined doubling's temporaries -- round 5, private segments)
 SSB_INL void combine_small_jac(g2_jac& acc, const g2_aff* __restrict__ pts, const uint32_t* __restrict__ idx,
                                const int64_t* c, uint32_t t) {
   uint64_t any = 0;
@@ -304,7 +305,7 @@ SSB_INL void combine_small_jac(g2_jac& acc, const g2_aff* __restrict__ pts, cons
   const int nb = any ? 64 - __builtin_clzll(any) : 0;
   jac_set_inf(acc);
   for (int b = nb - 1; b >= 0; --b) {
-    jac_dbl_inl(acc, acc);
+    jac_dbl(acc, acc);
     for (uint32_t i = 0; i < t; ++i) {
       uint64_t ps, ng;
       naf_masks((uint64_t)(c[i] < 0 ? -c[i] : c[i]), ps, ng);
@@ -312,7 +313,7 @@ SSB_INL void combine_small_jac(g2_jac& acc, const g2_aff* __restrict__ pts, cons
       if (p1 || n1) {
         g2_aff q = pts[idx[i]];
         if ((c[i] < 0) != n1) fp2_neg(q.y, q.y);
-        jac_add_aff_inl(acc, acc, q);
+        jac_add_aff(acc, acc, q);
       }
     }
   }
@@ -335,7 +336,7 @@ SSB_FN void unit_combine_small_at(uint8_t* out96, const g2_aff* __restrict__ pts
 // -- t products with small scalars (ids < 2^16, t = 3: |c_i| < 2^48) and ONE 255-bit product per job
 // (its four GLS digits, unit_gls_term) instead of t of them.  Returns false when a value does not
 // fit 62 bits, or ids repeat (the general path then runs).
-SSB_FN bool unit_lagrange_ratio(int64_t* c, uint64_t* M, const uint64_t* x, uint32_t t) {
+SSB_INL bool unit_lagrange_ratio(int64_t* c, uint64_t* M, const uint64_t* x, uint32_t t) {
   int64_t L = 1;
   for (uint32_t i = 0; i < t; ++i) {
     if (x[i] >= (1ull << 62)) return false;
