@@ -430,18 +430,6 @@ def main():
         per_gpu = -(-world // max(1, torch.cuda.device_count()))
         S = max(1, S // per_gpu)
     eng = Engine(local)
-    # the S slots' streams exist BEFORE the process group: each holds a hardware queue of its own and
-    # the engine reuses them whatever the slot configuration (ssb_ctx::streams_all); the process
-    # group's streams, created after, take the queues left.  (Process group first: recreated slot
-    # streams landed two to a queue -- RCCL at N = 1 9.15 M against 12.4 M, round 5.)
-    if eng._lib.ssb_set_slot_streams(eng.handle, 1) != 0 or eng._lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
-        raise RuntimeError("ssb_set_pipeline_depth: %s" % eng._lib.ssb_last_error(eng.handle))
-    if world > 1 or args.force_dist:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group("gloo")
     from safestakeoperator_amd.shard import BatchExchange, shard_jobs, shard_sizes
     sizes = None
     if strong:
@@ -558,7 +546,7 @@ def main():
     call_args = {}  # per (slot, key variant, input generation): the submit call's fixed arguments
     inputs = dict(d_sig=d_sig, d_ids=d_ids, d_jr=d_jr, d_roots=d_roots, gen=0)   # the batch step() submits
     group = []      # slots whose results are not exchanged yet
-    xchg = BatchExchange(strong, sizes=sizes, device=cdev) if dist is not None else None
+    xchg = None     # the process group's exchange (phase 2; phases 1 / 1b run before the group exists)
 
     def exchange_group():
         """RCCL all-gather over xGMI of the results of the batches since the last exchange, ONE
@@ -663,6 +651,18 @@ def main():
     if lib.ssb_set_slot_streams(eng.handle, args.slot_streams) != 0 or lib.ssb_set_pipeline_depth(eng.handle, S) != 0:
         raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
     streams.clear()
+    # The process group starts only now: the S slots' streams exist and hold a hardware queue each,
+    # and the group's streams, created after, take the queues left -- the slot configuration stays
+    # as it is from here on.  (Process group first, slots re-created after the latency phases: two
+    # slots shared a queue and RCCL at N = 1 measured 9.15 M against 12.4 M without it, round 5.)
+    # Phases 1 / 1b above are therefore per-rank and exchange nothing.
+    if world > 1 or args.force_dist:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+        xchg = BatchExchange(strong, sizes=sizes, device=cdev)
     # the master key's signature of every validator: every combined signature must equal it
     # (tests/test_generic_threshold.rs:35), checked for every slot's batch, untimed
     msig = eng.sign_batch(wl["master"], wl["job_root"], wl["roots"])

@@ -107,13 +107,6 @@ struct ssb_ctx {
   // (the kernels with the largest private segments stay off the slots' queues).  One-stream slots
   // run every stage on the slot's own stream and leave both idle.
   hipStream_t spec = nullptr, tail = nullptr;
-  // Every stream the context creates stays alive until ssb_destroy and is reused: a slot or
-  // context stream that is released returns here (FIFO), and a new one is taken from here first.
-  // Each holds a hardware queue of its own from its creation, so reconfiguring the slots (depth 1
-  // <-> 20, one <-> three streams) never hands a slot a queue that a stream created later -- the
-  // process group's, the caller's -- has been given meanwhile (round 5: after torch.distributed
-  // started, recreated slot streams landed two to a queue and the rate fell by a quarter).
-  std::vector<hipStream_t> streams_all, streams_free;
   // decoded public keys (ssb_pk_cache_set / ssb_pk_cache_add): affine points + DEC_* flags, indexed
   // by the caller; rows [0, pkc_n) are live, the arrays hold pkc_cap rows
   g1_aff* pkc_aff = nullptr; uint32_t* pkc_flags = nullptr; size_t pkc_n = 0, pkc_cap = 0;
@@ -186,8 +179,10 @@ void pick_slot(ssb_ctx* ctx, void* stream) {
 
 hipStream_t slot_tail(ssb_ctx* ctx) { return ctx->tail; }
 
-// The context-wide spec / tail streams are taken only while the slots are three-stream: one-stream
-// slots run every stage on the slot's stream, and the two streams then serve as slots' streams.
+// The context-wide spec / tail streams exist only while the slots are three-stream: one-stream slots
+// run every stage on the slot's stream, and an idle stream still holds one of the process's hardware
+// queues (more than ~23 mapped queues and the firmware time-slices them: measured 12.5 M partial
+// sigs/s at 23, 5.1 M at 24, 3.6 M at 25, round 5).
 int take_stream(ssb_ctx* ctx, hipStream_t* s);
 void give_stream(ssb_ctx* ctx, hipStream_t& s);
 int ctx_streams(ssb_ctx* ctx, bool on) {
@@ -212,26 +207,23 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 // streams = 3: main chain + hash_to_G2 + G1 side, overlapping inside the batch (lowest latency);
 // streams = 1: the whole batch in order on one stream (side[] alias it) -- one hardware queue per
 // slot, so many more slots fit the runtime's per-queue scratch reservations (highest throughput).
-// a stream from the context's pool (ssb_ctx::streams_free), created if the pool is empty; a new
-// stream's queue acquires its scratch at once, alone (streams are taken one after the other)
+// A stream of the context, created now; its queue acquires its scratch at once, alone (streams are
+// created one after the other: twenty slot queues growing their scratch at once on their first
+// batches is round 2's HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Released streams are destroyed, which
+// returns their hardware queues and scratch to the runtime.  (Round 5 tried keeping released streams
+// in a pool for the context's lifetime, so a slot never lands on a queue created later for someone
+// else: the idle pooled queues kept their scratch, and a 20-slot fallback batch after the collector
+// tests' contexts then failed with OUT_OF_RESOURCES.  bench.py instead creates its slots once, before
+// the process group.)
 int take_stream(ssb_ctx* ctx, hipStream_t* s) {
-  if (!ctx->streams_free.empty()) {
-    *s = ctx->streams_free.front();
-    ctx->streams_free.erase(ctx->streams_free.begin());
-    return SSB_OK;
-  }
+  (void)ctx;
   if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) { *s = nullptr; return SSB_EHIP; }
-  ctx->streams_all.push_back(*s);
   return launch::prime_queue(*s) ? SSB_EHIP : SSB_OK;
 }
 void give_stream(ssb_ctx* ctx, hipStream_t& s) {
-  if (s) ctx->streams_free.push_back(s);
+  (void)ctx;
+  if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); }
   s = nullptr;
-}
-void destroy_streams(ssb_ctx* ctx) {
-  for (hipStream_t x : ctx->streams_all) { hipStreamSynchronize(x); hipStreamDestroy(x); }
-  ctx->streams_all.clear();
-  ctx->streams_free.clear();
 }
 int init_slot(ssb_ctx* ctx, ssb_slot& S, int streams) {
   if (take_stream(ctx, &S.stream)) return SSB_EHIP;
@@ -719,15 +711,15 @@ int ssb_create(ssb_ctx** out, int device_ordinal) {
   if (!ctx) return SSB_ENOMEM;
   ctx->device = device_ordinal;
   ctx->hw_queues = ssb_hw_queue_budget();
-  if (init_slot(ctx, ctx->sl[0], ctx->slot_streams) != SSB_OK) { free_slot(ctx, ctx->sl[0]); destroy_streams(ctx); delete ctx; return SSB_EHIP; }
-  if (ctx_streams(ctx, ctx->slot_streams == 3) != SSB_OK) { free_slot(ctx, ctx->sl[0]); destroy_streams(ctx); delete ctx; return SSB_EHIP; }
+  if (init_slot(ctx, ctx->sl[0], ctx->slot_streams) != SSB_OK) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
+  if (ctx_streams(ctx, ctx->slot_streams == 3) != SSB_OK) { free_slot(ctx, ctx->sl[0]); delete ctx; return SSB_EHIP; }
   {  // [2^s](-g1) for the window pairs of the G2 MSM
     g1_aff h[64];
     g1_jac p; jac_from_aff(p, g1_neg_generator());
     for (int i = 0; i < 64; ++i) { jac_to_aff(h[i], p); jac_dbl(p, p); }
     if (hipMalloc(&ctx->negg1_pow, sizeof(h)) != hipSuccess ||
         hipMemcpy(ctx->negg1_pow, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
-      free_slot(ctx, ctx->sl[0]); ctx_streams(ctx, false); destroy_streams(ctx); delete ctx; return SSB_EHIP;
+      free_slot(ctx, ctx->sl[0]); ctx_streams(ctx, false); delete ctx; return SSB_EHIP;
     }
   }
   *out = ctx;
@@ -749,7 +741,6 @@ void ssb_destroy(ssb_ctx* ctx) {
   if (ctx->pkc_stage) hipFree(ctx->pkc_stage);
   ctx_streams(ctx, false);
   for (int i = 0; i < ctx->nslots; ++i) free_slot(ctx, ctx->sl[i]);
-  destroy_streams(ctx);
   delete ctx;
 }
 
