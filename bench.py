@@ -576,9 +576,13 @@ def main():
     # (the single-batch latency is timed without the per-stage hipEvents, in both slot forms -- three
     # streams, and the one-stream fused path the throughput run uses -- and batch_latency_ms is the
     # faster; the per-stage times come from three more batches with the events on)
-    def one_batch_latency(streams):
-        if lib.ssb_set_pipeline_depth(eng.handle, 1) != 0 or lib.ssb_set_slot_streams(eng.handle, streams) != 0:
+    def one_batch_latency(n_streams):
+        if lib.ssb_set_pipeline_depth(eng.handle, 1) != 0 or lib.ssb_set_slot_streams(eng.handle, n_streams) != 0:
             raise RuntimeError("ssb_set_pipeline_depth / ssb_set_slot_streams")
+        # (reconfiguring the slots destroys their streams: no cached handle of an old one may be
+        # passed as the caller's stream -- a use after free that crashed a run under rocprofv3, round 5)
+        streams.clear()
+        call_args.clear()
         step(0, 0)
         exchange_group()
         torch.cuda.synchronize(dev)

@@ -355,6 +355,23 @@ SSB_FN uint32_t combine_job(int j, const uint32_t* __restrict__ off, const uint3
   if (kind == 1u) combine_small_job(out96 + 96 * (size_t)j, sig_aff, ids, sel + b, t);
   return kind;
 }
+// Ratio jobs take the lane-uniform ratio combine only where they fill a wave: with fewer than
+// RATIO_MIN_JOBS of a wave's 64 jobs marked 2 (ids 1..n with a share skipped -- the jobs an invalid
+// share leaves behind -- are ratio jobs too, a few per wave), the wave would run the whole ratio
+// chain (~9k dependent Fp products on ONE lane) for them, and its latency set the batch's tail: at
+// 1e-2 invalid shares k_combine_sum averaged 11.6 ms and k_combine_terms_gls 4.9 ms per launch
+// (round 5).  Those jobs take the general combine instead (lambda_i from unit_lagrange_fast, four GLS
+// lanes per share, spread over many lanes).  Work per wave: ratio ~9k products whatever the number of
+// ratio lanes, general ~2.9k per 64 GLS lanes = 12 lanes per 3-of-n job: equal at ~16 jobs.
+// Every lane of the wave must call this (a ballot); the wave's 64 jobs are 64 consecutive js.
+constexpr uint32_t RATIO_MIN_JOBS = 16;
+SSB_INL uint32_t ratio_by_wave(uint32_t f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t m = __ballot(f == 2u);
+  if (f == 2u && (uint32_t)__popcll(m) < RATIO_MIN_JOBS) return 0u;
+#endif
+  return f;
+}
 // the ratio coefficients of a job combine_job marked 2 (recomputed: a few 64-bit operations)
 SSB_INL void ratio_coeffs(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                           const uint32_t* __restrict__ sel, const uint64_t* __restrict__ ids, int64_t* c,

@@ -156,7 +156,7 @@ __global__ void SSB_LB(64) k_select_combine(int n_jobs, uint32_t n_shares, const
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;
   select_job(j, n_shares, off, tt, ids, verdict, flags, sel, status, err, wst);
-  const uint32_t f = combine_job(j, off, tt, status, sel, ids, sig_aff, out96, ratio);
+  const uint32_t f = ratio_by_wave(combine_job(j, off, tt, status, sel, ids, sig_aff, out96, ratio));
   fast[j] = f;
   if (!f && status[j] == SSB_DVF_OK) lagrange_job(j, off, tt, ids, sel, lam);
 }

@@ -18,7 +18,7 @@ namespace k {
 // the scratch each slot queue reserves)
 SSB_FN void spec_job(int j, const spec_jobs& sj) {
   select_job(j, sj.n_shares, sj.off, sj.tt, sj.ids, (const uint8_t*)nullptr, sj.flags, sj.sel, sj.status, sj.err, sj.wst);
-  const uint32_t fj = combine_job(j, sj.off, sj.tt, sj.status, sj.sel, sj.ids, sj.sig_aff, sj.out96, sj.ratio);
+  const uint32_t fj = ratio_by_wave(combine_job(j, sj.off, sj.tt, sj.status, sj.sel, sj.ids, sj.sig_aff, sj.out96, sj.ratio));
   sj.fast[j] = fj;
   if (!fj && sj.status[j] == SSB_DVF_OK) lagrange_job(j, sj.off, sj.tt, sj.ids, sj.sel, sj.lam);
 }
