@@ -163,13 +163,22 @@ def long_branch_clobbers(objs):
             kernels = set(re.findall(r"\.name:\s+(\S+)", notes))
             p = subprocess.Popen([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co],
                                  stdout=subprocess.PIPE, text=True)
-            cur = None
-            for line in p.stdout:
-                if line.endswith(">:\n"):
-                    cur = line[line.index("<") + 1:-3]
-                elif "s_getpc_b64 s[30:31]" in line and cur not in kernels:
-                    bad[cur] = bad.get(cur, 0) + 1
+            for f, c in scan_disassembly(p.stdout, kernels).items():
+                bad[f] = bad.get(f, 0) + c
             p.wait()
+    return bad
+
+
+def scan_disassembly(lines, kernels):
+    """{function: count} of `s_getpc_b64 s[30:31]` in the non-kernel functions of an llvm-objdump -d
+    listing (an iterable of lines; `kernels`: the entry points' symbols, whose s[30:31] holds no return
+    address)."""
+    bad, cur = {}, None
+    for line in lines:
+        if line.rstrip("\n").endswith(">:"):
+            cur = line[line.index("<") + 1:line.rstrip("\n").rindex(">")]
+        elif "s_getpc_b64 s[30:31]" in line and cur is not None and cur not in kernels:
+            bad[cur] = bad.get(cur, 0) + 1
     return bad
 
 

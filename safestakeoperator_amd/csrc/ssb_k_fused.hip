@@ -80,6 +80,13 @@ SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, uint32_t* __restrict__ cnt,
 #ifndef SSB_DC_WAVES   // experiment knob: waves per SIMD the decode launch is built for
 #define SSB_DC_WAVES 2
 #endif
+// (the attribute's minimum alone lets the compiler trade registers for a third wave: 142 VGPRs and a
+// spilling sqrt table; SSB_DC_WAVES_MAX caps the waves so the registers stay)
+#ifdef SSB_DC_WAVES_MAX
+#define SSB_DC_ATTR amdgpu_waves_per_eu(SSB_DC_WAVES, SSB_DC_WAVES_MAX)
+#else
+#define SSB_DC_ATTR amdgpu_waves_per_eu(SSB_DC_WAVES)
+#endif
 // (blocks [3 nbd, 3 nbd + nbu): the hash's first stage, one lane per root, when the slot's counts
 // and tickets are already clean -- then no prep launch stands in front of the decode)
 // the roles out of line: each gets its own register allocation (inlined, the hash's and the decode's
@@ -121,7 +128,7 @@ SSB_ROLE void dc_pk_role(int s, const uint8_t* __restrict__ pk48, g1_aff* __rest
   pk_aff[s] = pk;
 }
 template <bool CACHED>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_DC_WAVES))) k_decode_count(int n, uint32_t nbd, const uint8_t* __restrict__ sig96,
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), SSB_DC_ATTR)) k_decode_count(int n, uint32_t nbd, const uint8_t* __restrict__ sig96,
                                            const uint8_t* __restrict__ pk48, const uint32_t* __restrict__ pk_index,
                                            uint32_t n_cache, const g1_aff* __restrict__ cache_aff,
                                            const uint32_t* __restrict__ cache_flags, g2_aff* __restrict__ sig_aff,
