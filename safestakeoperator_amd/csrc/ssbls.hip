@@ -183,11 +183,11 @@ hipStream_t slot_tail(ssb_ctx* ctx) { return ctx->tail; }
 // run every stage on the slot's stream, and an idle stream still holds one of the process's hardware
 // queues (more than ~23 mapped queues and the firmware time-slices them: measured 12.5 M partial
 // sigs/s at 23, 5.1 M at 24, 3.6 M at 25, round 5).
-int take_stream(ssb_ctx* ctx, hipStream_t* s, int prio_level);
+int take_stream(ssb_ctx* ctx, hipStream_t* s);
 void give_stream(ssb_ctx* ctx, hipStream_t& s);
 int ctx_streams(ssb_ctx* ctx, bool on) {
   for (hipStream_t* x : {&ctx->spec, &ctx->tail}) {
-    if (on && !*x && take_stream(ctx, x, 0)) return SSB_EHIP;
+    if (on && !*x && take_stream(ctx, x)) return SSB_EHIP;
     if (!on && *x) { hipStreamSynchronize(*x); give_stream(ctx, *x); }
   }
   return SSB_OK;
@@ -215,37 +215,21 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 // else: the idle pooled queues kept their scratch, and a 20-slot fallback batch after the collector
 // tests' contexts then failed with OUT_OF_RESOURCES.  bench.py instead creates its slots once, before
 // the process group.)
-int take_stream(ssb_ctx* ctx, hipStream_t* s, int prio_level = 0) {
+int take_stream(ssb_ctx* ctx, hipStream_t* s) {
   (void)ctx;
-  hipError_t e;
-  if (prio_level) {   // 1: the device's greatest priority, 2: between, 3: least (== default)
-    int least = 0, greatest = 0;
-    hipDeviceGetStreamPriorityRange(&least, &greatest);
-    const int pr = prio_level == 1 ? greatest : prio_level == 2 ? (least + greatest) / 2 : least;
-    e = hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr);
-  } else {
-    e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-  }
-  if (e != hipSuccess) { *s = nullptr; return SSB_EHIP; }
+  if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) { *s = nullptr; return SSB_EHIP; }
   return launch::prime_queue(*s) ? SSB_EHIP : SSB_OK;
 }
-// SSB_SLOT_PRIO=1 (experiment): the one-stream slots' streams in three priority bands by slot index
-// (slots 0-6 greatest, 7-13 middle, 14-19 least), so that a burst of batches finishes staggered
-// instead of all reaching their latency-bound tails together
-int slot_prio_level(const ssb_ctx* ctx, int slot, int streams) {
-  (void)ctx;
-  const char* v = getenv("SSB_SLOT_PRIO");
-  if (!v || streams != 1) return 0;
-  const int b = slot * 3 / 20 + 1;
-  return b > 3 ? 3 : b;
-}
+// (Round 5 measured slot streams in three priority bands -- hipStreamCreateWithPriority, so a burst's
+// batches would finish staggered: 20 steps 9.2-10.0 M against 12.6-12.7 M without, 200 steps 10.5 M
+// against 14.2-14.5 M, gpurun_out/r05prio.  Not kept.)
 void give_stream(ssb_ctx* ctx, hipStream_t& s) {
   (void)ctx;
   if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); }
   s = nullptr;
 }
 int init_slot(ssb_ctx* ctx, ssb_slot& S, int streams) {
-  if (take_stream(ctx, &S.stream, slot_prio_level(ctx, (int)(&S - ctx->sl), streams))) return SSB_EHIP;
+  if (take_stream(ctx, &S.stream)) return SSB_EHIP;
   S.shared = streams == 1;
   for (int i = 0; i < 2; ++i) {
     if (S.shared) S.side[i] = S.stream;
