@@ -550,16 +550,25 @@ SSB_INL fp fp_pick8(const fp* t, int i) {
 }
 // (_inl twins: bodies for the occupancy-2 per-share kernels, which must not call out of line --
 // a call's callee-saved registers and frame keep the kernel at one wave per SIMD)
+// (the odd powers as eight named values picked by a switch on the uniform digit: as an array indexed
+// by it, the compiler kept the table in scratch and every multiplication of the loop reloaded an
+// entry from there -- 12 scratch loads per step in each of the decompression's square roots, round 5)
 SSB_INL void fp_pow_sw_inl(fp& r, const fp& a, const uint8_t* sch, int n) {
-  fp t[8], a2;
-  t[0] = a;
+  fp t0 = a, t1, t2, t3, t4, t5, t6, t7, a2;
   fp_sqr(a2, a);
-  for (int i = 1; i < 8; ++i) fp_mul(t[i], t[i - 1], a2);
-  fp acc = fp_pick8(t, (sch[1] - 1) >> 1);
+  fp_mul(t1, t0, a2); fp_mul(t2, t1, a2); fp_mul(t3, t2, a2); fp_mul(t4, t3, a2);
+  fp_mul(t5, t4, a2); fp_mul(t6, t5, a2); fp_mul(t7, t6, a2);
+  auto pick = [&](int i) -> fp {
+    switch (i) {
+      case 0: return t0; case 1: return t1; case 2: return t2; case 3: return t3;
+      case 4: return t4; case 5: return t5; case 6: return t6; default: return t7;
+    }
+  };
+  fp acc = pick((sch[1] - 1) >> 1);
   for (int s = 1; s < n; ++s) {
     const int sq = sch[2 * s], d = sch[2 * s + 1];
     for (int k = 0; k < sq; ++k) fp_sqr(acc, acc);
-    if (d) { const fp m = fp_pick8(t, (d - 1) >> 1); fp_mul(acc, acc, m); }
+    if (d) { const fp m = pick((d - 1) >> 1); fp_mul(acc, acc, m); }
   }
   r = acc;
 }

@@ -91,7 +91,23 @@ SSB_INL void sort_scan_wave(uint32_t K, uint32_t K2, uint32_t* __restrict__ cnt,
 // and tickets are already clean -- then no prep launch stands in front of the decode)
 // the roles out of line: each gets its own register allocation (inlined, the hash's and the decode's
 // demands were merged into one allocation for every lane of the launch, and all of them spilled)
-SSB_ROLE void dc_hash_role(int i, const uint8_t* __restrict__ roots, const dst_arg& dst, fp2* __restrict__ u) {
+// a record of B bytes (a multiple of 16) into b: 16-byte loads when the array is 16-byte aligned (the
+// device buffers and workspaces are), else bytes -- one dwordx4 load per 16 bytes instead of 16
+// byte loads (round 5: the decode launch's instruction count and reported traffic)
+template <int B>
+SSB_INL void load_record(uint8_t* __restrict__ b, const uint8_t* __restrict__ rec, const uint8_t* __restrict__ base) {
+  if (((uintptr_t)base & 15u) == 0) {
+    const uint4* q = (const uint4*)rec;
+#pragma unroll
+    for (int k = 0; k < B / 16; ++k) ((uint4*)b)[k] = q[k];
+  } else {
+    for (int k = 0; k < B; ++k) b[k] = rec[k];
+  }
+}
+// (out of line, the DST by value: inlined, the kernel copied the 256-byte kernel argument into its
+// private frame at entry for the role's pointer -- in every wave of every role, 256 B of scratch
+// writes per share: most of the launch's HBM writes, round 5 PMC)
+SSB_FN void dc_hash_role(int i, const uint8_t* __restrict__ roots, const dst_arg dst, fp2* __restrict__ u) {
   uint8_t m[32];
   for (int k = 0; k < 32; ++k) m[k] = roots[32 * i + k];
   fp2 u0, u1;
@@ -115,14 +131,14 @@ SSB_ROLE void dc_sig_role(int s, const uint8_t* __restrict__ sig96, g2_aff* __re
     jm.share_root[s] = r;
   }
   uint8_t b[96];
-  for (int k = 0; k < 96; ++k) b[k] = sig96[96 * (size_t)s + k];
+  load_record<96>(b, sig96 + 96 * (size_t)s, sig96);
   g2_aff sig;
   sflags[s] = unit_decode_sig(sig, b);
   sig_aff[s] = sig;
 }
 SSB_ROLE void dc_pk_role(int s, const uint8_t* __restrict__ pk48, g1_aff* __restrict__ pk_aff, uint32_t* __restrict__ pflags) {
   uint8_t b[48];
-  for (int k = 0; k < 48; ++k) b[k] = pk48[48 * (size_t)s + k];
+  load_record<48>(b, pk48 + 48 * (size_t)s, pk48);
   g1_aff pk;
   pflags[s] = unit_decode_pk(pk, b);
   pk_aff[s] = pk;
