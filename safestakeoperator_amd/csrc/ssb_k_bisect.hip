@@ -662,9 +662,14 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
   const int ACC = F1, IN = F1 + 12;
   if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)ftot)[lane_];
   __syncthreads();
+  // (a root without suspects contributed m(O, H(r)) = 1: skipped -- with one invalid share per batch,
+  // 64 of the 65 values; every product here is a lane-program Fp12 product on this one block)
+  const fp one = fp_one();
   for (int i = 0; i <= n_roots; ++i) {
-    if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&fex[i])[lane_];
-    __syncthreads();
+    fp v = fp_zero();
+    if (lane_ < 12) { v = ((const fp*)&fex[i])[lane_]; g.s[IN + lane_] = v; }
+    const bool is_one = lane_ >= 12 || (lane_ == 0 ? fp_eq(v, one) : fp_is_zero(v));
+    if (__syncthreads_and(is_one ? 1 : 0)) continue;   // uniform: the value is 1
     f12_mul(g, ACC, IN, ACC);
   }
   f12_final_exp(g, ACC, TMP);
