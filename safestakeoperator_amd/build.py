@@ -182,13 +182,27 @@ def scan_disassembly(lines, kernels):
     return bad
 
 
+def _guards(objs):
+    try:
+        check_private_segments(objs, os.path.join(OBJDIR, "kernel_resources.json"))
+    except RuntimeError as e:
+        if not VARIANT:
+            raise
+        print("[ssbls] variant %s: %s" % (VARIANT, e), flush=True)   # experiment builds: reported only
+    clob = long_branch_clobbers(objs)
+    if clob:
+        raise RuntimeError("callable device functions whose long branches overwrite the return address "
+                           "s[30:31] (they would never return; split them into smaller out-of-line steps): %s"
+                           % clob)
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     want = _source_hash()
     if not force and os.path.exists(LIB) and os.path.exists(STAMP) and open(STAMP).read().strip() == want:
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
     headers = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(HERE, "..", "include", "ssbls.h")]
-    procs, objs = [], []
+    procs, objs, fresh = [], [], []
     for s in SOURCES:
         obj = os.path.join(OBJDIR, s.replace(".hip", ".o"))
         objs.append(obj)
@@ -207,19 +221,17 @@ def build(force: bool = False, verbose: bool = True) -> str:
         os.replace(obj + ".tmp", obj)
         with open(stamp, "w") as f:
             f.write(h + "\n")
-    # private-segment guard (before the library is replaced): kernel_resources.json beside the objects
+        fresh.append(stamp)
+    # private-segment and long-branch guards (before the library is replaced): kernel_resources.json
+    # beside the objects; a refused object's stamp is removed so that it does not pass as built next time
     if os.path.exists(os.path.join(LLVM, "clang-offload-bundler")):
         try:
-            check_private_segments(objs, os.path.join(OBJDIR, "kernel_resources.json"))
-        except RuntimeError as e:
-            if not VARIANT:
-                raise
-            print("[ssbls] variant %s: %s" % (VARIANT, e), flush=True)   # experiment builds: reported only
-        clob = long_branch_clobbers(objs)
-        if clob:
-            raise RuntimeError("callable device functions whose long branches overwrite the return address "
-                               "s[30:31] (they would never return; split them into smaller out-of-line steps): %s"
-                               % clob)
+            _guards(objs)
+        except RuntimeError:
+            for st in fresh:
+                if os.path.exists(st):
+                    os.remove(st)
+            raise
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
     if verbose:
         print("[ssbls] linking:", " ".join(cmd), flush=True)
