@@ -538,45 +538,21 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
     }
 }
 
-// -sum k_i pk_i over the suspects of one root's segment of the root-sorted order (lane 0; infinity
-// on the other lanes): products on the lanes, a lane tree
-SSB_FN g1_aff neg_suspect_sum(uint32_t sb, uint32_t nr, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
-                              const uint64_t* __restrict__ k64, const g1_aff* __restrict__ pk_aff) {
-  const int lane_ = threadIdx.x;
-  g1_jac acc;
-  jac_set_inf(acc);
-  for (uint32_t k = sb + lane_; k < sb + nr; k += 64) {
-    const uint32_t s = perm[k];
-    if (!(flags[s] & FLAG_SUSPECT)) continue;
-    const uint64_t kk = k64[s];
-    const uint32_t kw[2] = {(uint32_t)kk, (uint32_t)(kk >> 32)};
-    g1_jac p;
-    jac_mul_aff(p, pk_aff[s], kw, 2);
-    jac_add(acc, acc, p);
-  }
-  for (int h = 32; h >= 1; h >>= 1) {
-    const g1_jac o = shfl_down_pt(acc, h);
-    if (lane_ < h) jac_add(acc, acc, o);
-  }
-  g1_aff P;
-  P.inf = true;
-  if (lane_ == 0 && !jac_is_inf(acc)) { jac_to_aff(P, acc); fp_neg(P.y, P.y); }
-  return P;
-}
-
 // The committee stage's checks (after k_fb_rlc's consistency pass listed the suspects, nS <=
 // FB_SUSPECT_MAX; otherwise a no-op and the tree decides):
 //   * the EXCLUSION check -- the batch check without the suspects:
 //       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
-//       E_r = sum_{suspects of root r} k_i pk_i  (block r: products on the lanes, a lane tree),
-//       X   = sum_{suspects} k_i sig_i          (blocks n_roots .. +3: 4-bit-digit bucket sums),
-//     where ftot is the batch check's own Miller product (k_miller_final) -- by bilinearity this is
-//     the RLC check over every non-suspect candidate with the batch's own scalars (soundness 2^-63),
-//     at the cost of one Miller loop per root holding suspects: *xok = 1 decides them all valid;
+//       E_r = sum_{suspects of root r} k_i pk_i = sum_q 2^16q E_{r,q}  (blocks 4r + q),
+//       X   = sum_{suspects} k_i sig_i   = sum_q 2^16q X_q      (blocks 4 n_roots + q),
+//     the quarters' 4-bit-digit bucket sums, each paired on its own (ex_root_quarter, ex_quarter_point:
+//     the same value after the exponentiation), where ftot is the batch check's own Miller product
+//     (k_miller_final) -- by bilinearity this is the RLC check over every non-suspect candidate with
+//     the batch's own scalars (soundness 2^-63), at the cost of four Miller loops per root holding
+//     suspects: *xok = 1 decides them all valid;
 //   * every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's verify
-//     (blocks n_roots + 4 ..).
-// The pair blocks finish with completion tickets (xtk[0]: pairs, xtk[1]: X's quarters); the last
-// pair multiplies ftot by the n_roots + 1 Miller values and runs ONE final exponentiation.
+//     (blocks ex_pairs(n_roots) ..).
+// The pair blocks finish with a completion ticket (xtk[0]); the last pair multiplies ftot by the
+// ex_pairs(n_roots) Miller values (those without suspects skipped: 1) and runs ONE final exponentiation.
 // (the roles of k_fb_excl are out of line: each role's temporaries live in its own frame, and the
 // kernel's private segment is the largest role's, not their sum)
 struct ex_lds { fr_lds u; uint32_t flg, last, ncand; g1_aff sP; g2_aff sQ; };
@@ -595,51 +571,67 @@ SSB_FN void ex_singles(ex_lds& L, int first, uint32_t ns, const uint32_t* __rest
     if (lane_ == 0) verdict[s] = pass ? 1 : 0;
   }
 }
-// the exclusion pair of block `blk` (root r < n_roots: -E_r; n_roots .. +3: the quarters of X) into
-// fex[pair]; returns true in the block that must run the final product (tickets).  The two roles are
-// separate functions (each frame holds one role's temporaries; the deepest call chain of k_fb_excl
-// runs through the X role: quarter_sum's frame under this one).
-SSB_FN void ex_pair_root(ex_lds& L, int r, const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
-                         const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
-                         const uint64_t* __restrict__ k64, const g1_aff* __restrict__ pk_aff,
-                         const g2_aff* __restrict__ H) {
+// The exclusion pairs, one block each (k_fb_excl's blocks 0 .. ex_pairs(n_roots) - 1): the Miller value
+// into fex[pair], then ex_pair_ticket.  Root r's E_r and X are both split into the quarters of the
+// scalars (bits 16q .. 16q+15: quarter_sum's 4-bit-digit bucket sums on the block's lanes):
+//   block 4r + q           m(-[2^16q] E_{r,q}, H(r))   (ex_root_quarter),
+//   block 4 n_roots + q    m([2^16q] g1, X_q)          (ex_quarter_point),
+// whose product over q is m(-E_r, H(r)), resp. m(g1, X), after the final exponentiation.  No block
+// runs a 64-bit scalar product on one lane (the one-invalid batch's chain, round-5 trace: the root
+// pair holding its suspect ended at 6.9 ms, the X quarters at 2.8 ms).  Each role ends with the pair's
+// points in L.sP / L.sQ and the block synchronised (the bucket lists dead), then ex_pair_lds.
+// (roles out of line, called one after the other from the kernel: the quarter sum's frame and the
+// Miller loop's are never on the call chain together)
+SSB_FN void ex_root_quarter(ex_lds& L, int r, int q, const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                            const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
+                            const uint64_t* __restrict__ k64, const g1_aff* __restrict__ pk_aff,
+                            const g2_aff* __restrict__ H) {
+  const uint32_t* list = perm + start[r];
+  const uint32_t nr = cnt[r];
+  bool any = false;
+  for (uint32_t x = threadIdx.x; x < nr; x += 64) any |= (flags[list[x]] & FLAG_SUSPECT) != 0u;
+  if (!__syncthreads_or(any ? 1 : 0)) {   // uniform: no suspect in the root -- m(O, H(r)) = 1
+    if (threadIdx.x == 0) { g1_aff P; P.inf = true; L.sP = P; L.sQ = H[r]; }
+    __syncthreads();
+    return;
+  }
+  const g1_jac a = quarter_sum<fp>(L.u.b, list, nr, flags, FLAG_SUSPECT, k64, pk_aff, q);
+  if (threadIdx.x == 0) {
+    g1_jac t = a;
+    for (int i = 0; i < 16 * q; ++i) jac_dbl_inl(t, t);   // (infinity stays infinity: Z = 0)
+    g1_aff P;
+    jac_to_aff(P, t);
+    if (!P.inf) fp_neg(P.y, P.y);   // -[2^16q] E_{r,q}
+    L.sP = P;
+    L.sQ = H[r];
+  }
+  __syncthreads();
+}
+// X's quarter q (ex_quarter_point, then ex_pair_lds): X_q = sum over the suspects of (bits 16q .. 16q+15 of k_i) sig_i, paired with
+// [2^16q] g1 -- m(g1, X) is replaced by the product of the four m([2^16q] g1, X_q), equal after the
+// final exponentiation (X = sum_q 2^16q X_q).  Each quarter's block runs its own Miller loop: no
+// block waits for the other quarters, and the 48 doublings that combined them on one lane (with an
+// inversion and the combined Miller loop after them: the one-invalid batch's exclusion chain, 7.6 of
+// its 9.4 ms, round-5 trace) leave the critical path.
+// (two functions called one after the other from the kernel: the quarter sum's frame and the Miller
+// loop's are never on the call chain together)
+// (the quarter sum stored by quarter_sum_to, then its affine form and the pair's G1 point into LDS)
+SSB_FN void ex_quarter_point(ex_lds& L, int q, const g2_jac* __restrict__ Xq, const g1_aff* __restrict__ negg1_pow) {
+  if (threadIdx.x == 0) {
+    g2_aff Q;
+    { const g2_jac x = *Xq; jac_to_aff(Q, x); }
+    L.sQ = Q;
+    g1_aff P = negg1_pow[16 * q];
+    fp_neg(P.y, P.y);   // [2^16q] g1
+    L.sP = P;
+  }
+}
+SSB_FN void ex_pair_lds(ex_lds& L) {
   using namespace ssb::lane;
   grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, (int)threadIdx.x};
   const int F1 = BS_S0, B = F1 + 24;
-  const g1_aff P = neg_suspect_sum(start[r], cnt[r], perm, flags, k64, pk_aff);   // -E_r (lane 0)
-  __syncthreads();
   lp_init_consts(g);
-  miller_one(g, P, H[r], F1, B, L.flg);
-}
-// X's quarter q; returns false in the blocks that are not the last of the four (they are done)
-SSB_FN bool ex_pair_x(ex_lds& L, int q, uint32_t ns, const uint32_t* __restrict__ slist,
-                      const uint32_t* __restrict__ flags, const uint64_t* __restrict__ k64,
-                      const g2_aff* __restrict__ sig_aff, g2_jac* __restrict__ X4, uint32_t* __restrict__ xtk) {
-  using namespace ssb::lane;
-  const int lane_ = threadIdx.x;
-  {
-    const g2_jac acc = quarter_sum<fp2>(L.u.b, slist, ns, flags, FLAG_SUSPECT, k64, sig_aff, q);
-    if (lane_ == 0) X4[q] = acc;
-  }
-  __threadfence();
-  __syncthreads();
-  if (lane_ == 0) L.last = atomicAdd(&xtk[1], 1u) == 3u ? 1u : 0u;
-  __syncthreads();
-  if (!L.last) return false;
-  __threadfence();
-  {
-    const g2_aff Q = combine_quarters<fp2>(X4);
-    if (lane_ == 0) L.sQ = Q;
-  }
-  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
-  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
-  const int F1 = BS_S0, B = F1 + 24;
-  lp_init_consts(g);
-  if (lane_ == 0) { L.sP = g1_neg_generator(); fp_neg(L.sP.y, L.sP.y); }   // +g1
-  __syncthreads();
   miller_one(g, L.sP, L.sQ, F1, B, L.flg);
-  if (lane_ == 0) xtk[1] = 0u;
-  return true;
 }
 // the pair's Miller value into fex[pair], then the pairs' ticket: true in the block that runs the product
 SSB_INL bool ex_pair_ticket(ex_lds& L, int n_roots, int pair, fp12* __restrict__ fex, uint32_t* __restrict__ xtk) {
@@ -647,11 +639,11 @@ SSB_INL bool ex_pair_ticket(ex_lds& L, int n_roots, int pair, fp12* __restrict__
   if (lane_ < 12) ((fp*)&fex[pair])[lane_] = L.u.s[lane::LP_NCODE_CONST + BS_S0 + lane_];   // (g.s + F1 of the roles)
   __threadfence();
   __syncthreads();
-  if (lane_ == 0) L.last = atomicAdd(&xtk[0], 1u) == (uint32_t)n_roots ? 1u : 0u;
+  if (lane_ == 0) L.last = atomicAdd(&xtk[0], 1u) == (uint32_t)(launch::ex_pairs(n_roots) - 1) ? 1u : 0u;
   __syncthreads();
   return L.last != 0;
 }
-// ftot * prod of the n_roots + 1 exclusion values, ONE final exponentiation -> *xok
+// ftot * prod of the ex_pairs(n_roots) exclusion values, ONE final exponentiation -> *xok
 SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, const fp12* __restrict__ fex,
                      uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok) {
   using namespace ssb::lane;
@@ -662,15 +654,24 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
   const int ACC = F1, IN = F1 + 12;
   if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)ftot)[lane_];
   __syncthreads();
-  // (a root without suspects contributed m(O, H(r)) = 1: skipped -- with one invalid share per batch,
-  // 64 of the 65 values; every product here is a lane-program Fp12 product on this one block)
+  // (a quarter without suspects contributed m(O, Q) = 1: skipped -- with one invalid share per batch,
+  // 256 of the 260 values.  Lane i tests value base + i, a ballot lists the others; every product
+  // here is a lane-program Fp12 product on this one block)
   const fp one = fp_one();
-  for (int i = 0; i <= n_roots; ++i) {
-    fp v = fp_zero();
-    if (lane_ < 12) { v = ((const fp*)&fex[i])[lane_]; g.s[IN + lane_] = v; }
-    const bool is_one = lane_ >= 12 || (lane_ == 0 ? fp_eq(v, one) : fp_is_zero(v));
-    if (__syncthreads_and(is_one ? 1 : 0)) continue;   // uniform: the value is 1
-    f12_mul(g, ACC, IN, ACC);
+  const int np = launch::ex_pairs(n_roots);
+  for (int base = 0; base < np; base += 64) {
+    bool keep = false;
+    if (base + lane_ < np) {
+      const fp* v = (const fp*)&fex[base + lane_];
+      keep = !fp_eq(v[0], one);
+      for (int k = 1; k < 12 && !keep; ++k) keep = !fp_is_zero(v[k]);
+    }
+    for (uint64_t m = __ballot(keep); m; m &= m - 1) {   // uniform
+      const int i = base + __builtin_ctzll(m);
+      if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&fex[i])[lane_];
+      __syncthreads();
+      f12_mul(g, ACC, IN, ACC);
+    }
   }
   f12_final_exp(g, ACC, TMP);
   const bool pass = f12_slots_one(g, ACC);
@@ -727,14 +728,13 @@ SSB_FN void ex_group_check(ex_lds& L, const uint32_t* __restrict__ list, uint32_
 // The committee stage's checks, after k_fb_rlc's consistency pass listed the suspects (nS of them):
 //   nS <= FB_SUSPECT_MAX -- the EXCLUSION check, the batch check without the suspects:
 //       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
-//       E_r = sum_{suspects of root r} k_i pk_i  (block r: products on the lanes, a lane tree),
-//       X   = sum_{suspects} k_i sig_i          (blocks n_roots .. +3: 4-bit-digit bucket sums),
-//     where ftot is the batch check's own Miller product (k_miller_final) -- by bilinearity this is
-//     the RLC check over every non-suspect candidate with the batch's own scalars (soundness 2^-63),
-//     at the cost of one Miller loop per root holding suspects: *xok = 1 decides them all valid;
+//       E_r and X split into the quarters of the scalars, one pair block per quarter (blocks 4r + q,
+//       then 4 n_roots + q: see ex_root_quarter), ftot the batch check's own Miller product
+//       (k_miller_final) -- by bilinearity the RLC check over every non-suspect candidate with the
+//       batch's own scalars (soundness 2^-63): *xok = 1 decides them all valid;
 //     and every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's
-//     verify (blocks n_roots + 4 ..).  The pair blocks finish with completion tickets (xtk[0]: pairs,
-//     xtk[1]: X's quarters); the last pair runs the product and ONE final exponentiation;
+//     verify (blocks ex_pairs(n_roots) ..).  The pair blocks finish with a completion ticket (xtk[0]); the
+//     last pair runs the product and ONE final exponentiation;
 //   nS > FB_SUSPECT_MAX -- GROUP-TEST mode (e.g. a faulty operator in every committee): *xok = 2, and
 //     the blocks run one RLC check per (root, operator-id bucket) group of candidates, k_fb_root
 //     deduces the rest from the committee relations (deduce_job), k_fb_single checks what is left;
@@ -748,8 +748,10 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
                                      const fp12* __restrict__ ftot, fp12* __restrict__ fex, g2_jac* __restrict__ X4,
                                      uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict,
                                      const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ kstart,
-                                     uint32_t* __restrict__ cursor, g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1) {
+                                     uint32_t* __restrict__ cursor, g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1,
+                                     const g1_aff* __restrict__ negg1_pow) {
   if (*ok) return;   // uniform: the batch passed
+  SSB_TRACE_T0();
   const uint32_t ns = *nS;
   const int blk = blockIdx.x, lane_ = threadIdx.x;
   const bool gmode = ns > FB_SUSPECT_MAX && kcnt;
@@ -769,6 +771,7 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
       const uint32_t* list = perm + kstart[key];
       quarter_sum_to<fp2>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, sig_aff, (int)q, gX2 + 4 * key + q);
       quarter_sum_to<fp>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, pk_aff, (int)q, gX1 + 4 * key + q);
+      SSB_TRACE(TR_EX_ITEM);
       __threadfence();
       __syncthreads();
       if (lane_ == 0) L.last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
@@ -785,21 +788,35 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
       if (!m) continue;   // uniform
       group_combine(L, gX2 + 4 * key, gX1 + 4 * key);
       __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+      SSB_TRACE(TR_EX_GCOMB);
       ex_group_check(L, list, gn, m, flags, H[key / NB], verdict);
+      SSB_TRACE(TR_EX_GCHECK);
     }
     return;
   }
-  if (blk >= n_roots + 4) {   // the suspects, one pairing check each
-    ex_singles(L, n_roots + 4, ns, slist, share_root, sig_aff, pk_aff, H, verdict);
+  const int npairs = launch::ex_pairs(n_roots);
+  if (blk >= npairs) {   // the suspects, one pairing check each
+    ex_singles(L, npairs, ns, slist, share_root, sig_aff, pk_aff, H, verdict);
+    SSB_TRACE(TR_EX_SINGLE);
     return;
   }
-  if (blk < n_roots) {
-    ex_pair_root(L, blk, start, cnt, perm, flags, k64, pk_aff, H);
-  } else if (!ex_pair_x(L, blk - n_roots, ns, slist, flags, k64, sig_aff, X4, xtk)) {
-    return;
+  if (blk < 4 * n_roots) {
+    ex_root_quarter(L, blk >> 2, blk & 3, start, cnt, perm, flags, k64, pk_aff, H);
+    ex_pair_lds(L);
+    SSB_TRACE(TR_EX_ROOTPAIR);
+  } else {
+    const int q = blk - 4 * n_roots;
+    quarter_sum_to<fp2>(L.u.b, slist, ns, flags, FLAG_SUSPECT, k64, sig_aff, q, X4 + q);
+    SSB_TRACE(TR_EX_QSUM);
+    ex_quarter_point(L, q, X4 + q, negg1_pow);   // (lane 0 wrote X4[q] and reads it back)
+    __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+    ex_pair_lds(L);
+    SSB_TRACE(TR_EX_PAIR);
   }
-  if (ex_pair_ticket(L, n_roots, blk < n_roots ? blk : n_roots, fex, xtk))
+  if (ex_pair_ticket(L, n_roots, blk, fex, xtk)) {
     ex_final(L, n_roots, ftot, fex, xtk, xok);
+    SSB_TRACE(TR_EX_FINAL);
+  }
 }
 
 // Few shares in failing roots (<= FB_SINGLE_MAX after level 0): each of them checked alone,
@@ -974,11 +991,11 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + nb((size_t)cj.n_jobs, 64) + 1), dim3(64), 0, st, n, key, ok, flags,
                      fw.k64, fast_verdicts ? verdict : (uint8_t*)nullptr, prep, cj, sig, fw.slist, fw.nS);
   if (committee)
-    hipLaunchKernelGGL(k_fb_excl, dim3((unsigned)n_roots + 4 + EX_SINGLE_BLOCKS), dim3(64), 0, st, n_roots, ok,
+    hipLaunchKernelGGL(k_fb_excl, dim3((unsigned)ex_pairs(n_roots) + EX_SINGLE_BLOCKS), dim3(64), 0, st, n_roots, ok,
                        (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
                        (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
                        fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart,
-                       fw.cursor, fw.rsig, fw.rpk);
+                       fw.cursor, fw.rsig, fw.rpk, fw.negg1_pow);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
                      (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                      (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,
@@ -1006,3 +1023,5 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
 
 }  // namespace launch
 }  // namespace ssb
+
+SSB_TRACE_READER(bisect)

@@ -21,7 +21,8 @@
 // translation unit (read back by ssb_debug_trace_<tu>), so the critical path inside a fused launch
 // can be read without perturbing it; the product library compiles these to nothing.
 #ifdef SSB_TRACE_TAIL
-enum { TR_W2_G2 = 1, TR_W2_G1, TR_W2_HORNER, TR_W2_CLEAR, TR_W2_AFFINE, TR_MF_MILLER, TR_MF_GROUP, TR_MF_PRODUCT, TR_MF_FINAL };
+enum { TR_W2_G2 = 1, TR_W2_G1, TR_W2_HORNER, TR_W2_CLEAR, TR_W2_AFFINE, TR_MF_MILLER, TR_MF_GROUP, TR_MF_PRODUCT, TR_MF_FINAL,
+       TR_EX_ITEM, TR_EX_GCOMB, TR_EX_GCHECK, TR_EX_SINGLE, TR_EX_PAIR, TR_EX_FINAL, TR_EX_ROOTPAIR, TR_EX_QSUM };
 static __device__ unsigned long long ssb_trace_buf[4 * 2048];
 static __device__ unsigned int ssb_trace_n;
 #define SSB_TRACE_T0() const unsigned long long trace_t0_ = wall_clock64()
@@ -279,14 +280,18 @@ struct fb_ws {
   g1_jac* rpk;
   uint8_t *gv0, *gv1;
   // the committee stage (aggregate batches on the fused path; all null otherwise): slist n words,
-  // fex n_roots + 1 values, ftot = the batch check's Miller product before the final exponentiation
+  // fex ex_pairs(n_roots) values, ftot = the batch check's Miller product before the final exponentiation
   // (k_miller_final), nS / xtk: two words of the slot's ticket block (zero on entry, zeroed again
   // by their consumers), xok one word
   uint32_t *slist, *nS, *xtk, *xok;
   fp12* fex;
   const fp12* ftot;
   uint32_t *kcnt, *kstart;   // per (root, id bucket) key: fb_keys(n_roots) words each (cursor too)
+  const g1_aff* negg1_pow;   // [2^s](-g1), s < 64 (the exclusion check pairs quarter q of X with [2^16q] g1)
 };
+// the exclusion check's Fp12 values: one per quarter of every root's E_r and of X (k_fb_excl's
+// pair blocks, in that order)
+constexpr int ex_pairs(int n_roots) { return 4 * n_roots + 4; }
 // the jobs of an aggregate batch (share_off, t, ids), for the committee stage of the fallback
 struct fb_jobs { int n_jobs; const uint32_t* off; const uint32_t* tt; const uint64_t* ids; };
 int fallback_log2_branch();

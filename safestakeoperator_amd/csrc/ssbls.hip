@@ -456,7 +456,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          3 * align_up(n_roots * 4) + align_up(n * 4) + align_up(fb_prod_slots(n, n_roots) * sizeof(g2_jac)) +
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
          align_up(n * 8) + align_up(4 * n_roots * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4) +
-         align_up(n * 4) + align_up(4) + align_up((n_roots + 1) * sizeof(fp12)) + align_up(ntk_words(np) * 4) +
+         align_up(n * 4) + align_up(4) + align_up((size_t)launch::ex_pairs((int)n_roots) * sizeof(fp12)) + align_up(ntk_words(np) * 4) +
          3 * align_up(launch::fb_keys(n_roots) * 4);
 }
 
@@ -485,7 +485,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.gst = c.take<uint32_t>((size_t)launch::fallback_levels(n) * (n_roots + 1));
   w.gv0 = c.take<uint8_t>(n + n_roots); w.gv1 = c.take<uint8_t>(n + n_roots);
   w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(4 * n_roots); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
-  w.slist = c.take<uint32_t>(n); w.xok = c.take<uint32_t>(1); w.fex = c.take<fp12>(n_roots + 1);
+  w.slist = c.take<uint32_t>(n); w.xok = c.take<uint32_t>(1); w.fex = c.take<fp12>((size_t)launch::ex_pairs((int)n_roots));
   w.kcnt = c.take<uint32_t>(launch::fb_keys(n_roots)); w.kstart = c.take<uint32_t>(launch::fb_keys(n_roots));
   w.npairs = n_roots + w.plan.g2.W;
   return w;
@@ -680,7 +680,8 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
       launch::fb_ws fw{w.rcnt, w.rstart, w.rcur, w.perm, w.gst, w.rtk, w.nfail, w.k64, w.fbX, w.rsig, w.rpk, w.gv0, w.gv1,
                        cm ? w.slist : nullptr, cm ? (uint32_t*)ptk : nullptr, cm ? (uint32_t*)ptk + 1 : nullptr,
                        cm ? w.xok : nullptr, cm ? w.fex : nullptr,
-                       cm ? w.f + w.npairs + (w.npairs + 7) / 8 : nullptr, cm ? w.kcnt : nullptr, cm ? w.kstart : nullptr};
+                       cm ? w.f + w.npairs + (w.npairs + 7) / 8 : nullptr, cm ? w.kcnt : nullptr, cm ? w.kstart : nullptr,
+                       ctx->negg1_pow};
       const launch::fb_jobs fj = cm ? launch::fb_jobs{sj->n_jobs, sj->off, sj->tt, sj->ids} : launch::fb_jobs{0, nullptr, nullptr, nullptr};
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, w.f,
                               fw, d_verdict, true, fj);
