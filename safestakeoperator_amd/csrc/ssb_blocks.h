@@ -360,15 +360,17 @@ SSB_FN uint32_t combine_job(int j, const uint32_t* __restrict__ off, const uint3
 // share leaves behind -- are ratio jobs too, a few per wave), the wave would run the whole ratio
 // chain (~9k dependent Fp products on ONE lane) for them, and its latency set the batch's tail: at
 // 1e-2 invalid shares k_combine_sum averaged 11.6 ms and k_combine_terms_gls 4.9 ms per launch
-// (round 5).  Those jobs take the general combine instead (lambda_i from unit_lagrange_fast, four GLS
-// lanes per share, spread over many lanes).  Work per wave: ratio ~9k products whatever the number of
-// ratio lanes, general ~2.9k per 64 GLS lanes = 12 lanes per 3-of-n job: equal at ~16 jobs.
+// (round 5).  Those jobs are marked 3: each runs on a workgroup of its own, its products spread
+// over eight lane groups (k_combine_sum's extra blocks, ratio_lane_job) -- the general combine
+// they took before (four GLS lanes per share, each a ~2.9k-product chain on one lane) still set a
+// 7.7-9.9 ms k_combine_terms_gls on the 1e-2 batch's chain (round 5, depth-1 trace).
 // Every lane of the wave must call this (a ballot); the wave's 64 jobs are 64 consecutive js.
 constexpr uint32_t RATIO_MIN_JOBS = 16;
+static_assert(RATIO_MIN_JOBS - 1 == RATIO_LANE_PER_WAVE, "k_combine_sum's extra blocks per wave");
 SSB_INL uint32_t ratio_by_wave(uint32_t f) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t m = __ballot(f == 2u);
-  if (f == 2u && (uint32_t)__popcll(m) < RATIO_MIN_JOBS) return 0u;
+  if (f == 2u && (uint32_t)__popcll(m) < RATIO_MIN_JOBS) return 3u;
 #endif
   return f;
 }

@@ -9,9 +9,197 @@
 #endif
 #include "ssb_kernels.h"
 #include "ssb_blocks.h"
+#include "ssb_lane_ops.h"
 
 namespace ssb {
 namespace k {
+
+// ---- fast 3: the ratio combine of a job on one workgroup's eight lane groups ----
+// (ratio jobs in a wave holding fewer than RATIO_MIN_JOBS of them; lambda_i = c_i / M)
+//   T = sum c_i sig_i       group i (< 8, then i + 8, ..) [c_i] sig_i, signed 4-bit windows (the job's
+//                           window count), the groups' terms summed by a tree through LDS;
+//   [M^-1] T                the four base-u digits k_q of M^-1 mod r (rc_digits): group q (< 4)
+//                           [k_q] (-1)^q psi^q(T), 16 windows, the tree again;
+//   affine + compress       lane 0.
+// Every product of a point operation is spread over the group's 8 lanes (the G2 lane programs,
+// ssb_lane_ops.h), so no lane runs a whole scalar chain.  All groups run the same program (the
+// window count is the job's); an inactive group works on a stand-in and its result and checks are
+// dropped.  An exceptional addition in an active group (an input at infinity, equal or opposite
+// points: degenerate or adversarial shares) sends the job to the exact single-lane combine
+// (unit_combine_ratio_w4 in the job's table region) -- as does ra.exact (SSB_RATIO_LANE_EXACT=1).
+namespace rl {
+using namespace ssb::lane;
+constexpr int NG = 8;
+constexpr int S0 = G2_ADD_SCRATCH;
+static_assert(S0 >= G2_MADD_SCRATCH && S0 >= G2_DBL_SCRATCH && S0 >= G2_PSI_SCRATCH, "program scratch");
+// group-relative slots: BASE, the table of odd multiples, ACC, TMP, X (a partner's point), SUM
+constexpr int BASE = S0, TAB = BASE + 6, ACC = TAB + 48, TMP = ACC + 6, X = TMP + 6, SUM = X + 6, GS = SUM + 6;
+struct lds { fp s[LP_NCODE_CONST + NG * GS]; uint32_t flg[NG]; };
+
+// dst = sign(d) (|d|) B from the table (d odd)
+SSB_INL void pick(grp& g, int d, int dst) {
+  const int e = TAB + 6 * (((d < 0 ? -d : d) - 1) >> 1);
+  LP_FOR(8) {
+    if (role < 6) {
+      fp v = g.s[e + role];
+      if (d < 0 && (role == 2 || role == 3)) fp_neg(v, v);
+      g.s[dst + role] = v;
+    }
+  }
+  LP_SYNC();
+}
+// ACC = [m] BASE for an odd m < 2^(4W) (per group; W uniform): table of the odd multiples, regular
+// signed windows (sw4_digit, as rc_joint_sum)
+SSB_FN void mul_odd(grp& g, uint64_t m, int W, uint32_t& exc) {
+  g2_dbl(g, BASE, TMP);
+  lg_copy<8>(g, BASE, TAB, 6);
+  for (int j = 1; j < 8; ++j) g2_add(g, TAB + 6 * (j - 1), TMP, TAB + 6 * j, exc);
+  pick(g, sw4_digit(m, W - 1, W), ACC);
+  for (int w = W - 2; w >= 0; --w) {
+    g2_dbl(g, ACC, ACC); g2_dbl(g, ACC, ACC); g2_dbl(g, ACC, ACC); g2_dbl(g, ACC, ACC);
+    pick(g, sw4_digit(m, w, W), TMP);
+    g2_add(g, ACC, TMP, ACC, exc);
+  }
+}
+// ACC = [a] BASE, negated when neg, for a != 0 (even a: [a | 1] BASE - BASE; the subtraction runs in
+// every group when any active group needs it, kept where needed)
+SSB_FN void mul_signed(grp& g, uint64_t a, bool neg, bool act, int W, uint32_t& exc) {
+  uint32_t e = 0;
+  mul_odd(g, a | 1ull, W, e);
+  const bool even = !(a & 1ull);
+  if (__syncthreads_or(even && act ? 1 : 0)) {   // uniform
+    LP_FOR(8) {
+      if (role < 6) {
+        fp v = g.s[BASE + role];
+        if (role == 2 || role == 3) fp_neg(v, v);
+        g.s[TMP + role] = v;
+      }
+    }
+    LP_SYNC();
+    uint32_t e2 = 0;
+    g2_add(g, ACC, TMP, X, e2);
+    if (even) {
+      e |= e2;
+      LP_FOR(8) { if (role < 6) g.s[ACC + role] = g.s[X + role]; }
+    }
+    LP_SYNC();
+  }
+  if (neg) {
+    LP_FOR(8) { if (role == 2 || role == 3) { fp v = g.s[ACC + role]; fp_neg(v, v); g.s[ACC + role] = v; } }
+  }
+  LP_SYNC();
+  if (act) exc |= e;
+}
+// slot S of groups 0 .. n-1 summed into group 0's (a tree: round h adds group gi + h into gi)
+SSB_FN void tree(grp& g, lfp* groups, int gi, int n, int S, uint32_t& exc) {
+  for (int h = 1; h < n; h <<= 1) {
+    const bool has = (gi % (2 * h)) == 0 && gi + h < n;
+    LP_FOR(8) { if (role < 6) g.s[X + role] = has ? groups[(gi + h) * GS + S + role] : g.s[S + role]; }
+    LP_SYNC();
+    uint32_t e = 0;
+    g2_add(g, S, X, TMP, e);
+    if (has) {
+      exc |= e;
+      LP_FOR(8) { if (role < 6) g.s[S + role] = g.s[TMP + role]; }
+    }
+    LP_SYNC();
+  }
+}
+}  // namespace rl
+
+// coefficient c_i of job j, its window count W and M (the coefficient array in this frame only)
+SSB_FN int64_t ratio_ci(int j, uint32_t i, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                        const uint32_t* __restrict__ sel, const uint64_t* __restrict__ ids, int* W, uint64_t* M) {
+  int64_t c[FAST_T];
+  ratio_coeffs(j, off, tt, sel, ids, c, M);
+  *W = rc_windows(c, tt[j]);
+  return c[i < tt[j] ? i : 0u];
+}
+// the exact single-lane ratio combine of job j (phase T into rT[j] / rk[j], then phase K)
+SSB_FN void ratio_lane_exact(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                             const uint32_t* __restrict__ sel, uint8_t* __restrict__ out96, const ratio_args& ra) {
+  {
+    int64_t c[FAST_T];
+    uint64_t M;
+    ratio_coeffs(j, off, tt, sel, ra.ids, c, &M);
+    unit_ratio_T(ra.rT + j, ra.rk + 4 * (size_t)j, ra.sig, sel + off[j], c, tt[j], M, rc_windows(c, tt[j]),
+                 ra.tabs + (size_t)j * RC_TAB_BYTES);
+  }
+  unit_ratio_K(out96 + 96 * (size_t)j, ra.rT + j, ra.rk + 4 * (size_t)j, ra.tabs + (size_t)j * RC_TAB_BYTES);
+}
+// the fast-3 job of extra block b (wave b % nw, its (b / nw)-th fast-3 job), or nothing; returns the
+// job when it must be redone exactly (ratio_lane_exact, called by the kernel: the two frames are
+// never on one call chain), else -1.  Uniform.
+SSB_FN int ratio_lane_job(rl::lds& L, int b, int nw, int n_jobs, const uint32_t* __restrict__ off,
+                           const uint32_t* __restrict__ tt, const uint32_t* __restrict__ sel,
+                           const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, const ratio_args& ra) {
+  using namespace ssb::lane;
+  const int w = b % nw, slot = b / nw, lane_ = threadIdx.x;
+  const int jl = 64 * w + lane_;
+  uint64_t m = __ballot(jl < n_jobs && fast[jl] == 3u);
+  if (__popcll(m) <= slot) return -1;   // uniform
+  for (int i = 0; i < slot; ++i) m &= m - 1;
+  const int j = 64 * w + __builtin_ctzll(m);
+  const uint32_t t = tt[j], b0 = off[j];
+  uint32_t exc = 0;
+  if (!ra.exact) {
+    const int gi = lane_ >> 3;
+    lfp* groups = (lfp*)L.s + LP_NCODE_CONST;
+    grp g{(lfp*)L.s, groups + gi * rl::GS, 0, 0, 0, (lu32*)&L.flg[gi], lane_ & 7};
+    lp_init_consts(g);
+    // T
+    int W = 1;
+    uint64_t M = 1;
+    for (uint32_t p = 0; p * rl::NG < t; ++p) {
+      const uint32_t i = p * rl::NG + (uint32_t)gi;
+      const bool act = i < t;
+      const int64_t ci = ratio_ci(j, i, off, tt, sel, ra.ids, &W, &M);   // (W, M: the job's, every lane)
+      {
+        const g2_aff q = ra.sig[sel[b0 + (act ? i : 0u)]];
+        if (g.role < 4) g.s[rl::BASE + g.role] = ((const fp*)&q)[g.role];
+        else if (g.role < 6) g.s[rl::BASE + g.role] = g.role == 4 ? fp_one() : fp_zero();
+      }
+      __syncthreads();
+      rl::mul_signed(g, (uint64_t)(ci < 0 ? -ci : ci), ci < 0, act, W, exc);
+      if (p == 0) {
+        lg_copy<8>(g, rl::ACC, rl::SUM, 6);
+      } else {
+        uint32_t e = 0;
+        g2_add(g, rl::SUM, rl::ACC, rl::TMP, e);
+        if (act) {
+          exc |= e;
+          if (g.role < 6) g.s[rl::SUM + g.role] = g.s[rl::TMP + g.role];
+        }
+        __syncthreads();
+      }
+    }
+    rl::tree(g, groups, gi, (int)(t < (uint32_t)rl::NG ? t : (uint32_t)rl::NG), rl::SUM, exc);
+    // [M^-1] T: group q's base (-1)^q psi^q(T)
+    uint64_t kk[4];
+    rc_digits(kk, M);
+    const int q = gi & 3;
+    if (g.role < 6) g.s[rl::BASE + g.role] = groups[rl::SUM + g.role];
+    __syncthreads();
+    for (int r = 1; r < 4; ++r) {
+      g2_psi(g, rl::BASE, rl::TMP);
+      if (q >= r && g.role < 6) g.s[rl::BASE + g.role] = g.s[rl::TMP + g.role];
+      __syncthreads();
+    }
+    if ((q & 1) && (g.role == 2 || g.role == 3)) { fp v = g.s[rl::BASE + g.role]; fp_neg(v, v); g.s[rl::BASE + g.role] = v; }
+    __syncthreads();
+    rl::mul_signed(g, kk[q], false, gi < 4, 16, exc);
+    rl::tree(g, groups, gi, 4, rl::ACC, exc);
+  }
+  if (ra.exact || __syncthreads_or(exc ? 1 : 0)) return j;
+  if (lane_ == 0) {
+    g2_jac R;
+    for (int k = 0; k < 6; ++k) ((fp*)&R)[k] = L.s[LP_NCODE_CONST + rl::ACC + k];
+    g2_aff a;
+    jac_to_aff(a, R);
+    g2_compress(out96 + 96 * (size_t)j, a);
+  }
+  return -1;
+}
 
 __global__ void k_select(int n_jobs, uint32_t n_shares, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
                          const uint64_t* __restrict__ ids, const uint8_t* __restrict__ verdict,
@@ -110,12 +298,22 @@ __global__ void SSB_LB(64) k_combine_terms_gls(int n, uint32_t n_jobs, const uin
   term[4 * (size_t)s + q] = r;
 }
 // stride: terms per share (1: k_combine_terms, 4: k_combine_terms_gls).  Jobs of the ratio combine
-// (fast 2; ra.rT != nullptr) run its phase K here: [M^-1] T from rT[j], compressed (unit_ratio_K).
+// (fast 2; ra.rT != nullptr) run its phase K here: [M^-1] T from rT[j], compressed (unit_ratio_K);
+// blocks past the jobs' (RATIO_LANE_PER_WAVE per wave of 64 jobs) run the fast-3 jobs whole
+// (ratio_lane_job; ra.sig != nullptr).
 __global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ tt, const int32_t* __restrict__ status,
                                                     const g2_jac* __restrict__ term, const uint32_t* __restrict__ skip_if_ok,
                                                     const uint32_t* __restrict__ fast, uint8_t* __restrict__ out96, int stride,
                                                     const uint32_t* __restrict__ sel, ratio_args ra) {
+  const int nbs = (n_jobs + 63) / 64;
+  if ((int)blockIdx.x >= nbs) {   // extra blocks: the fast-3 jobs, one workgroup each (uniform)
+    if (!fast || !ra.sig || !ra.rT || (skip_if_ok && *skip_if_ok)) return;
+    __shared__ rl::lds L;
+    const int jx = ratio_lane_job(L, (int)blockIdx.x - nbs, nbs, n_jobs, off, tt, sel, fast, out96, ra);
+    if (jx >= 0 && threadIdx.x == 0) ratio_lane_exact(jx, off, tt, sel, out96, ra);
+    return;
+  }
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
   if (skip_if_ok && *skip_if_ok) return;

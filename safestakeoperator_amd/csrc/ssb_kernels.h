@@ -66,7 +66,11 @@ struct spec_jobs {
 
 // the ratio combine's arguments riding in k_combine_terms_gls (phase T, blocks past nbt) and
 // k_combine_sum (phase K): the jobs' ids, the per-job table regions, the per-job T
-struct ratio_args { const uint64_t* ids; uint8_t* tabs; g2_jac* rT; uint64_t* rk; uint32_t nbt; };
+struct ratio_args { const uint64_t* ids; uint8_t* tabs; g2_jac* rT; uint64_t* rk; uint32_t nbt;
+                    const g2_aff* sig; uint32_t exact; };
+// k_combine_sum's extra blocks, per 64-job wave: one per fast-3 job a wave can hold (ratio jobs in a
+// wave with fewer than RATIO_MIN_JOBS of them -- ssb_blocks.h -- run on lane groups, one workgroup each)
+constexpr unsigned RATIO_LANE_PER_WAVE = 15;
 
 // share -> (job, root) of an aggregate batch (share_lookup, ssb_blocks.h)
 struct job_map {

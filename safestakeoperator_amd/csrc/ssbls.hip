@@ -1089,7 +1089,10 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
   uint64_t* rk = c.take<uint64_t>(4 * n_jobs);
   // the ratio combine rides in the terms launch (phase T: its blocks past nbt) and the sum launch (phase K)
   const unsigned nbt = nblk(4 * n, 64), nbr = nblk(n_jobs, 64);
-  const ratio_args ra{ids, rtab, ratio ? rT : nullptr, rk, nbt};
+  const ratio_args ra{ids, rtab, ratio ? rT : nullptr, rk, nbt, w.sig_aff, getenv("SSB_RATIO_LANE_EXACT") ? 1u : 0u};
+  // k_combine_sum: one thread per job, then the lane-group blocks of the fast-3 jobs (ratio jobs a wave
+  // holds too few of: RATIO_LANE_PER_WAVE blocks per wave, those without a job leave at once)
+  const unsigned nbsum = nblk(n_jobs, 64) * (ratio ? 1u + RATIO_LANE_PER_WAVE : 1u);
   if (wire && n) {   // the records' hex -> the 96-byte compressed form, first on the slot's stream
     uint8_t* sig_ws = c.take<uint8_t>(n * 96);
     { timed tm(ctx, "k_wire_sig", st); launch::wire_sig(st, (int)n, wire, stride, sig_ws, wire_status, 0); }
@@ -1108,7 +1111,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
                          (const uint8_t*)nullptr, w.flags, (const uint32_t*)nullptr, sel, out_status, out_err, w.sig_aff, fast,
                          out_sig96, lam, ratio, wire ? wire_status : (int32_t*)nullptr); }
     if (nbt + (ratio ? nbr : 0)) { timed tm(ctx, "k_combine_terms", sc); hipLaunchKernelGGL(k_combine_terms_gls, dim3(nbt + (ratio ? nbr : 0)), dim3(64), 0, sc, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, (const uint32_t*)nullptr, (const uint32_t*)fast, term, ra); }
-    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4, (const uint32_t*)sel, ra); }
+    { timed tm(ctx, "k_combine_sum", sc); hipLaunchKernelGGL(k_combine_sum, dim3(nbsum), dim3(64), 0, sc, (int)n_jobs, share_off, t, out_status, term, (const uint32_t*)nullptr, (const uint32_t*)fast, out_sig96, 4, (const uint32_t*)sel, ra); }
     hipEventRecord(ctx->cur->ev_comb, sc);
   };
   // one-stream slots: the speculative pass rides in the window-sum launch (msm_both), no stream
@@ -1143,7 +1146,7 @@ int aggregate_dev(ssb_ctx* ctx, size_t n_jobs, size_t n_shares, const uint32_t* 
     hipLaunchKernelGGL(k_combine_terms_gls, dim3(nbt + (ratio ? nbr : 0)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, share_off, t, out_status, sel, lam, w.sig_aff, gate2, (const uint32_t*)fast, term, ra);
   }
   { timed tm(ctx, "k_combine_sum", st);
-    hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate2, (const uint32_t*)fast, out_sig96, 4, (const uint32_t*)sel, ra); }
+    hipLaunchKernelGGL(k_combine_sum, dim3(nbsum), dim3(64), 0, st, (int)n_jobs, share_off, t, out_status, term, gate2, (const uint32_t*)fast, out_sig96, 4, (const uint32_t*)sel, ra); }
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipEventRecord(ctx->cur->ev_out, st));
   ctx->cur->out_pending = true;
@@ -1550,7 +1553,7 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   // unsafe_aggregate does not subgroup-check its inputs (blst.rs:77-84): always the exact 255-bit path
   hipLaunchKernelGGL(k_lagrange, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_ids, sel, d_st, (const uint32_t*)nullptr, (const uint32_t*)nullptr, lam);
   if (n) hipLaunchKernelGGL(k_combine_terms, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, (uint32_t)n_jobs, share_job, d_off, tt, d_st, sel, lam, sig_aff, (const uint32_t*)nullptr, (const uint32_t*)nullptr, term);
-  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out, 1, (const uint32_t*)nullptr, ratio_args{nullptr, nullptr, nullptr, nullptr, 0u});
+  hipLaunchKernelGGL(k_combine_sum, dim3(nblk(n_jobs, 64)), dim3(64), 0, st, (int)n_jobs, d_off, tt, d_st, term, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out, 1, (const uint32_t*)nullptr, ratio_args{nullptr, nullptr, nullptr, nullptr, 0u, nullptr, 0u});
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));

@@ -108,3 +108,20 @@ def test_knobs_tree_only_and_no_ratio(engine, monkeypatch):
     V, t, n, R = 1024, 3, 4, 16
     wl = bench.make_workload(engine, V, t, n, R, rank=26, ids="registry", invalid_rate=0.01)
     _check(engine, wl, V, t, n)
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["lane_groups", "exact_knob"])
+@pytest.mark.parametrize("t,n,V", [(3, 4, 1024), (9, 13, 512)], ids=["3of4", "9of13"])
+def test_few_ratio_jobs_per_wave(engine, monkeypatch, t, n, V, exact):
+    """Operator ids 1..n with a share skipped (an invalid share among the first t): the Lagrange
+    coefficients are ratios c_i / M, a few such jobs per 64-job wave -- each combined on one
+    workgroup's eight lane groups (k_combine_sum's extra blocks, ratio_lane_job: [c_i] sig_i per group,
+    9-of-13 in two passes over the groups, then [M^-1] T by the four base-u digits); with
+    SSB_RATIO_LANE_EXACT=1 every such job takes the exact single-lane fallback instead.  Every status,
+    verdict and combined signature == the C oracle."""
+    if exact:
+        monkeypatch.setenv("SSB_RATIO_LANE_EXACT", "1")
+    wl = bench.make_workload(engine, V, t, n, 16, rank=27, invalid_rate=0.02)
+    bad = [i for i, v in enumerate(wl["valid"]) if not v]
+    assert any(i % n < t for i in bad)                   # some job skips one of its first t shares
+    _check(engine, wl, V, t, n)
