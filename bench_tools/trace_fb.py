@@ -46,7 +46,9 @@ def main(pattern):
     dst = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
     s = ctypes.c_void_p(lib.ssb_slot_stream(eng.handle, 0))
     buf = (ctypes.c_ulonglong * (4 * 2048))()
-    lib.ssb_debug_trace_bisect(buf)   # clear
+    traced = hasattr(lib, "ssb_debug_trace_bisect")   # (the product library: verdicts only)
+    if traced:
+        lib.ssb_debug_trace_bisect(buf)   # clear
     valid = np.asarray(wl["valid"], dtype=np.uint8)
     for i in range(3):
         rc = lib.ssb_threshold_aggregate_batch_cached_dev(eng.handle, V, N, d_off.data_ptr(), d_t.data_ptr(), d_sig.data_ptr(),
@@ -56,6 +58,9 @@ def main(pattern):
         assert rc == 0, lib.ssb_last_error(eng.handle)
         torch.cuda.synchronize()
         ok = bool((ver.cpu().numpy() == valid).all())
+        if not traced:
+            print("batch %d verdicts_ok %s" % (i, ok))
+            continue
         m = lib.ssb_debug_trace_bisect(buf)
         if i < 2:
             continue

@@ -40,6 +40,10 @@ using launch::fb_jobs;
 // committee stage: at most this many suspect shares are checked one by one (beyond it the tree decides)
 constexpr uint32_t FB_SUSPECT_MAX = 2048;
 constexpr unsigned EX_SINGLE_BLOCKS = 512;
+// group-test mode: the order the blocks take the (key, quarter) items in (a prime multiplier)
+constexpr uint32_t EX_ITEM_MIX = 1000003u;
+// the exclusion check's parts of X: slices of at most this many suspects (EX_X_PARTS of them cover all)
+constexpr uint32_t EX_X_SHARES = (FB_SUSPECT_MAX + launch::EX_X_PARTS - 1) / launch::EX_X_PARTS;
 // grid of the fallback launches that stride over their work (k_fb_single, k_fb_level):
 // most failed batches leave them at their first test, and a grid of thousands of blocks waited
 // milliseconds for free slots behind the other pipeline slots' waves (round 4 profile of the 1e-2
@@ -543,7 +547,7 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
 //   * the EXCLUSION check -- the batch check without the suspects:
 //       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
 //       E_r = sum_{suspects of root r} k_i pk_i = sum_q 2^16q E_{r,q}  (blocks 4r + q),
-//       X   = sum_{suspects} k_i sig_i   = sum_q 2^16q X_q      (blocks 4 n_roots + q),
+//       X   = sum_{suspects} k_i sig_i   = sum_{p,q} 2^16q X_{p,q}  (blocks 4 n_roots + 4p + q: parts p of the suspects),
 //     the quarters' 4-bit-digit bucket sums, each paired on its own (ex_root_quarter, ex_quarter_point:
 //     the same value after the exponentiation), where ftot is the batch check's own Miller product
 //     (k_miller_final) -- by bilinearity this is the RLC check over every non-suspect candidate with
@@ -551,8 +555,9 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
 //     suspects: *xok = 1 decides them all valid;
 //   * every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's verify
 //     (blocks ex_pairs(n_roots) ..).
-// The pair blocks finish with a completion ticket (xtk[0]); the last pair multiplies ftot by the
-// ex_pairs(n_roots) Miller values (those without suspects skipped: 1) and runs ONE final exponentiation.
+// The pair blocks finish with completion tickets (ex_pair_ticket: per root, then xtk[0]); the last
+// multiplies ftot by the root products and the X values (those without suspects skipped: 1) and runs
+// ONE final exponentiation.
 // (the roles of k_fb_excl are out of line: each role's temporaries live in its own frame, and the
 // kernel's private segment is the largest role's, not their sum)
 struct ex_lds { fr_lds u; uint32_t flg, last, ncand; g1_aff sP; g2_aff sQ; };
@@ -573,13 +578,16 @@ SSB_FN void ex_singles(ex_lds& L, int first, uint32_t ns, const uint32_t* __rest
 }
 // The exclusion pairs, one block each (k_fb_excl's blocks 0 .. ex_pairs(n_roots) - 1): the Miller value
 // into fex[pair], then ex_pair_ticket.  Root r's E_r and X are both split into the quarters of the
-// scalars (bits 16q .. 16q+15: quarter_sum's 4-bit-digit bucket sums on the block's lanes):
-//   block 4r + q           m(-[2^16q] E_{r,q}, H(r))   (ex_root_quarter),
-//   block 4 n_roots + q    m([2^16q] g1, X_q)          (ex_quarter_point),
-// whose product over q is m(-E_r, H(r)), resp. m(g1, X), after the final exponentiation.  No block
-// runs a 64-bit scalar product on one lane (the one-invalid batch's chain, round-5 trace: the root
-// pair holding its suspect ended at 6.9 ms, the X quarters at 2.8 ms).  Each role ends with the pair's
-// points in L.sP / L.sQ and the block synchronised (the bucket lists dead), then ex_pair_lds.
+// scalars (bits 16q .. 16q+15: quarter_sum's 4-bit-digit bucket sums on the block's lanes), and X
+// also into parts, P slices of the suspect list (P = ceil(nS / EX_X_SHARES) <= EX_X_PARTS):
+//   block 4r + q                  m(-[2^16q] E_{r,q}, H(r))        (ex_root_quarter),
+//   block 4 n_roots + 4p + q      m([2^16q] g1, X_{p,q})           (ex_quarter_point; p >= P: 1),
+// whose product is m(-E_r, H(r)), resp. m(g1, X), after the final exponentiation.  No block runs a
+// 64-bit scalar product on one lane (the one-invalid batch's chain, round-5 trace: the root pair
+// holding its suspect ended at 6.9 ms, the X quarters at 2.8 ms), nor a bucket sum over hundreds of
+// suspects (1e-2 invalid: ~650 suspects, the four X quarter sums ended at 4.3-6.2 ms).  Each role
+// ends with the pair's points in L.sP / L.sQ and the block synchronised (the bucket lists dead),
+// then ex_pair_lds.
 // (roles out of line, called one after the other from the kernel: the quarter sum's frame and the
 // Miller loop's are never on the call chain together)
 SSB_FN void ex_root_quarter(ex_lds& L, int r, int q, const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
@@ -633,17 +641,62 @@ SSB_FN void ex_pair_lds(ex_lds& L) {
   lp_init_consts(g);
   miller_one(g, L.sP, L.sQ, F1, B, L.flg);
 }
-// the pair's Miller value into fex[pair], then the pairs' ticket: true in the block that runs the product
-SSB_INL bool ex_pair_ticket(ex_lds& L, int n_roots, int pair, fp12* __restrict__ fex, uint32_t* __restrict__ xtk) {
+// ACC *= prod of fex[first + k * stride] (k < count), the values equal to 1 skipped (a quarter without
+// suspects contributed m(O, Q) = 1).  Lane i tests value k = base + i, a ballot lists the others;
+// every product is a lane-program Fp12 product on this block.
+SSB_FN void ex_mul_values(lane::grp& g, const fp12* __restrict__ fex, int first, int count, int stride, int ACC, int IN) {
+  using namespace ssb::lane;
   const int lane_ = threadIdx.x;
-  if (lane_ < 12) ((fp*)&fex[pair])[lane_] = L.u.s[lane::LP_NCODE_CONST + BS_S0 + lane_];   // (g.s + F1 of the roles)
+  const fp one = fp_one();
+  for (int base = 0; base < count; base += 64) {
+    bool keep = false;
+    if (base + lane_ < count) {
+      const fp* v = (const fp*)&fex[first + (base + lane_) * stride];
+      keep = !fp_eq(v[0], one);
+      for (int k = 1; k < 12 && !keep; ++k) keep = !fp_is_zero(v[k]);
+    }
+    for (uint64_t m = __ballot(keep); m; m &= m - 1) {   // uniform
+      const int i = first + (base + __builtin_ctzll(m)) * stride;
+      if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&fex[i])[lane_];
+      __syncthreads();
+      f12_mul(g, ACC, IN, ACC);
+    }
+  }
+}
+// The pair's Miller value into fex[pair], then the tickets: a root's four quarter blocks first meet on
+// rtk[r] (zeroed by fb_prep_block, zeroed again here for k_fb_root), the last multiplies the four
+// values into fex[4r]; the root products and the X blocks then meet on xtk[0] -- true in the block
+// that runs the final product.  (ex_final then multiplies n_roots + 4 EX_X_PARTS values, not every
+// quarter's: with 1e-2 invalid shares ~60 of 64 roots hold suspects.)
+SSB_FN bool ex_pair_ticket(ex_lds& L, int n_roots, int pair, fp12* __restrict__ fex, uint32_t* __restrict__ xtk,
+                           uint32_t* __restrict__ rtk) {
+  using namespace ssb::lane;
+  const int lane_ = threadIdx.x;
+  if (lane_ < 12) ((fp*)&fex[pair])[lane_] = L.u.s[LP_NCODE_CONST + BS_S0 + lane_];   // (g.s + F1 of the roles)
   __threadfence();
   __syncthreads();
-  if (lane_ == 0) L.last = atomicAdd(&xtk[0], 1u) == (uint32_t)(launch::ex_pairs(n_roots) - 1) ? 1u : 0u;
+  if (pair < 4 * n_roots) {   // uniform
+    const int r = pair >> 2;
+    if (lane_ == 0) L.last = atomicAdd(&rtk[r], 1u) == 3u ? 1u : 0u;
+    __syncthreads();
+    if (!L.last) return false;
+    __threadfence();
+    grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
+    const int ACC = BS_S0, IN = BS_S0 + 12;
+    if (lane_ < 12) g.s[ACC + lane_] = lane_ == 0 ? fp_one() : fp_zero();
+    __syncthreads();
+    ex_mul_values(g, fex, 4 * r, 4, 1, ACC, IN);
+    if (lane_ < 12) ((fp*)&fex[4 * r])[lane_] = g.s[ACC + lane_];
+    if (lane_ == 0) rtk[r] = 0u;
+    __threadfence();
+    __syncthreads();
+  }
+  if (lane_ == 0) L.last = atomicAdd(&xtk[0], 1u) == (uint32_t)(n_roots + 4 * launch::EX_X_PARTS - 1) ? 1u : 0u;
   __syncthreads();
   return L.last != 0;
 }
-// ftot * prod of the ex_pairs(n_roots) exclusion values, ONE final exponentiation -> *xok
+// ftot * prod of the exclusion values (the root products fex[4r], the X blocks'), ONE final
+// exponentiation -> *xok
 SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, const fp12* __restrict__ fex,
                      uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok) {
   using namespace ssb::lane;
@@ -654,25 +707,8 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
   const int ACC = F1, IN = F1 + 12;
   if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)ftot)[lane_];
   __syncthreads();
-  // (a quarter without suspects contributed m(O, Q) = 1: skipped -- with one invalid share per batch,
-  // 256 of the 260 values.  Lane i tests value base + i, a ballot lists the others; every product
-  // here is a lane-program Fp12 product on this one block)
-  const fp one = fp_one();
-  const int np = launch::ex_pairs(n_roots);
-  for (int base = 0; base < np; base += 64) {
-    bool keep = false;
-    if (base + lane_ < np) {
-      const fp* v = (const fp*)&fex[base + lane_];
-      keep = !fp_eq(v[0], one);
-      for (int k = 1; k < 12 && !keep; ++k) keep = !fp_is_zero(v[k]);
-    }
-    for (uint64_t m = __ballot(keep); m; m &= m - 1) {   // uniform
-      const int i = base + __builtin_ctzll(m);
-      if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&fex[i])[lane_];
-      __syncthreads();
-      f12_mul(g, ACC, IN, ACC);
-    }
-  }
+  ex_mul_values(g, fex, 0, n_roots, 4, ACC, IN);
+  ex_mul_values(g, fex, 4 * n_roots, 4 * launch::EX_X_PARTS, 1, ACC, IN);
   f12_final_exp(g, ACC, TMP);
   const bool pass = f12_slots_one(g, ACC);
   if (lane_ == 0) { *xok = pass ? 1u : 0u; xtk[0] = 0u; }
@@ -697,16 +733,82 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
 // ONE RLC check and the candidates' verdicts on a pass (or for a one-candidate group).  Two functions
 // called one after the other from the kernel: the combines' frame and the pairing check's frame are
 // never on the call chain together (private segment: the deeper of the two, not their sum).
+// sum_q 2^(16q) X[q] by Horner (16 doublings and an addition per quarter) as lane programs: every
+// group of the wave runs the same operation on the same values in the same slots (one wave in
+// lockstep: identical stores), so the 48-doubling chain costs 48 programs, not 48 one-lane
+// doublings (round-5 trace of the faulty-operator batch: the one-lane combine took 3.2 ms of every
+// group's 9 ms chain).  Result in slots ACC (Jacobian); returns the additions' exception flags
+// (an infinite quarter, equal or opposite partial sums: the caller's one-lane combine then).
+SSB_FN uint32_t gc_horner_g2(ex_lds& L, const g2_jac* __restrict__ X, int ACC, int TMP) {
+  using namespace ssb::lane;
+  const int role = threadIdx.x % G2_ADD_G;
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, role};
+  uint32_t exc = 0;
+  if (role < 6) g.s[ACC + role] = ((const fp*)&X[3])[role];
+  __syncthreads();
+  for (int q = 2; q >= 0; --q) {
+    for (int i = 0; i < 16; ++i) g2_dbl(g, ACC, ACC);
+    if (role < 6) g.s[TMP + role] = ((const fp*)&X[q])[role];
+    __syncthreads();
+    g2_add(g, ACC, TMP, ACC, exc);
+  }
+  return exc;
+}
+SSB_FN uint32_t gc_horner_g1(ex_lds& L, const g1_jac* __restrict__ X, int ACC, int TMP) {
+  using namespace ssb::lane;
+  const int role = threadIdx.x % G1_ADD_G;
+  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, role};
+  uint32_t exc = 0;
+  if (role < 3) g.s[ACC + role] = ((const fp*)&X[3])[role];
+  __syncthreads();
+  for (int q = 2; q >= 0; --q) {
+    for (int i = 0; i < 16; ++i) g1_dbl(g, ACC, ACC);
+    if (role < 3) g.s[TMP + role] = ((const fp*)&X[q])[role];
+    __syncthreads();
+    g1_add(g, ACC, TMP, ACC, exc);
+  }
+  return exc;
+}
+// the lane programs' Jacobian result (slots S0 ..) to affine in L.sQ / L.sP (lane 0), or the one-lane
+// combine after an exception -- each step out of line, so group_combine's frame holds no point
+SSB_FN void gc_store_g2(ex_lds& L, int S0) {
+  if (threadIdx.x != 0) return;
+  g2_jac R;
+  for (int k = 0; k < 6; ++k) ((fp*)&R)[k] = L.u.s[lane::LP_NCODE_CONST + S0 + k];
+  g2_aff Q;
+  jac_to_aff(Q, R);
+  L.sQ = Q;
+}
+SSB_FN void gc_store_g1(ex_lds& L, int S0) {
+  if (threadIdx.x != 0) return;
+  g1_jac R;
+  for (int k = 0; k < 3; ++k) ((fp*)&R)[k] = L.u.s[lane::LP_NCODE_CONST + S0 + k];
+  g1_aff P;
+  jac_to_aff(P, R);
+  L.sP = P;
+}
+SSB_FN void gc_exact_g2(ex_lds& L, const g2_jac* __restrict__ X2) {
+  const g2_aff Q = combine_quarters<fp2>(X2);
+  if (threadIdx.x == 0) L.sQ = Q;
+}
+SSB_FN void gc_exact_g1(ex_lds& L, const g1_jac* __restrict__ X1) {
+  const g1_aff P = combine_quarters<fp>(X1);
+  if (threadIdx.x == 0) L.sP = P;
+}
 SSB_FN void group_combine(ex_lds& L, const g2_jac* __restrict__ X2, const g1_jac* __restrict__ X1) {
-  const int lane_ = threadIdx.x;
+  using namespace ssb::lane;
+  constexpr int S0 = lane::G2_ADD_SCRATCH > lane::G1_ADD_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G1_ADD_SCRATCH;
+  static_assert(S0 >= lane::G2_DBL_SCRATCH && S0 >= lane::G1_DBL_SCRATCH && S0 + 12 <= BS_SLOTS, "slots");
   {
-    const g2_aff Q = combine_quarters<fp2>(X2);
-    if (lane_ == 0) L.sQ = Q;
+    grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, (int)threadIdx.x};
+    lp_init_consts(g);
+    __syncthreads();
   }
-  {
-    const g1_aff P = combine_quarters<fp>(X1);
-    if (lane_ == 0) L.sP = P;
-  }
+  if (gc_horner_g2(L, X2, S0, S0 + 6)) gc_exact_g2(L, X2);   // uniform (every lane reads the one flag word)
+  else gc_store_g2(L, S0);
+  __syncthreads();
+  if (gc_horner_g1(L, X1, S0, S0 + 3)) gc_exact_g1(L, X1);
+  else gc_store_g1(L, S0);
 }
 SSB_FN void ex_group_check(ex_lds& L, const uint32_t* __restrict__ list, uint32_t gn, uint32_t m,
                            uint32_t* __restrict__ flags, const g2_aff& h, uint8_t* __restrict__ verdict) {
@@ -729,7 +831,7 @@ SSB_FN void ex_group_check(ex_lds& L, const uint32_t* __restrict__ list, uint32_
 //   nS <= FB_SUSPECT_MAX -- the EXCLUSION check, the batch check without the suspects:
 //       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
 //       E_r and X split into the quarters of the scalars, one pair block per quarter (blocks 4r + q,
-//       then 4 n_roots + q: see ex_root_quarter), ftot the batch check's own Miller product
+//       then 4 n_roots + 4p + q for the parts of X: see ex_root_quarter), ftot the batch check's own Miller product
 //       (k_miller_final) -- by bilinearity the RLC check over every non-suspect candidate with the
 //       batch's own scalars (soundness 2^-63): *xok = 1 decides them all valid;
 //     and every suspect checked alone, e(pk_s, H(r)) e(-g1, sig_s) == 1, exactly the reference's
@@ -749,7 +851,7 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
                                      uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict,
                                      const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ kstart,
                                      uint32_t* __restrict__ cursor, g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1,
-                                     const g1_aff* __restrict__ negg1_pow) {
+                                     const g1_aff* __restrict__ negg1_pow, uint32_t* __restrict__ rtk) {
   if (*ok) return;   // uniform: the batch passed
   SSB_TRACE_T0();
   const uint32_t ns = *nS;
@@ -764,7 +866,14 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
     if (blk == 0 && lane_ == 0) *xok = 2u;
     const uint32_t NB = (uint32_t)launch::fb_nbuckets(n_roots);
     const uint32_t items = 4u * (uint32_t)n_roots * NB;
-    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+    // the items in a scattered order (it = s * P mod items, P a prime not dividing items: a
+    // bijection), striding over the blocks.  In key order the non-empty keys' items sit at fixed
+    // offsets inside every root's 64 items, and with a grid that is a multiple of 64 (832 blocks) a
+    // stride kept every block on the same offsets: a quarter of the blocks got all the busy items
+    // (the faulty-operator batch's last items ended at 30.9 ms against a 7 ms median, round-5 trace).
+    const uint32_t mix = (items % EX_ITEM_MIX) ? EX_ITEM_MIX : 1u;
+    for (uint32_t s = blockIdx.x; s < items; s += gridDim.x) {
+      const uint32_t it = (uint32_t)(((uint64_t)s * mix) % items);
       const uint32_t key = it >> 2, q = it & 3;
       const uint32_t gn = kcnt[key];
       if (!gn) continue;   // (uniform: the four items of an empty key all skip: no ticket)
@@ -805,15 +914,21 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
     ex_pair_lds(L);
     SSB_TRACE(TR_EX_ROOTPAIR);
   } else {
-    const int q = blk - 4 * n_roots;
-    quarter_sum_to<fp2>(L.u.b, slist, ns, flags, FLAG_SUSPECT, k64, sig_aff, q, X4 + q);
-    SSB_TRACE(TR_EX_QSUM);
-    ex_quarter_point(L, q, X4 + q, negg1_pow);   // (lane 0 wrote X4[q] and reads it back)
+    const int x = blk - 4 * n_roots, q = x & 3, part = x >> 2;
+    const uint32_t P = (ns + EX_X_SHARES - 1) / EX_X_SHARES, per = (ns + P - 1) / P;   // (ns >= 1)
+    const uint32_t b0 = (uint32_t)part * per;
+    if ((uint32_t)part < P && b0 < ns) {   // uniform
+      quarter_sum_to<fp2>(L.u.b, slist + b0, ns - b0 < per ? ns - b0 : per, flags, FLAG_SUSPECT, k64, sig_aff, q, X4 + x);
+      SSB_TRACE(TR_EX_QSUM);
+      ex_quarter_point(L, q, X4 + x, negg1_pow);   // (lane 0 wrote X4[x] and reads it back)
+    } else if (lane_ == 0) {
+      g1_aff P0; P0.inf = true; L.sP = P0;   // (no part: m(O, .) = 1)
+    }
     __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
     ex_pair_lds(L);
     SSB_TRACE(TR_EX_PAIR);
   }
-  if (ex_pair_ticket(L, n_roots, blk, fex, xtk)) {
+  if (ex_pair_ticket(L, n_roots, blk, fex, xtk, rtk)) {
     ex_final(L, n_roots, ftot, fex, xtk, xok);
     SSB_TRACE(TR_EX_FINAL);
   }
@@ -995,7 +1110,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
                        (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
                        (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
                        fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart,
-                       fw.cursor, fw.rsig, fw.rpk, fw.negg1_pow);
+                       fw.cursor, fw.rsig, fw.rpk, fw.negg1_pow, fw.rtk);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
                      (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                      (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,

@@ -293,9 +293,11 @@ struct fb_ws {
   uint32_t *kcnt, *kstart;   // per (root, id bucket) key: fb_keys(n_roots) words each (cursor too)
   const g1_aff* negg1_pow;   // [2^s](-g1), s < 64 (the exclusion check pairs quarter q of X with [2^16q] g1)
 };
-// the exclusion check's Fp12 values: one per quarter of every root's E_r and of X (k_fb_excl's
-// pair blocks, in that order)
-constexpr int ex_pairs(int n_roots) { return 4 * n_roots + 4; }
+// the exclusion check's Fp12 values: one per quarter of every root's E_r, then one per quarter of
+// every part of X (the suspect list cut into up to EX_X_PARTS slices; k_fb_excl's pair blocks, in
+// that order)
+constexpr int EX_X_PARTS = 16;
+constexpr int ex_pairs(int n_roots) { return 4 * n_roots + 4 * EX_X_PARTS; }
 // the jobs of an aggregate batch (share_off, t, ids), for the committee stage of the fallback
 struct fb_jobs { int n_jobs; const uint32_t* off; const uint32_t* tt; const uint64_t* ids; };
 int fallback_log2_branch();
