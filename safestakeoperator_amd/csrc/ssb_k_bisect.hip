@@ -40,8 +40,6 @@ using launch::fb_jobs;
 // committee stage: at most this many suspect shares are checked one by one (beyond it the tree decides)
 constexpr uint32_t FB_SUSPECT_MAX = 2048;
 constexpr unsigned EX_SINGLE_BLOCKS = 512;
-// group-test mode: the order the blocks take the (key, quarter) items in (a prime multiplier)
-constexpr uint32_t EX_ITEM_MIX = 1000003u;
 // the exclusion check's parts of X: slices of at most this many suspects (EX_X_PARTS of them cover all)
 constexpr uint32_t EX_X_SHARES = (FB_SUSPECT_MAX + launch::EX_X_PARTS - 1) / launch::EX_X_PARTS;
 // grid of the fallback launches that stride over their work (k_fb_single, k_fb_level):
@@ -60,7 +58,7 @@ constexpr unsigned FB_GRID_MAX = 512;
 // stores of one workgroup are ordered by them).
 struct fb_prep_args { int n_roots, L, lb; const uint32_t* share_root; uint32_t* cnt; uint32_t* start; uint32_t* cursor;
                       uint32_t* gst; uint32_t* perm; uint32_t* rtk; uint32_t* nfail; const uint64_t* ids;
-                      uint32_t* kcnt; uint32_t* kstart; };
+                      uint32_t* kcnt; uint32_t* kstart; uint32_t* klist; };
 SSB_INL uint32_t fb_bucket(uint64_t id, int nb) {
   return nb > 1 ? (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> 60) & (uint32_t)(nb - 1) : 0u;
 }
@@ -86,7 +84,12 @@ SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   __syncthreads();
   if (t == 0) {
     uint32_t acc = 0;
-    for (int k = 0; k < K; ++k) { ks[k] = acc; cursor[k] = acc; acc += kc[k]; }
+    uint32_t m = 0;
+    for (int k = 0; k < K; ++k) {
+      ks[k] = acc; cursor[k] = acc; acc += kc[k];
+      if (a.klist && kc[k]) a.klist[m++] = (uint32_t)k;
+    }
+    if (a.klist) a.klist[K] = m;   // (the group-test items: four per listed key)
   }
   __syncthreads();
   if (NB > 1)
@@ -851,12 +854,13 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
                                      uint32_t* __restrict__ xtk, uint32_t* __restrict__ xok, uint8_t* __restrict__ verdict,
                                      const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ kstart,
                                      uint32_t* __restrict__ cursor, g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1,
-                                     const g1_aff* __restrict__ negg1_pow, uint32_t* __restrict__ rtk) {
+                                     const g1_aff* __restrict__ negg1_pow, uint32_t* __restrict__ rtk,
+                                     const uint32_t* __restrict__ klist) {
   if (*ok) return;   // uniform: the batch passed
   SSB_TRACE_T0();
   const uint32_t ns = *nS;
   const int blk = blockIdx.x, lane_ = threadIdx.x;
-  const bool gmode = ns > FB_SUSPECT_MAX && kcnt;
+  const bool gmode = ns > FB_SUSPECT_MAX && kcnt && klist;
   if (ns == 0 || (ns > FB_SUSPECT_MAX && !gmode)) {   // nothing to exclude / no group keys: the tree decides
     if (blk == 0 && lane_ == 0) *xok = 0u;
     return;
@@ -865,16 +869,14 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
   if (gmode) {   // group-test mode: blocks stride over the (key, quarter) items
     if (blk == 0 && lane_ == 0) *xok = 2u;
     const uint32_t NB = (uint32_t)launch::fb_nbuckets(n_roots);
-    const uint32_t items = 4u * (uint32_t)n_roots * NB;
-    // the items in a scattered order (it = s * P mod items, P a prime not dividing items: a
-    // bijection), striding over the blocks.  In key order the non-empty keys' items sit at fixed
-    // offsets inside every root's 64 items, and with a grid that is a multiple of 64 (832 blocks) a
-    // stride kept every block on the same offsets: a quarter of the blocks got all the busy items
-    // (the faulty-operator batch's last items ended at 30.9 ms against a 7 ms median, round-5 trace).
-    const uint32_t mix = (items % EX_ITEM_MIX) ? EX_ITEM_MIX : 1u;
-    for (uint32_t s = blockIdx.x; s < items; s += gridDim.x) {
-      const uint32_t it = (uint32_t)(((uint64_t)s * mix) % items);
-      const uint32_t key = it >> 2, q = it & 3;
+    // four items per non-empty key (klist: fb_prep_block), striding over the blocks: every block
+    // takes at most ceil(items / grid) of them, a key's four quarters run on neighbouring blocks.
+    // (Over all n_roots * NB keys in key order, a grid that is a multiple of 64 kept every block on
+    // the same offsets inside each root's 64 items -- a quarter of the blocks got every busy item, the
+    // faulty-operator batch's last items ended at 30.9 ms against a 7 ms median, round-5 trace.)
+    const uint32_t items = 4u * klist[n_roots * NB];
+    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+      const uint32_t key = klist[it >> 2], q = it & 3;
       const uint32_t gn = kcnt[key];
       if (!gn) continue;   // (uniform: the four items of an empty key all skip: no ticket)
       const uint32_t* list = perm + kstart[key];
@@ -1102,7 +1104,8 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   const fb_jobs cj = committee ? jobs : fb_jobs{0, nullptr, nullptr, nullptr};
   const uint32_t* xok = committee ? fw.xok : nullptr;
   const fb_prep_args prep{n_roots, L, lb, share_root, fw.cnt, fw.start, fw.cursor, fw.gst, fw.perm, fw.rtk, fw.nfail,
-                          committee ? jobs.ids : nullptr, committee ? fw.kcnt : nullptr, committee ? fw.kstart : nullptr};
+                          committee ? jobs.ids : nullptr, committee ? fw.kcnt : nullptr, committee ? fw.kstart : nullptr,
+                          committee ? fw.klist : nullptr};
   hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + nb((size_t)cj.n_jobs, 64) + 1), dim3(64), 0, st, n, key, ok, flags,
                      fw.k64, fast_verdicts ? verdict : (uint8_t*)nullptr, prep, cj, sig, fw.slist, fw.nS);
   if (committee)
@@ -1110,7 +1113,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
                        (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
                        (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
                        fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart,
-                       fw.cursor, fw.rsig, fw.rpk, fw.negg1_pow, fw.rtk);
+                       fw.cursor, fw.rsig, fw.rpk, fw.negg1_pow, fw.rtk, (const uint32_t*)fw.klist);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
                      (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                      (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,

@@ -292,6 +292,7 @@ struct fb_ws {
   const fp12* ftot;
   uint32_t *kcnt, *kstart;   // per (root, id bucket) key: fb_keys(n_roots) words each (cursor too)
   const g1_aff* negg1_pow;   // [2^s](-g1), s < 64 (the exclusion check pairs quarter q of X with [2^16q] g1)
+  uint32_t* klist;   // the non-empty keys in key order, their count at [fb_keys(n_roots)] (group-test items)
 };
 // the exclusion check's Fp12 values: one per quarter of every root's E_r, then one per quarter of
 // every part of X (the suspect list cut into up to EX_X_PARTS slices; k_fb_excl's pair blocks, in

@@ -427,7 +427,7 @@ struct verify_ws {
   g1_jac* rpk; uint32_t* rcnt; uint32_t* rstart; uint32_t* rcur; uint32_t* perm;   // per-share G1 path
   g2_jac* rsig; uint32_t* gst; uint8_t* gv0; uint8_t* gv1;                         // failed-batch group tests
   uint64_t* k64; g2_jac* fbX; uint32_t* rtk; uint32_t* nfail;                                     // (level 0 per root)
-  uint32_t* slist; uint32_t* xok; fp12* fex; uint32_t* kcnt; uint32_t* kstart;      // committee stage
+  uint32_t* slist; uint32_t* xok; fp12* fex; uint32_t* kcnt; uint32_t* kstart; uint32_t* klist;   // committee stage
   size_t npairs;
 };
 // Miller values of the pairs plus the levels of the 8-ary product tree
@@ -459,7 +459,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
          align_up(n * 8) + align_up(fb_x_slots(n_roots) * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4) +
          align_up(n * 4) + align_up(4) + align_up((size_t)launch::ex_pairs((int)n_roots) * sizeof(fp12)) + align_up(ntk_words(np) * 4) +
-         3 * align_up(launch::fb_keys(n_roots) * 4);
+         3 * align_up(launch::fb_keys(n_roots) * 4) + align_up((launch::fb_keys(n_roots) + 1) * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) {
@@ -489,6 +489,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(fb_x_slots(n_roots)); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
   w.slist = c.take<uint32_t>(n); w.xok = c.take<uint32_t>(1); w.fex = c.take<fp12>((size_t)launch::ex_pairs((int)n_roots));
   w.kcnt = c.take<uint32_t>(launch::fb_keys(n_roots)); w.kstart = c.take<uint32_t>(launch::fb_keys(n_roots));
+  w.klist = c.take<uint32_t>(launch::fb_keys(n_roots) + 1);
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
@@ -683,7 +684,7 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
                        cm ? w.slist : nullptr, cm ? (uint32_t*)ptk : nullptr, cm ? (uint32_t*)ptk + 1 : nullptr,
                        cm ? w.xok : nullptr, cm ? w.fex : nullptr,
                        cm ? w.f + w.npairs + (w.npairs + 7) / 8 : nullptr, cm ? w.kcnt : nullptr, cm ? w.kstart : nullptr,
-                       ctx->negg1_pow};
+                       ctx->negg1_pow, cm ? w.klist : nullptr};
       const launch::fb_jobs fj = cm ? launch::fb_jobs{sj->n_jobs, sj->off, sj->tt, sj->ids} : launch::fb_jobs{0, nullptr, nullptr, nullptr};
       launch::fallback_bisect(fbs, (int)n, (int)n_roots, key, w.ok, w.flags, d_share_root, w.H, w.sig_aff, w.pk_aff, w.f,
                               fw, d_verdict, true, fj);
