@@ -53,11 +53,16 @@
  *     without synchronising.
  *   - Return value of every function: SSB_OK or a negative SSB_E* code (ssb_last_error() has
  *     the message).  No C++ exception crosses this ABI.  A context is thread-safe: every entry
- *     point holds the context's lock for its whole call, so the threads of a process can share ONE
- *     context (the collector's worker, direct callers, key registration); their calls are
- *     serialised.  ssb_last_error is the message of the context's last failed call (read it on the
- *     thread that got the error before another call on the context fails).  ssb_destroy must not
- *     race with other calls on the context.
+ *     point holds the context's lock while it enqueues its work, so the threads of a process can
+ *     share ONE context (the collector's worker, direct callers, key registration).  The synchronous
+ *     entry points (ssb_unsafe_aggregate_batch, ssb_sign_batch, ssb_sk_to_pk_batch,
+ *     ssb_pk_validate_batch, ssb_lagrange_coeffs, ssb_hash_to_g2*, ssb_verify_batch,
+ *     ssb_decode_wire_sigs, ssb_feldman_verify_batch, ssb_dleq_verify_batch) run one at a time per
+ *     context, on an idle pipeline slot when there is one, and wait for their results OUTSIDE the
+ *     lock, so the other threads' batches keep launching meanwhile.  ssb_last_error is the message of
+ *     the context's last failed call, copied per calling thread (read it on the thread that got the
+ *     error before another call on the context fails).  ssb_destroy must not race with other calls
+ *     on the context.
  */
 #ifndef SSBLS_H
 #define SSBLS_H
@@ -269,9 +274,11 @@ int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket);
  * table (ssb_pk_cache_add).  Up to `in_flight` windows run on the device while the next one fills;
  * every job's result is exactly threshold_aggregate's for that job alone (generic_threshold.rs:132-175).
  * The collector sets the context to one-stream slots at pipeline depth in_flight (and leaves it so
- * after ssb_collector_destroy).  The context stays usable by other threads while the collector
- * exists -- every entry point takes the context's lock -- so ONE context per process serves the
- * collector, direct calls (unsafe_aggregate, signing, key validation) and key registration. */
+ * after ssb_collector_destroy).  While a collector is attached the slot configuration is its own:
+ * ssb_set_pipeline_depth / ssb_set_slot_streams return SSB_EINVAL, and a second collector on the
+ * context must use the same in_flight.  The context stays usable by other threads while the
+ * collector exists -- every entry point takes the context's lock -- so ONE context per process serves
+ * the collector, direct calls (unsafe_aggregate, signing, key validation) and key registration. */
 typedef struct ssb_collector ssb_collector;
 typedef struct ssb_job_result {
   uint8_t sig96[96];     /* the combined signature (status SSB_DVF_OK) */
@@ -319,8 +326,10 @@ int ssb_collector_submit(ssb_collector* col, uint32_t t, uint32_t n, const uint8
                          const uint64_t* ids, const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb,
                          void* user);
 /* A job whose shares are the wire records as received (a SSB_COLLECTOR_WIRE collector): share i is
- * wire[i] (wire_len[i] bytes; a record of another length than 202, or a NULL one, never deserializes:
- * the share is absent).  Otherwise as ssb_collector_submit; the bytes are copied before it returns. */
+ * wire[i] (wire_len[i] bytes).  As bincode::deserialize (bincode 1.3.3, trailing bytes allowed) the
+ * first 202 bytes are decoded and any further bytes ignored; a shorter record, or a NULL one, never
+ * deserializes: the share is absent.  Otherwise as ssb_collector_submit; the bytes are copied before
+ * it returns. */
 int ssb_collector_submit_wire(ssb_collector* col, uint32_t t, uint32_t n, const uint8_t* const* wire,
                               const size_t* wire_len, const uint32_t* pk_index, const uint64_t* ids,
                               const uint8_t* root32, ssb_job_result* result, ssb_job_done_fn cb, void* user);
@@ -411,6 +420,35 @@ int ssb_pk_validate_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint8_t* 
 
 /* lagrange_coeffs for one id set: out 32-byte little-endian scalars (blst_scalar.b layout). */
 int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* out32);
+
+/* ---- Local-signing window -----------------------------------------------------
+ * The batched form of DvfSigner::local_sign_and_store's SecretKey::sign (src/node/dvfcore.rs:241-251),
+ * which every duty reaches once per validator (src/validation/signing_method.rs:318; selection proofs
+ * and RANDAO reveals included, :269-292).  Submissions from any number of threads join the open
+ * window; a worker thread closes it at max_jobs submissions or window_us after its first (or on
+ * flush), signs it with ONE ssb_sign_batch (each distinct root hashed once) and completes every
+ * submission: sig96 = compress([sk] hash_to_G2(root)) with the POP DST of src/crypto/impls/blst.rs:11,
+ * byte for byte SecretKey::sign's output.  The keys are wiped from the library's buffers once used. */
+typedef struct ssb_signer ssb_signer;
+typedef struct ssb_sign_result {
+  uint8_t sig96[96];   /* the signature (rc == SSB_OK) */
+  int32_t rc;          /* SSB_OK, or the window's ssb_sign_batch error */
+  uint32_t done;       /* 0 while pending; 1 (written last, release) when final */
+} ssb_sign_result;
+/* Called on the signer's worker thread after `done` is set; must not block or call ssb_signer_*. */
+typedef void (*ssb_sign_done_fn)(void* user, const ssb_sign_result* result);
+int ssb_signer_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t window_us, ssb_signer** out);
+/* Drains: every submission is signed and delivered before it returns. */
+void ssb_signer_destroy(ssb_signer* s);
+/* One signature: sk32le the secret scalar (32 bytes little-endian, 0 < sk < r -- a lighthouse
+ * SecretKey's bytes reversed), root32 the signing root; `result` (caller-owned, valid until done)
+ * receives it, then `cb` (may be NULL) is called with `user`.  Thread-safe; the key is copied. */
+int ssb_signer_submit(ssb_signer* s, const uint8_t* sk32le, const uint8_t* root32, ssb_sign_result* result,
+                      ssb_sign_done_fn cb, void* user);
+int ssb_signer_wait(ssb_signer* s, const ssb_sign_result* result);
+/* Close the open window now and wait until every submission made before the call is delivered. */
+int ssb_signer_flush(ssb_signer* s);
+int ssb_signer_stats(ssb_signer* s, uint64_t* windows, uint64_t* signatures);
 
 #ifdef __cplusplus
 }

@@ -1373,3 +1373,24 @@ int bls_oracle_pk_validate(const uint8_t* pk48, uint8_t* out48) {
   g1_compress(out48, &a);
   return 1;
 }
+
+/* SecretKey::sign (src/node/dvfcore.rs:241-243 -> lighthouse -> blst): [sk] hash_to_G2(msg) with the
+   POP DST, compressed.  sk 32-byte big-endian, 0 < sk < r.  Returns 1, or 0 for an invalid key. */
+int bls_oracle_sign(const uint8_t* sk32be, const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen, uint8_t* out96) {
+  bls_oracle_init();
+  uint64_t k[4];
+  for (int i = 0; i < 4; ++i) {
+    uint64_t v = 0;
+    for (int b = 0; b < 8; ++b) v = (v << 8) | sk32be[8 * (3 - i) + b];
+    k[i] = v;
+  }
+  int lt = 0, nz = (k[0] | k[1] | k[2] | k[3]) != 0;
+  for (int i = 3; i >= 0; --i) if (k[i] != RL[i]) { lt = k[i] < RL[i]; break; }
+  if (!lt || !nz) return 0;
+  g2_aff h; hash_to_g2(&h, msg, mlen, dst, dlen);
+  g2_jac hj, s; g2_from_aff(&hj, &h);
+  g2_mul(&s, &hj, k, 4);
+  g2_aff a; g2_to_aff(&a, &s);
+  g2_compress(out96, &a);
+  return 1;
+}

@@ -40,6 +40,7 @@ def load():
                                                        _u8p, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         lib.bls_oracle_sk_to_pk.argtypes = [_u8p, _u8p]
         lib.bls_oracle_pk_validate.argtypes = [_u8p, _u8p]
+        lib.bls_oracle_sign.argtypes = [_u8p, _u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p]
         lib.bls_oracle_init()
         _lib = lib
     return _lib
@@ -153,3 +154,14 @@ def pk_validate(pk48):
     p, _a = _b(pk48)
     ok = bool(lib.bls_oracle_pk_validate(p, ctypes.cast(out, _u8p)))
     return ok, bytes(out)
+
+
+def sign(sk32be, msg, dst=DST_POP):
+    """bls::SecretKey::sign (src/node/dvfcore.rs:241-243): [sk] hash_to_G2(msg) compressed (96 B),
+    or None for a key outside (0, r)."""
+    lib = load()
+    out = (ctypes.c_uint8 * 96)()
+    s, _a = _b(sk32be)
+    m, _m = _b(msg)
+    d, _d = _b(dst)
+    return bytes(out) if lib.bls_oracle_sign(s, m, len(msg), d, len(dst), ctypes.cast(out, _u8p)) else None

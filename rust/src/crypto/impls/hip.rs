@@ -52,6 +52,20 @@ pub struct SsbCtx {
 pub struct SsbCollector {
     _private: [u8; 0],
 }
+#[repr(C)]
+pub struct SsbSigner {
+    _private: [u8; 0],
+}
+
+/// `ssb_sign_result` (include/ssbls.h).
+#[repr(C)]
+pub struct SsbSignResult {
+    pub sig96: [u8; 96],
+    pub rc: i32,
+    pub done: u32,
+}
+
+pub type SignDoneFn = extern "C" fn(user: *mut c_void, result: *const SsbSignResult);
 
 /// `ssb_job_result` (include/ssbls.h).
 #[repr(C)]
@@ -91,6 +105,9 @@ extern "C" {
                                  pk_index: *const u32, ids: *const u64, root32: *const u8, result: *mut SsbJobResult,
                                  cb: Option<JobDoneFn>, user: *mut c_void) -> c_int;
     fn ssb_collector_flush(col: *mut SsbCollector) -> c_int;
+    fn ssb_signer_create(ctx: *mut SsbCtx, max_jobs: u32, window_us: u32, out: *mut *mut SsbSigner) -> c_int;
+    fn ssb_signer_submit(s: *mut SsbSigner, sk32le: *const u8, root32: *const u8, result: *mut SsbSignResult,
+                         cb: Option<SignDoneFn>, user: *mut c_void) -> c_int;
 }
 
 const SSB_COLLECTOR_WIRE: u32 = 1;
@@ -108,10 +125,12 @@ pub fn engine_error(msg: String) -> DvfError {
     DvfError::UnexpectedCall(format!("ssbls: {}", msg))
 }
 
-/// The process's engine: its context, the collector on it, and the compressed-key -> table-row map.
+/// The process's engine: its context, the collector and the local-signing window on it, and the
+/// compressed-key -> table-row map.
 pub struct Engine {
     ctx: *mut SsbCtx,
     col: *mut SsbCollector,
+    signer: *mut SsbSigner,
     rows: RwLock<HashMap<[u8; 48], u32>>,
 }
 // The library serialises every call on the context, and the collector's submit and key registration
@@ -122,12 +141,15 @@ unsafe impl Sync for Engine {}
 lazy_static! {
     /// Created on first use: device `SSB_DEVICE` (default 0), collector knobs read once --
     /// `SSB_COLLECT_MAX_JOBS` (default 4096, the C2 batch of BASELINE.json), `SSB_COLLECT_WINDOW_US`
-    /// (default 5000), `SSB_COLLECT_IN_FLIGHT` (default 20).
+    /// (default 5000), `SSB_COLLECT_IN_FLIGHT` (default 20) -- and the signing window's
+    /// `SSB_SIGN_MAX_JOBS` (default 4096) and `SSB_SIGN_WINDOW_US` (default 1000).
     pub static ref ENGINE: Result<Engine, String> = Engine::create(
         env_or("SSB_DEVICE", 0i32),
         env_or("SSB_COLLECT_MAX_JOBS", 4096u32),
         env_or("SSB_COLLECT_WINDOW_US", 5000u32),
         env_or("SSB_COLLECT_IN_FLIGHT", 20i32),
+        env_or("SSB_SIGN_MAX_JOBS", 4096u32),
+        env_or("SSB_SIGN_WINDOW_US", 1000u32),
     );
 }
 
@@ -207,8 +229,30 @@ pub enum Shares<'a> {
     Wire(&'a [&'a [u8]]),
 }
 
+/// One submitted signature: the library writes `result` in place, then calls `sign_done` with this box.
+struct PendingSign {
+    result: SsbSignResult,
+    reply: Option<tokio::sync::oneshot::Sender<Result<Signature, DvfError>>>,
+}
+
+/// ssb_sign_done_fn, on the signing window's worker thread.
+extern "C" fn sign_done(user: *mut c_void, _result: *const SsbSignResult) {
+    let _ = std::panic::catch_unwind(|| {
+        let mut p: Box<PendingSign> = unsafe { Box::from_raw(user as *mut PendingSign) };
+        let out = if p.result.rc == 0 {
+            Signature::deserialize(&p.result.sig96).map_err(DvfError::from)
+        } else {
+            Err(engine_error(format!("ssb_sign_batch failed ({})", p.result.rc)))
+        };
+        if let Some(tx) = p.reply.take() {
+            let _ = tx.send(out); // the duty task may have been dropped: nothing to do
+        }
+    });
+}
+
 impl Engine {
-    fn create(device: i32, max_jobs: u32, window_us: u32, in_flight: i32) -> Result<Self, String> {
+    fn create(device: i32, max_jobs: u32, window_us: u32, in_flight: i32, sign_jobs: u32, sign_window_us: u32)
+              -> Result<Self, String> {
         let mut ctx: *mut SsbCtx = std::ptr::null_mut();
         let rc = unsafe { ssb_create(&mut ctx, device) };
         if rc != 0 || ctx.is_null() {
@@ -222,7 +266,41 @@ impl Engine {
         if rc != 0 || col.is_null() {
             return Err(format!("ssb_collector_create2 returned {}: {}", rc, last_error(ctx)));
         }
-        Ok(Self { ctx, col, rows: RwLock::new(HashMap::new()) })
+        let mut signer: *mut SsbSigner = std::ptr::null_mut();
+        let rc = unsafe { ssb_signer_create(ctx, sign_jobs.max(1), sign_window_us, &mut signer) };
+        if rc != 0 || signer.is_null() {
+            return Err(format!("ssb_signer_create returned {}", rc));
+        }
+        Ok(Self { ctx, col, signer, rows: RwLock::new(HashMap::new()) })
+    }
+
+    /// `SecretKey::sign(msg)` into the signing window; `reply` receives the signature.  The key's
+    /// bytes (big-endian from lighthouse, little-endian for the library) are wiped after the copy.
+    pub fn sign_submit(&self, sk: &bls::SecretKey, msg: Hash256,
+                       reply: tokio::sync::oneshot::Sender<Result<Signature, DvfError>>) -> Result<(), DvfError> {
+        let mut le = [0u8; 32];
+        {
+            let be = sk.serialize();
+            for (i, b) in be.as_bytes().iter().enumerate() {
+                le[31 - i] = *b;
+            }
+        }
+        let raw = Box::into_raw(Box::new(PendingSign {
+            result: SsbSignResult { sig96: [0u8; 96], rc: 0, done: 0 },
+            reply: Some(reply),
+        }));
+        let rc = unsafe {
+            ssb_signer_submit(self.signer, le.as_ptr(), msg.as_bytes().as_ptr(), &mut (*raw).result, Some(sign_done),
+                              raw as *mut c_void)
+        };
+        for b in le.iter_mut() {
+            unsafe { std::ptr::write_volatile(b, 0) };
+        }
+        if rc != 0 {
+            drop(unsafe { Box::from_raw(raw) });
+            return Err(engine_error(format!("ssb_signer_submit returned {}", rc)));
+        }
+        Ok(())
     }
 
     /// Table rows of these keys if every one is registered already (no library call).

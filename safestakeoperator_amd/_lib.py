@@ -67,6 +67,13 @@ SIGNATURES = {
     "ssb_collector_stats": (ctypes.c_int, [ctypes.c_void_p, _u64p, _u64p, _u64p]),
     "ssb_collector_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _u64p]),
+    "ssb_signer_create": (ctypes.c_int, [_ctx, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    "ssb_signer_destroy": (None, [ctypes.c_void_p]),
+    "ssb_signer_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_signer_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "ssb_signer_flush": (ctypes.c_int, [ctypes.c_void_p]),
+    "ssb_signer_stats": (ctypes.c_int, [ctypes.c_void_p, _u64p, _u64p]),
     "ssb_verify_batch_dev": (ctypes.c_int, [_ctx, _sz, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz,
                                             ctypes.c_void_p, _u8p, _sz, ctypes.c_uint64, ctypes.c_void_p,
                                             ctypes.c_void_p]),
@@ -106,6 +113,15 @@ class JobResult(ctypes.Structure):
 
 # ssb_job_done_fn: void (*)(void* user, const ssb_job_result* result)
 JOB_DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(JobResult))
+
+
+class SignResult(ctypes.Structure):
+    """ssb_sign_result (include/ssbls.h): one local signature from the signing window."""
+    _fields_ = [("sig96", ctypes.c_uint8 * 96), ("rc", ctypes.c_int32), ("done", ctypes.c_uint32)]
+
+
+# ssb_sign_done_fn: void (*)(void* user, const ssb_sign_result* result)
+SIGN_DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(SignResult))
 
 
 def header_symbols():

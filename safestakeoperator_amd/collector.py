@@ -140,6 +140,74 @@ def result_of(r: "_lib.JobResult") -> Union[bytes, DvfError, Exception]:
         return bytes(r.sig96)
     return _error_from(int(r.status), int(r.err[0]), int(r.err[1]))
 
+class LocalSigner:
+    """The local-signing window (include/ssbls.h, ssb_signer_*): the batched form of
+    `DvfSigner::local_sign_and_store`'s `SecretKey::sign` (src/node/dvfcore.rs:241-251), which every
+    duty of every validator reaches once (src/validation/signing_method.rs:318 -- attestations, blocks,
+    aggregates, selection proofs and RANDAO reveals).  `submit(sk, root)` returns a Future of the
+    96-byte signature; the library's worker signs each window with one ssb_sign_batch (every distinct
+    root hashed once).  Mirrors rust/src/validation/impls/slot_signer.rs."""
+
+    def __init__(self, engine: Engine, max_jobs: int = 4096, window_s: float = 0.002):
+        self.engine = engine
+        self._lib = engine._lib
+        h = ctypes.c_void_p()
+        rc = self._lib.ssb_signer_create(engine.handle, int(max_jobs), int(round(window_s * 1e6)), ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError("ssb_signer_create failed (%d)" % rc)
+        self._h = h
+        self._ids = itertools.count(1)
+        self._inflight: Dict[int, Tuple[Future, "_lib.SignResult"]] = {}
+        self._cb = _lib.SIGN_DONE_FN(self._done)   # kept alive as long as the signer
+
+    def submit(self, sk: int, root: bytes) -> Future:
+        if not 0 < int(sk) < (1 << 255) or len(root) != 32:
+            raise ValueError("a secret scalar in (0, r) and a 32-byte signing root")
+        fut: Future = Future()
+        res = _lib.SignResult()
+        key = next(self._ids)
+        self._inflight[key] = (fut, res)
+        skb = int(sk).to_bytes(32, "little")
+        rc = self._lib.ssb_signer_submit(self._h, skb, bytes(root), ctypes.addressof(res), self._cb, ctypes.c_void_p(key))
+        if rc != 0:
+            self._inflight.pop(key, None)
+            raise RuntimeError("ssb_signer_submit failed (%d)" % rc)
+        return fut
+
+    def sign(self, sk: int, root: bytes, timeout: Optional[float] = None) -> bytes:
+        """SecretKey::sign(root), blocking."""
+        return self.submit(sk, root).result(timeout)
+
+    def _done(self, user, res_p) -> None:
+        """ssb_sign_done_fn, on the library's worker thread."""
+        fut, res = self._inflight.pop(int(user or 0))
+        if not fut.set_running_or_notify_cancel():
+            return
+        if res.rc == 0:
+            fut.set_result(bytes(res.sig96))
+        else:
+            fut.set_exception(RuntimeError("ssb_sign_batch failed (%d)" % res.rc))
+
+    def flush(self) -> None:
+        self._lib.ssb_signer_flush(self._h)
+
+    def stats(self) -> Tuple[int, int]:
+        w, n = ctypes.c_uint64(), ctypes.c_uint64()
+        self._lib.ssb_signer_stats(self._h, ctypes.byref(w), ctypes.byref(n))
+        return int(w.value), int(n.value)
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.ssb_signer_destroy(self._h)   # signs and delivers every submission
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
 BatchFn = Callable[[int, Sequence[ThresholdJob]], List[Union[bytes, DvfError]]]
 
 

@@ -33,7 +33,9 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ssbls.h"
@@ -41,6 +43,7 @@
 namespace ssb {
 int ctx_device(const ssb_ctx* ctx);
 std::recursive_mutex& ctx_mutex(ssb_ctx* ctx);
+int ctx_attach_collector(ssb_ctx* ctx, int d, int in_flight);
 }
 
 namespace {
@@ -135,8 +138,13 @@ namespace {
 void wait_new_window(ssb_collector* c, window* w, uint64_t gen) {
   c->n_full_waits.fetch_add(1, std::memory_order_relaxed);
   std::unique_lock<std::mutex> lk(c->mu);
+  // (also when w's reservation word already carries gen's tag and is open: reset() stores gen before
+  // the word, so a submitter may have read the new gen beside the old closed word -- then nothing
+  // would change until some other submitter filled w)
   c->cv_submit.wait(lk, [&] {
-    return c->open.load(std::memory_order_acquire) != w || w->gen.load(std::memory_order_acquire) != gen || c->stopping;
+    const uint64_t r = w->resv.load(std::memory_order_acquire);
+    return c->open.load(std::memory_order_acquire) != w || w->gen.load(std::memory_order_acquire) != gen || c->stopping ||
+           (!(r & CLOSED) && (r & TAG_FIELD) == tag_of(gen));
   });
 }
 
@@ -173,6 +181,12 @@ void ssb_collector::seal(window* w) {
   std::lock_guard<std::recursive_mutex> g(ssb::ctx_mutex(ctx));   // the slot's stream and the launches, atomically
   const int k = (int)(slot_rr++ % in_flight);
   void* st = ssb_slot_stream(ctx, k);
+  if (!st) {   // (cannot happen while attached: the slots are ours) -- nothing launched, nothing to wait for
+    w->rc = SSB_EINVAL;
+    w->ev_ok = false;
+    n_windows.fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
   uint8_t* d = w->d;
   if (wire)
     w->rc = ssb_threshold_aggregate_batch_wire_cached_dev(
@@ -356,10 +370,16 @@ int ssb_collector_create2(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, 
   int rc;
   {
     std::lock_guard<std::recursive_mutex> g(ssb::ctx_mutex(ctx));
-    if ((rc = ssb_set_slot_streams(ctx, 1)) || (rc = ssb_set_pipeline_depth(ctx, in_flight))) return rc;
+    // attached: ssb_set_pipeline_depth / ssb_set_slot_streams refuse to change the slots until
+    // ssb_collector_destroy detaches (the worker picks slots round robin over in_flight of them)
+    if ((rc = ssb::ctx_attach_collector(ctx, 1, in_flight))) return rc;
   }
+  auto detach = [&] {
+    std::lock_guard<std::recursive_mutex> g(ssb::ctx_mutex(ctx));
+    ssb::ctx_attach_collector(ctx, -1, 0);
+  };
   ssb_collector* c = new (std::nothrow) ssb_collector();
-  if (!c) return SSB_ENOMEM;
+  if (!c) { detach(); return SSB_ENOMEM; }
   c->ctx = ctx;
   c->device = ssb::ctx_device(ctx);
   c->J = max_jobs;
@@ -371,11 +391,11 @@ int ssb_collector_create2(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, 
   uint32_t rt = 1;
   while (rt < 2 * max_jobs) rt <<= 1;
   c->rtab.assign(rt, 0u);
-  if (hipSetDevice(c->device) != hipSuccess) { delete c; return SSB_EHIP; }
+  if (hipSetDevice(c->device) != hipSuccess) { delete c; detach(); return SSB_EHIP; }
   const size_t J = max_jobs, N = max_shares;
   for (int i = 0; i < 2 * in_flight + 2; ++i) {
     window* w = new (std::nothrow) window();
-    if (!w) { free_windows(c); delete c; return SSB_ENOMEM; }
+    if (!w) { free_windows(c); delete c; detach(); return SSB_ENOMEM; }
     c->all.push_back(w);
     size_t o = 0;
     auto at = [&](size_t bytes) { const size_t r = o; o += al(bytes); return r; };
@@ -390,6 +410,7 @@ int ssb_collector_create2(ssb_ctx* ctx, uint32_t max_jobs, uint32_t max_shares, 
       if (w->h) { hipHostFree(w->h); w->h = nullptr; }
       free_windows(c);
       delete c;
+      detach();
       return SSB_ENOMEM;
     }
     w->res.assign(J, nullptr);
@@ -424,6 +445,10 @@ void ssb_collector_destroy(ssb_collector* c) {
   if (c->worker.joinable()) c->worker.join();        // closes the last window, then sealing_done
   if (c->deliverer.joinable()) c->deliverer.join();  // delivers every window on the device
   free_windows(c);
+  {
+    std::lock_guard<std::recursive_mutex> g(ssb::ctx_mutex(c->ctx));
+    ssb::ctx_attach_collector(c->ctx, -1, 0);
+  }
   delete c;
 }
 
@@ -499,13 +524,13 @@ int ssb_collector_submit_wire(ssb_collector* c, uint32_t t, uint32_t n, const ui
   if (!c || !c->wire || !result || !root32 || t == 0 || t > SSB_MAX_T || n > MAX_JOB_SHARES ||
       (n && (!wire || !wire_len || !pk_index || !ids)))
     return SSB_EINVAL;
-  // a record of any other length than 202 bytes cannot be a bincode Signature: its length field or
-  // its digits fail on the device (the record is copied as received, truncated or zero-padded)
+  // bincode::deserialize (bincode 1.3: trailing bytes allowed) reads the first 202 bytes of a record:
+  // a longer record is decoded from those, a shorter one cannot be a Signature (its length
+  // field is overwritten so that it never parses on the device: the share is absent)
   return submit_job(c, t, n, [&](uint8_t* d, uint32_t i) {
     const size_t l = wire[i] ? (wire_len[i] < WIRE_REC ? wire_len[i] : WIRE_REC) : 0;
     if (l) memcpy(d, wire[i], l);
-    if (l < WIRE_REC) memset(d + l, 0, WIRE_REC - l);
-    if (wire[i] && wire_len[i] != WIRE_REC) { const uint64_t bad = ~0ull; memcpy(d, &bad, 8); }   // never parses
+    if (l < WIRE_REC) { memset(d + l, 0, WIRE_REC - l); const uint64_t bad = ~0ull; memcpy(d, &bad, 8); }
   }, pk_index, ids, root32, result, cb, user);
 }
 
@@ -544,6 +569,172 @@ int ssb_collector_stats(ssb_collector* c, uint64_t* windows, uint64_t* jobs, uin
   if (windows) *windows = c->n_windows.load();
   if (jobs) *jobs = c->n_jobs.load();
   if (shares) *shares = c->n_shares.load();
+  return SSB_OK;
+}
+
+}  // extern "C"
+
+// ---- The local-signing window -------------------------------------------------
+// Every duty of every validator an operator serves ends its local part with ONE
+// DvfSigner::local_sign_and_store(signing_root) -> SecretKey::sign (src/node/dvfcore.rs:241-251; the
+// call at src/validation/signing_method.rs:318 for attestations, blocks, aggregates, and the selection
+// proofs / RANDAO reveals of :269-292): one G2 scalar multiplication and one hash_to_G2 on a tokio
+// task each.  Here those calls become ssb_signer_submit: the worker closes a window at max_jobs
+// submissions or window_us after its first, hashes every distinct root once and signs the whole
+// window with one ssb_sign_batch, then completes each submission (result + callback).  The secret
+// keys are wiped from the window's host buffer once signed.
+namespace {
+struct sign_job {
+  uint8_t sk[32];   // little-endian scalar
+  uint8_t root[32];
+  ssb_sign_result* r;
+  ssb_sign_done_fn cb;
+  void* user;
+};
+void wipe(void* p, size_t n) {
+  volatile uint8_t* v = (volatile uint8_t*)p;
+  for (size_t i = 0; i < n; ++i) v[i] = 0;
+}
+}  // namespace
+
+struct ssb_signer {
+  ssb_ctx* ctx = nullptr;
+  int device = 0;
+  uint32_t J = 1;
+  int64_t window_ns = 0;
+  std::mutex mu;
+  std::condition_variable cv_worker, cv_done;
+  std::vector<sign_job> open;      // the filling window
+  int64_t t_first = 0;
+  bool stopping = false;
+  uint64_t submitted = 0, delivered = 0, flush_upto = 0;
+  std::atomic<uint64_t> n_windows{0};
+  std::thread worker;
+
+  void run() {
+    hipSetDevice(device);
+    std::vector<sign_job> win;
+    std::vector<uint8_t> sk, roots, out;
+    std::vector<uint32_t> ridx;
+    std::unordered_map<std::string, uint32_t> rmap;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      const int64_t now = now_ns();
+      const bool due = !open.empty() && (stopping || open.size() >= J || flush_upto > delivered || now - t_first >= window_ns);
+      if (!due) {
+        if (stopping && open.empty()) break;
+        if (open.empty()) cv_worker.wait(lk);
+        else cv_worker.wait_for(lk, std::chrono::nanoseconds(std::max<int64_t>(1000, t_first + window_ns - now)));
+        continue;
+      }
+      win.swap(open);
+      open.clear();
+      lk.unlock();
+      const size_t n = win.size();
+      sk.resize(32 * n); ridx.resize(n); roots.clear(); out.assign(96 * n, 0); rmap.clear();
+      for (size_t i = 0; i < n; ++i) {
+        memcpy(sk.data() + 32 * i, win[i].sk, 32);
+        auto it = rmap.emplace(std::string((const char*)win[i].root, 32), (uint32_t)rmap.size()).first;
+        if (it->second == roots.size() / 32) roots.insert(roots.end(), win[i].root, win[i].root + 32);
+        ridx[i] = it->second;
+      }
+      static const uint8_t dst[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";   // src/crypto/impls/blst.rs:11
+      const int rc = ssb_sign_batch(ctx, n, sk.data(), ridx.data(), roots.size() / 32, roots.data(), dst, sizeof(dst) - 1,
+                                    out.data());
+      wipe(sk.data(), sk.size());
+      for (size_t i = 0; i < n; ++i) {
+        wipe(win[i].sk, 32);
+        ssb_sign_result* r = win[i].r;
+        if (rc == SSB_OK) memcpy(r->sig96, out.data() + 96 * i, 96);
+        else memset(r->sig96, 0, 96);
+        r->rc = rc;
+        __atomic_store_n(&r->done, 1u, __ATOMIC_RELEASE);
+        if (win[i].cb) win[i].cb(win[i].user, r);
+      }
+      win.clear();
+      n_windows.fetch_add(1, std::memory_order_relaxed);
+      lk.lock();
+      delivered += n;
+      cv_done.notify_all();
+    }
+    cv_done.notify_all();
+  }
+};
+
+extern "C" {
+
+int ssb_signer_create(ssb_ctx* ctx, uint32_t max_jobs, uint32_t window_us, ssb_signer** out) {
+  if (!out) return SSB_EINVAL;
+  *out = nullptr;
+  if (!ctx || max_jobs == 0 || max_jobs > MAX_WINDOW_JOBS) return SSB_EINVAL;
+  ssb_signer* s = new (std::nothrow) ssb_signer();
+  if (!s) return SSB_ENOMEM;
+  s->ctx = ctx;
+  s->device = ssb::ctx_device(ctx);
+  s->J = max_jobs;
+  s->window_ns = (int64_t)window_us * 1000;
+  s->open.reserve(max_jobs);
+  s->worker = std::thread([s] { s->run(); });
+  *out = s;
+  return SSB_OK;
+}
+
+void ssb_signer_destroy(ssb_signer* s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->stopping = true;
+  }
+  s->cv_worker.notify_all();
+  if (s->worker.joinable()) s->worker.join();   // signs and delivers what was submitted
+  delete s;
+}
+
+int ssb_signer_submit(ssb_signer* s, const uint8_t* sk32le, const uint8_t* root32, ssb_sign_result* result,
+                      ssb_sign_done_fn cb, void* user) {
+  if (!s || !sk32le || !root32 || !result) return SSB_EINVAL;
+  __atomic_store_n(&result->done, 0u, __ATOMIC_RELAXED);
+  sign_job j;
+  memcpy(j.sk, sk32le, 32);
+  memcpy(j.root, root32, 32);
+  j.r = result; j.cb = cb; j.user = user;
+  bool wake;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (s->stopping) { wipe(j.sk, 32); return SSB_EINVAL; }
+    if (s->open.empty()) s->t_first = now_ns();
+    s->open.push_back(j);
+    ++s->submitted;
+    wake = s->open.size() == 1 || s->open.size() >= s->J;
+  }
+  wipe(j.sk, 32);
+  if (wake) s->cv_worker.notify_one();
+  return SSB_OK;
+}
+
+int ssb_signer_wait(ssb_signer* s, const ssb_sign_result* r) {
+  if (!s || !r) return SSB_EINVAL;
+  if (__atomic_load_n(&r->done, __ATOMIC_ACQUIRE)) return SSB_OK;
+  std::unique_lock<std::mutex> lk(s->mu);
+  s->cv_done.wait(lk, [&] { return __atomic_load_n(&r->done, __ATOMIC_ACQUIRE) != 0; });
+  return SSB_OK;
+}
+
+int ssb_signer_flush(ssb_signer* s) {
+  if (!s) return SSB_EINVAL;
+  std::unique_lock<std::mutex> lk(s->mu);
+  const uint64_t target = s->submitted;
+  if (target > s->flush_upto) s->flush_upto = target;
+  s->cv_worker.notify_one();
+  s->cv_done.wait(lk, [&] { return s->delivered >= target; });
+  return SSB_OK;
+}
+
+int ssb_signer_stats(ssb_signer* s, uint64_t* windows, uint64_t* signatures) {
+  if (!s) return SSB_EINVAL;
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (windows) *windows = s->n_windows.load();
+  if (signatures) *signatures = s->delivered;
   return SSB_OK;
 }
 

@@ -18,6 +18,8 @@
 //   k_combine_terms   lambda_i * sig_i  (verified shares: GLS, 4 digits on 4 lanes; a-4 unsafe: 255-bit)
 //   k_combine_sum     sum, affine, compress                                 (a-4)
 #include <hip/hip_runtime.h>
+#include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -84,6 +86,10 @@ struct ssb_ctx {
   // threads of a process -- the collector's worker, a ThresholdSignature caller, registration --
   // and their calls are serialised (recursive: entry points call entry points)
   std::recursive_mutex mu;
+  // the synchronous entry points (SSB_SYNC_LOCK): one at a time -- they share the io arena -- and
+  // their final wait runs outside `mu`
+  std::mutex sync_mu;
+  int collectors = 0;               // attached ssb_collectors: the slot configuration is theirs
   int device = 0;
   // hardware queues the HIP runtime gives this process (GPU_MAX_HW_QUEUES, read by HIP when it
   // initialises; HIP's default is 4): ssb_set_pipeline_depth refuses more slot streams than fit
@@ -135,6 +141,24 @@ namespace {
   } while (0)
 
 #define SSB_LOCK(ctx) std::lock_guard<std::recursive_mutex> ssb_lock_((ctx)->mu)
+// Synchronous entry points (the call waits for its own work, then returns host results): one at a
+// time per context (sync_mu), on an idle slot when there is one (pick_idle_slot), and their final
+// wait runs OUTSIDE the context lock, so a collector's worker keeps launching windows on the other
+// slots meanwhile (a direct unsafe_aggregate held the lock through its stream
+// synchronize, and seal() could launch on no slot until it returned).
+#define SSB_SYNC_LOCK(ctx)                                                            \
+  std::unique_lock<std::mutex> ssb_sync_((ctx)->sync_mu);                             \
+  std::unique_lock<std::recursive_mutex> ssb_lock_((ctx)->mu)
+#define SSB_SYNC_WAIT(st)                                                             \
+  do {                                                                                \
+    ssb_lock_.unlock();                                                               \
+    const hipError_t e_ = hipStreamSynchronize(st);                                   \
+    if (e_ != hipSuccess) {                                                           \
+      ssb_lock_.lock();                                                               \
+      ctx->err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e_);       \
+      return SSB_EHIP;                                                                \
+    }                                                                                 \
+  } while (0)
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 const fp12 FP12_ONE_HOST = fp12_one();
@@ -175,6 +199,20 @@ void pick_slot(ssb_ctx* ctx, void* stream) {
     }
   ctx->cur = &ctx->sl[ctx->next];
   ctx->next = (ctx->next + 1) % ctx->nslots;
+}
+
+// The slot a synchronous call runs on: an idle one (its streams empty, no host batch pending), so the
+// call does not queue behind pipelined batches; else the current one.
+void pick_idle_slot(ssb_ctx* ctx) {
+  for (int k = 0; k < ctx->nslots; ++k) {
+    ssb_slot& S = ctx->sl[(ctx->next + k) % ctx->nslots];
+    if (S.host_ticket || hipStreamQuery(S.stream) != hipSuccess) continue;
+    if (!S.shared && (hipStreamQuery(S.side[0]) != hipSuccess || hipStreamQuery(S.side[1]) != hipSuccess)) continue;
+    if (S.out_pending && hipEventQuery(S.ev_out) != hipSuccess) continue;
+    ctx->cur = &S;
+    break;
+  }
+  (void)hipGetLastError();   // (hipErrorNotReady of the queries is not an error of this call)
 }
 
 hipStream_t slot_tail(ssb_ctx* ctx) { return ctx->tail; }
@@ -703,6 +741,22 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
 namespace ssb {
 int ctx_device(const ssb_ctx* ctx) { return ctx->device; }   // (ssb_collector.hip)
 std::recursive_mutex& ctx_mutex(ssb_ctx* ctx) { return ctx->mu; }
+// (ssb_collector.hip, under the context lock) a collector attaches with one-stream slots at depth
+// in_flight -- configuring the context if it is the first -- or detaches (d < 0)
+int ctx_attach_collector(ssb_ctx* ctx, int d, int in_flight) {
+  if (d < 0) { if (ctx->collectors > 0) --ctx->collectors; return SSB_OK; }
+  if (ctx->collectors) {
+    if (ctx->slot_streams != 1 || ctx->nslots != in_flight) {
+      ctx->err = "another collector is attached with a different in_flight (" + std::to_string(ctx->nslots) + ")";
+      return SSB_EINVAL;
+    }
+  } else {
+    int rc;
+    if ((rc = ssb_set_slot_streams(ctx, 1)) || (rc = ssb_set_pipeline_depth(ctx, in_flight))) return rc;
+  }
+  ++ctx->collectors;
+  return SSB_OK;
+}
 }
 
 extern "C" {
@@ -780,9 +834,20 @@ int check_queue_budget(ssb_ctx* ctx, int depth, int streams) {
 }
 }  // namespace
 
+namespace {
+// a collector owns the slot configuration it was created with: its worker picks slots round robin
+// over in_flight of them (a depth below in_flight left it a null slot stream)
+int check_no_collector(ssb_ctx* ctx) {
+  if (!ctx->collectors) return SSB_OK;
+  ctx->err = "a collector is attached to this context: its slot configuration cannot change (ssb_collector_destroy first)";
+  return SSB_EINVAL;
+}
+}  // namespace
+
 int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
   if (!ctx) return SSB_EINVAL;
   SSB_LOCK(ctx);
+  if (int rc = check_no_collector(ctx)) return rc;
   if (ssb_check_pipeline_config(depth, ctx->slot_streams) != SSB_OK) {
     ctx->err = "pipeline depth x streams per slot outside the supported range (one-stream slots: depth 1..20; three-stream slots: depth 1..5)";
     return SSB_EINVAL;
@@ -804,6 +869,7 @@ int ssb_set_pipeline_depth(ssb_ctx* ctx, int depth) {
 int ssb_set_slot_streams(ssb_ctx* ctx, int streams) {
   if (!ctx) return SSB_EINVAL;
   SSB_LOCK(ctx);
+  if (int rc = check_no_collector(ctx)) return rc;
   if (ssb_check_pipeline_config(ctx->nslots, streams) != SSB_OK) {
     ctx->err = "streams per slot must be 1 or 3, and three-stream slots at most 5 (lower the depth first)";
     return SSB_EINVAL;
@@ -841,7 +907,16 @@ void* ssb_slot_stream(ssb_ctx* ctx, int slot) {
   return (void*)ctx->sl[slot].stream;
 }
 
-const char* ssb_last_error(const ssb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+// a copy taken under the context lock, per calling thread: a failure on another thread cannot free
+// the string while the caller reads it
+const char* ssb_last_error(const ssb_ctx* ctx) {
+  if (!ctx) return "null context";
+  thread_local std::string copy;
+  ssb_ctx* c = const_cast<ssb_ctx*>(ctx);
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  copy = c->err;
+  return copy.c_str();
+}
 
 int ssb_last_kernel_ms(const ssb_ctx* ctx_c, const char* name, float* ms) {
   ssb_ctx* ctx = const_cast<ssb_ctx*>(ctx_c);
@@ -884,12 +959,13 @@ namespace {
 int hash_to_g2_impl(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t* lens, const uint8_t* dst, size_t dst_len,
                     uint8_t* out192) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!msgs32 || !out192) { ctx->err = "null pointer"; return SSB_EINVAL; }
   if (lens)
     for (size_t i = 0; i < n; ++i) if (lens[i] > 32) { ctx->err = "message longer than 32 bytes"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   size_t need = align_up(n * 32) + align_up(n) + align_up(n * sizeof(g2_aff)) + align_up(n * 192) + align_up(launch::hash_ws_bytes(n));
   if ((rc = ensure_ws(ctx, need))) return rc;
@@ -903,7 +979,7 @@ int hash_to_g2_impl(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uint8_t
   hipLaunchKernelGGL(k_serialize_g2, dim3(nblk(n, 64)), dim3(64), 0, ctx->cur->stream, (int)n, d_h, d_out);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out192, d_out, n * 192, hipMemcpyDeviceToHost, ctx->cur->stream));
-  SSB_HIP(hipStreamSynchronize(ctx->cur->stream));
+  { hipStream_t st = ctx->cur->stream; SSB_SYNC_WAIT(st); }
   return SSB_OK;
 }
 }  // namespace
@@ -921,12 +997,13 @@ int ssb_hash_to_g2_msgs(ssb_ctx* ctx, size_t n, const uint8_t* msgs32, const uin
 int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* commitments48, const uint64_t* ids,
                              const uint8_t* shares32, const uint8_t* h48, uint8_t* verdicts) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!commitments48 || !ids || !shares32 || !h48 || !verdicts || t == 0 || t > 1024 || n > (size_t)INT32_MAX) {
     ctx->err = "null pointer, t not in [1, 1024] or n too large"; return SSB_EINVAL;
   }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   int rc;
   if ((rc = ensure_ws(ctx, align_up(n * t * 48) + align_up(n * 8) + align_up(n * 32) + align_up(48) +
                                align_up(sizeof(g1_aff)) + align_up(4) + align_up(n)))) return rc;
@@ -943,17 +1020,18 @@ int ssb_feldman_verify_batch(ssb_ctx* ctx, size_t n, size_t t, const uint8_t* co
   { timed tm(ctx, "k_feldman_share"); launch::feldman_share(st, (int)n, (int)t, d_c, d_x, d_s, d_h, d_hf, d_v); }
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
 int ssb_dleq_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* points48, const uint8_t* c32, const uint8_t* r32,
                           uint8_t* verdicts) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!points48 || !c32 || !r32 || !verdicts || n > (size_t)INT32_MAX) { ctx->err = "null pointer or n too large"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   int rc;
   if ((rc = ensure_ws(ctx, align_up(n * 192) + 2 * align_up(n * 32) + align_up(n)))) return rc;
   carve c{(char*)ctx->cur->ws};
@@ -966,7 +1044,7 @@ int ssb_dleq_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* points48, const
   { timed tm(ctx, "k_dleq_verify"); launch::dleq_verify(st, (int)n, d_p, d_c, d_r, d_v); }
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
@@ -986,12 +1064,13 @@ int ssb_decode_wire_sigs_dev(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t
 
 int ssb_decode_wire_sigs(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t stride, uint8_t* out96, int32_t* status) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!wire || !out96 || !status || stride < launch::WIRE_SIG_BYTES || n > (size_t)INT32_MAX) {
     ctx->err = "null pointer, stride < 202 or n too large"; return SSB_EINVAL;
   }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   int rc;
   if ((rc = ensure_ws(ctx, align_up(n * stride) + align_up(n * 96) + align_up(n * 4)))) return rc;
   carve c{(char*)ctx->cur->ws};
@@ -1002,7 +1081,7 @@ int ssb_decode_wire_sigs(ssb_ctx* ctx, size_t n, const uint8_t* wire, size_t str
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out96, d_out, n * 96, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(status, d_st, n * 4, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
@@ -1010,11 +1089,12 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
                      size_t n_roots, const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint64_t rlc_seed,
                      uint8_t* verdicts) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!pk48 || !sig96 || !root_idx || !roots32 || !verdicts || n_roots == 0) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
   for (size_t i = 0; i < n; ++i) if (root_idx[i] >= n_roots) { ctx->err = "root_idx out of range"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   size_t io = align_up(n * 48) + align_up(n * 96) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n);
   if ((rc = ensure_io(ctx, io))) return rc;
@@ -1031,7 +1111,7 @@ int ssb_verify_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, const uint8_t*
   verify_ws w = carve_verify(c, n, n_roots);
   if ((rc = run_verify(ctx, w, n, n_roots, d_sig, d_pk, nullptr, d_root, d_roots, d, rlc_seed, d_v, [] {}, st))) return rc;
   SSB_HIP(hipMemcpyAsync(verdicts, d_v, n, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
@@ -1487,14 +1567,24 @@ int ssb_threshold_aggregate_batch_cached_submit(ssb_ctx* ctx, size_t n_jobs, con
 
 int ssb_batch_wait(ssb_ctx* ctx, uint64_t ticket) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  std::unique_lock<std::recursive_mutex> ssb_lock_(ctx->mu);
   if (ticket == 0) return SSB_OK;
   const int k = (int)(ticket & 0xff);
   // only generations never issued are unknown; any issued ticket that no live slot holds was
   // delivered (its slot reused, waited before, or removed by ssb_set_pipeline_depth /
   // ssb_set_slot_streams / ssb_pk_cache_*, which deliver first) -- unless its delivery failed
   if ((ticket >> 8) == 0 || (ticket >> 8) > ctx->ticket_gen || k >= SSB_MAX_SLOTS) { ctx->err = "unknown ticket"; return SSB_EINVAL; }
-  if (k < ctx->nslots && ctx->sl[k].host_ticket == ticket) (void)deliver_host(ctx, ctx->sl[k]);
+  // the batch is waited for OUTSIDE the context lock (polled: each query under the lock, so the slot
+  // and its event stay valid), so other threads' batches -- a collector's windows -- launch meanwhile
+  // (ADVICE r5); the delivery itself (host copies) runs under the lock
+  for (;;) {
+    if (!(k < ctx->nslots && ctx->sl[k].host_ticket == ticket)) break;   // delivered by another call
+    if (hipEventQuery(ctx->sl[k].ev_host) != hipErrorNotReady) { (void)deliver_host(ctx, ctx->sl[k]); break; }
+    ssb_lock_.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    ssb_lock_.lock();
+  }
+  (void)hipGetLastError();   // (hipErrorNotReady of the queries)
   auto it = ctx->failed_tickets.find(ticket);
   if (it != ctx->failed_tickets.end()) {
     ctx->failed_tickets.erase(it);
@@ -1520,7 +1610,7 @@ int ssb_threshold_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* s
 int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* share_off, const uint8_t* sig96,
                                const uint64_t* ids, uint8_t* out_sig96, int32_t* out_status) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n_jobs == 0) return SSB_OK;
   if (!share_off || !out_sig96 || !out_status) { ctx->err = "null pointer"; return SSB_EINVAL; }
   if (share_off[0] != 0) { ctx->err = "share_off[0] must be 0"; return SSB_EINVAL; }
@@ -1531,6 +1621,7 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   const size_t n = share_off[n_jobs];
   if (n && (!sig96 || !ids)) { ctx->err = "null share arrays"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   int rc;
   size_t io = align_up(n * 96) + align_up(n * 8) + align_up((n_jobs + 1) * 4) + align_up(n_jobs * 96) + align_up(n_jobs * 4);
   if ((rc = ensure_io(ctx, io))) return rc;
@@ -1560,18 +1651,19 @@ int ssb_unsafe_aggregate_batch(ssb_ctx* ctx, size_t n_jobs, const uint32_t* shar
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n_jobs * 96, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_status, d_st, n_jobs * 4, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
 int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t* root_idx, size_t n_roots,
                    const uint8_t* roots32, const uint8_t* dst, size_t dst_len, uint8_t* out_sig96) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!sk32le || !root_idx || !roots32 || !out_sig96 || n_roots == 0) { ctx->err = "null pointer or no roots"; return SSB_EINVAL; }
   for (size_t i = 0; i < n; ++i) if (root_idx[i] >= n_roots) { ctx->err = "root_idx out of range"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   dst_arg d; int rc = fill_dst(ctx, d, dst, dst_len); if (rc) return rc;
   size_t need = align_up(n * 32) + align_up(n * 4) + align_up(n_roots * 32) + align_up(n_roots * sizeof(g2_aff)) + align_up(n * 96) +
                 align_up(launch::hash_ws_bytes(n_roots));
@@ -1588,16 +1680,17 @@ int ssb_sign_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, const uint32_t
   { timed tm(ctx, "k_sign"); hipLaunchKernelGGL(k_sign, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sk, d_ri, d_h, d_out); }
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_sig96, d_out, n * 96, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
 int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* out_pk48) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!sk32le || !out_pk48) { ctx->err = "null pointer"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   int rc;
   size_t need = align_up(n * 32) + align_up(n * 48);
   if ((rc = ensure_ws(ctx, need))) return rc;
@@ -1608,16 +1701,17 @@ int ssb_sk_to_pk_batch(ssb_ctx* ctx, size_t n, const uint8_t* sk32le, uint8_t* o
   hipLaunchKernelGGL(k_sk_to_pk, dim3(nblk(n, 64)), dim3(64), 0, st, (int)n, d_sk, d_out);
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_pk48, d_out, n * 48, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
 int ssb_pk_validate_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint8_t* out_valid, uint8_t* out_pk48) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (n == 0) return SSB_OK;
   if (!pk48 || !out_valid || !out_pk48 || n > (size_t)INT32_MAX) { ctx->err = "null pointer or n too large"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   int rc;
   if ((rc = ensure_ws(ctx, 2 * align_up(n * 48) + align_up(n)))) return rc;
   carve c{(char*)ctx->cur->ws};
@@ -1628,16 +1722,17 @@ int ssb_pk_validate_batch(ssb_ctx* ctx, size_t n, const uint8_t* pk48, uint8_t* 
   SSB_HIP(hipGetLastError());
   SSB_HIP(hipMemcpyAsync(out_valid, d_v, n, hipMemcpyDeviceToHost, st));
   SSB_HIP(hipMemcpyAsync(out_pk48, d_out, n * 48, hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   return SSB_OK;
 }
 
 int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* out32) {
   if (!ctx) return SSB_EINVAL;
-  SSB_LOCK(ctx);
+  SSB_SYNC_LOCK(ctx);
   if (t == 0) return SSB_OK;
   if (!ids || !out32 || t > SSB_MAX_T) { ctx->err = "bad arguments"; return SSB_EINVAL; }
   SSB_HIP(hipSetDevice(ctx->device));
+  pick_idle_slot(ctx);
   int rc;
   size_t need = align_up(8 * 4) + align_up(t * 8) + align_up(t * 4) + align_up(4) + align_up(t * sizeof(fr));
   if ((rc = ensure_ws(ctx, need))) return rc;
@@ -1656,7 +1751,7 @@ int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* ou
   SSB_HIP(hipGetLastError());
   std::vector<fr> lam(t);
   SSB_HIP(hipMemcpyAsync(lam.data(), d_lam, t * sizeof(fr), hipMemcpyDeviceToHost, st));
-  SSB_HIP(hipStreamSynchronize(st));
+  SSB_SYNC_WAIT(st);
   for (size_t i = 0; i < t; ++i)
     for (int k = 0; k < 8; ++k)
       for (int b = 0; b < 4; ++b) out32[32 * i + 4 * k + b] = (uint8_t)(lam[i].l[k] >> (8 * b));

@@ -163,6 +163,7 @@ def _wire_case(eng):
     sigs[96 * (9 * n + 1):96 * (9 * n + 2)] = wl2["sigs"][96 * (9 * n + 1):96 * (9 * n + 2)]       # present, invalid
     put(9 * n + 1, wire_records(bytes(sigs[96 * (9 * n + 1):96 * (9 * n + 2)])))
     lens[11 * n + 3] = 150; absent.add(11 * n + 3)                                                  # truncated record
+    lens[17 * n + 2] = 260   # trailing bytes after the record: bincode::deserialize ignores them (present)
     inf = b"\xc0" + b"\x00" * 95
     sigs[96 * (13 * n + 2):96 * (13 * n + 3)] = inf                                                 # infinity: present, invalid
     put(13 * n + 2, wire_records(inf))
@@ -206,7 +207,8 @@ def test_wire_collector_drops_undecodable_shares(eng):
         res = [_lib.JobResult() for _ in range(V)]
         keep = []
         for v in range(V):
-            recs = [rec[202 * (v * n + i):202 * (v * n + i) + lens[v * n + i]] for i in range(n)]
+            recs = [rec[202 * (v * n + i):202 * (v * n + i) + min(lens[v * n + i], 202)] +
+                    (b"\x07junk" * 12)[:max(0, lens[v * n + i] - 202)] for i in range(n)]
             r_ = np.ascontiguousarray(rows[v * n:(v + 1) * n], dtype=np.uint32)
             ids = np.asarray(wl["ids"][v * n:(v + 1) * n], dtype=np.uint64)
             keep.append((r_, ids))
@@ -234,7 +236,7 @@ def test_wire_aggregate_entry_point(eng):
     wl, rec, lens, absent, (o_out, o_st, o_err, o_ver), (V, t, n, R) = _wire_case(eng)
     rec = bytearray(rec)
     for s, l in enumerate(lens):
-        if l != 202:
+        if l < 202:
             rec[202 * s:202 * s + 8] = (0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")   # what the collector stores
     N = V * n
     eng.pk_cache_set(wl["share_pks"])
@@ -267,3 +269,156 @@ def test_wire_aggregate_entry_point(eng):
     assert sorted(np.nonzero(wst)[0].tolist()) == sorted(absent)
     assert wst[3 * n + 1] == 1 and wst[5 * n] == 2 and wst[5 * n + 2] == 3 and wst[7 * n + 1] == 4 and wst[9 * n] == 4
     assert wst[11 * n + 3] == 1 and wst[13 * n + 2] == 0 and wst[15 * n + 1] == 0
+
+
+def test_collector_owns_slot_configuration(eng):
+    """while a collector is attached its slots are its own -- ssb_set_pipeline_depth /
+    ssb_set_slot_streams return SSB_EINVAL (a depth below in_flight used to leave its worker a null
+    slot stream), a second collector must use the same in_flight; after ssb_collector_destroy the
+    context is reconfigurable again."""
+    lib = eng._lib
+    col = NativeCollector(eng, max_jobs=64, window_s=0.001, in_flight=2)
+    try:
+        assert lib.ssb_set_pipeline_depth(eng.handle, 1) == -1
+        assert b"collector is attached" in lib.ssb_last_error(eng.handle)
+        assert lib.ssb_set_slot_streams(eng.handle, 3) == -1
+        with pytest.raises(RuntimeError):
+            NativeCollector(eng, max_jobs=64, window_s=0.001, in_flight=3)
+        col2 = NativeCollector(eng, max_jobs=64, window_s=0.001, in_flight=2)
+        col2.close()
+        assert lib.ssb_set_pipeline_depth(eng.handle, 3) == -1   # still attached: col
+        # the collector still works after the refused calls (every golden-free job of a small batch)
+        V, t, n, R = 64, 3, 4, 4
+        wl = bench.make_workload(eng, V, t, n, R, rank=41)
+        rows = col.rows(wl["share_pks"])
+        _, res = collbench_run(col, wl, V, n, t, rows, V, threads=2)
+        _check(res, V, n, *_oracle(wl, V, t, n))
+    finally:
+        col.close()
+    assert lib.ssb_set_pipeline_depth(eng.handle, 3) == 0 and lib.ssb_set_slot_streams(eng.handle, 1) == 0
+    assert lib.ssb_set_pipeline_depth(eng.handle, 1) == 0
+
+
+def test_collector_beside_direct_calls(eng):
+    """ONE engine serves a live collector and direct calls from another thread at the same
+    time -- native submitters push 4 x 1,024 C2-shaped jobs while a Python thread runs whole
+    threshold_aggregate_batch calls (host buffers: ssb_batch_wait polls outside the context lock),
+    unsafe_aggregate (a synchronous entry point: waits outside the lock, on an idle slot when there is
+    one) and registers new keys (ssb_pk_cache_add).  Every collector job == the C oracle, every direct
+    result == the oracle / the master signature, and new keys get fresh rows."""
+    from safestakeoperator_amd import ThresholdSignature
+    V, t, n, R = 1024, 3, 4, 16
+    wl = bench.make_workload(eng, V, t, n, R, rank=43, invalid_rate=0.01)
+    o = _oracle(wl, V, t, n)
+    wd = bench.make_workload(eng, 48, t, n, 4, rank=44)
+    od_out, od_st, od_err, _ = _oracle(wd, 48, t, n)
+    extra = bench.make_workload(eng, 64, t, n, 2, rank=45)["share_pks"]
+    col = NativeCollector(eng, max_jobs=256, window_s=0.001, in_flight=4)
+    errors, direct = [], {"batch": 0, "unsafe": 0}
+    stop = threading.Event()
+
+    def direct_calls():
+        try:
+            ts = ThresholdSignature(t, eng)
+            k = 0
+            while not stop.is_set() or k < 3:
+                jobs = [ThresholdJob([wd["sigs"][96 * (v * n + i):96 * (v * n + i + 1)] for i in range(n)],
+                                     wd["share_pks"][v * n:(v + 1) * n], wd["ids"][v * n:(v + 1) * n],
+                                     wd["roots"][wd["job_root"][v]]) for v in range(48)]
+                out = ts.threshold_aggregate_batch(jobs)
+                for v in range(48):
+                    assert od_st[v] == 0 and out[v] == od_out[v].tobytes(), ("batch", v)
+                direct["batch"] += 1
+                v = k % 48
+                u = ts.unsafe_aggregate([wd["sigs"][96 * (v * n + i):96 * (v * n + i + 1)] for i in range(t)],
+                                        wd["ids"][v * n:v * n + t])
+                assert u == od_out[v].tobytes(), ("unsafe", v)
+                direct["unsafe"] += 1
+                if k == 1:
+                    rows = eng.pk_cache_add(extra)
+                    assert len(set(rows.tolist())) == len(extra) and min(rows.tolist()) >= V * n
+                k += 1
+        except BaseException as e:  # noqa: BLE001 (reported by the main thread)
+            errors.append(e)
+
+    try:
+        rows = col.rows(wl["share_pks"])
+        th = threading.Thread(target=direct_calls)
+        th.start()
+        try:
+            _, res = collbench_run(col, wl, V, n, t, rows, 4 * V, threads=4)
+        finally:
+            stop.set()
+            th.join(120)
+        assert not th.is_alive(), "direct-call thread did not finish"
+        assert not errors, errors
+        _check(res, V, n, *o)
+        assert direct["batch"] >= 3 and direct["unsafe"] >= 3
+    finally:
+        col.close()
+
+
+def test_slot_collector_job_over_64_shares(eng):
+    """A job of more than 64 shares through SlotCollector.submit (beyond the native collector's
+    per-job limit) takes the engine's own batched call for that job alone, on the collector's engine,
+    while the collector runs: 3-of-65 with the first two shares invalid == the C oracle (the combine
+    of shares 3..5), and a 65-share job beside ordinary ones."""
+    V, t, n, R = 2, 3, 65, 1
+    wl = bench.make_workload(eng, V, t, n, R, rank=47)
+    bad = bench.make_workload(eng, V, t, n, R, rank=48)
+    sigs = bytearray(wl["sigs"])
+    sigs[0:192] = bad["sigs"][0:192]          # validator 0: shares 1, 2 from another key
+    wl["sigs"] = bytes(sigs)
+    o_out, o_st, o_err, _ = _oracle(wl, V, t, n)
+    small = bench.make_workload(eng, 8, 3, 4, 1, rank=49)
+    so_out, so_st, _, _ = _oracle(small, 8, 3, 4)
+    with SlotCollector(eng, max_jobs=64, window_s=0.002, in_flight=2) as col:
+        futs = []
+        for v in range(V):
+            futs.append(col.submit(t, ThresholdJob([wl["sigs"][96 * (v * n + i):96 * (v * n + i + 1)] for i in range(n)],
+                                                   wl["share_pks"][v * n:(v + 1) * n], wl["ids"][v * n:(v + 1) * n],
+                                                   wl["roots"][wl["job_root"][v]])))
+        sf = [col.submit(3, ThresholdJob([small["sigs"][96 * (v * 4 + i):96 * (v * 4 + i + 1)] for i in range(4)],
+                                         small["share_pks"][v * 4:(v + 1) * 4], small["ids"][v * 4:(v + 1) * 4],
+                                         small["roots"][0])) for v in range(8)]
+        for v in range(V):
+            assert o_st[v] == 0 and futs[v].result(60) == o_out[v].tobytes(), v
+        for v in range(8):
+            assert so_st[v] == 0 and sf[v].result(60) == so_out[v].tobytes(), v
+
+
+def test_local_signer_matches_oracle_sign(eng):
+    """The local-signing window (ssb_signer_*, SURVEY.md §8f-3) behind DvfSigner::local_sign_and_store
+    (src/node/dvfcore.rs:241-251; every duty's SecretKey::sign, signing_method.rs:318, selection
+    proofs and RANDAO reveals included): 1,536 signatures from 24 concurrent submitters -- 64 shared
+    roots (the validators of one attestation committee sign one root) plus 512 roots signed once --
+    in several windows; every signature == the C oracle's SecretKey::sign byte for byte, and the
+    Ethereum consensus-spec `sign` vector through the window."""
+    import hashlib
+    from safestakeoperator_amd.collector import LocalSigner
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    shared = [hashlib.sha256(b"duty-root" + i.to_bytes(4, "little")).digest() for i in range(64)]
+    work = []
+    for i in range(1536):
+        sk = 1 + int.from_bytes(hashlib.sha256(b"local-sk" + i.to_bytes(4, "little")).digest(), "big") % (R - 1)
+        root = shared[i % 64] if i % 3 else hashlib.sha256(b"own-root" + i.to_bytes(4, "little")).digest()
+        work.append((sk, root))
+    kat = json.load(open(os.path.join(GOLD, "known_answers.json")))["eth_sign"][0]
+    out = {}
+    with LocalSigner(eng, max_jobs=512, window_s=0.002) as signer:
+        def task(k):
+            for i in range(k, len(work), 24):
+                out[i] = signer.submit(*work[i])
+        th = [threading.Thread(target=task, args=(k,)) for k in range(24)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        kat_sig = signer.sign(int(kat["privkey"], 16), bytes.fromhex(kat["message"]), timeout=60)
+        res = {i: f.result(60) for i, f in out.items()}
+        signer.flush()
+        w, n = signer.stats()
+    assert kat_sig.hex() == kat["signature"]
+    assert n == len(work) + 1 and w >= 3
+    for i, (sk, root) in enumerate(work):
+        assert res[i] == bls_c.sign(sk.to_bytes(32, "big"), root), i

@@ -40,6 +40,17 @@ def test_eth_sign_vector_verifies():
     assert not bls_c.verify(pk, bytes(bad), msg)
 
 
+def test_eth_sign_vector_signs():
+    """bls_c.sign (the signer tests' oracle) reproduces the Ethereum consensus-spec `sign` vector
+    (POP DST, src/crypto/impls/blst.rs:11) byte for byte, and refuses keys outside (0, r)."""
+    v = _load("known_answers.json")["eth_sign"][0]
+    sk, msg = bytes.fromhex(v["privkey"]), bytes.fromhex(v["message"])
+    assert bls_c.sign(sk, msg).hex() == v["signature"]
+    assert bls_c.sign(b"\0" * 32, msg) is None
+    r = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    assert bls_c.sign(r.to_bytes(32, "big"), msg) is None
+
+
 @pytest.mark.parametrize("case", _load("threshold_cases.json")["cases"], ids=lambda c: c["name"])
 def test_threshold_golden_cases(case):
     sigs = [bytes.fromhex(s) for s in case["sigs"]]

@@ -43,6 +43,8 @@ def test_patches_apply_in_order(tmp_path):
     assert "bincode::deserialize::<Signature>(&data)" in op
     oc = (tmp_path / "src/validation/operator_committees.rs").read_text()
     assert "register_committee_keys(&def.operator_public_keys)" in oc
+    dc = (tmp_path / "src/node/dvfcore.rs").read_text()   # f-3: every duty's local signature batched
+    assert "slot_signer::sign(&self.local_keypair.sk, message).await" in dc and "let sig = self.local_sign(message);" in dc
     gt = (tmp_path / "src/crypto/generic_threshold.rs").read_text()
     assert "fn threshold_aggregate_batch" in gt and "pub struct ThresholdJob" in gt
 
