@@ -356,6 +356,9 @@ def main():
     ap.add_argument("--no-registry", dest="registry_leg", action="store_false",
                     help="skip the registry-operator-id leg (value_registry: the same path and --steps, ids from "
                          "the registry contract instead of 1..n)")
+    ap.add_argument("--no-adversarial", dest="adversarial_legs", action="store_false",
+                    help="skip the adversarial legs (value_invalid_1e2, value_bad_operator: the same path and --steps "
+                         "with 1%% of the shares invalid / one faulty operator in every committee)")
     ap.add_argument("--sustained-steps", type=int, default=1000,
                     help="length of the sustained-rate run reported as value_sustained (0: skip)")
     ap.add_argument("--collector-windows", type=int, default=200,
@@ -816,6 +819,28 @@ def main():
         coll = dict(seconds=c_sec, jobs=n_jobs, windows=cw[0], ok=collector_ok(c_res, n_jobs), profile=cprof)
         w_sec, w_res, _, ww, _ = collector_leg(True)
         coll.update(wire_seconds=w_sec, wire_windows=ww[0], wire_ok=collector_ok(w_res, n_jobs))
+    # adversarial legs: the same path, slots, key table and --steps with invalid shares -- 1% of the shares
+    # signed over the wrong root (invalid_1e2), and every share of operator 1 invalid, a faulty operator in
+    # every committee (bad_operator) -- the inputs the reference's per-share scan exists for
+    # (generic_threshold.rs:149-169).  Every batch fails its RLC check and takes the exact fallback;
+    # statuses, every share verdict and every combined signature are checked like the headline's.
+    adv = {}
+    if args.adversarial_legs and args.ids == "seq" and not strong and not args.final_verify and not wl["n_bad"]:
+        for gi, (name, kw) in enumerate((("invalid_1e2", dict(invalid_rate=0.01)), ("bad_operator", dict(bad_operator=1)))):
+            torch.cuda.synchronize(dev)
+            wl_a = make_workload(eng, V, t, n, n_roots, rank, **kw)
+            assert wl_a["pks"] == wl["pks"]   # (the same keys: the key table stands)
+            va = np.asarray(wl_a["valid"], dtype=np.uint8)
+            inputs.update(d_sig=dt8(wl_a["sigs"]), gen=10 + gi)
+            truth.update(valid=va, job_ok=va.reshape(V, n).sum(axis=1) >= t, msig=msig_arr)
+            use_cache[0] = True
+            streams.clear()
+            ok_a = warm_and_check()
+            el_a = timed_run()
+            ok_a = ok_a and check_slots()
+            adv[name] = dict(seconds=el_a, ok=ok_a, n_bad=wl_a["n_bad"])
+        inputs.update(d_sig=d_sig, gen=0)
+        truth.update(valid=valid, job_ok=job_ok, msig=msig_arr)
     # the same path and the same --steps on committees with REGISTRY operator ids (distinct pseudo-random
     # ids in [1, 2^16) per committee, src/node/node.rs:470-474): the Lagrange coefficients are ratios of
     # small integers, so the combine is [M^-1](sum c_i sig_i) per job (k_combine_ratio) where ids 1..n
@@ -838,10 +863,11 @@ def main():
         reg = dict(seconds=elapsed_reg, ok=ok_r)
     ok_st = ok_comb = ok_head and ok_other and ok_timed and ok_x and ok_host and ok_sus and (
         coll is None or (coll["ok"] and coll["wire_ok"]))
-    ok_st = ok_st and (reg is None or reg["ok"])
+    ok_st = ok_st and (reg is None or reg["ok"]) and all(a["ok"] for a in adv.values())
     if dist is not None:
         tt = torch.tensor([elapsed, elapsed_other, elapsed_sus or 0.0, coll["seconds"] if coll else 0.0,
-                           reg["seconds"] if reg else 0.0, coll["wire_seconds"] if coll else 0.0],
+                           reg["seconds"] if reg else 0.0, coll["wire_seconds"] if coll else 0.0,
+                           adv["invalid_1e2"]["seconds"] if adv else 0.0, adv["bad_operator"]["seconds"] if adv else 0.0],
                           dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, elapsed_other = float(tt[0].item()), float(tt[1].item())
@@ -853,6 +879,8 @@ def main():
             reg["seconds"] = float(tt[4].item())
         if coll:
             coll["wire_seconds"] = float(tt[5].item())
+        if adv:
+            adv["invalid_1e2"]["seconds"], adv["bad_operator"]["seconds"] = float(tt[6].item()), float(tt[7].item())
         okt = torch.tensor([1 if (ok_st and ok_comb) else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_all = bool(okt.item())
@@ -974,6 +1002,17 @@ def main():
                                    "operator ids: distinct pseudo-random ids in [1, 2^16) per committee "
                                    "(src/node/node.rs:470-474); lambda_i = c_i / M, combined as [M^-1](sum c_i sig_i), "
                                    "one lane per job (k_combine_ratio)") if reg else None),
+            "value_invalid_1e2": (round(V_glob * n * args.steps / adv["invalid_1e2"]["seconds"], 1) if adv else None),
+            "value_bad_operator": (round(V_glob * n * args.steps / adv["bad_operator"]["seconds"], 1) if adv else None),
+            "adversarial": ({k: dict(ms_per_step=round(a["seconds"] / args.steps * 1e3, 3), steps=args.steps,
+                                     invalid_shares_per_batch=a["n_bad"], frac_of_value=round(elapsed / a["seconds"], 3),
+                                     results_ok=a["ok"]) for k, a in adv.items()} | {
+                                "path": "the headline path (same slots, steps, key cache) with invalid shares: "
+                                        "invalid_1e2 -- 1% of the shares signed over the next root; bad_operator -- every "
+                                        "share of operator 1 invalid (a faulty operator in every committee).  Every batch "
+                                        "fails its RLC check and takes the exact fallback (committee stage, exclusion "
+                                        "check / group tests); statuses, share verdicts and combined signatures checked"}
+                            if adv else None),
             "host_buffers": "every batch's inputs start in, and its results end in, ordinary host memory: "
                             "ssb_threshold_aggregate_batch%s_submit copies them into the slot's pinned device-mapped "
                             "staging buffer, the kernels read / write it in place over PCIe, ssb_batch_wait delivers "

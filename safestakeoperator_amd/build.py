@@ -267,4 +267,5 @@ def build_collbench(verbose: bool = True) -> str:
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
-    build_collbench()
+    if not VARIANT:   # (bench_tools/libcollbench.so links the product library only)
+        build_collbench()

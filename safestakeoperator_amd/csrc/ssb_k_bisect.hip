@@ -58,7 +58,7 @@ constexpr unsigned FB_GRID_MAX = 512;
 // stores of one workgroup are ordered by them).
 struct fb_prep_args { int n_roots, L, lb; const uint32_t* share_root; uint32_t* cnt; uint32_t* start; uint32_t* cursor;
                       uint32_t* gst; uint32_t* perm; uint32_t* rtk; uint32_t* nfail; const uint64_t* ids;
-                      uint32_t* kcnt; uint32_t* kstart; uint32_t* klist; };
+                      uint32_t* kcnt; uint32_t* kstart; uint32_t* klist; uint32_t* ictr; };
 SSB_INL uint32_t fb_bucket(uint64_t id, int nb) {
   return nb > 1 ? (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> 60) & (uint32_t)(nb - 1) : 0u;
 }
@@ -78,6 +78,7 @@ SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   for (int k = t; k < K; k += NT) kc[k] = 0u;
   for (int r = t; r < n_roots; r += NT) a.rtk[r] = 0u;
   if (t == 0) *a.nfail = 0u;
+  if (t == 0 && a.ictr) *a.ictr = 0u;   // k_fb_excl's group-test item counter (the next launch on the stream)
   __syncthreads();
   for (int s = t; s < n; s += NT)
     if (share_root[s] < (uint32_t)n_roots) atomicAdd(&kc[key(s)], 1u);
@@ -563,7 +564,7 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
 // ONE final exponentiation.
 // (the roles of k_fb_excl are out of line: each role's temporaries live in its own frame, and the
 // kernel's private segment is the largest role's, not their sum)
-struct ex_lds { fr_lds u; uint32_t flg, last, ncand; g1_aff sP; g2_aff sQ; };
+struct ex_lds { fr_lds u; uint32_t flg, last, ncand, item; g1_aff sP; g2_aff sQ; };
 SSB_FN void ex_singles(ex_lds& L, int first, uint32_t ns, const uint32_t* __restrict__ slist,
                        const uint32_t* __restrict__ share_root, const g2_aff* __restrict__ sig_aff,
                        const g1_aff* __restrict__ pk_aff, const g2_aff* __restrict__ H, uint8_t* __restrict__ verdict) {
@@ -866,17 +867,34 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
     return;
   }
   __shared__ ex_lds L;
-  if (gmode) {   // group-test mode: blocks stride over the (key, quarter) items
+  if (gmode) {   // group-test mode: blocks take (key, quarter) items from a counter
     if (blk == 0 && lane_ == 0) *xok = 2u;
     const uint32_t NB = (uint32_t)launch::fb_nbuckets(n_roots);
-    // four items per non-empty key (klist: fb_prep_block), striding over the blocks: every block
-    // takes at most ceil(items / grid) of them, a key's four quarters run on neighbouring blocks.
-    // (Over all n_roots * NB keys in key order, a grid that is a multiple of 64 kept every block on
-    // the same offsets inside each root's 64 items -- a quarter of the blocks got every busy item, the
-    // faulty-operator batch's last items ended at 30.9 ms against a 7 ms median, round-5 trace.)
+    // four items per non-empty key (klist: fb_prep_block), handed out in order by an item counter
+    // (xtk[1], zeroed by fb_prep_block in k_fb_rlc, the previous launch on the stream): a block that
+    // finishes an item takes the next one, so a block busy with a key's combine and check holds up no
+    // items, and a key's four quarters run on four blocks at once.  (Static strides: over all n_roots x
+    // NB keys in key order a quarter of the blocks got every busy item, 30.9 ms against a 7 ms median;
+    // over the non-empty keys 14.2 ms, round-5 traces.)  The item index travels from lane 0 to the
+    // wave through LDS (L.item, outside the union the item's bucket lists reuse), and is checked
+    // against `items` before any item-indexed access; the counter overshoots by one fetch per block,
+    // harmlessly (nothing reads it past `items`).
     const uint32_t items = 4u * klist[n_roots * NB];
-    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+    uint32_t* ictr = xtk + 1;
+    for (;;) {
+      if (lane_ == 0) L.item = atomicAdd(ictr, 1u);
+      __syncthreads();
+      const uint32_t it = __builtin_amdgcn_readfirstlane(L.item);
+      __syncthreads();   // (every lane has read L.item before lane 0 writes the next)
+      if (it >= items) break;   // uniform
       const uint32_t key = klist[it >> 2], q = it & 3;
+#ifdef SSB_FB_CHECKS
+      if (key >= (uint32_t)n_roots * NB || (it >> 2) >= klist[n_roots * NB]) {
+        if (lane_ == 0) printf("[fb-check] k_fb_excl block %u: item %u of %u -> key %u (keys %u)\n", blockIdx.x, it, items,
+                               key, (uint32_t)n_roots * NB);
+        break;
+      }
+#endif
       const uint32_t gn = kcnt[key];
       if (!gn) continue;   // (uniform: the four items of an empty key all skip: no ticket)
       const uint32_t* list = perm + kstart[key];
@@ -1105,7 +1123,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
   const uint32_t* xok = committee ? fw.xok : nullptr;
   const fb_prep_args prep{n_roots, L, lb, share_root, fw.cnt, fw.start, fw.cursor, fw.gst, fw.perm, fw.rtk, fw.nfail,
                           committee ? jobs.ids : nullptr, committee ? fw.kcnt : nullptr, committee ? fw.kstart : nullptr,
-                          committee ? fw.klist : nullptr};
+                          committee ? fw.klist : nullptr, committee ? fw.xtk + 1 : nullptr};
   hipLaunchKernelGGL(k_fb_rlc, dim3(nb((size_t)n, 64) + nb((size_t)cj.n_jobs, 64) + 1), dim3(64), 0, st, n, key, ok, flags,
                      fw.k64, fast_verdicts ? verdict : (uint8_t*)nullptr, prep, cj, sig, fw.slist, fw.nS);
   if (committee)

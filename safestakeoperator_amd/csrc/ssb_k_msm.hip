@@ -276,19 +276,21 @@ __global__ void SSB_LB(64) k_rlc_pk(int n, rlc_key key, const uint32_t* __restri
 // subgroup check of every decodable signature (psi(P) == [x]P, sig_groupcheck)
 __global__ void SSB_LB2(64) k_subgroup(int n, const uint32_t* __restrict__ sflags,
                                                  const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags) {
+  __shared__ uint32_t keep[r28::KEEP_WORDS * 64];
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const uint32_t sf = sflags[s];
-  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s], (r28::keep_t*)keep + threadIdx.x) : 0u;
 }
 
 // exact single-lane redo of the shares whose lane-group subgroup check met an exceptional addition
 __global__ void SSB_LB2(64) k_subgroup_fix(int n, const uint32_t* __restrict__ sflags, const g2_aff* __restrict__ sig_aff,
                                           const uint32_t* __restrict__ exc, uint32_t* __restrict__ gflags) {
+  __shared__ uint32_t keep[r28::KEEP_WORDS * 64];
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n || !exc[s]) return;
   const uint32_t sf = sflags[s];
-  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+  gflags[s] = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s], (r28::keep_t*)keep + threadIdx.x) : 0u;
 }
 
 // subgroup checks (blocks [0, nbs)) with the hash's SWU map riding along (the next nbm blocks)
@@ -305,10 +307,12 @@ SSB_ROLE void sg_scatter_role(int i, const sort_scatter& sc) {
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(SSB_SG_WAVES))) k_subgroup_map(int n, uint32_t nbs, const uint32_t* __restrict__ sflags,
                                            const g2_aff* __restrict__ sig_aff, uint32_t* __restrict__ gflags, h2c_fuse h,
                                            uint32_t nbm, sort_scatter sc) {
-  __shared__ h2c_cand cs[64];
+  // LDS: the map role's candidates, or the subgroup lanes' affine points (r28::KEEP_WORDS words each)
+  constexpr size_t SG_LDS = H2C_MAP_LDS > r28::KEEP_WORDS * 64 * 4 ? H2C_MAP_LDS : r28::KEEP_WORDS * 64 * 4;
+  __shared__ __attribute__((aligned(16))) char lds[SG_LDS];
   if (blockIdx.x >= nbs) {
     const uint32_t b = blockIdx.x - nbs;
-    if (b < nbm) { sg_map_role(b, cs, h); return; }
+    if (b < nbm) { sg_map_role(b, (h2c_cand*)lds, h); return; }
     const int i = (b - nbm) * 64 + threadIdx.x;
     if (i < sc.n) sg_scatter_role(i, sc);
     return;
@@ -316,7 +320,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const uint32_t sf = sflags[s];
-  const uint32_t gf = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s]) : 0u;
+  const uint32_t gf = ((sf & DEC_OK) && !(sf & DEC_INF)) ? unit_subgroup(sig_aff[s], (r28::keep_t*)lds + threadIdx.x) : 0u;
   gflags[s] = gf;
   if (sc.flags) {
     uint32_t f = combine_flags(sf, sc.pflags[s], gf);

@@ -5,6 +5,7 @@
 #pragma once
 #include "ssb_pairing.h"
 #include "ssb_h2c.h"
+#include "ssb_f28.h"
 
 namespace ssb {
 
@@ -91,7 +92,21 @@ SSB_FN uint32_t unit_decode(g2_aff& sig, g1_aff& pk, const uint8_t* sig96, const
 // run two waves per SIMD (SSB_LB2), which a call's frame and callee-saved registers prevent.
 SSB_INL uint32_t unit_decode_sig(g2_aff& sig, const uint8_t* sig96) { return g2_decompress_inl(sig, sig96); }
 SSB_INL uint32_t unit_decode_pk(g1_aff& pk, const uint8_t* pk48) { return g1_decompress_inl(pk, pk48); }
-SSB_INL uint32_t unit_subgroup(const g2_aff& sig) { return g2_in_subgroup_inl(sig) ? DEC_IN_GROUP : 0u; }
+// The per-share subgroup checks run in the reduced radix (ssb_f28.h: 14 x 28-bit limbs, one
+// v_mad_u64_u32 per limb product); SSB_SG_ENGINE=1 builds keep the engine's 12 x 32-bit form (A/B), and
+// the op counter counts the algorithm in the engine's form (its units define the roofline's MADs).
+// keep: the lane's r28::KEEP_WORDS words of LDS at stride 64 (the block's array + threadIdx.x)
+SSB_INL uint32_t unit_subgroup(const g2_aff& sig, r28::keep_t* keep) {
+#if defined(SSB_SG_ENGINE) || defined(SSB_OPCOUNT)
+  (void)keep;
+  return g2_in_subgroup_inl(sig) ? DEC_IN_GROUP : 0u;
+#elif defined(__HIP_DEVICE_COMPILE__)
+  return r28::g2_in_subgroup_keep<64>(sig, keep) ? DEC_IN_GROUP : 0u;
+#else
+  (void)keep;
+  return r28::g2_in_subgroup(sig) ? DEC_IN_GROUP : 0u;
+#endif
+}
 // (k odd: the RLC scalars are rlc_scalar_odd)
 SSB_FN void unit_rlc_sig(g2_jac& r, const g2_aff& sig, uint64_t k) {
   const uint32_t kw[2] = {(uint32_t)k, (uint32_t)(k >> 32)};

@@ -9,6 +9,7 @@
 #include <sstream>
 #include "../../safestakeoperator_amd/csrc/ssb_units.h"
 #include "../../safestakeoperator_amd/csrc/ssb_lane_ops.h"
+#include "../../safestakeoperator_amd/csrc/ssb_f28.h"
 
 #ifdef SSB_OPCOUNT
 ssb_opcounts g_ssb_counts;
@@ -232,6 +233,50 @@ int main() {
       g2_aff a1, a2; jac_to_aff(a1, r1); jac_to_aff(a2, r2);
       uint8_t o1[96], o2[96]; g2_compress(o1, a1); g2_compress(o2, a2);
       printf("%s %s\n", hex(o1, 96).c_str(), hex(o2, 96).c_str());
+    } else if (cmd == "sg28") {  // sg28 <n> -> "<agree> <total> <in> <out>": reduced-radix subgroup test vs the engine's
+      int n = 0; is >> n;
+      int agree = 0, tot = 0, nin = 0, nout = 0;
+      uint8_t m[32];
+      for (int k = 0; k < 32; ++k) m[k] = (uint8_t)(0x5b * k + 7);
+      auto check = [&](const g2_aff& P) {
+        const bool a = g2_in_subgroup_inl(P), b = r28::g2_in_subgroup(P);
+        agree += a == b; ++tot; nin += a; nout += !a;
+      };
+      g2_aff inf; inf.inf = 1; inf.x = fp2_zero(); inf.y = fp2_zero();
+      check(inf);
+      for (int i = 0; i < n; ++i) {
+        m[0] = (uint8_t)i; m[1] = (uint8_t)(i >> 8);
+        g2_aff P, Hraw;
+        hash_to_g2(P, m, (const uint8_t*)DST, (int)strlen(DST));                // in G2
+        check(P);
+        uint8_t uni[256]; expand_message_xmd_256(uni, m, (const uint8_t*)DST, (int)strlen(DST));
+        fp2 u; fp_from_be64_mod(u.c0, uni); fp_from_be64_mod(u.c1, uni + 64);
+        fp2 x, y; map_to_curve_sswu(x, y, u); iso3_map(Hraw, x, y);              // on E2, not in G2
+        check(Hraw);
+        g2_jac j; jac_from_aff(j, P); jac_add_aff(j, j, Hraw); g2_aff S; jac_to_aff(S, j);   // P + Hraw: not in G2
+        check(S);
+        g2_aff nP = P; fp2_neg(nP.y, nP.y); check(nP);                          // -P: in G2
+        const uint32_t kw[2] = {(uint32_t)(0x9e3779b9u * (i + 1)), (uint32_t)i};
+        jac_mul_aff(j, P, kw, 2); g2_aff kP; jac_to_aff(kP, j); if (!kP.inf) check(kP);   // [k]P: in G2
+      }
+      // the reduced-radix arithmetic itself: products, two-product sums, fold / canon against the engine
+      int aok = 0, an = 0;
+      uint64_t z = 0x9E3779B97F4A7C15ull;
+      auto rnd = [&](fp& v) { for (int k = 0; k < 12; ++k) { z ^= z << 13; z ^= z >> 7; z ^= z << 17; v.l[k] = (uint32_t)z; } v.l[11] &= 0x0fffffffu; fp t; fp_to_mont(t, v); v = t; };
+      auto back = [&](const r28::f& a) { r28::f y; r28::fold(y, a); r28::f c; r28::canon(c, y); fp o; r28::to32(o.l, c);
+                                         fp k = fp_zero(); k.l[11] = 1u << 24; fp t; fp_mul(t, o, k); return t; };   // (x 2^392) 2^376 / 2^384 = x 2^384: engine form
+      for (int i = 0; i < 2000; ++i) {
+        fp a, b, c, d; rnd(a); rnd(b); rnd(c); rnd(d);
+        r28::f A, B, C, D, R; r28::from_engine(A, a); r28::from_engine(B, b); r28::from_engine(C, c); r28::from_engine(D, d);
+        fp want; fp_mul(want, a, b);
+        r28::mul(R, A, B); aok += fp_eq(back(R), want); ++an;
+        fp w2; fp_mul(w2, c, d); fp_add(w2, w2, want);
+        r28::mul2(R, A, B, C, D); aok += fp_eq(back(R), w2); ++an;
+        // a value near the bounds: A + 64 p, folded
+        r28::f Big; for (int k = 0; k < 14; ++k) Big.l[k] = A.l[k] + r28::K64P[k]; r28::norm(Big);
+        aok += fp_eq(back(Big), a); ++an;
+      }
+      printf("%d %d %d %d %d %d\n", agree, tot, nin, nout, aok, an);
     } else if (cmd == "invtest") {  // invtest N -> "<ok> <n>": fp_inv (safegcd) == Fermat, a * a^-1 == 1
       int n = 0; is >> n;
       uint64_t z = 0x243F6A8885A308D3ull;
@@ -283,7 +328,7 @@ int main() {
       if (!(fl & FLAG_CANDIDATE)) { printf("ERR not a candidate\n"); fflush(stdout); continue; }
       unit_decode_sig(sig, sb.data()); rec("decode_sig", 1);
       unit_decode_pk(pk, pkb.data()); rec("decode_pk", 1);
-      unit_subgroup(sig); rec("subgroup", 1);
+      unit_subgroup(sig, nullptr); rec("subgroup", 1);
       const int NS = 16;
       g2_jac rs; g1_jac rp;
       for (int i = 0; i < NS; ++i) unit_rlc_sig(rs, sig, rlc_scalar(0x5AFE57A4Eull, (uint64_t)i));
