@@ -290,6 +290,53 @@ def cpu_baseline(wl, t, n, gpu_out=None, n_val=4096, n_val_share=1024, threads=N
                 seconds_total=round(sum(ts_rlc) + sum(ts_share), 2))
 
 
+class Exchanger:
+    """The helper thread of exchange_group: for each group in submission order, wait (on the host)
+    for the group's batch events, then issue its all-gather (BatchExchange.flush) -- the same order
+    on every rank, and drain() before any other collective (barrier, all_reduce) of the main
+    thread.  submit() returns a Future of the collective's handles."""
+
+    def __init__(self, xchg, dev):
+        import queue
+        import threading
+        self.xchg, self.dev = xchg, dev
+        self.q = queue.Queue()
+        self.t = threading.Thread(target=self._run, name="bench-exchange", daemon=True)
+        self.t.start()
+
+    def submit(self, items):
+        from concurrent.futures import Future
+        fut = Future()
+        self.q.put((items, fut))
+        return fut
+
+    def _run(self):
+        import torch
+        if self.dev is not None and getattr(self.dev, "type", "cpu") == "cuda":
+            torch.cuda.set_device(self.dev)
+        while True:
+            job = self.q.get()
+            try:
+                if job is None:
+                    return
+                items, fut = job
+                try:
+                    for _, ev in items:
+                        ev.synchronize()
+                    fut.set_result(self.xchg.flush([o for o, _ in items]))
+                except BaseException as e:  # noqa: BLE001 (re-raised by the main thread's job.result())
+                    fut.set_exception(e)
+            finally:
+                self.q.task_done()
+
+    def drain(self):
+        self.q.join()
+
+    def close(self):
+        self.q.put(None)
+        self.t.join()
+
+
 def launch_command(n, argv, port):
     """The torch.distributed.run command bench.py --gpus N runs itself when no launcher set WORLD_SIZE."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
@@ -461,16 +508,21 @@ def main():
     d_t = torch.full((V,), t, dtype=torch.int32, device=dev)
     d_jr = torch.tensor(wl["job_root"], dtype=torch.int32, device=dev)
     d_roots = dt8(b"".join(wl["roots"]))
-    outs = [dict(out=torch.empty((V, 96), dtype=torch.uint8, device=dev), st=torch.empty((V,), dtype=torch.int32, device=dev),
-                 err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev),
-                 fv=torch.empty((V,), dtype=torch.uint8, device=dev))
-            for _ in range(S)]
+    def out_set():
+        return dict(out=torch.empty((V, 96), dtype=torch.uint8, device=dev), st=torch.empty((V,), dtype=torch.int32, device=dev),
+                    err=torch.empty((V, 2), dtype=torch.int64, device=dev), ver=torch.empty((N,), dtype=torch.uint8, device=dev),
+                    fv=torch.empty((V,), dtype=torch.uint8, device=dev))
+    # with a process group every slot alternates between TWO output sets: a batch's results are all-
+    # gathered while the slot's next batch writes the other set (exchange_group)
+    out_sets = [[out_set(), out_set()] if dist_run else [out_set()] for _ in range(S)]
+    sel = [0] * S                                   # the set slot k's last batch wrote
+    outs = [o[0] for o in out_sets]                 # slot k's last batch's outputs
     dst_arr = (ctypes.c_uint8 * len(DST)).from_buffer_copy(DST)
     lib = eng._lib
     seed_base = 0x5AFE57A4E ^ (rank << 40)
 
     streams = {}
-    pending = {}    # slot -> in-flight all-gather handles reading that slot's output buffers
+    pending = {}    # id(output set) -> the exchange job (all-gather handles) reading that set
 
     # validator registration (outside the timed region): every operator key decompressed once, and
     # with the final verify the validators' master keys after them (table rows N .. N+V-1)
@@ -499,7 +551,8 @@ def main():
     def step(i, k):
         """batch i on pipeline slot k (engine slot k, output buffers k); the caller's stream is the
         slot's own main stream (ssb_slot_stream), so the bench adds no hardware queue"""
-        o = outs[k]
+        sel[k] = (sel[k] + 1) % len(out_sets[k])
+        o = outs[k] = out_sets[k][sel[k]]
         if k not in streams:
             streams[k] = torch.cuda.ExternalStream(lib.ssb_slot_stream(eng.handle, k), device=dev)
         s = streams[k]
@@ -511,16 +564,17 @@ def main():
                                               h_in["roots"], seed=(seed_base + i) & (2 ** 64 - 1),
                                               pk_index=h_in["pkidx"] if use_cache[0] else None)
             return
-        # the slot's output buffers are rewritten by this batch: order it after the all-gather of the
-        # slot's previous batch (a stream wait, the host does not block)
-        pend = pending.pop(k, [])
-        if pend:
-            with torch.cuda.stream(s):
-                for w in pend:
+        # this output set is rewritten by this batch: order it after the all-gather that read it (two
+        # batches of this slot ago: issued long since, so neither the host nor the stream waits in
+        # practice -- a stream wait on RCCL's event)
+        job = pending.pop(id(o), None)
+        if job is not None:
+            for w in job.result():
+                with torch.cuda.stream(s):
                     w.wait()
         # (the argument tuple of slot k is built once: the timed loop's host time per submit is the
         # library's, not Python's -- the last batch of a round starts that much later)
-        key = (k, use_cache[0], s.cuda_stream, inputs["gen"])
+        key = (k, sel[k], use_cache[0], s.cuda_stream, inputs["gen"])
         a = call_args.get(key)
         if a is None:
             a = call_args[key] = (
@@ -550,28 +604,32 @@ def main():
     inputs = dict(d_sig=d_sig, d_ids=d_ids, d_jr=d_jr, d_roots=d_roots, gen=0)   # the batch step() submits
     group = []      # slots whose results are not exchanged yet
     xchg = None     # the process group's exchange (phase 2; phases 1 / 1b run before the group exists)
+    exchanger = None   # its helper thread
 
     def exchange_group():
         """RCCL all-gather over xGMI of the results of the batches since the last exchange, ONE
-        collective per array for the group (fewer, larger collectives: with one hardware queue per
-        slot, an all-gather per batch would keep RCCL's stream active beside the 20 slot queues, and
-        past 20 active queues the firmware time-slices them).  Asynchronous: RCCL's stream waits
-        for the group's batches, no slot stream waits for RCCL -- only a slot's next batch, which
-        rewrites its output buffers, waits for the all-gather that reads them.  Weak scaling:
-        every rank's own batch (shard.exchange); strong: this rank's shard of the one global
-        batch, reassembled per batch in the global order (shard.exchange_var)."""
+        collective per array for the group (fewer, larger collectives).  Issued by a helper thread
+        (exchanger) once the group's batches have FINISHED -- an event per slot, waited on the host
+        -- so no GPU queue sits blocked on them: round 5 issued it at once, with RCCL's stream and
+        one slot stream waiting on the whole group, and the 1,000-step sustained rate at N = 1 fell to
+        0.76x of the run without the process group (profiles/r05_rccl_n1.json): a stream blocked on a
+        barrier still holds its hardware queue, and past ~20 active queues the firmware time-slices
+        them.  The slot's next batch writes its OTHER output set, so the main thread never waits for
+        the exchange; the batch after it, which rewrites this set, waits (a stream wait) for the
+        all-gather that read it.  Weak scaling: every rank's own batch (shard.exchange); strong: this
+        rank's shard of the one global batch, reassembled per batch in the global order
+        (shard.exchange_var)."""
         if dist is None or not group:
             group.clear()
             return
-        s = streams[group[-1]]
-        with torch.cuda.stream(s):
-            for k in group[:-1]:
-                ev = torch.cuda.Event()
-                ev.record(streams[k])
-                s.wait_event(ev)
-            works = xchg.flush([outs[k] for k in group])
+        items = []
         for k in group:
-            pending[k] = works
+            ev = torch.cuda.Event()
+            ev.record(streams[k])
+            items.append((outs[k], ev))
+        job = exchanger.submit(items)
+        for o, _ in items:
+            pending[id(o)] = job
         group.clear()
 
     # phase 1: single-batch latency and per-kernel times (depth 1, no overlap between batches)
@@ -670,6 +728,7 @@ def main():
         else:
             dist.init_process_group("gloo")
         xchg = BatchExchange(strong, sizes=sizes, device=cdev)
+        exchanger = Exchanger(xchg, dev)
     # the master key's signature of every validator: every combined signature must equal it
     # (tests/test_generic_threshold.rs:35), checked for every slot's batch, untimed
     msig = eng.sign_batch(wl["master"], wl["job_root"], wl["roots"])
@@ -702,11 +761,15 @@ def main():
             for k in range(S):
                 step(k, k)
                 exchange_group()
+                if exchanger is not None:
+                    exchanger.drain()
                 torch.cuda.synchronize(dev)
             primed.append(1)
         for i in range(max(args.warmup, S)):
             step(i, i % S)
         exchange_group()
+        if exchanger is not None:
+            exchanger.drain()
         torch.cuda.synchronize(dev)
         return check_slots(host=use_host[0])
 
@@ -742,6 +805,8 @@ def main():
         if use_host[0]:
             for pb in host_io.values():   # every batch's outputs delivered to host memory
                 pb.wait()
+        if exchanger is not None:
+            exchanger.drain()             # every group's collective issued before the barrier below
         torch.cuda.synchronize(dev)
         if dbg:
             print("host ms per submit:", " ".join("%.2f" % x for x in host_ms), file=sys.stderr)
@@ -1040,6 +1105,8 @@ def main():
             rec["cpu_baseline"] = cpu_baseline(wl, t, n, gpu_out=outs[0]["out"].cpu().numpy(), n_val=min(4096, V),
                                                n_val_share=min(1024, V))
         print(json.dumps(rec), flush=True)
+    if exchanger is not None:
+        exchanger.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -345,6 +345,7 @@ enum : uint32_t {
 };
 
 // blst_p2_uncompress semantics.  Returns DEC_* bits (0 on BLST_BAD_ENCODING / NOT_ON_CURVE).
+template <bool INL = true>
 SSB_INL uint32_t g2_decompress_inl(g2_aff& r, const uint8_t* in) {
   const uint8_t b0 = in[0];
   r.inf = 0;
@@ -367,13 +368,13 @@ SSB_INL uint32_t g2_decompress_inl(g2_aff& r, const uint8_t* in) {
   fp2 b = fp2_from_c(FP2_B2);
   fp2_add(y2, y2, b);
   fp2 y;
-  if (!fp2_sqrt_inl(y, y2)) return 0;
+  if (!fp2_sqrt_inl<INL>(y, y2)) return 0;
   const bool want = (b0 & 0x20) != 0;
   if (fp2_lex_largest(y) != want) fp2_neg(y, y);
   r.x = x; r.y = y;
   return DEC_OK;
 }
-SSB_FN uint32_t g2_decompress(g2_aff& r, const uint8_t* in) { return g2_decompress_inl(r, in); }
+SSB_FN uint32_t g2_decompress(g2_aff& r, const uint8_t* in) { return g2_decompress_inl<false>(r, in); }
 
 SSB_INL uint32_t g1_decompress_inl(g1_aff& r, const uint8_t* in) {
   const uint8_t b0 = in[0];

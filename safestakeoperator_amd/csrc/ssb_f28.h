@@ -1,4 +1,4 @@
-// ssb_f28.h -- reduced-radix Fp for the per-share G2 subgroup checks (round 6).
+// ssb_f28.h -- the per-share G2 subgroup checks in the reduced radix of ssb_f28_field.h (round 6).
 //
 // Fp as 14 limbs of 28 bits, Montgomery form with R = 2^392 (p < 2^381: 11 bits of slack).  The
 // product is product-scanning (FIPS) with ONE 64-bit accumulator per column and no carry handling
@@ -20,181 +20,9 @@
 // with the engine's on subgroup points, non-subgroup curve points and infinity, host and GPU).
 #pragma once
 #include "ssb_curve.h"
-#include "ssb_f28_consts.h"
 
 namespace ssb {
 namespace r28 {
-
-struct f { uint32_t l[14]; };
-struct f2 { f c0, c1; };
-constexpr uint32_t M28 = (1u << 28) - 1;
-
-// re-slice a 12 x 32-bit integer (< 2^384) into 14 x 28-bit limbs
-SSB_INL void from32(f& r, const uint32_t* w) {
-#pragma unroll
-  for (int k = 0; k < 14; ++k) {
-    const int b = 28 * k, i = b >> 5, s = b & 31;
-    uint32_t v = w[i < 12 ? i : 11] >> s;
-    if (s > 4 && i + 1 < 12) v |= w[i + 1] << (32 - s);
-    r.l[k] = i < 12 ? (v & M28) : 0u;
-  }
-}
-// ... and back (a normalized value < 2^384)
-SSB_INL void to32(uint32_t* w, const f& a) {
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const int b = 32 * i, k = b / 28, s = b % 28;
-    uint32_t v = a.l[k] >> s;
-    if (k + 1 < 14) v |= a.l[k + 1] << (28 - s);
-    if (s > 24 && k + 2 < 14) v |= a.l[k + 2] << (56 - s);
-    w[i] = v;
-  }
-}
-
-// r = a b / 2^392 mod p, r < 2p normalized.  Requires every limb product < 2^60 and a b < R p.
-SSB_INL void mul(f& r, const f& a, const f& b) {
-  SSB_CNT(fp_mul);
-  uint32_t m[14];
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 27; ++k) {
-#pragma unroll
-    for (int j = 0; j < 14; ++j)
-      if (k - j >= 0 && k - j < 14) acc += (uint64_t)a.l[j] * b.l[k - j];
-#pragma unroll
-    for (int j = 0; j < 14; ++j)
-      if (j < k && k - j < 14) acc += (uint64_t)m[j] * P28[k - j];
-    if (k < 14) {
-      m[k] = ((uint32_t)acc * P28_INV) & M28;
-      acc += (uint64_t)m[k] * P28[0];   // the low 28 bits become zero
-    } else {
-      r.l[k - 14] = (uint32_t)acc & M28;
-    }
-    acc >>= 28;
-  }
-  r.l[13] = (uint32_t)acc;
-}
-// r = (a b + c d) / 2^392 mod p, r < 2p: both products summed into each column before the column's
-// reduction (one reduction for two products).  Requires limb products < 2^58 and a b + c d < R p.
-SSB_INL void mul2(f& r, const f& a, const f& b, const f& c, const f& d) {
-  uint32_t m[14];
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 27; ++k) {
-#pragma unroll
-    for (int j = 0; j < 14; ++j)
-      if (k - j >= 0 && k - j < 14) acc += (uint64_t)a.l[j] * b.l[k - j];
-#pragma unroll
-    for (int j = 0; j < 14; ++j)
-      if (k - j >= 0 && k - j < 14) acc += (uint64_t)c.l[j] * d.l[k - j];
-#pragma unroll
-    for (int j = 0; j < 14; ++j)
-      if (j < k && k - j < 14) acc += (uint64_t)m[j] * P28[k - j];
-    if (k < 14) {
-      m[k] = ((uint32_t)acc * P28_INV) & M28;
-      acc += (uint64_t)m[k] * P28[0];
-    } else {
-      r.l[k - 14] = (uint32_t)acc & M28;
-    }
-    acc >>= 28;
-  }
-  r.l[13] = (uint32_t)acc;
-}
-
-// carry normalization: limbs 0..12 < 2^28 (inputs: limbs < 2^31)
-SSB_INL void norm(f& x) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 13; ++i) {
-    const uint32_t v = x.l[i] + c;
-    x.l[i] = v & M28;
-    c = v >> 28;
-  }
-  x.l[13] += c;
-}
-// r = a + b (normalized)
-SSB_INL void add(f& r, const f& a, const f& b) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = a.l[i] + b.l[i];
-  norm(r);
-}
-// r = a + b, limbs NOT normalized (< 2^29 for normalized inputs): a product operand only
-SSB_INL void add_raw(f& r, const f& a, const f& b) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = a.l[i] + b.l[i];
-}
-// r = a + K - b (normalized), K a spread multiple of p (gen_f28.py) above b's value
-SSB_INL void sub(f& r, const f& a, const f& b, const uint32_t* K) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = a.l[i] + K[i] - b.l[i];
-  norm(r);
-}
-// r = K - b, limbs NOT normalized (< 2^29): a product operand only
-SSB_INL void neg_raw(f& r, const f& b, const uint32_t* K) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = K[i] - b.l[i];
-}
-SSB_INL void dbl(f& r, const f& a) { add(r, a, a); }
-// r = k a (normalized), k <= 8
-SSB_INL void mul_small(f& r, const f& a, uint32_t k) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = a.l[i] * k;
-  norm(r);
-}
-// r = 2 (a + KK - b - c) (normalized), KK a double-spread multiple of p above b + c
-SSB_INL void dbl_sub_sub(f& r, const f& a, const f& b, const f& c, const uint32_t* KK) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = 2u * (a.l[i] + KK[i] - b.l[i] - c.l[i]);
-  norm(r);
-}
-// r = a + KK - 2 b (normalized), KK a double-spread multiple of p above 2b
-SSB_INL void sub_dbl(f& r, const f& a, const f& b, const uint32_t* KK) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = a.l[i] + KK[i] - 2u * b.l[i];
-  norm(r);
-}
-// r == x (mod p), r < 2p; x normalized, x < 2^12 p.  q = floor((x >> 336) / ((p >> 336) + 1)) is at
-// most floor(x / p) and at least floor(x / p) - 1, so x - q p lies in [0, 2p).
-SSB_INL void fold(f& r, const f& x) {
-  const uint64_t hi = ((uint64_t)x.l[13] << 28) | x.l[12];
-  const uint32_t q = (uint32_t)((double)hi * F28_INV_PHI);
-  int64_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < 13; ++i) {
-    acc += (int64_t)x.l[i] - (int64_t)((uint64_t)q * P28[i]);
-    r.l[i] = (uint32_t)acc & M28;
-    acc >>= 28;   // (arithmetic)
-  }
-  r.l[13] = (uint32_t)(acc + (int64_t)x.l[13] - (int64_t)((uint64_t)q * P28[13]));
-}
-// canonical residue of x < 2p (normalized): x or x - p
-SSB_INL void canon(f& r, const f& x) {
-  f t;
-  int32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    const int32_t v = (int32_t)x.l[i] - (int32_t)P28[i] + br;
-    t.l[i] = (uint32_t)v & M28;
-    br = v >> 28;   // 0 or -1 (limbs < 2^28)
-  }
-  const bool keep = br != 0;   // x < p
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.l[i] = keep ? x.l[i] : t.l[i];
-}
-// x == 0 (mod p) for a normalized x < 2^12 p
-SSB_INL bool is_zero(const f& x) {
-  f y; fold(y, x);
-  f z; canon(z, y);
-  uint32_t o = 0;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) o |= z.l[i];
-  return o == 0;
-}
-// a == b (mod p) for normalized values below 2^12 p and 63 p
-SSB_INL bool eq(const f& a, const f& b) { f d; sub(d, a, b, K64P); return is_zero(d); }
-SSB_INL f cst(const uint32_t* c) { f r; for (int i = 0; i < 14; ++i) r.l[i] = c[i]; return r; }
-// the engine's Montgomery form (R = 2^384) -> this one (R = 2^392): value * 2^400 / 2^392, < 2p
-SSB_INL void from_engine(f& r, const fp& a) { f t; from32(t, a.l); mul(r, t, cst(C_2_400)); }
 
 // ---- Fp2 = Fp[u] / (u^2 + 1) ----
 SSB_INL void add2(f2& r, const f2& a, const f2& b) { add(r.c0, a.c0, b.c0); add(r.c1, a.c1, b.c1); }

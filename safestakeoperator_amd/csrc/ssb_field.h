@@ -553,7 +553,17 @@ SSB_INL fp fp_pick8(const fp* t, int i) {
 // (the odd powers as eight named values picked by a switch on the uniform digit: as an array indexed
 // by it, the compiler kept the table in scratch and every multiplication of the loop reloaded an
 // entry from there -- 12 scratch loads per step in each of the decompression's square roots, round 5)
+}  // namespace ssb
+#include "ssb_f28_field.h"
+namespace ssb {
+// The square roots' exponentiations run in the reduced radix (ssb_f28_field.h, r28::pow_sw: one
+// v_mad_u64_u32 per limb product); SSB_POW_ENGINE=1 builds keep the engine's products (A/B), and the op
+// counter counts the engine's form.
 SSB_INL void fp_pow_sw_inl(fp& r, const fp& a, const uint8_t* sch, int n) {
+#if !defined(SSB_POW_ENGINE) && !defined(SSB_OPCOUNT)
+  r28::pow_sw(r, a, sch, n);
+  return;
+#endif
   fp t0 = a, t1, t2, t3, t4, t5, t6, t7, a2;
   fp_sqr(a2, a);
   fp_mul(t1, t0, a2); fp_mul(t2, t1, a2); fp_mul(t3, t2, a2); fp_mul(t4, t3, a2);
@@ -573,6 +583,13 @@ SSB_INL void fp_pow_sw_inl(fp& r, const fp& a, const uint8_t* sch, int n) {
   r = acc;
 }
 SSB_FN void fp_pow_sw(fp& r, const fp& a, const uint8_t* sch, int n) { fp_pow_sw_inl(r, a, sch, n); }
+// INL = false: the power out of line.  The callable square roots and decompression take that form --
+// four inline powers put their function past the 128 KB reach of a short branch, and a callable
+// function's long branch overwrites its return address (build.py, long_branch_clobbers).
+template <bool INL>
+SSB_INL void fp_pow_sw_sel(fp& r, const fp& a, const uint8_t* sch, int n) {
+  if constexpr (INL) fp_pow_sw_inl(r, a, sch, n); else fp_pow_sw(r, a, sch, n);
+}
 
 // Binary extended Euclid (variable time: inputs on this path are public).  For the Montgomery
 // form aR it returns (aR)^{-1} * R^3 / R = a^{-1} R.  inv(0) = 0.  About 4x fewer dependent
@@ -770,14 +787,15 @@ SSB_FN void fp_inv(fp& r, const fp& a) {
   mp_mont_mul<12>(r.l, t.l, P_R3, P_LIMBS, P_INV32);        // (aR)^-1 -> a^-1 R
 }
 // returns true iff a is a square; r = a^((p+1)/4) (a root when it is)
+template <bool INL = true>
 SSB_INL bool fp_sqrt_inl(fp& r, const fp& a) {
   fp s, s2;
-  fp_pow_sw_inl(s, a, EXPW_P_PLUS_1_DIV_4, EXPW_P_PLUS_1_DIV_4_N);
+  fp_pow_sw_sel<INL>(s, a, EXPW_P_PLUS_1_DIV_4, EXPW_P_PLUS_1_DIV_4_N);
   fp_sqr(s2, s);
   r = s;
   return fp_eq(s2, a);
 }
-SSB_FN bool fp_sqrt(fp& r, const fp& a) { return fp_sqrt_inl(r, a); }
+SSB_FN bool fp_sqrt(fp& r, const fp& a) { return fp_sqrt_inl<false>(r, a); }
 // ZCash sign: canonical(a) > (p-1)/2
 SSB_INL bool fp_lex_largest(const fp& a) {
   fp c; fp_from_mont(c, a);
@@ -906,12 +924,13 @@ SSB_FN void fp2_inv(fp2& r, const fp2& a) {
 }
 // Square root in Fp2 by the norm method (p = 3 mod 4).  Any root is returned; the caller fixes
 // the sign.  Returns false iff a is not a square.
+template <bool INL = true>
 SSB_INL bool fp2_sqrt_inl(fp2& r, const fp2& a) {
   if (fp_is_zero(a.c1)) {
     fp s;
-    if (fp_sqrt_inl(s, a.c0)) { r.c0 = s; r.c1 = fp_zero(); return true; }
+    if (fp_sqrt_inl<INL>(s, a.c0)) { r.c0 = s; r.c1 = fp_zero(); return true; }
     fp na; fp_neg(na, a.c0);
-    bool ok = fp_sqrt_inl(s, na);
+    bool ok = fp_sqrt_inl<INL>(s, na);
     r.c0 = fp_zero(); r.c1 = s;
     return ok;
   }
@@ -919,11 +938,11 @@ SSB_INL bool fp2_sqrt_inl(fp2& r, const fp2& a) {
   fp_sqr(n, a.c0);
   fp_sqr(t, a.c1);
   fp_add(n, n, t);
-  if (!fp_sqrt_inl(s, n)) return false;
+  if (!fp_sqrt_inl<INL>(s, n)) return false;
   fp c, half = fp_from_c(FP_HALF);
   fp_add(c, a.c0, s);
   fp_mul(c, c, half);                       // c = (a0 + s)/2  (nonzero since a1 != 0)
-  fp_pow_sw_inl(t, c, EXPW_P_MINUS_3_DIV_4, EXPW_P_MINUS_3_DIV_4_N);  // t = c^((p-3)/4)
+  fp_pow_sw_sel<INL>(t, c, EXPW_P_MINUS_3_DIV_4, EXPW_P_MINUS_3_DIV_4_N);  // t = c^((p-3)/4)
   fp x, x2;
   fp_mul(x, c, t);                          // x^2 = c if c is a square, else -c
   fp_sqr(x2, x);
@@ -942,7 +961,7 @@ SSB_INL bool fp2_sqrt_inl(fp2& r, const fp2& a) {
   r = y;
   return fp2_eq(chk, a);
 }
-SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) { return fp2_sqrt_inl(r, a); }
+SSB_FN bool fp2_sqrt(fp2& r, const fp2& a) { return fp2_sqrt_inl<false>(r, a); }
 // ZCash sign for Fp2: c1 > (p-1)/2, or c0 > (p-1)/2 when c1 == 0
 SSB_INL bool fp2_lex_largest(const fp2& a) {
   if (!fp_is_zero(a.c1)) return fp_lex_largest(a.c1);

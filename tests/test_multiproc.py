@@ -212,3 +212,66 @@ def test_bench_batch_exchange_gloo_world2(strong):
         assert p.exitcode == 0
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] and r[2] for r in res), res
+
+
+# ---- bench.py's exchanger: the helper thread that issues each group's all-gather once the group's
+# batches are done, in group order on every rank, drained before the main thread's own collectives ----
+class _Done:
+    """a stand-in for a recorded torch.cuda.Event: ready after `delay` seconds"""
+    def __init__(self, delay):
+        import time
+        self.t = time.monotonic() + delay
+
+    def synchronize(self):
+        import time
+        time.sleep(max(0.0, self.t - time.monotonic()))
+
+
+def _exchanger_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from safestakeoperator_amd.shard import BatchExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, J, G, rounds = 3, 17, 4, 5
+    gver, gsig, gst, gerr = _stub_global(J, n)
+    ex = bench.Exchanger(BatchExchange(strong=False), None)
+    ok = True
+    futs = []
+    for r in range(rounds):
+        outs = [dict(ver=gver ^ ((rank + b) & 1), out=gsig + rank, st=gst + 100 * r + 10 * b + rank, err=gerr)
+                for b in range(G)]
+        # rank 1's batches "finish" later than rank 0's: the collectives must still pair up in group order
+        futs.append((r, ex.submit([(o, _Done(0.02 * rank * (G - b))) for b, o in enumerate(outs)])))
+    ex.drain()
+    dist.barrier()                         # the main thread's own collective, after the drain
+    for r, f in futs:
+        for w in f.result(timeout=60):
+            w.wait()
+    ok_last, res = ex.xchg.check_last()    # the last group, every rank's rows
+    ok = ok and ok_last and all(torch.equal(res[b][x][2], gst + 100 * (rounds - 1) + 10 * b + x)
+                                for b in range(G) for x in range(world))
+    ex.close()
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_exchanger_gloo_world2():
+    """bench.Exchanger over gloo at world 2: five groups of four batches submitted with staggered
+    completion times, drained, then a barrier; every group's collective pairs with the same group on the
+    other rank (the last group's gathered statuses carry its round number), and nothing deadlocks."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchanger_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(r[0] for r in res) == [0, 1] and all(r[1] for r in res), res
