@@ -8,7 +8,7 @@ OUT=${1:-gpurun_out/r06ab}
 mkdir -p $OUT
 X="--warmup 5 --no-cpu-baseline --no-host-buffers --collector-windows 0 --sustained-steps 1000 --no-registry --no-adversarial"
 for rep in 1 2; do
-  VS="product eng"; [ $rep = 1 ] && VS="product eng sg32"
+  VS="product eng"
   for v in $VS; do
     if [ $v = product ]; then unset SSB_LIB_VARIANT; else export SSB_LIB_VARIANT=$v; fi
     timeout -k 10 300 python -u bench.py $X --steps 20 > $OUT/${v}_$rep.json 2> $OUT/${v}_$rep.err || { echo "bench $v failed"; tail -5 $OUT/${v}_$rep.err; exit 1; }

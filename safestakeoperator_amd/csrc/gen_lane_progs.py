@@ -876,12 +876,12 @@ class Emitter:
             else:
                 # u = m * v mod p, left to right over the bits of m (per-role m)
                 nb = max(m.bit_length() for m in mg)
-                out.append("      { fp v_, u_; lp_ld(v_, g, %s);" % src)
+                out.append("      { lv v_, u_; lp_ld(v_, g, %s);" % src)
                 top = [(m >> (nb - 1)) & 1 for m in mg]
                 if all(top):
                     out.append("        u_ = v_;")
                 else:
-                    out.append("        u_ = fp_zero(); lp_sel(u_, v_, u_, LP_BIT(%s));" % self.bits(top))
+                    out.append("        u_ = lv_zero(); lp_sel(u_, v_, u_, LP_BIT(%s));" % self.bits(top))
                 for bit in range(nb - 2, -1, -1):
                     out.append("        lp_dbl_mod(u_);")
                     bs = [(m >> bit) & 1 for m in mg]
@@ -902,10 +902,10 @@ class Emitter:
             else:
                 if first:
                     fn = {"pos": "%s = u_;", "neg": "lp_pminus(%s, u_);",
-                          "mix": "{ fp n_; lp_pminus(n_, u_); lp_sel(%s, n_, u_, LP_BIT(" + self.bits(sg) + ")); }"}[uni]
+                          "mix": "{ lv n_; lp_pminus(n_, u_); lp_sel(%s, n_, u_, LP_BIT(" + self.bits(sg) + ")); }"}[uni]
                 else:
-                    fn = {"pos": "lp_add_raw(%s, u_);", "neg": "{ fp n_; lp_pminus(n_, u_); lp_add_raw(%s, n_); }",
-                          "mix": "{ fp n_; lp_pminus(n_, u_); lp_sel(n_, n_, u_, LP_BIT(" + self.bits(sg) + ")); lp_add_raw(%s, n_); }"}[uni]
+                    fn = {"pos": "lp_add_raw(%s, u_);", "neg": "{ lv n_; lp_pminus(n_, u_); lp_add_raw(%s, n_); }",
+                          "mix": "{ lv n_; lp_pminus(n_, u_); lp_sel(n_, n_, u_, LP_BIT(" + self.bits(sg) + ")); lp_add_raw(%s, n_); }"}[uni]
                 out.append("        " + fn % var + " }")
         return T
 
@@ -913,8 +913,9 @@ class Emitter:
     def simple(f, maxw):
         return f is None or (len(f.c) <= maxw and all(abs(c) == 1 for c in f.c.values()))
 
-    def emit_acc(self, var, forms, exact):
-        """var = the forms' values via the accumulator engine: < 2p, or < p when exact."""
+    def emit_acc(self, var, forms, fold):
+        """var = the forms' values via the accumulator engine: folded below 2p (a stored value, or an
+        operand whose bound needs it), else < 2p sum|c| (acc_bound)."""
         G, out = self.G, self.lines
         tl = [terms_of(f) if f is not None else [] for f in forms]
         T = max([len(t) for t in tl] + [1])
@@ -937,16 +938,33 @@ class Emitter:
                 out.append("        la_ld_neg(A_, g, %s, %s);" % (src, self.sel(cn)))
             else:
                 out.append("        la_ld_mix(A_, g, %s, %s, %s);" % (src, self.sel(cp), self.sel(cn)))
-        out.append("        la_fin(%s, A_, %s, %s); }" % (var, self.sel(Ks), "true" if exact else "false"))
+        out.append("        la_fin(%s, A_, %s, %s); }" % (var, self.sel(Ks), "true" if fold else "false"))
 
     def reduce_line(self, forms):
-        """Forms evaluate to values <= w*p (terms <= p each); reduce to [0, p)."""
-        w = max(wt(f) for f in forms)
+        """Plain sums (terms < 4p, every limb < 2^29, <= MAXM terms: limbs < 2^32) -> a slot value
+        (< 2p): normalized and folded, except single positive unit terms (copies)."""
         exact = all(wt(f) <= 1 and all(c == 1 for c in f.c.values()) for f in forms)
         if exact:
             return None
-        steps = 1 if w <= 1 else (2 if w <= 2 else (3 if w <= 4 else 4))
-        return "      lp_reduce%d(LP_T);" % steps
+        return "      lp_reduce(LP_T);"
+
+    # bounds of the reduced-radix runtime (ssb_lane.h): slot values < 2p with limbs < 2^28; a plain
+    # sum's negative term K4P - v is < 4p with limbs < 2^29; an accumulator form without its fold is
+    # < 2p sum|c| with normalized limbs.  A product needs x y < 2^392 p (~2521 p^2; kept <= 2400 p^2)
+    # and limb products <= 2^60 (its 64-bit columns).
+    @staticmethod
+    def simple_bound(forms):
+        return max(sum(4 if sg else 2 for (sg, m, sym) in terms_of(f)) for f in forms if f is not None)
+
+    @staticmethod
+    def simple_limb_bits(forms):
+        import math
+        return max(math.log2(sum((1 << 29) if sg else (1 << 28) for (sg, m, sym) in terms_of(f)))
+                   for f in forms if f is not None)
+
+    @staticmethod
+    def acc_bound(forms):
+        return max(2 * sum(m for (sg, m, sym) in terms_of(f)) for f in forms if f is not None)
 
     def emit(self):
         s, G = self.s, self.G
@@ -974,7 +992,7 @@ class Emitter:
                 out.append("    LP_DECL_T;")
                 if kind == "prod":
                     out.append("    LP_FOR(%d) {" % G)
-                    out.append("      fp x, y;")
+                    out.append("      lv x, y;")
                     xs = [s.prods[it[1]][0] for it in chunk]
                     ys = [s.prods[it[1]][1] for it in chunk]
                     xp = all(self.simple(f, MAXT) for f in xs)
@@ -988,15 +1006,38 @@ class Emitter:
                             yp, by = False, 2
                     if bx * by > 9:
                         xp = yp = False
+                    Bx = self.simple_bound(xs) if xp else self.acc_bound(xs)
+                    By = self.simple_bound(ys) if yp else self.acc_bound(ys)
+                    fx = fy = False
+                    while Bx * By > 2400:
+                        if not xp and not fx and (Bx >= By or yp or fy):
+                            fx, Bx = True, 2
+                        elif not yp and not fy:
+                            fy, By = True, 2
+                        else:
+                            raise AssertionError((P.name, Bx, By))
+                    nx = ny = False
+                    if xp and yp:
+                        lx, ly = self.simple_limb_bits(xs), self.simple_limb_bits(ys)
+                        if lx + ly > 60:
+                            if lx >= ly:
+                                nx, lx = True, 28
+                            else:
+                                ny, ly = True, 28
+                        assert lx + ly <= 60, (P.name, lx, ly)
                     if xp:
                         self.emit_form("x", xs)
+                        if nx:
+                            out.append("      lp_norm(x);")
                     else:
-                        self.emit_acc("x", xs, False)
+                        self.emit_acc("x", xs, fx)
                     if yp:
                         self.emit_form("y", ys)
+                        if ny:
+                            out.append("      lp_norm(y);")
                     else:
-                        self.emit_acc("y", ys, False)
-                    out.append("      fp_mul(LP_T, x, y);")
+                        self.emit_acc("y", ys, fy)
+                    out.append("      lp_mul(LP_T, x, y);")
                     out.append("    }")
                     dst = [C_SCR + s.slot[it] if s.slot[it] is not None else junk for it in chunk]
                     dst += [junk] * (G - len(dst))
@@ -1087,14 +1128,14 @@ def const_init_table():
     out = []
     for nm in CONSTS:
         if nm == "ZERO":
-            out.append("fp_zero()")
+            out.append("lv_zero()")
         elif nm == "FP_ONE":
-            out.append("fp_one()")
+            out.append("lv_one()")
         elif nm == "FP_B1":
-            out.append("fp_from_c(FP_B1)")
+            out.append("lv_in(fp_from_c(FP_B1))")
         else:
             base, comp = nm.rsplit(".", 1)
-            out.append("fp_from_c(%s.%s)" % (base, comp))
+            out.append("lv_in(fp_from_c(%s.%s))" % (base, comp))
     return out
 
 
@@ -1104,13 +1145,13 @@ def main():
     consts = const_init_table()
     init = ["template <class GR> SSB_LP_FN void lp_init_consts(GR g) {",
             "  LP_FOR_ALL_CONSTS(i) {"]
-    init.append("    fp v;")
+    init.append("    lv v;")
     init.append("    switch (i) {")
     for i, c in enumerate(consts):
         init.append("      case %d: v = %s; break;" % (i, c))
-    init.append("      default: v = fp_zero();")
+    init.append("      default: v = lv_zero();")
     init.append("    }")
-    init.append("    g.k[i] = v;")
+    init.append("    lp_put(g.k + i, v);")
     init.append("  }")
     init.append("  LP_SYNC();")
     init.append("}")

@@ -194,8 +194,8 @@ SSB_INL void h2c_map_block(uint32_t bid, h2c_cand* cs, int n, const fp2* __restr
 // 3: q0 + q1 and the cofactor clearing as lane-group programs (8 lanes per root, 8 roots per block)
 constexpr int H2C_S0 = lane::G2_ADD_SCRATCH > lane::G2_MADD_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G2_MADD_SCRATCH;
 constexpr int H2C_GS = H2C_S0 + 6 + 4 + 6 + 30;
-constexpr size_t H2C_CLEAR_LDS = (lane::LP_NCODE_CONST + 8 * H2C_GS) * sizeof(fp) + 8 * sizeof(uint32_t);
-SSB_INL void h2c_clear_block(uint32_t bid, fp* lds, int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
+constexpr size_t H2C_CLEAR_LDS = (lane::LP_NCODE_CONST + 8 * H2C_GS) * sizeof(lane::lslot) + 8 * sizeof(uint32_t);
+SSB_INL void h2c_clear_block(uint32_t bid, lane::lslot* lds, int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
                              uint32_t* __restrict__ exc_out) {
   using namespace ssb::lane;
   uint32_t* flg = (uint32_t*)(lds + LP_NCODE_CONST + 8 * H2C_GS);
@@ -208,16 +208,16 @@ SSB_INL void h2c_clear_block(uint32_t bid, fp* lds, int n, const g2_aff* __restr
   {
     g2_aff a0, a1;
     if (act) { a0 = q[2 * i]; a1 = q[2 * i + 1]; } else { a0.x = fp2_zero(); a0.y = fp2_one(); a1 = a0; a1.x = fp2_one(); }
-    if (role < 4) { g.s[P + role] = ((const fp*)&a0)[role]; g.s[Q1 + role] = ((const fp*)&a1)[role]; }
-    if (role == 4) g.s[P + 4] = fp_one();
-    if (role == 5) g.s[P + 5] = fp_zero();
+    if (role < 4) { lp_put(g.s + P + role, lv_in(((const fp*)&a0)[role])); lp_put(g.s + Q1 + role, lv_in(((const fp*)&a1)[role])); }
+    if (role == 4) lp_put(g.s + P + 4, lv_one());
+    if (role == 5) lp_put(g.s + P + 5, lv_zero());
   }
   __syncthreads();
   uint32_t exc = 0;
   g2_madd(g, P, Q1, P, exc);      // q0 + q1 (q0, q1 never infinity: iso3_map of the SWU points)
   g2_clear_cofactor(g, P, R, W, exc);
   if (act) {
-    if (role < 6) ((fp*)&hj[i])[role] = g.s[R + role];
+    if (role < 6) ((fp*)&hj[i])[role] = lv_out(lp_get(g.s + R + role));
     if (role == 0) exc_out[i] = exc;
   }
 }

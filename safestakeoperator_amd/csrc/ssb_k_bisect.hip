@@ -329,7 +329,7 @@ SSB_INL bool f12_slots_one(const lane::grp& g, int F) {
   __syncthreads();
   const int lane_ = threadIdx.x;
   bool one = true;
-  if (lane_ < 12) { const fp v = g.s[F + lane_]; one = lane_ == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v); }
+  if (lane_ < 12) { const fp v = lane::lv_out(lane::lp_get(g.s + F + lane_)); one = lane_ == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v); }
   return __syncthreads_and(one ? 1 : 0) != 0;
 }
 
@@ -340,21 +340,21 @@ SSB_FN bool pair_check(lane::grp& g, const g1_aff& P, const g2_aff& Q, const g2_
   const int lane_ = threadIdx.x;
   const g1_aff ng = g1_neg_generator();
   if (!P.inf && !Q.inf) {                  // e(S_pk, H(r)) e(-g1, S_sig), one two-pair loop
-    if (lane_ < 4) { g.s[B + lane_] = ((const fp*)&h)[lane_]; g.s[B + 6 + lane_] = ((const fp*)&Q)[lane_]; }
-    if (lane_ == 4) { g.s[B + 4] = P.x; g.s[B + 10] = ng.x; }
-    if (lane_ == 5) { g.s[B + 5] = P.y; g.s[B + 11] = ng.y; }
+    if (lane_ < 4) { lp_put(g.s + B + lane_, lv_in(((const fp*)&h)[lane_])); lp_put(g.s + B + 6 + lane_, lv_in(((const fp*)&Q)[lane_])); }
+    if (lane_ == 4) { lp_put(g.s + B + 4, lv_in(P.x)); lp_put(g.s + B + 10, lv_in(ng.x)); }
+    if (lane_ == 5) { lp_put(g.s + B + 5, lv_in(P.y)); lp_put(g.s + B + 11, lv_in(ng.y)); }
     __syncthreads();
     f12_miller2(g, F1, B, BP);
   } else if (!P.inf || !Q.inf) {           // one pair at infinity
     const g2_aff q = P.inf ? Q : h;
-    if (lane_ < 4) g.s[B + lane_] = ((const fp*)&q)[lane_];
-    if (lane_ == 4) g.s[B + 4] = P.inf ? ng.x : P.x;
-    if (lane_ == 5) g.s[B + 5] = P.inf ? ng.y : P.y;
+    if (lane_ < 4) lp_put(g.s + B + lane_, lv_in(((const fp*)&q)[lane_]));
+    if (lane_ == 4) lp_put(g.s + B + 4, lv_in(P.inf ? ng.x : P.x));
+    if (lane_ == 5) lp_put(g.s + B + 5, lv_in(P.inf ? ng.y : P.y));
     __syncthreads();
     f12_miller(g, F1, B);
   } else {
     const fp12 one = fp12_one();
-    if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&one)[lane_];
+    if (lane_ < 12) lp_put(g.s + F1 + lane_, lv_in(((const fp*)&one)[lane_]));
     __syncthreads();
   }
   f12_final_exp(g, F1, TMP);
@@ -364,7 +364,7 @@ SSB_FN bool pair_check(lane::grp& g, const g1_aff& P, const g2_aff& Q, const g2_
 // LDS of k_fb_root: the root's bucket lists (the point trees move through cross-lane shuffles, so
 // the block's LDS stays small enough for two waves per SIMD)
 struct fr_bucket_lds { uint32_t list[4 * FR_CHUNK]; uint32_t cnt[64], off[64], cur[64]; };
-union fr_lds { fr_bucket_lds b; fp s[lane::LP_NCODE_CONST + BS_SLOTS]; };
+union fr_lds { fr_bucket_lds b; lane::lslot s[lane::LP_NCODE_CONST + BS_SLOTS]; };
 template <class P> SSB_INL P shfl_down_pt(const P& p, int off) {
   P r;
   const int* a = (const int*)&p;
@@ -468,8 +468,8 @@ SSB_FN void miller_one(lane::grp& g, const g1_aff& P, const g2_aff& Q, int F1, i
   if (lane_ == 0) {
     flg = (P.inf || Q.inf) ? 1u : 0u;
     if (!(P.inf || Q.inf)) {
-      g.s[B + 0] = Q.x.c0; g.s[B + 1] = Q.x.c1; g.s[B + 2] = Q.y.c0; g.s[B + 3] = Q.y.c1;
-      g.s[B + 4] = P.x; g.s[B + 5] = P.y;
+      lp_put(g.s + B + 0, lv_in(Q.x.c0)); lp_put(g.s + B + 1, lv_in(Q.x.c1)); lp_put(g.s + B + 2, lv_in(Q.y.c0)); lp_put(g.s + B + 3, lv_in(Q.y.c1));
+      lp_put(g.s + B + 4, lv_in(P.x)); lp_put(g.s + B + 5, lv_in(P.y));
     }
   }
   __syncthreads();
@@ -477,7 +477,7 @@ SSB_FN void miller_one(lane::grp& g, const g1_aff& P, const g2_aff& Q, int F1, i
   __syncthreads();
   if (one) {
     const fp12 o = fp12_one();
-    if (lane_ < 12) g.s[F1 + lane_] = ((const fp*)&o)[lane_];
+    if (lane_ < 12) lp_put(g.s + F1 + lane_, lv_in(((const fp*)&o)[lane_]));
     __syncthreads();
   } else {
     f12_miller(g, F1, B);
@@ -529,7 +529,7 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
   lp_init_consts(g);
   const int F1 = BS_S0, B = F1 + 24, TMP = B + 12 + 4, FR = TMP + 72;
   miller_one(g, g1_neg_generator(), Q, F1, B, flg);   // e(-g1, O) = 1: the root's value is f[r] alone
-  if (lane_ < 12) g.s[FR + lane_] = ((const fp*)&froot[r])[lane_];
+  if (lane_ < 12) lp_put(g.s + FR + lane_, lv_in(((const fp*)&froot[r])[lane_]));
   __syncthreads();
   f12_mul(g, F1, FR, F1);
   f12_final_exp(g, F1, TMP);
@@ -661,7 +661,7 @@ SSB_FN void ex_mul_values(lane::grp& g, const fp12* __restrict__ fex, int first,
     }
     for (uint64_t m = __ballot(keep); m; m &= m - 1) {   // uniform
       const int i = first + (base + __builtin_ctzll(m)) * stride;
-      if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&fex[i])[lane_];
+      if (lane_ < 12) lp_put(g.s + IN + lane_, lv_in(((const fp*)&fex[i])[lane_]));
       __syncthreads();
       f12_mul(g, ACC, IN, ACC);
     }
@@ -676,7 +676,7 @@ SSB_FN bool ex_pair_ticket(ex_lds& L, int n_roots, int pair, fp12* __restrict__ 
                            uint32_t* __restrict__ rtk) {
   using namespace ssb::lane;
   const int lane_ = threadIdx.x;
-  if (lane_ < 12) ((fp*)&fex[pair])[lane_] = L.u.s[LP_NCODE_CONST + BS_S0 + lane_];   // (g.s + F1 of the roles)
+  if (lane_ < 12) ((fp*)&fex[pair])[lane_] = lane::slot_out(L.u.s[LP_NCODE_CONST + BS_S0 + lane_]);   // (g.s + F1 of the roles)
   __threadfence();
   __syncthreads();
   if (pair < 4 * n_roots) {   // uniform
@@ -687,10 +687,10 @@ SSB_FN bool ex_pair_ticket(ex_lds& L, int n_roots, int pair, fp12* __restrict__ 
     __threadfence();
     grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
     const int ACC = BS_S0, IN = BS_S0 + 12;
-    if (lane_ < 12) g.s[ACC + lane_] = lane_ == 0 ? fp_one() : fp_zero();
+    if (lane_ < 12) lp_put(g.s + ACC + lane_, lane_ == 0 ? lv_one() : lv_zero());
     __syncthreads();
     ex_mul_values(g, fex, 4 * r, 4, 1, ACC, IN);
-    if (lane_ < 12) ((fp*)&fex[4 * r])[lane_] = g.s[ACC + lane_];
+    if (lane_ < 12) ((fp*)&fex[4 * r])[lane_] = lv_out(lp_get(g.s + ACC + lane_));
     if (lane_ == 0) rtk[r] = 0u;
     __threadfence();
     __syncthreads();
@@ -709,7 +709,7 @@ SSB_FN void ex_final(ex_lds& L, int n_roots, const fp12* __restrict__ ftot, cons
   grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, lane_};
   const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
   const int ACC = F1, IN = F1 + 12;
-  if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)ftot)[lane_];
+  if (lane_ < 12) lp_put(g.s + ACC + lane_, lv_in(((const fp*)ftot)[lane_]));
   __syncthreads();
   ex_mul_values(g, fex, 0, n_roots, 4, ACC, IN);
   ex_mul_values(g, fex, 4 * n_roots, 4 * launch::EX_X_PARTS, 1, ACC, IN);
@@ -748,11 +748,11 @@ SSB_FN uint32_t gc_horner_g2(ex_lds& L, const g2_jac* __restrict__ X, int ACC, i
   const int role = threadIdx.x % G2_ADD_G;
   grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, role};
   uint32_t exc = 0;
-  if (role < 6) g.s[ACC + role] = ((const fp*)&X[3])[role];
+  if (role < 6) lp_put(g.s + ACC + role, lv_in(((const fp*)&X[3])[role]));
   __syncthreads();
   for (int q = 2; q >= 0; --q) {
     for (int i = 0; i < 16; ++i) g2_dbl(g, ACC, ACC);
-    if (role < 6) g.s[TMP + role] = ((const fp*)&X[q])[role];
+    if (role < 6) lp_put(g.s + TMP + role, lv_in(((const fp*)&X[q])[role]));
     __syncthreads();
     g2_add(g, ACC, TMP, ACC, exc);
   }
@@ -763,11 +763,11 @@ SSB_FN uint32_t gc_horner_g1(ex_lds& L, const g1_jac* __restrict__ X, int ACC, i
   const int role = threadIdx.x % G1_ADD_G;
   grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, role};
   uint32_t exc = 0;
-  if (role < 3) g.s[ACC + role] = ((const fp*)&X[3])[role];
+  if (role < 3) lp_put(g.s + ACC + role, lv_in(((const fp*)&X[3])[role]));
   __syncthreads();
   for (int q = 2; q >= 0; --q) {
     for (int i = 0; i < 16; ++i) g1_dbl(g, ACC, ACC);
-    if (role < 3) g.s[TMP + role] = ((const fp*)&X[q])[role];
+    if (role < 3) lp_put(g.s + TMP + role, lv_in(((const fp*)&X[q])[role]));
     __syncthreads();
     g1_add(g, ACC, TMP, ACC, exc);
   }
@@ -778,7 +778,7 @@ SSB_FN uint32_t gc_horner_g1(ex_lds& L, const g1_jac* __restrict__ X, int ACC, i
 SSB_FN void gc_store_g2(ex_lds& L, int S0) {
   if (threadIdx.x != 0) return;
   g2_jac R;
-  for (int k = 0; k < 6; ++k) ((fp*)&R)[k] = L.u.s[lane::LP_NCODE_CONST + S0 + k];
+  for (int k = 0; k < 6; ++k) ((fp*)&R)[k] = lane::slot_out(L.u.s[lane::LP_NCODE_CONST + S0 + k]);
   g2_aff Q;
   jac_to_aff(Q, R);
   L.sQ = Q;
@@ -786,7 +786,7 @@ SSB_FN void gc_store_g2(ex_lds& L, int S0) {
 SSB_FN void gc_store_g1(ex_lds& L, int S0) {
   if (threadIdx.x != 0) return;
   g1_jac R;
-  for (int k = 0; k < 3; ++k) ((fp*)&R)[k] = L.u.s[lane::LP_NCODE_CONST + S0 + k];
+  for (int k = 0; k < 3; ++k) ((fp*)&R)[k] = lane::slot_out(L.u.s[lane::LP_NCODE_CONST + S0 + k]);
   g1_aff P;
   jac_to_aff(P, R);
   L.sP = P;
@@ -976,7 +976,7 @@ __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__
     return;
   }
   // (xv == 2: group-test mode's leftovers)
-  __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
+  __shared__ lslot lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ uint32_t flg;
   const int lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
@@ -1016,7 +1016,7 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
   using namespace ssb::lane;
   if (*ok || (xok && *xok)) return;  // uniform: the batch passed / the committee stage decided it
   if (*nfail <= FB_SINGLE_MAX) return;   // (level 0 ran in k_fb_root; k_fb_single decides the few shares of failing roots)
-  __shared__ fp lds[LP_NCODE_CONST + BS_SLOTS];
+  __shared__ lslot lds[LP_NCODE_CONST + BS_SLOTS];
   __shared__ g2_jac red[64];
   __shared__ g1_aff sP;
   __shared__ g2_aff sQ;

@@ -34,16 +34,16 @@ constexpr int S0 = G2_ADD_SCRATCH;
 static_assert(S0 >= G2_MADD_SCRATCH && S0 >= G2_DBL_SCRATCH && S0 >= G2_PSI_SCRATCH, "program scratch");
 // group-relative slots: BASE, the table of odd multiples, ACC, TMP, X (a partner's point), SUM
 constexpr int BASE = S0, TAB = BASE + 6, ACC = TAB + 48, TMP = ACC + 6, X = TMP + 6, SUM = X + 6, GS = SUM + 6;
-struct lds { fp s[LP_NCODE_CONST + NG * GS]; uint32_t flg[NG]; };
+struct lds { lslot s[LP_NCODE_CONST + NG * GS]; uint32_t flg[NG]; };
 
 // dst = sign(d) (|d|) B from the table (d odd)
 SSB_INL void pick(grp& g, int d, int dst) {
   const int e = TAB + 6 * (((d < 0 ? -d : d) - 1) >> 1);
   LP_FOR(8) {
     if (role < 6) {
-      fp v = g.s[e + role];
-      if (d < 0 && (role == 2 || role == 3)) fp_neg(v, v);
-      g.s[dst + role] = v;
+      lv v = lp_get(g.s + e + role);
+      if (d < 0 && (role == 2 || role == 3)) lv_neg(v);
+      lp_put(g.s + dst + role, v);
     }
   }
   LP_SYNC();
@@ -70,9 +70,9 @@ SSB_FN void mul_signed(grp& g, uint64_t a, bool neg, bool act, int W, uint32_t& 
   if (__syncthreads_or(even && act ? 1 : 0)) {   // uniform
     LP_FOR(8) {
       if (role < 6) {
-        fp v = g.s[BASE + role];
-        if (role == 2 || role == 3) fp_neg(v, v);
-        g.s[TMP + role] = v;
+        lv v = lp_get(g.s + BASE + role);
+        if (role == 2 || role == 3) lv_neg(v);
+        lp_put(g.s + TMP + role, v);
       }
     }
     LP_SYNC();
@@ -85,7 +85,7 @@ SSB_FN void mul_signed(grp& g, uint64_t a, bool neg, bool act, int W, uint32_t& 
     LP_SYNC();
   }
   if (neg) {
-    LP_FOR(8) { if (role == 2 || role == 3) { fp v = g.s[ACC + role]; fp_neg(v, v); g.s[ACC + role] = v; } }
+    LP_FOR(8) { if (role == 2 || role == 3) { lv v = lp_get(g.s + ACC + role); lv_neg(v); lp_put(g.s + ACC + role, v); } }
   }
   LP_SYNC();
   if (act) exc |= e;
@@ -156,8 +156,8 @@ SSB_FN int ratio_lane_job(rl::lds& L, int b, int nw, int n_jobs, const uint32_t*
       const int64_t ci = ratio_ci(j, i, off, tt, sel, ra.ids, &W, &M);   // (W, M: the job's, every lane)
       {
         const g2_aff q = ra.sig[sel[b0 + (act ? i : 0u)]];
-        if (g.role < 4) g.s[rl::BASE + g.role] = ((const fp*)&q)[g.role];
-        else if (g.role < 6) g.s[rl::BASE + g.role] = g.role == 4 ? fp_one() : fp_zero();
+        if (g.role < 4) lp_put(g.s + rl::BASE + g.role, lv_in(((const fp*)&q)[g.role]));
+        else if (g.role < 6) lp_put(g.s + rl::BASE + g.role, g.role == 4 ? lv_one() : lv_zero());
       }
       __syncthreads();
       rl::mul_signed(g, (uint64_t)(ci < 0 ? -ci : ci), ci < 0, act, W, exc);
@@ -185,7 +185,7 @@ SSB_FN int ratio_lane_job(rl::lds& L, int b, int nw, int n_jobs, const uint32_t*
       if (q >= r && g.role < 6) g.s[rl::BASE + g.role] = g.s[rl::TMP + g.role];
       __syncthreads();
     }
-    if ((q & 1) && (g.role == 2 || g.role == 3)) { fp v = g.s[rl::BASE + g.role]; fp_neg(v, v); g.s[rl::BASE + g.role] = v; }
+    if ((q & 1) && (g.role == 2 || g.role == 3)) { lv v = lp_get(g.s + rl::BASE + g.role); lv_neg(v); lp_put(g.s + rl::BASE + g.role, v); }
     __syncthreads();
     rl::mul_signed(g, kk[q], false, gi < 4, 16, exc);
     rl::tree(g, groups, gi, 4, rl::ACC, exc);
@@ -193,7 +193,7 @@ SSB_FN int ratio_lane_job(rl::lds& L, int b, int nw, int n_jobs, const uint32_t*
   if (ra.exact || __syncthreads_or(exc ? 1 : 0)) return j;
   if (lane_ == 0) {
     g2_jac R;
-    for (int k = 0; k < 6; ++k) ((fp*)&R)[k] = L.s[LP_NCODE_CONST + rl::ACC + k];
+    for (int k = 0; k < 6; ++k) ((fp*)&R)[k] = slot_out(L.s[LP_NCODE_CONST + rl::ACC + k]);
     g2_aff a;
     jac_to_aff(a, R);
     g2_compress(out96 + 96 * (size_t)j, a);

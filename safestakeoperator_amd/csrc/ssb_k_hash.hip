@@ -32,7 +32,7 @@ __global__ void SSB_LB(64) k_h2c_map(int n, const fp2* __restrict__ u, g2_aff* _
 // 3: q0 + q1 and the cofactor clearing (h2c_clear_block, ssb_blocks.h)
 __global__ void SSB_LB(64) k_h2c_clear(int n, const g2_aff* __restrict__ q, g2_jac* __restrict__ hj,
                                                   uint32_t* __restrict__ exc_out) {
-  __shared__ fp lds[H2C_CLEAR_LDS / sizeof(fp) + 1];
+  __shared__ lane::lslot lds[H2C_CLEAR_LDS / sizeof(lane::lslot) + 1];
   h2c_clear_block(blockIdx.x, lds, n, q, hj, exc_out);
 }
 

@@ -28,7 +28,7 @@ constexpr int SG_GS = G2S0 + 20;
 __global__ void SSB_LB(64) k_lane_subgroup(int n, const uint32_t* __restrict__ sflags,
                                                       const g2_aff* __restrict__ sig, uint32_t* __restrict__ gflags,
                                                       uint32_t* __restrict__ exc_out) {
-  __shared__ fp lds[LP_NCODE_CONST + G2NG * SG_GS];
+  __shared__ lslot lds[LP_NCODE_CONST + G2NG * SG_GS];
   __shared__ uint32_t flg[G2NG];
   const int gi = threadIdx.x / G2G, role = threadIdx.x % G2G;
   const int s = blockIdx.x * G2NG + gi;
@@ -38,7 +38,7 @@ __global__ void SSB_LB(64) k_lane_subgroup(int n, const uint32_t* __restrict__ s
   const int P = G2S0, ACC = P + 4, TMP = ACC + 6;
   {
     const g2_aff q = act ? sig[s] : dummy_g2();
-    if (role < 4) g.s[P + role] = ((const fp*)&q)[role];
+    if (role < 4) lp_put(g.s + P + role, lv_in(((const fp*)&q)[role]));
   }
   __syncthreads();
   uint32_t exc = 0;

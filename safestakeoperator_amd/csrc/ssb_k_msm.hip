@@ -235,7 +235,7 @@ __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* _
     return;
   }
   bid -= nblk1;
-  h2c_clear_block(bid, (fp*)lds, h.n, h.q, h.hj, h.exc);
+  h2c_clear_block(bid, (lane::lslot*)lds, h.n, h.q, h.hj, h.exc);
   SSB_TRACE(TR_W2_CLEAR);
   if (tl.tickets && last_block(&tl.tickets[2], (uint32_t)(h.n + 7) / 8, &last)) {
     for (uint32_t b = 0; b * 64 < (uint32_t)h.n; ++b) h2c_affine_block(b, h.n, h.q, h.hj, h.exc, h.exact_all, h.out);

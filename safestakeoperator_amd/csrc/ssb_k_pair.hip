@@ -32,7 +32,7 @@ constexpr int ML_SLOTS = ML_S0 + 18 + 6;
 __global__ void SSB_LB(64) k_miller_pairs(int npairs, const g1_aff* __restrict__ Pa,
                                                      const g2_aff* __restrict__ Qa, fp12* __restrict__ f, spec_jobs sj) {
   using namespace ssb::lane;
-  __shared__ fp lds[LP_NCODE_CONST + ML_SLOTS];
+  __shared__ lslot lds[LP_NCODE_CONST + ML_SLOTS];
   __shared__ uint32_t flg;
   const int p = blockIdx.x, lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
@@ -50,12 +50,12 @@ __global__ void SSB_LB(64) k_miller_pairs(int npairs, const g1_aff* __restrict__
   }
   lp_init_consts(g);
   const int F = ML_S0, B = F + 18;
-  if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
-  if (lane_ == 4) g.s[B + 4] = P.x;
-  if (lane_ == 5) g.s[B + 5] = P.y;
+  if (lane_ < 4) lp_put(g.s + B + lane_, lv_in(((const fp*)&Q)[lane_]));
+  if (lane_ == 4) lp_put(g.s + B + 4, lv_in(P.x));
+  if (lane_ == 5) lp_put(g.s + B + 5, lv_in(P.y));
   __syncthreads();
   f12_miller(g, F, B);
-  if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
+  if (lane_ < 12) ((fp*)&f[p])[lane_] = lv_out(lp_get(g.s + F + lane_));
 }
 
 // Exact per-share verification e(pk, H(m)) * e(-g1, sig) == 1, run when the RLC batch check
@@ -74,7 +74,7 @@ __global__ void SSB_LB(64) k_fallback_lane(int n, const uint32_t* __restrict__ o
                                                       const g1_aff* __restrict__ pk_aff, uint8_t* __restrict__ verdict) {
   using namespace ssb::lane;
   if (*ok) return;  // uniform: the batch passed
-  __shared__ fp lds[LP_NCODE_CONST + FB_SLOTS];
+  __shared__ lslot lds[LP_NCODE_CONST + FB_SLOTS];
   __shared__ uint32_t flg;
   const int lane_ = threadIdx.x;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
@@ -86,9 +86,9 @@ __global__ void SSB_LB(64) k_fallback_lane(int n, const uint32_t* __restrict__ o
     const g2_aff h = H[share_root[s]], sg = sig_aff[s];
     const g1_aff ng = g1_neg_generator();
     // e(pk, H(m)) e(-g1, sig) before the final exponentiation (candidates: pk, sig not infinity)
-    if (lane_ < 4) { g.s[B + lane_] = ((const fp*)&h)[lane_]; g.s[B + 6 + lane_] = ((const fp*)&sg)[lane_]; }
-    if (lane_ == 4) { g.s[B + 4] = pk.x; g.s[B + 10] = ng.x; }
-    if (lane_ == 5) { g.s[B + 5] = pk.y; g.s[B + 11] = ng.y; }
+    if (lane_ < 4) { lp_put(g.s + B + lane_, lv_in(((const fp*)&h)[lane_])); lp_put(g.s + B + 6 + lane_, lv_in(((const fp*)&sg)[lane_])); }
+    if (lane_ == 4) { lp_put(g.s + B + 4, lv_in(pk.x)); lp_put(g.s + B + 10, lv_in(ng.x)); }
+    if (lane_ == 5) { lp_put(g.s + B + 5, lv_in(pk.y)); lp_put(g.s + B + 11, lv_in(ng.y)); }
     __syncthreads();
     f12_miller2(g, F1, B, BP);
     f12_final_exp(g, F1, TMP);
@@ -104,20 +104,20 @@ __global__ void SSB_LB(64) k_fallback_lane(int n, const uint32_t* __restrict__ o
 // out[w] = prod of in[8w .. 8w+7]
 __global__ void SSB_LB(64) k_fp12_prod8(int n, const fp12* __restrict__ in, fp12* __restrict__ out) {
   using namespace ssb::lane;
-  __shared__ fp lds[LP_NCODE_CONST + FP12_MUL_SCRATCH + 24];
+  __shared__ lslot lds[LP_NCODE_CONST + FP12_MUL_SCRATCH + 24];
   __shared__ uint32_t flg;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, (int)threadIdx.x};
   lp_init_consts(g);
   const int ACC = FP12_MUL_SCRATCH, IN = ACC + 12;
   const int b = blockIdx.x * 8, e = min(n, b + 8);
-  if (threadIdx.x < 12) g.s[ACC + threadIdx.x] = ((const fp*)&in[b])[threadIdx.x];
+  if (threadIdx.x < 12) lp_put(g.s + ACC + threadIdx.x, lv_in(((const fp*)&in[b])[threadIdx.x]));
   __syncthreads();
   for (int i = b + 1; i < e; ++i) {
-    if (threadIdx.x < 12) g.s[IN + threadIdx.x] = ((const fp*)&in[i])[threadIdx.x];
+    if (threadIdx.x < 12) lp_put(g.s + IN + threadIdx.x, lv_in(((const fp*)&in[i])[threadIdx.x]));
     __syncthreads();
     f12_mul(g, ACC, IN, ACC);
   }
-  if (threadIdx.x < 12) ((fp*)&out[blockIdx.x])[threadIdx.x] = g.s[ACC + threadIdx.x];
+  if (threadIdx.x < 12) ((fp*)&out[blockIdx.x])[threadIdx.x] = lv_out(lp_get(g.s + ACC + threadIdx.x));
 }
 
 // product of the n values, then ONE final exponentiation -> batch verdict
@@ -127,15 +127,15 @@ constexpr int FE_S0 = lane::FP12_MUL_SCRATCH;
 __global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint32_t* __restrict__ ok, int nv,
                                         const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdict) {
   using namespace ssb::lane;
-  __shared__ fp lds[LP_NCODE_CONST + FE_S0 + 12 + 12 + 84];
+  __shared__ lslot lds[LP_NCODE_CONST + FE_S0 + 12 + 12 + 84];
   __shared__ uint32_t flg;
   grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, (int)threadIdx.x};
   lp_init_consts(g);
   const int ACC = FE_S0, IN = ACC + 12, TMP = IN + 12;
-  if (threadIdx.x < 12) g.s[ACC + threadIdx.x] = ((const fp*)&in[0])[threadIdx.x];
+  if (threadIdx.x < 12) lp_put(g.s + ACC + threadIdx.x, lv_in(((const fp*)&in[0])[threadIdx.x]));
   __syncthreads();
   for (int i = 1; i < n; ++i) {
-    if (threadIdx.x < 12) g.s[IN + threadIdx.x] = ((const fp*)&in[i])[threadIdx.x];
+    if (threadIdx.x < 12) lp_put(g.s + IN + threadIdx.x, lv_in(((const fp*)&in[i])[threadIdx.x]));
     __syncthreads();
     f12_mul(g, ACC, IN, ACC);
   }
@@ -143,7 +143,7 @@ __global__ void SSB_LB(64) k_final_lane(int n, const fp12* __restrict__ in, uint
   if (threadIdx.x == 0) {  // == 1, read slot by slot (an fp12 local would sit in scratch)
     bool one = true;
     for (int k = 0; k < 12; ++k) {
-      const fp v = g.s[ACC + k];
+      const fp v = lv_out(lp_get(g.s + ACC + k));
       one = one && (k == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v));
     }
     *ok = one ? 1u : 0u;
@@ -174,7 +174,7 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
                                           fp12* __restrict__ f, spec_jobs sj, uint32_t* __restrict__ tk,
                                           uint32_t* __restrict__ ok) {
   using namespace ssb::lane;
-  __shared__ fp lds[LP_NCODE_CONST + MF_SLOTS];
+  __shared__ lslot lds[LP_NCODE_CONST + MF_SLOTS];
   __shared__ uint32_t flg, last;
   SSB_TRACE_T0();
   const int p = blockIdx.x, lane_ = threadIdx.x;
@@ -193,12 +193,12 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
       if (lane_ == 0) f[p] = fp12_one();
     } else {
       const int F = ML_S0, B = F + 18;
-      if (lane_ < 4) g.s[B + lane_] = ((const fp*)&Q)[lane_];
-      if (lane_ == 4) g.s[B + 4] = P.x;
-      if (lane_ == 5) g.s[B + 5] = P.y;
+      if (lane_ < 4) lp_put(g.s + B + lane_, lv_in(((const fp*)&Q)[lane_]));
+      if (lane_ == 4) lp_put(g.s + B + 4, lv_in(P.x));
+      if (lane_ == 5) lp_put(g.s + B + 5, lv_in(P.y));
       __syncthreads();
       f12_miller(g, F, B);
-      if (lane_ < 12) ((fp*)&f[p])[lane_] = g.s[F + lane_];
+      if (lane_ < 12) ((fp*)&f[p])[lane_] = lv_out(lp_get(g.s + F + lane_));
     }
   }
   SSB_TRACE(TR_MF_MILLER);
@@ -210,14 +210,14 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
   if (!last) return;
   __threadfence();
   const int ACC = FE_S0, IN = ACC + 12, TMP = IN + 12;
-  if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)&f[gb])[lane_];
+  if (lane_ < 12) lp_put(g.s + ACC + lane_, lv_in(((const fp*)&f[gb])[lane_]));
   __syncthreads();
   for (int i = gb + 1; i < ge; ++i) {
-    if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&f[i])[lane_];
+    if (lane_ < 12) lp_put(g.s + IN + lane_, lv_in(((const fp*)&f[i])[lane_]));
     __syncthreads();
     f12_mul(g, ACC, IN, ACC);
   }
-  if (lane_ < 12) ((fp*)&f[npairs + gi])[lane_] = g.s[ACC + lane_];
+  if (lane_ < 12) ((fp*)&f[npairs + gi])[lane_] = lv_out(lp_get(g.s + ACC + lane_));
   SSB_TRACE(TR_MF_GROUP);
   __threadfence();
   __syncthreads();
@@ -225,22 +225,22 @@ __global__ void SSB_LB(64) k_miller_final(int npairs, const g1_aff* __restrict__
   __syncthreads();
   if (!last) return;
   __threadfence();
-  if (lane_ < 12) g.s[ACC + lane_] = ((const fp*)&f[npairs])[lane_];
+  if (lane_ < 12) lp_put(g.s + ACC + lane_, lv_in(((const fp*)&f[npairs])[lane_]));
   __syncthreads();
   for (int i = 1; i < ng; ++i) {
-    if (lane_ < 12) g.s[IN + lane_] = ((const fp*)&f[npairs + i])[lane_];
+    if (lane_ < 12) lp_put(g.s + IN + lane_, lv_in(((const fp*)&f[npairs + i])[lane_]));
     __syncthreads();
     f12_mul(g, ACC, IN, ACC);
   }
   SSB_TRACE(TR_MF_PRODUCT);
   // the product before the final exponentiation, for the exclusion check of a failed batch
   // (k_fb_excl: the batch check without its suspect shares, by bilinearity from this value)
-  if (lane_ < 12) ((fp*)&f[npairs + ng])[lane_] = g.s[ACC + lane_];
+  if (lane_ < 12) ((fp*)&f[npairs + ng])[lane_] = lv_out(lp_get(g.s + ACC + lane_));
   f12_final_exp(g, ACC, TMP);
   if (lane_ == 0) {  // == 1, read slot by slot (an fp12 local would sit in scratch)
     bool one = true;
     for (int k = 0; k < 12; ++k) {
-      const fp v = g.s[ACC + k];
+      const fp v = lv_out(lp_get(g.s + ACC + k));
       one = one && (k == 0 ? fp_eq(v, fp_one()) : fp_is_zero(v));
     }
     *ok = one ? 1u : 0u;

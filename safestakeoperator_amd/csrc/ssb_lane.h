@@ -9,11 +9,17 @@
 //   448..479 input A, 480..511 input B, 512..543 output D          -> g.s[g.a/b/d + ...]
 // (A, B, D are group-relative slot indices chosen by the caller, beyond the scratch area.)
 //
-// Values in slots are fully reduced (< p).  A product operand of up to 3 terms is formed WITHOUT
-// reduction (negative terms enter as p - v, so the value is <= 3p); 3p * 3p < p * 2^384 keeps the
-// Montgomery product's output < 2p before its final conditional subtraction, so fp_mul accepts
-// it.  Materialised forms have up to 8 terms (<= 8p < 2^384) and are reduced by conditional
-// subtraction of 4p, 2p, p, p.
+// Values live in the reduced radix (ssb_f28_field.h: 14 x 28-bit limbs, Montgomery R = 2^392, one
+// v_mad_u64_u32 per limb product -- 496 VALU instructions per product against the 12 x 32-bit
+// engine's 671), lazily reduced: a slot holds a normalized value < 2p.  A product operand of up to
+// 3 terms is formed WITHOUT reduction (a negative term enters as K4P - v, K4P a 'spread' 4p whose
+// limbs dominate v's, so a term is < 4p and the form < 12p; 12p * 12p < p * 2^392 keeps the product's
+// output < 2p); the generator normalizes an operand whose limbs would make a limb product >= 2^60.
+// Materialised forms (up to 8 terms, every limb < 2^32) are normalized and folded below 2p (one
+// quotient estimate from the top limbs).  Values enter and leave the slots through lv_in / lv_out
+// (the engine's 12 x 32-bit Montgomery form, R = 2^384: a shift by 8 bits and a fold in, an 8-bit
+// Montgomery step and a conditional subtraction out), so the kernels' global data stays in the
+// engine's form.
 //
 // The same source runs on the host (tests): LP_FOR loops over the roles of one group, and the
 // stores of a pass happen after every role computed, like the lockstep lanes of a wave.
@@ -32,7 +38,9 @@ constexpr int LP_NCODE_CONST = 48, LP_NSCRATCH = 400;
 #else
 #define SSB_LDS
 #endif
-typedef SSB_LDS fp lfp;
+using lv = r28::f;                                  // a lane value (registers)
+struct alignas(16) lslot { uint32_t w[16]; };       // its LDS slot: 14 limbs, padded to four 16-byte words
+typedef SSB_LDS lslot lfp;
 typedef SSB_LDS uint32_t lu32;
 
 struct grp {       // passed BY VALUE to the programs (lives in registers)
@@ -52,13 +60,13 @@ struct grp {       // passed BY VALUE to the programs (lives in registers)
 #endif
 #define SSB_LP_TABLE alignas(16) constexpr
 #if defined(__HIP_DEVICE_COMPILE__)
-#define LP_DECL_T fp T_
+#define LP_DECL_T lv T_
 #define LP_FOR(G) for (int role = g.role, once_ = 1; once_; once_ = 0)
 #define LP_T T_
 #define LP_SYNC() __syncthreads()
 #define LP_FOR_ALL_CONSTS(i) for (int i = threadIdx.x; i < LP_NCODE_CONST; i += blockDim.x)
 #else
-#define LP_DECL_T fp T_[64]
+#define LP_DECL_T lv T_[64]
 #define LP_FOR(G) for (int role = 0; role < (G); ++role)
 #define LP_T T_[role]
 #define LP_SYNC() ((void)0)
@@ -96,134 +104,169 @@ template <int N> SSB_INL void lp_load_codes(lp_u4c* cw, const uint32_t* row) {
 #pragma unroll
   for (int k = 0; k < N; ++k) cw[k] = p[k];
 }
-SSB_INL fp lp_get(const lfp* p) {
+SSB_INL lv lp_get(const lfp* p) {
   const SSB_LDS lp_u4* q = (const SSB_LDS lp_u4*)p;
   const lp_u4 a = q[0], b = q[1], c = q[2];
-  fp r;
+  const uint32_t d0 = p->w[12], d1 = p->w[13];
+  lv r;
   r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
   r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
   r.l[8] = c.x; r.l[9] = c.y; r.l[10] = c.z; r.l[11] = c.w;
+  r.l[12] = d0; r.l[13] = d1;
   return r;
 }
-SSB_INL void lp_put(lfp* p, const fp& v) {
+SSB_INL void lp_put(lfp* p, const lv& v) {
   SSB_LDS lp_u4* q = (SSB_LDS lp_u4*)p;
   q[0] = lp_u4{v.l[0], v.l[1], v.l[2], v.l[3]};
   q[1] = lp_u4{v.l[4], v.l[5], v.l[6], v.l[7]};
   q[2] = lp_u4{v.l[8], v.l[9], v.l[10], v.l[11]};
+  p->w[12] = v.l[12]; p->w[13] = v.l[13];
 }
 #else
-SSB_INL fp lp_get(const lfp* p) { return *p; }
-SSB_INL void lp_put(lfp* p, const fp& v) { *p = v; }
+SSB_INL lv lp_get(const lfp* p) { lv r; for (int i = 0; i < 14; ++i) r.l[i] = p->w[i]; return r; }
+SSB_INL void lp_put(lfp* p, const lv& v) { for (int i = 0; i < 14; ++i) p->w[i] = v.l[i]; }
 #endif
 
-// ---- 12-limb helpers without modular reduction ----
-SSB_INL void lp_add_raw(fp& x, const fp& v) {
+// ---- lane values ----
+SSB_INL lv lv_zero() { lv r; for (int i = 0; i < 14; ++i) r.l[i] = 0u; return r; }
+SSB_INL lv lv_one() { return r28::cst(r28::ONE28); }
+// carry normalization of limbs up to 2^32 - 1: limbs 0..12 < 2^28, the rest in the top limb
+SSB_INL void lv_norm(lv& x) {
   uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) x.l[i] = addc(x.l[i], v.l[i], c, c);
+  for (int i = 0; i < 13; ++i) {
+    const uint32_t v = (x.l[i] & r28::M28) + c;
+    c = (x.l[i] >> 28) + (v >> 28);
+    x.l[i] = v & r28::M28;
+  }
+  x.l[13] += c;
 }
-SSB_INL void lp_pminus(fp& r, const fp& v) {  // p - v (v < p)
-  uint32_t br = 0;
+// the engine's form a 2^384 (< p) -> a 2^392 (< 2p): the 12 x 32-bit limbs re-sliced 8 bits up, folded
+SSB_INL lv lv_in(const fp& a) {
+  lv r;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) r.l[i] = subb(P_LIMBS[i], v.l[i], br, br);
+  for (int k = 0; k < 14; ++k) {
+    const int b = 28 * k - 8;
+    uint32_t v;
+    if (b < 0) {
+      v = a.l[0] << 8;
+    } else {
+      const int i = b >> 5, s = b & 31;
+      v = a.l[i] >> s;
+      if (s > 4 && i + 1 < 12) v |= a.l[i + 1] << (32 - s);
+    }
+    r.l[k] = v & r28::M28;
+  }
+  r28::fold(r, r);
+  return r;
 }
-SSB_INL void lp_sel(fp& r, const fp& a, const fp& b, uint32_t s) {  // r = s ? a : b
+// ... and back: x 2^-8 by one 8-bit Montgomery step ((x + m p) / 2^8, < 1.01 p), then canonical
+SSB_INL fp lv_out(const lv& x) {
+  const uint32_t m = (x.l[0] * r28::P28_INV) & 0xffu;
+  uint32_t z[14];
+  uint64_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) r.l[i] = s ? a.l[i] : b.l[i];
+  for (int i = 0; i < 14; ++i) {
+    c += (uint64_t)m * r28::P28[i] + x.l[i];
+    z[i] = i < 13 ? (uint32_t)c & r28::M28 : (uint32_t)c;
+    c >>= 28;
+  }
+  lv y;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) y.l[i] = ((z[i] >> 8) | (i < 13 ? z[i + 1] << 20 : 0u)) & (i < 13 ? r28::M28 : ~0u);
+  lv cn; r28::canon(cn, y);
+  fp r; r28::to32(r.l, cn);
+  return r;
+}
+SSB_INL bool lv_is_zero(const lv& x) { return r28::is_zero(x); }
+// -x (< 2p)
+SSB_INL void lv_neg(lv& x) {
+  lv t; r28::neg_raw(t, x, r28::K4P); lv_norm(t); r28::fold(x, t);
+}
+SSB_INL void lp_put_in(lfp* p, const fp& v) { lp_put(p, lv_in(v)); }
+SSB_INL fp lp_get_out(const lfp* p) { return lv_out(lp_get(p)); }
+// a slot reached through a generic pointer (an LDS struct passed by reference) -> the engine's form
+SSB_INL fp slot_out(const lslot& s) { lv v; for (int i = 0; i < 14; ++i) v.l[i] = s.w[i]; return lv_out(v); }
+
+// ---- forms without modular reduction ----
+SSB_INL void lp_add_raw(lv& x, const lv& v) {
+#pragma unroll
+  for (int i = 0; i < 14; ++i) x.l[i] += v.l[i];
+}
+SSB_INL void lp_pminus(lv& r, const lv& v) { r28::neg_raw(r, v, r28::K4P); }   // 4p - v (v < 2p: limbs >= 0)
+SSB_INL void lp_sel(lv& r, const lv& a, const lv& b, uint32_t s) {  // r = s ? a : b
+#pragma unroll
+  for (int i = 0; i < 14; ++i) r.l[i] = s ? a.l[i] : b.l[i];
 }
 
-template <class GR> SSB_INL void lp_ld(fp& x, const GR& g, uint32_t c) { x = lp_get(lp_ptr(g, c)); }
-template <class GR> SSB_INL void lp_ld_neg(fp& x, const GR& g, uint32_t c) { lp_pminus(x, lp_get(lp_ptr(g, c))); }
-template <class GR> SSB_INL void lp_ld_sgn(fp& x, const GR& g, uint32_t c, uint32_t s) {
-  const fp v = lp_get(lp_ptr(g, c));
-  fp n; lp_pminus(n, v);
+template <class GR> SSB_INL void lp_ld(lv& x, const GR& g, uint32_t c) { x = lp_get(lp_ptr(g, c)); }
+template <class GR> SSB_INL void lp_ld_neg(lv& x, const GR& g, uint32_t c) { lp_pminus(x, lp_get(lp_ptr(g, c))); }
+template <class GR> SSB_INL void lp_ld_sgn(lv& x, const GR& g, uint32_t c, uint32_t s) {
+  const lv v = lp_get(lp_ptr(g, c));
+  lv n; lp_pminus(n, v);
   lp_sel(x, n, v, s);
 }
-template <class GR> SSB_INL void lp_acc(fp& x, const GR& g, uint32_t c) { lp_add_raw(x, lp_get(lp_ptr(g, c))); }
-template <class GR> SSB_INL void lp_acc_neg(fp& x, const GR& g, uint32_t c) {
-  fp n; lp_pminus(n, lp_get(lp_ptr(g, c)));
+template <class GR> SSB_INL void lp_acc(lv& x, const GR& g, uint32_t c) { lp_add_raw(x, lp_get(lp_ptr(g, c))); }
+template <class GR> SSB_INL void lp_acc_neg(lv& x, const GR& g, uint32_t c) {
+  lv n; lp_pminus(n, lp_get(lp_ptr(g, c)));
   lp_add_raw(x, n);
 }
-template <class GR> SSB_INL void lp_acc_sgn(fp& x, const GR& g, uint32_t c, uint32_t s) {
-  const fp v = lp_get(lp_ptr(g, c));
-  fp n; lp_pminus(n, v);
-  fp t; lp_sel(t, n, v, s);
+template <class GR> SSB_INL void lp_acc_sgn(lv& x, const GR& g, uint32_t c, uint32_t s) {
+  const lv v = lp_get(lp_ptr(g, c));
+  lv n; lp_pminus(n, v);
+  lv t; lp_sel(t, n, v, s);
   lp_add_raw(x, t);
 }
-template <class GR> SSB_INL void lp_st(const GR& g, uint32_t c, const fp& v) { lp_put(lp_ptr(g, c), v); }
+template <class GR> SSB_INL void lp_st(const GR& g, uint32_t c, const lv& v) { lp_put(lp_ptr(g, c), v); }
 
-// modular doubling / addition of reduced values (< p)
-SSB_INL void lp_csub(fp& x, const uint32_t* mp);
-SSB_INL void lp_dbl_mod(fp& u) { fp t = u; lp_add_raw(u, t); lp_csub(u, P_LIMBS); }
-SSB_INL void lp_add_mod(fp& u, const fp& v) { lp_add_raw(u, v); lp_csub(u, P_LIMBS); }
-SSB_INL void lp_add_mod_sel(fp& u, const fp& v, uint32_t s) { fp t = u; lp_add_mod(t, v); lp_sel(u, t, u, s); }
-
-// x >= m*p ? x - m*p : x   (m*p given as limbs)
-SSB_INL void lp_csub(fp& x, const uint32_t* mp) {
-  fp t;
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) t.l[i] = subb(x.l[i], mp[i], br, br);
-  lp_sel(x, x, t, br);
-}
-constexpr uint32_t LP_P2[12] = {0xffff5556u, 0x73fdffffu, 0x62a7ffffu, 0x3d57fffdu, 0xed61ec48u, 0xce61a541u,
-                                0xe70a257eu, 0xc8ee9709u, 0x869759aeu, 0x96374f6cu, 0x72ffcd34u, 0x340223d4u};
-constexpr uint32_t LP_P4[12] = {0xfffeaaacu, 0xe7fbffffu, 0xc54ffffeu, 0x7aaffffau, 0xdac3d890u, 0x9cc34a83u,
-                                0xce144afdu, 0x91dd2e13u, 0x0d2eb35du, 0x2c6e9ed9u, 0xe5ff9a69u, 0x680447a8u};
-SSB_INL void lp_reduce1(fp& x) { lp_csub(x, P_LIMBS); }
-SSB_INL void lp_reduce2(fp& x) { lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
-SSB_INL void lp_reduce3(fp& x) { lp_csub(x, LP_P2); lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
-SSB_INL void lp_reduce4(fp& x) { lp_csub(x, LP_P4); lp_csub(x, LP_P2); lp_csub(x, P_LIMBS); lp_csub(x, P_LIMBS); }
+// a materialised sum (<= 8 terms, < 32p) -> a slot value (< 2p, normalized)
+SSB_INL void lp_reduce(lv& x) { lv_norm(x); r28::fold(x, x); }
+// modular doubling / addition of slot values (the multiple-of-v forms; kept below 2p)
+SSB_INL void lp_dbl_mod(lv& u) { lv t = u; lp_add_raw(u, t); lp_reduce(u); }
+SSB_INL void lp_add_mod(lv& u, const lv& v) { lp_add_raw(u, v); lp_reduce(u); }
+SSB_INL void lp_add_mod_sel(lv& u, const lv& v, uint32_t s) { lv t = u; lp_add_mod(t, v); lp_sel(u, t, u, s); }
+// an operand whose limbs are too wide for the product's 64-bit columns
+SSB_INL void lp_norm(lv& x) { lv_norm(x); }
+// the product (< 2p, normalized)
+SSB_INL void lp_mul(lv& r, const lv& x, const lv& y) { r28::mul(r, x, y); }
 
 // ---- the accumulator engine for long / scaled forms ----------------------------------------
-// value = sum_pos c v + sum_neg |c| (p - v), per 32-bit limb in 64-bit accumulators (ONE
-// v_mad_u64_u32 per limb and term, no carry chain), then a signed carry propagation and one
-// Barrett-style step: q = floor(top / (p_hi + 1)) underestimates value / p, so value - q p lies in
-// [0, 2p) (an operand for fp_mul) and one conditional subtraction makes it < p (a stored value).
-struct lacc { uint64_t a[12], b[12]; };
+// value = sum_pos c v - sum_neg c v + 2K p (K = sum_neg c: v < 2p, so the value is >= 0), per 28-bit
+// limb in one signed 64-bit accumulator (ONE v_mad_i64_i32 per limb and term, positive and negative
+// coefficients alike), then a signed carry propagation; with `fold` the result is brought below 2p
+// (a stored value, or an operand whose bound would break the product's), else it stays < 2p sum|c|.
+struct lacc { int64_t a[14]; };
 SSB_INL void la_zero(lacc& x) {
 #pragma unroll
-  for (int i = 0; i < 12; ++i) { x.a[i] = 0; x.b[i] = 0; }
+  for (int i = 0; i < 14; ++i) x.a[i] = 0;
 }
-SSB_INL void la_pos(lacc& x, const fp& v, uint32_t c) {
+SSB_INL void la_add(lacc& x, const lv& v, int32_t c) {
 #pragma unroll
-  for (int i = 0; i < 12; ++i) x.a[i] = (uint64_t)v.l[i] * c + x.a[i];
+  for (int i = 0; i < 14; ++i) x.a[i] += (int64_t)(int32_t)v.l[i] * (int64_t)c;
 }
-SSB_INL void la_neg(lacc& x, const fp& v, uint32_t c) {
-#pragma unroll
-  for (int i = 0; i < 12; ++i) x.b[i] = (uint64_t)v.l[i] * c + x.b[i];
-}
-SSB_INL void la_mix(lacc& x, const fp& v, uint32_t cp, uint32_t cn) { la_pos(x, v, cp); la_neg(x, v, cn); }
+SSB_INL void la_pos(lacc& x, const lv& v, uint32_t c) { la_add(x, v, (int32_t)c); }
+SSB_INL void la_neg(lacc& x, const lv& v, uint32_t c) { la_add(x, v, -(int32_t)c); }
+SSB_INL void la_mix(lacc& x, const lv& v, uint32_t cp, uint32_t cn) { la_add(x, v, (int32_t)cp - (int32_t)cn); }
 template <class GR> SSB_INL void la_ld_pos(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_pos(x, lp_get(lp_ptr(g, code)), c); }
 template <class GR> SSB_INL void la_ld_neg(lacc& x, const GR& g, uint32_t code, uint32_t c) { la_neg(x, lp_get(lp_ptr(g, code)), c); }
 template <class GR> SSB_INL void la_ld_mix(lacc& x, const GR& g, uint32_t code, uint32_t cp, uint32_t cn) {
   la_mix(x, lp_get(lp_ptr(g, code)), cp, cn);
 }
-constexpr double LA_INV_PHI = 1.0 / (436277738.0 + 1.0) * (1.0 - 1e-12);  // 1 / ((p >> 352) + 1), rounded down
-SSB_INL void la_fin(fp& r, const lacc& x, uint32_t K, bool exact) {
+SSB_INL void la_fin(lv& r, const lacc& x, uint32_t K, bool fold) {
+  const int64_t k2 = 2 * (int64_t)K;
   int64_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const uint64_t t = (uint64_t)P_LIMBS[i] * K + x.a[i];
-    const int64_t d = (int64_t)(t - x.b[i]) + carry;
-    r.l[i] = (uint32_t)d;
-    carry = d >> 32;
+  for (int i = 0; i < 13; ++i) {
+    const int64_t t = x.a[i] + k2 * (int64_t)r28::P28[i] + carry;
+    r.l[i] = (uint32_t)t & r28::M28;
+    carry = t >> 28;   // (arithmetic)
   }
-  const uint64_t hi = ((uint64_t)carry << 32) | r.l[11];  // value >> 352 (carry >= 0: value >= 0)
-  const uint32_t q = (uint32_t)((double)hi * LA_INV_PHI);
-  uint64_t pc = 0;
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const uint64_t pr = (uint64_t)P_LIMBS[i] * q + pc;
-    pc = pr >> 32;
-    r.l[i] = subb(r.l[i], (uint32_t)pr, br, br);
-  }
-  if (exact) { lp_csub(r, P_LIMBS); lp_csub(r, P_LIMBS); }
+  r.l[13] = (uint32_t)(x.a[13] + k2 * (int64_t)r28::P28[13] + carry);
+  if (fold) r28::fold(r, r);
 }
 
-template <class GR> SSB_INL void lp_chk(const GR& g, const fp& v, uint32_t bit) {
-  if (bit < 31u && fp_is_zero(v)) {
+template <class GR> SSB_INL void lp_chk(const GR& g, const lv& v, uint32_t bit) {
+  if (bit < 31u && lv_is_zero(v)) {
 #if defined(__HIP_DEVICE_COMPILE__)
     atomicOr((uint32_t*)g.flag, 1u << bit);
 #else

@@ -48,10 +48,8 @@ template <class GR> SSB_INL void g1_madd(GR& g, int a, int b, int d, uint32_t& e
 template <int G, class GR> SSB_INL void lg_aff_to_jac(GR& g, int src, int dst, int ncoord) {
   LP_FOR(G) {
     for (int i = role; i < ncoord + ncoord / 2; i += G) {
-      fp v;
-      if (i < ncoord) v = g.s[src + i];
-      else v = (i == ncoord) ? fp_one() : fp_zero();
-      g.s[dst + i] = v;
+      if (i < ncoord) g.s[dst + i] = g.s[src + i];
+      else lp_put(g.s + dst + i, (i == ncoord) ? lv_one() : lv_zero());
     }
   }
   LP_SYNC();
@@ -90,9 +88,9 @@ template <class GR> SSB_INL void g2_mul_u64_odd(GR& g, int p, uint64_t k, int ta
     const int e = tab + 6 * (((d < 0 ? -d : d) - 1) >> 1);
     LP_FOR(G) {
       if (role < 6) {
-        fp v = g.s[e + role];
-        if (d < 0 && (role == 2 || role == 3)) fp_neg(v, v);
-        g.s[tmp + role] = v;
+        lv v = lp_get(g.s + e + role);
+        if (d < 0 && (role == 2 || role == 3)) lv_neg(v);
+        lp_put(g.s + tmp + role, v);
       }
     }
     LP_SYNC();
@@ -119,9 +117,9 @@ template <class GR> SSB_INL void g1_mul_u64_odd(GR& g, int p, uint64_t k, int ta
     const int e = tab + 3 * (((d < 0 ? -d : d) - 1) >> 1);
     LP_FOR(G) {
       if (role < 3) {
-        fp v = g.s[e + role];
-        if (d < 0 && role == 1) fp_neg(v, v);
-        g.s[tmp + role] = v;
+        lv v = lp_get(g.s + e + role);
+        if (d < 0 && role == 1) lv_neg(v);
+        lp_put(g.s + tmp + role, v);
       }
     }
     LP_SYNC();
@@ -142,9 +140,9 @@ template <class GR> SSB_INL bool g2_subgroup_check(GR& g, int p, int acc, int tm
   g.a = p; g.d = tmp; lp_g2_npsi_aff(g);
   g.a = acc; g.b = tmp; g.d = tmp + 4; lp_g2_eq_aff(g);
   // [|x|]P at infinity (2-torsion met by a doubling) is exceptional: exact fallback
-  if (fp_is_zero(g.s[acc + 4]) && fp_is_zero(g.s[acc + 5])) exc |= 1u;
+  if (lv_is_zero(lp_get(g.s + acc + 4)) && lv_is_zero(lp_get(g.s + acc + 5))) exc |= 1u;
   bool eq = true;
-  for (int i = 0; i < 4; ++i) eq = eq && fp_is_zero(g.s[tmp + 4 + i]);
+  for (int i = 0; i < 4; ++i) eq = eq && lv_is_zero(lp_get(g.s + tmp + 4 + i));
   return eq;
 }
 
@@ -153,9 +151,9 @@ template <class GR> SSB_INL void g2_neg_copy(GR& g, int src, int dst) {
   constexpr int G = G2_ADD_G;
   LP_FOR(G) {
     if (role < 6) {
-      fp v = g.s[src + role];
-      if (role == 2 || role == 3) fp_neg(v, v);
-      g.s[dst + role] = v;
+      lv v = lp_get(g.s + src + role);
+      if (role == 2 || role == 3) lv_neg(v);
+      lp_put(g.s + dst + role, v);
     }
   }
   LP_SYNC();
@@ -193,13 +191,12 @@ template <class GR> SSB_INL void g2_clear_cofactor(GR& g, int p, int r, int w, u
 }
 
 // ---- Fp12 programs (G = 64, one group per wave) ----
+// an fp12 (engine form) out of / into 12 slots, in the fields' order (c0.c0.c0, c0.c0.c1, c0.c1.c0, ..)
 SSB_INL void ld12(fp12& f, const lfp* s) {
-  fp2* v[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-  for (int k = 0; k < 6; ++k) { v[k]->c0 = s[2 * k]; v[k]->c1 = s[2 * k + 1]; }
+  for (int k = 0; k < 12; ++k) ((fp*)&f)[k] = lv_out(lp_get(s + k));
 }
 SSB_INL void st12(lfp* s, const fp12& f) {
-  const fp2 v[6] = {f.c0.c0, f.c0.c1, f.c0.c2, f.c1.c0, f.c1.c1, f.c1.c2};
-  for (int k = 0; k < 6; ++k) { s[2 * k] = v[k].c0; s[2 * k + 1] = v[k].c1; }
+  for (int k = 0; k < 12; ++k) lp_put(s + k, lv_in(((const fp*)&f)[k]));
 }
 template <class GR> SSB_INL void f12_mul(GR& g, int a, int b, int d) { g.a = a; g.b = b; g.d = d; lp_fp12_mul(g); }
 template <class GR> SSB_INL void f12_cyc_sqr(GR& g, int a, int d) { g.a = a; g.d = d; lp_fp12_cyc_sqr(g); }
@@ -231,10 +228,16 @@ template <class GR> SSB_INL void f12_cyc_exp_x(GR& g, int r, int f) {
 // slots d[0..11] = (a[0..5] as an Fp6)^-1 (the w-half zero), on one lane; out of line, so its
 // Fp6 temporaries live in its own frame, not in every kernel that runs a final exponentiation
 SSB_FN void fp6_inv_slots(const lfp* a, lfp* d) {
-  // the slots hold an fp6's fields in order (c0.c0, c0.c1, c1.c0, ..): invert in place through flat
-  // pointers, no copies in a frame
-  fp6_inv(*(fp6*)(d), *(const fp6*)(a));
-  for (int k = 6; k < 12; ++k) d[k] = fp_zero();
+  // the slots hold an fp6's fields in order (c0.c0, c0.c1, c1.c0, ..): the six values in the engine's
+  // form are laid out as an fp6 in the bytes of d's slots [0, 6) and inverted into those of [6, 11),
+  // through flat pointers (no copies in a frame), then brought back into slots [0, 6)
+  static_assert(6 * sizeof(lslot) >= sizeof(fp6) && 5 * sizeof(lslot) >= sizeof(fp6), "fp6 in the slots");
+  fp6* x = (fp6*)(d);
+  fp6* y = (fp6*)(d + 6);
+  for (int k = 0; k < 6; ++k) { const fp v = lv_out(lp_get(a + k)); ((fp*)x)[k] = v; }
+  fp6_inv(*y, *x);
+  for (int k = 0; k < 6; ++k) { const fp v = ((const fp*)y)[k]; lp_put(d + k, lv_in(v)); }
+  for (int k = 6; k < 12; ++k) lp_put(d + k, lv_zero());
 }
 
 // final exponentiation of the Fp12 value at `f` (in place); 7 x 12 work slots at `tmp`.
@@ -286,11 +289,8 @@ template <class GR> SSB_INL void f12_final_exp(GR& g, int f, int tmp) {
 template <class GR> SSB_INL void f12_miller(GR& g, int F, int b) {
   LP_FOR(64) {
     if (role < 18) {
-      fp v;
-      if (role < 12) v = (role == 0) ? fp_one() : fp_zero();
-      else if (role < 16) v = g.s[b + role - 12];
-      else v = (role == 16) ? fp_one() : fp_zero();
-      g.s[F + role] = v;
+      if (role >= 12 && role < 16) g.s[F + role] = g.s[b + role - 12];
+      else lp_put(g.s + F + role, (role == 0 || role == 16) ? lv_one() : lv_zero());
     }
   }
   LP_SYNC();
@@ -309,15 +309,15 @@ template <class GR> SSB_INL void f12_miller(GR& g, int F, int b) {
 template <class GR> SSB_INL void f12_miller2(GR& g, int F, int b, int bp) {
   LP_FOR(64) {
     if (role < 28) {
-      fp v;
-      if (role < 12) v = (role == 0) ? fp_one() : fp_zero();
-      else if (role < 16) v = g.s[b + role - 12];                       // T1 = (Q1, 1)
-      else if (role < 18) v = (role == 16) ? fp_one() : fp_zero();
-      else if (role < 22) v = g.s[b + 6 + role - 18];                   // T2 = (Q2, 1)
-      else if (role < 24) v = (role == 22) ? fp_one() : fp_zero();
-      else v = g.s[b + (role < 26 ? 4 + role - 24 : 10 + role - 26)];   // (P1, P2)
-      if (role < 24) g.s[F + role] = v;
-      else g.s[bp + role - 24] = v;
+      lv v;
+      if (role < 12) v = (role == 0) ? lv_one() : lv_zero();
+      else if (role < 16) v = lp_get(g.s + b + role - 12);                       // T1 = (Q1, 1)
+      else if (role < 18) v = (role == 16) ? lv_one() : lv_zero();
+      else if (role < 22) v = lp_get(g.s + b + 6 + role - 18);                   // T2 = (Q2, 1)
+      else if (role < 24) v = (role == 22) ? lv_one() : lv_zero();
+      else v = lp_get(g.s + b + (role < 26 ? 4 + role - 24 : 10 + role - 26));   // (P1, P2)
+      if (role < 24) lp_put(g.s + F + role, v);
+      else lp_put(g.s + bp + role - 24, v);
     }
   }
   LP_SYNC();

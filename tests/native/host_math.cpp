@@ -54,29 +54,31 @@ static bool verify_full(const g1_aff& pk, const g2_aff& sig, const g2_aff& h) {
 
 // ---- lane-group programs (host emulation, role loop) against the single-lane code ----
 struct host_group {
-  std::vector<fp> K, S;
+  std::vector<lane::lslot> K, S;
   uint32_t flag = 0;
   lane::grp g;
   host_group() : K(lane::LP_NCODE_CONST), S(lane::LP_NSCRATCH + 256) {
     g = lane::grp{K.data(), S.data(), 0, 0, 0, &flag, 0};
     lane::lp_init_consts(g);
   }
-  fp* u(int i) { return &S[lane::LP_NSCRATCH + i]; }
+  lane::lslot* u(int i) { return &S[lane::LP_NSCRATCH + i]; }
+  void put(int i, const fp& v) { lane::lp_put(u(i), lane::lv_in(v)); }
+  fp get(int i) { return lane::lv_out(lane::lp_get(u(i))); }
   int U(int i) const { return lane::LP_NSCRATCH + i; }
 };
 template <class F> static void put_jac(host_group& h, int at, const jac<F>& p) {
-  const fp* q = (const fp*)&p; for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) *h.u(at + i) = q[i];
+  const fp* q = (const fp*)&p; for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) h.put(at + i, q[i]);
 }
 template <class F> static bool eq_jac(host_group& h, int at, const jac<F>& p) {
   const fp* q = (const fp*)&p; bool ok = true;
-  for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) ok = ok && fp_eq(*h.u(at + i), q[i]);
+  for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) ok = ok && fp_eq(h.get(at + i), q[i]);
   return ok;
 }
 template <class F> static void put_aff(host_group& h, int at, const aff<F>& p) {
-  const fp* q = (const fp*)&p; for (int i = 0; i < (int)(2 * sizeof(F) / sizeof(fp)); ++i) *h.u(at + i) = q[i];
+  const fp* q = (const fp*)&p; for (int i = 0; i < (int)(2 * sizeof(F) / sizeof(fp)); ++i) h.put(at + i, q[i]);
 }
 template <class F> static bool same_point(host_group& h, int at, const jac<F>& p) {
-  jac<F> r; fp* q = (fp*)&r; for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) q[i] = *h.u(at + i);
+  jac<F> r; fp* q = (fp*)&r; for (int i = 0; i < (int)(3 * sizeof(F) / sizeof(fp)); ++i) q[i] = h.get(at + i);
   aff<F> a, b; jac_to_aff(a, r); jac_to_aff(b, p);
   return a.inf == b.inf && (a.inf || (f_eq(a.x, b.x) && f_eq(a.y, b.y)));
 }
@@ -170,7 +172,7 @@ static void lane_selftest(const uint8_t* seed32) {
       lane::st12(g.s + h.U(0), m); lane::f12_final_exp(g, h.U(0), h.U(12)); lane::ld12(r2, g.s + h.U(0)); ok += fp12_eq(r1, r2); ++n; }
     { // Miller loop of (pk, P)
       const int F = h.U(100), Bq = h.U(130);
-      g.s[Bq] = P.x.c0; g.s[Bq + 1] = P.x.c1; g.s[Bq + 2] = P.y.c0; g.s[Bq + 3] = P.y.c1; g.s[Bq + 4] = pk.x; g.s[Bq + 5] = pk.y;
+      lane::lp_put(g.s + Bq, lane::lv_in(P.x.c0)); lane::lp_put(g.s + Bq + 1, lane::lv_in(P.x.c1)); lane::lp_put(g.s + Bq + 2, lane::lv_in(P.y.c0)); lane::lp_put(g.s + Bq + 3, lane::lv_in(P.y.c1)); lane::lp_put(g.s + Bq + 4, lane::lv_in(pk.x)); lane::lp_put(g.s + Bq + 5, lane::lv_in(pk.y));
       // (the lane loop runs homogeneous-projective steps, the single-lane one Jacobian: the Miller
       // values differ by an Fp2 factor per line, which the final exponentiation removes)
       lane::f12_miller(g, F, Bq); lane::ld12(r2, g.s + F);
@@ -179,13 +181,13 @@ static void lane_selftest(const uint8_t* seed32) {
     { // two-pair Miller loop of (pk, P) and (-g1, Q): == the product of the two single loops after
       // the final exponentiation
       const int F = h.U(100), Bq = h.U(130), Bp = h.U(142);
-      g.s[Bq] = P.x.c0; g.s[Bq + 1] = P.x.c1; g.s[Bq + 2] = P.y.c0; g.s[Bq + 3] = P.y.c1; g.s[Bq + 4] = pk.x; g.s[Bq + 5] = pk.y;
-      g.s[Bq + 6] = Q.x.c0; g.s[Bq + 7] = Q.x.c1; g.s[Bq + 8] = Q.y.c0; g.s[Bq + 9] = Q.y.c1; g.s[Bq + 10] = ng.x; g.s[Bq + 11] = ng.y;
+      lane::lp_put(g.s + Bq, lane::lv_in(P.x.c0)); lane::lp_put(g.s + Bq + 1, lane::lv_in(P.x.c1)); lane::lp_put(g.s + Bq + 2, lane::lv_in(P.y.c0)); lane::lp_put(g.s + Bq + 3, lane::lv_in(P.y.c1)); lane::lp_put(g.s + Bq + 4, lane::lv_in(pk.x)); lane::lp_put(g.s + Bq + 5, lane::lv_in(pk.y));
+      lane::lp_put(g.s + Bq + 6, lane::lv_in(Q.x.c0)); lane::lp_put(g.s + Bq + 7, lane::lv_in(Q.x.c1)); lane::lp_put(g.s + Bq + 8, lane::lv_in(Q.y.c0)); lane::lp_put(g.s + Bq + 9, lane::lv_in(Q.y.c1)); lane::lp_put(g.s + Bq + 10, lane::lv_in(ng.x)); lane::lp_put(g.s + Bq + 11, lane::lv_in(ng.y));
       lane::f12_miller2(g, F, Bq, Bp); lane::ld12(r2, g.s + F);
       fp12 m, e1, e2; fp12_mul(m, f1, f2); final_exponentiation(e1, m); final_exponentiation(e2, r2); ok += fp12_eq(e1, e2); ++n;
       // and (pk, P) with (-pk, P): a check that holds, e(pk, P) e(-pk, P) == 1
       g1_aff npk = pk; fp_neg(npk.y, pk.y);
-      g.s[Bq + 6] = P.x.c0; g.s[Bq + 7] = P.x.c1; g.s[Bq + 8] = P.y.c0; g.s[Bq + 9] = P.y.c1; g.s[Bq + 10] = npk.x; g.s[Bq + 11] = npk.y;
+      lane::lp_put(g.s + Bq + 6, lane::lv_in(P.x.c0)); lane::lp_put(g.s + Bq + 7, lane::lv_in(P.x.c1)); lane::lp_put(g.s + Bq + 8, lane::lv_in(P.y.c0)); lane::lp_put(g.s + Bq + 9, lane::lv_in(P.y.c1)); lane::lp_put(g.s + Bq + 10, lane::lv_in(npk.x)); lane::lp_put(g.s + Bq + 11, lane::lv_in(npk.y));
       lane::f12_miller2(g, F, Bq, Bp); lane::f12_final_exp(g, F, h.U(12)); lane::ld12(r2, g.s + F); ok += fp12_is_one(r2); ++n; } }
   printf("%d %d\n", ok, n);
 }
@@ -486,30 +488,39 @@ int main() {
         n += 2; bad += !same(w1, g1v); bad += !same(w2, g2v);
       }
       printf("%d %d\n", n - bad, n);
-    } else if (cmd == "lafin") {  // lafin <trials>: accumulator engine vs repeated modular add/sub
+    } else if (cmd == "lafin") {  // lafin <trials>: accumulator engine (reduced radix) vs repeated modular add/sub
       int trials; is >> trials;
       uint64_t st = 0x9E3779B97F4A7C15ull;
       auto rnd = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
       int bad = 0;
+      lane::lv pm1 = r28::cst(r28::P28); pm1.l[0] -= 1;                 // p - 1
+      lane::lv tpm1; r28::add(tpm1, pm1, r28::cst(r28::P28));             // 2p - 1 (the slot bound)
       for (int tr = 0; tr < trials; ++tr) {
         const int t = 1 + (int)(rnd() % 16);
         lane::lacc A; lane::la_zero(A);
         uint32_t K = 0;
         fp want = fp_zero();
         for (int k = 0; k < t; ++k) {
-          fp v;
+          lane::lv v;
           const int kind = (int)(rnd() % 4);
-          for (int i = 0; i < 12; ++i) v.l[i] = kind == 0 ? 0u : (kind == 1 ? P_LIMBS[i] : (uint32_t)rnd());
-          if (kind == 1) v.l[0] -= 1;                       // p - 1
-          if (kind >= 2) { v.l[11] &= 0x0fffffffu; }         // < p
-          const int m = (tr & 1) ? 1 + (int)(rnd() % 300) : 1 + (int)(rnd() % 3);
+          if (kind == 0) v = lane::lv_zero();
+          else if (kind == 1) v = pm1;
+          else if (kind == 2) v = tpm1;
+          else { fp e; for (int i = 0; i < 12; ++i) e.l[i] = (uint32_t)rnd(); e.l[11] &= 0x0fffffffu; v = lane::lv_in(e); }
+          const fp ve = lane::lv_out(v);
+          const int m = (tr & 1) ? 1 + (int)(rnd() % 60) : 1 + (int)(rnd() % 3);
           const bool neg = rnd() & 1;
           if (neg) { lane::la_neg(A, v, (uint32_t)m); K += (uint32_t)m; } else lane::la_pos(A, v, (uint32_t)m);
-          for (int j = 0; j < m; ++j) { if (neg) fp_sub(want, want, v); else fp_add(want, want, v); }
+          for (int j = 0; j < m; ++j) { if (neg) fp_sub(want, want, ve); else fp_add(want, want, ve); }
         }
-        fp r, r2; lane::la_fin(r, A, K, true); lane::la_fin(r2, A, K, false);
-        fp r2m; lane::lp_csub(r2, P_LIMBS); r2m = r2; lane::lp_csub(r2m, P_LIMBS);
-        if (!fp_eq(r, want) || !fp_eq(r2m, want)) ++bad;
+        lane::lv r, r2; lane::la_fin(r, A, K, true); lane::la_fin(r2, A, K, false);
+        lane::lv r2f; r28::fold(r2f, r2);
+        if (!fp_eq(lane::lv_out(r), want) || !fp_eq(lane::lv_out(r2f), want)) ++bad;
+        // the fold's bound: r <= 2p - 1 (normalized limbs, compared from the top)
+        int cmp = 0;
+        for (int i = 13; i >= 0 && cmp == 0; --i) cmp = r.l[i] < tpm1.l[i] ? -1 : (r.l[i] > tpm1.l[i] ? 1 : 0);
+        for (int i = 0; i < 13; ++i) if (r.l[i] >> 28) cmp = 1;
+        if (cmp > 0) ++bad;
       }
       printf("%d\n", bad);
     } else if (cmd == "lane") {  // lane <seed32hex>: lane-group programs vs single-lane code

@@ -207,8 +207,9 @@ def test_bucket_madd_matches_generic(host_exe):
 
 
 def test_accumulator_engine_reduction(host_exe):
-    """la_fin (sum of scaled +-terms, one Barrett-style step) equals the modular sum, including the
-    edge values 0 and p-1 and coefficients up to 300 per term."""
+    """la_fin (the lane programs' sum of scaled +-terms in the reduced radix, one signed accumulator per
+    28-bit limb, folded below 2p) equals the modular sum, including the edge values 0, p-1 and 2p-1
+    (the slot bound) and coefficients up to 60 per term; the unfolded form is congruent."""
     assert _run(host_exe, ["lafin 20000"]) == ["0"]
 
 
