@@ -144,6 +144,16 @@ def kernel_mads(mads, V, t, n, n_roots, pk_cached=True):
     }
 
 
+def valu_per_mad(sq, mads):
+    """SQ_INSTS_VALU of the roofline launch (committed PMC summary: instructions per wave x waves) per
+    64 algorithmic MADs (one wave-instruction's worth), or None."""
+    try:
+        rb = sq["roofline_batch"]
+        return round(rb["valu_insts_per_wave"] * rb["SQ_WAVES"] / (mads / 64.0), 3)
+    except (KeyError, TypeError, ZeroDivisionError):
+        return None
+
+
 def pmc_traffic(kernel, shares=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (FETCH_SIZE x 2 on
     gfx950 + WRITE_SIZE, separate passes; bench_tools/pmc_summary.py), or None."""
@@ -996,6 +1006,9 @@ def main():
                                   rf["R"], rf["shares"], rf["shares"] // 64),
                     "results_ok": rf["ok"],
                     "pmc_sq": sq,   # SQ_INSTS_VALU / wave and VALU-active / busy cycle: roofline batch and pipelined C2
+                    # VALU wave-instructions issued per algorithmic MAD wave-instruction (SQ_INSTS_VALU of the
+                    # roofline launch / (MADs / 64)): 2 is the engine product's floor (a v_addc per MAD)
+                    "valu_insts_per_mad": valu_per_mad(sq, sg_mads),
                     "k_decode_count": {"achieved": round(dec_mads / (rf["ms"]["k_decode"] * 1e-3) / 1e12, 4),
                                        "frac": round(dec_mads / (rf["ms"]["k_decode"] * 1e-3) / MAD_PEAK_MEASURED, 5),
                                        "avg_launch_ms": round(rf["ms"]["k_decode"], 4), "mads_per_launch": dec_mads,

@@ -426,7 +426,8 @@ int ssb_lagrange_coeffs(ssb_ctx* ctx, size_t t, const uint64_t* ids, uint8_t* ou
  * which every duty reaches once per validator (src/validation/signing_method.rs:318; selection proofs
  * and RANDAO reveals included, :269-292).  Submissions from any number of threads join the open
  * window; a worker thread closes it at max_jobs submissions or window_us after its first (or on
- * flush), signs it with ONE ssb_sign_batch (each distinct root hashed once) and completes every
+ * flush) -- a window holds at most max_jobs: what arrives while one is being signed opens the next --
+ * signs it with ONE ssb_sign_batch (each distinct root hashed once) and completes every
  * submission: sig96 = compress([sk] hash_to_G2(root)) with the POP DST of src/crypto/impls/blst.rs:11,
  * byte for byte SecretKey::sign's output.  The keys are wiped from the library's buffers once used. */
 typedef struct ssb_signer ssb_signer;

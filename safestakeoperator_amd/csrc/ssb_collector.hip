@@ -629,6 +629,11 @@ struct ssb_signer {
       }
       win.swap(open);
       open.clear();
+      if (win.size() > J) {   // submitters filled past max_jobs while the last window ran: the rest waits
+        open.assign(win.begin() + J, win.end());   // (its first job has waited since t_first: due at once)
+        wipe(&win[J], (win.size() - J) * sizeof(sign_job));
+        win.resize(J);
+      }
       lk.unlock();
       const size_t n = win.size();
       sk.resize(32 * n); ridx.resize(n); roots.clear(); out.assign(96 * n, 0); rmap.clear();
