@@ -484,6 +484,23 @@ SSB_FN void miller_one(lane::grp& g, const g1_aff& P, const g2_aff& Q, int F1, i
   }
 }
 
+// S_r = sum_q 2^(16q) X_q, then the root's check FE(f[r] * e(-g1, S_r)) == 1 (k_fb_root's last block of
+// the root); out of line, so the root's point is not in the kernel's frame under the other chains
+SSB_FN bool root_check(fr_lds& u, uint32_t& flg, const g2_jac* __restrict__ Xr, const fp12* __restrict__ fr) {
+  using namespace ssb::lane;
+  const int lane_ = threadIdx.x;
+  const g2_aff Q = combine_quarters<fp2>(Xr);
+  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+  grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
+  lp_init_consts(g);
+  const int F1 = BS_S0, B = F1 + 24, TMP = B + 12 + 4, FR = TMP + 72;
+  miller_one(g, g1_neg_generator(), Q, F1, B, flg);   // e(-g1, O) = 1: the root's value is f[r] alone
+  if (lane_ < 12) lp_put(g.s + FR + lane_, lv_in(((const fp*)fr)[lane_]));
+  __syncthreads();
+  f12_mul(g, F1, FR, F1);
+  f12_final_exp(g, F1, TMP);
+  return f12_slots_one(g, F1);
+}
 __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __restrict__ ok,
                                      const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
                                      const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gst,
@@ -522,18 +539,7 @@ __global__ void SSB_LB2(64) k_fb_root(int L, int n_roots, const uint32_t* __rest
   __syncthreads();
   if (!last) return;
   __threadfence();
-  // S_r = sum_q 2^(16q) X_q, then the root's check FE(f[r] * e(-g1, S_r)) == 1
-  const g2_aff Q = combine_quarters<fp2>(X + 4 * r);
-  __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
-  grp g{(lfp*)u.s, (lfp*)u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&flg, lane_};
-  lp_init_consts(g);
-  const int F1 = BS_S0, B = F1 + 24, TMP = B + 12 + 4, FR = TMP + 72;
-  miller_one(g, g1_neg_generator(), Q, F1, B, flg);   // e(-g1, O) = 1: the root's value is f[r] alone
-  if (lane_ < 12) lp_put(g.s + FR + lane_, lv_in(((const fp*)&froot[r])[lane_]));
-  __syncthreads();
-  f12_mul(g, F1, FR, F1);
-  f12_final_exp(g, F1, TMP);
-  const bool pass = f12_slots_one(g, F1);
+  const bool pass = root_check(u, flg, X + 4 * r, froot + r);
   if (lane_ == 0) {
     gv0[gst[r]] = pass ? 1 : 0;
     if (!pass) atomicAdd(nfail, nr);   // shares in failing roots
@@ -1002,6 +1008,41 @@ __global__ void SSB_LB(64) k_fb_single(int n_roots, const uint32_t* __restrict__
 // slower.)
 // gv_prev / gv_cur: per-group results of the previous / this level (1 pass, 0 fail).
 constexpr int LV_THREADS = 64;
+// the group's sums S_sig = sum k_i sig_i, S_pk = sum k_i pk_i over its candidates [a, b) of perm (lane-
+// strided, LDS tree), affine into *sQ / *sP, the candidate count into *ncand; out of line, so the
+// points it holds are not in the kernel's frame under the pairing check's chain
+SSB_FN void level_group_sums(uint64_t a, uint64_t b, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flags,
+                             const g2_jac* __restrict__ rsig, const g1_jac* __restrict__ rpk, g2_jac* red, g1_aff* sP,
+                             g2_aff* sQ, uint32_t* ncand) {
+  const int lane_ = threadIdx.x;
+  if (lane_ == 0) *ncand = 0u;
+  __syncthreads();
+  g2_jac acc2; jac_set_inf(acc2);
+  g1_jac acc1; jac_set_inf(acc1);
+  uint32_t nc = 0;
+  for (uint64_t k = a + lane_; k < b; k += 64) {
+    const uint32_t s = perm[k];
+    if (flags[s] & FLAG_CANDIDATE) { jac_add(acc2, acc2, rsig[s]); jac_add(acc1, acc1, rpk[s]); ++nc; }
+  }
+  if (nc) atomicAdd(ncand, nc);
+  red[lane_] = acc2;
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (lane_ < w) { g2_jac o = red[lane_ + w]; jac_add(acc2, acc2, o); red[lane_] = acc2; }
+    __syncthreads();
+  }
+  if (lane_ == 0) { g2_aff q; jac_to_aff(q, acc2); *sQ = q; }
+  __syncthreads();
+  g1_jac* red1 = (g1_jac*)red;
+  red1[lane_] = acc1;
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (lane_ < w) { g1_jac o = red1[lane_ + w]; jac_add(acc1, acc1, o); red1[lane_] = acc1; }
+    __syncthreads();
+  }
+  if (lane_ == 0) { g1_aff p; jac_to_aff(p, acc1); *sP = p; }
+  __syncthreads();
+}
 // (the group sums and the two-pair loop do not fit 256 registers: one wave per SIMD, whatever the
 // TU asks -- a waves_per_eu(1) attribute here would lift the shared out-of-line callees to 512 for
 // every kernel of the TU)
@@ -1051,38 +1092,8 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
         continue;
       }
     }
-    bool pass = true;
-    {
-    // sums over the group's candidates
-    if (lane_ == 0) ncand = 0u;
-    __syncthreads();
-    g2_jac acc2; jac_set_inf(acc2);
-    g1_jac acc1; jac_set_inf(acc1);
-    uint32_t nc = 0;
-    for (uint64_t k = a + lane_; k < b; k += 64) {
-      const uint32_t s = perm[k];
-      if (flags[s] & FLAG_CANDIDATE) { jac_add(acc2, acc2, rsig[s]); jac_add(acc1, acc1, rpk[s]); ++nc; }
-    }
-    if (nc) atomicAdd(&ncand, nc);
-    red[lane_] = acc2;
-    __syncthreads();
-    for (int w = 32; w > 0; w >>= 1) {
-      if (lane_ < w) { g2_jac o = red[lane_ + w]; jac_add(acc2, acc2, o); red[lane_] = acc2; }
-      __syncthreads();
-    }
-    if (lane_ == 0) { g2_aff q; jac_to_aff(q, acc2); sQ = q; }
-    __syncthreads();
-    g1_jac* red1 = (g1_jac*)red;
-    red1[lane_] = acc1;
-    __syncthreads();
-    for (int w = 32; w > 0; w >>= 1) {
-      if (lane_ < w) { g1_jac o = red1[lane_ + w]; jac_add(acc1, acc1, o); red1[lane_] = acc1; }
-      __syncthreads();
-    }
-    if (lane_ == 0) { g1_aff p; jac_to_aff(p, acc1); sP = p; }
-    __syncthreads();
-    if (ncand) pass = pair_check(g, sP, sQ, H[r], F1, B, BP, TMP);
-    }
+    level_group_sums(a, b, perm, flags, rsig, rpk, red, &sP, &sQ, &ncand);
+    const bool pass = ncand ? pair_check(g, sP, sQ, H[r], F1, B, BP, TMP) : true;
     if (lane_ == 0) gv_cur[gid] = pass ? 1 : 0;
     if (pass || lg == 0)
       for (uint64_t k = a + lane_; k < b; k += 64) {

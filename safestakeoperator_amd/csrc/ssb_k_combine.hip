@@ -115,20 +115,18 @@ SSB_FN int64_t ratio_ci(int j, uint32_t i, const uint32_t* __restrict__ off, con
   *W = rc_windows(c, tt[j]);
   return c[i < tt[j] ? i : 0u];
 }
-// the exact single-lane ratio combine of job j (phase T into rT[j] / rk[j], then phase K)
-SSB_FN void ratio_lane_exact(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
-                             const uint32_t* __restrict__ sel, uint8_t* __restrict__ out96, const ratio_args& ra) {
-  {
-    int64_t c[FAST_T];
-    uint64_t M;
-    ratio_coeffs(j, off, tt, sel, ra.ids, c, &M);
-    unit_ratio_T(ra.rT + j, ra.rk + 4 * (size_t)j, ra.sig, sel + off[j], c, tt[j], M, rc_windows(c, tt[j]),
-                 ra.tabs + (size_t)j * RC_TAB_BYTES);
-  }
-  unit_ratio_K(out96 + 96 * (size_t)j, ra.rT + j, ra.rk + 4 * (size_t)j, ra.tabs + (size_t)j * RC_TAB_BYTES);
+// the exact single-lane ratio combine of job j, phase T into rT[j] / rk[j] (phase K follows in the
+// kernel: the two phases' frames are never on one call chain)
+SSB_FN void ratio_lane_exact_T(int j, const uint32_t* __restrict__ off, const uint32_t* __restrict__ tt,
+                               const uint32_t* __restrict__ sel, const ratio_args& ra) {
+  int64_t c[FAST_T];
+  uint64_t M;
+  ratio_coeffs(j, off, tt, sel, ra.ids, c, &M);
+  unit_ratio_T(ra.rT + j, ra.rk + 4 * (size_t)j, ra.sig, sel + off[j], c, tt[j], M, rc_windows(c, tt[j]),
+               ra.tabs + (size_t)j * RC_TAB_BYTES);
 }
 // the fast-3 job of extra block b (wave b % nw, its (b / nw)-th fast-3 job), or nothing; returns the
-// job when it must be redone exactly (ratio_lane_exact, called by the kernel: the two frames are
+// job when it must be redone exactly (ratio_lane_exact_T + phase K, called by the kernel: the frames are
 // never on one call chain), else -1.  Uniform.
 SSB_FN int ratio_lane_job(rl::lds& L, int b, int nw, int n_jobs, const uint32_t* __restrict__ off,
                            const uint32_t* __restrict__ tt, const uint32_t* __restrict__ sel,
@@ -292,10 +290,9 @@ __global__ void SSB_LB(64) k_combine_terms_gls(int n, uint32_t n_jobs, const uin
   if (fast && fast[j]) return;
   const uint32_t k = (uint32_t)s - off[j];
   if (status[j] != SSB_DVF_OK || k >= tt[j]) return;
-  const fr l = lam[s];
-  g2_jac r;
-  unit_combine_term_gls(r, sig_aff[sel[s]], l.l, q);
-  term[4 * (size_t)s + q] = r;
+  // (the term written in place: jac_mul_aff stores its result once, at the end -- a local point here
+  // would sit in the kernel's frame, under the chain of the ratio jobs' phase T)
+  unit_combine_term_gls(term[4 * (size_t)s + q], sig_aff[sel[s]], lam[s].l, q);
 }
 // stride: terms per share (1: k_combine_terms, 4: k_combine_terms_gls).  Jobs of the ratio combine
 // (fast 2; ra.rT != nullptr) run its phase K here: [M^-1] T from rT[j], compressed (unit_ratio_K);
@@ -311,7 +308,10 @@ __global__ void SSB_LB(64) k_combine_sum(int n_jobs, const uint32_t* __restrict_
     if (!fast || !ra.sig || !ra.rT || (skip_if_ok && *skip_if_ok)) return;
     __shared__ rl::lds L;
     const int jx = ratio_lane_job(L, (int)blockIdx.x - nbs, nbs, n_jobs, off, tt, sel, fast, out96, ra);
-    if (jx >= 0 && threadIdx.x == 0) ratio_lane_exact(jx, off, tt, sel, out96, ra);
+    if (jx >= 0 && threadIdx.x == 0) {
+      ratio_lane_exact_T(jx, off, tt, sel, ra);
+      unit_ratio_K(out96 + 96 * (size_t)jx, ra.rT + jx, ra.rk + 4 * (size_t)jx, ra.tabs + (size_t)jx * RC_TAB_BYTES);
+    }
     return;
   }
   int j = blockIdx.x * blockDim.x + threadIdx.x;
