@@ -81,47 +81,12 @@ SSB_INL void g2_dbl(f2& X, f2& Y, f2& Z) {
   mul2x(Z3, y2, Z, K8P);         // 4 * 4 + 4 * 8 = 48;  Z3 = 2YZ < 2
   X = X3; Y = Y3; Z = Z3;
 }
-// Mixed addition acc + (x2, y2) (madd-2007-bl, x2, y2 < 2p), Z3 = 2 Z1 H.  Like g2_add_aff_sg: acc at
-// infinity gives the point; acc == +-P (H == 0) returns false -- then [k -+ 1]P = O for the chain's
-// prefix k, so P is not of order r.
-SSB_INL bool g2_madd(f2& X1, f2& Y1, f2& Z1, const f2& x2, const f2& y2) {
-  if (is_zero2(Z1)) {
-    X1 = x2; Y1 = y2;
-    Z1.c0 = cst(ONE28);
-    for (int i = 0; i < 14; ++i) Z1.c1.l[i] = 0u;
-    return true;
-  }
-  f2 Z1Z1, U2, t, S2, H, rr, HH, I, J, V, X3, Y3, Z3, w;
-  sqr2(Z1Z1, Z1, K8P);           // < (2, 4)
-  mul2x(U2, x2, Z1Z1, K8P);      // 2 * 4 + 2 * 8 = 24;  < 2
-  mul2x(t, y2, Z1, K8P);         // < 2
-  mul2x(S2, t, Z1Z1, K8P);       // < 2
-  sub2(H, U2, X1, K16P);         // < 18
-  if (is_zero2(H)) return false;
-  sub2(rr, S2, Y1, K4P);         // < 6
-  dbl2(rr, rr);                  // < 12
-  sqr2(HH, H, K32P);             // 2 * 18 * 50 = 1800;  < (2, 4)
-  dbl2(I, HH); dbl2(I, I);       // < 16
-  mul2x(J, H, I, K32P);          // 18 * 16 + 18 * 32 = 864;  < 2
-  mul2x(V, X1, I, K32P);         // 12 * 16 + 12 * 32 = 576;  < 2
-  sqr2(X3, rr, K16P);            // 2 * 12 * 28 = 672;  < (2, 4)
-  f2 jv; dbl2(jv, V); add2(jv, jv, J);   // < 6
-  sub2(X3, X3, jv, K8P);         // < 12
-  sub2(w, V, X3, K16P);          // < 18
-  mul2x(Y3, rr, w, K32P);        // 12 * 18 + 12 * 32 = 600;  < 2
-  f2 yj; mul2x(yj, Y1, J, K4P);  // < 2
-  dbl2(yj, yj);                  // < 4
-  sub2(Y3, Y3, yj, K8P);         // < 10
-  fold2(Y3, Y3);                 // < 2
-  mul2x(Z3, Z1, H, K32P);        // 4 * 18 + 4 * 32 = 200;  < 2
-  dbl2(Z3, Z3);                  // < 4
-  X1 = X3; Y1 = Y3; Z1 = Z3;
-  return true;
-}
-// The affine point (x2, y2: 56 words) is read at the five additions and at the end only: it waits in
-// per-lane memory `keep` (LDS on the device, word k of the lane at keep[k * S]) instead of 56 live
-// registers through the 63 doublings -- in registers the loop spilled its point state to scratch
-// every iteration (X, Y, Z: 336 B loaded and stored per doubling).
+// Per-lane LDS the additions park the accumulator's X and Y in (word k of the lane at keep[k * S]):
+// with X1, Y1, Z1, the affine point and the formula's temporaries all live the addition held more
+// than the 256 registers of the kernel's two waves per SIMD, and spilled ~170 scratch accesses per
+// addition (4.8 KB of HBM traffic per share at 8 x C2, gpurun_out/r06i).  The affine point itself is
+// re-read from the input (global memory, engine form, L2-resident) at each use and converted by a
+// shift (from_engine_shift), so it holds no registers through the 63 doublings either.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define SSB_F28_LDS __attribute__((address_space(3)))
 #else
@@ -141,42 +106,77 @@ template <int S> SSB_INL void keep_ld(f2& a, const keep_t* k) {
   for (int i = 0; i < 14; ++i) { a.c0.l[i] = v[i * S]; a.c1.l[i] = v[(14 + i) * S]; }
 }
 constexpr int KEEP_WORDS = 56;
+// a coordinate of the input point, read at its use (the empty asm is a compiler barrier: the loads
+// are not hoisted into registers that would live through the loop), < 2p
+SSB_INL void ld_coord(f2& r, const fp2& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __asm__ __volatile__("" ::: "memory");
+#endif
+  from_engine_shift(r.c0, a.c0);
+  from_engine_shift(r.c1, a.c1);
+}
+// Mixed addition acc + P (madd-2007-bl, P's coordinates < 2p), Z3 = 2 Z1 H, X1 / Y1 parked in `keep`
+// while the products run.  acc at infinity gives the point; acc == +-P (H == 0) returns false -- then
+// [k -+ 1]P = O for the chain's prefix k, so P is not of order r.
+template <int S> SSB_INL bool g2_madd(f2& X1, f2& Y1, f2& Z1, const g2_aff& p, keep_t* keep) {
+  if (is_zero2(Z1)) {
+    ld_coord(X1, p.x); ld_coord(Y1, p.y);
+    Z1.c0 = cst(ONE28);
+    for (int i = 0; i < 14; ++i) Z1.c1.l[i] = 0u;
+    return true;
+  }
+  keep_st<S>(keep, X1);
+  keep_st<S>(keep + 28 * S, Y1);
+  f2 Z1Z1, U2, S2, H;
+  sqr2(Z1Z1, Z1, K8P);           // < (2, 4)
+  { f2 x2; ld_coord(x2, p.x); mul2x(U2, x2, Z1Z1, K8P); }                  // 2 * 4 + 2 * 8 = 24;  < 2
+  { f2 y2, t; ld_coord(y2, p.y); mul2x(t, y2, Z1, K8P); mul2x(S2, t, Z1Z1, K8P); }   // < 2
+  { f2 X; keep_ld<S>(X, keep); sub2(H, U2, X, K16P); }                     // X1 < 12: H < 18
+  if (is_zero2(H)) return false;
+  f2 Z3; mul2x(Z3, Z1, H, K32P);  // 4 * 18 + 4 * 32 = 200;  < 2
+  dbl2(Z3, Z3);                  // < 4
+  f2 rr; { f2 Y; keep_ld<S>(Y, keep + 28 * S); sub2(rr, S2, Y, K4P); }    // Y1 < 2: < 6
+  dbl2(rr, rr);                  // < 12
+  f2 I, J;
+  { f2 HH; sqr2(HH, H, K32P); dbl2(I, HH); dbl2(I, I); }                   // 2 * 18 * 50 = 1800;  I < 16
+  mul2x(J, H, I, K32P);          // 18 * 16 + 18 * 32 = 864;  < 2
+  f2 V; { f2 X; keep_ld<S>(X, keep); mul2x(V, X, I, K32P); }               // 12 * 16 + 12 * 32 = 576;  < 2
+  f2 X3; sqr2(X3, rr, K16P);     // 2 * 12 * 28 = 672;  < (2, 4)
+  { f2 jv; dbl2(jv, V); add2(jv, jv, J); sub2(X3, X3, jv, K8P); }          // jv < 6: X3 < 12
+  f2 Y3; { f2 w; sub2(w, V, X3, K16P); mul2x(Y3, rr, w, K32P); }           // w < 18; 12 * 18 + 12 * 32 = 600;  < 2
+  { f2 Y, yj; keep_ld<S>(Y, keep + 28 * S); mul2x(yj, Y, J, K4P); dbl2(yj, yj); sub2(Y3, Y3, yj, K8P); }   // yj < 4: < 10
+  fold2(Y3, Y3);                 // < 2
+  X1 = X3; Y1 = Y3; Z1 = Z3;
+  return true;
+}
 // psi(P) == [x]P, x = -|x|: [|x|]P by the wave-uniform double-and-add chain, then
 // X == psi(P).x Z^2 and -Y == psi(P).y Z^3 (mod p).  keep: KEEP_WORDS words at stride S.
 template <int S> SSB_INL bool g2_in_subgroup_keep(const g2_aff& p, keep_t* keep) {
   if (p.inf) return true;
-  {
-    f2 x2, y2;
-    from_engine2(x2, p.x);         // < 2
-    from_engine2(y2, p.y);
-    keep_st<S>(keep, x2);
-    keep_st<S>(keep + 28 * S, y2);
-  }
   f2 X, Y, Z;
-  keep_ld<S>(X, keep);
-  keep_ld<S>(Y, keep + 28 * S);
+  ld_coord(X, p.x);              // < 2
+  ld_coord(Y, p.y);
   Z.c0 = cst(ONE28);
   for (int i = 0; i < 14; ++i) Z.c1.l[i] = 0u;
   for (int i = 62; i >= 0; --i) {
     g2_dbl(X, Y, Z);
-    if ((BLS_X_ABS >> i) & 1ull) {
-      f2 x2, y2;
-      keep_ld<S>(x2, keep);
-      keep_ld<S>(y2, keep + 28 * S);
-      if (!g2_madd(X, Y, Z, x2, y2)) return false;
-    }
+    if ((BLS_X_ABS >> i) & 1ull)
+      if (!g2_madd<S>(X, Y, Z, p, keep)) return false;
   }
   if (is_zero2(Z)) return false;   // [x]P = O, psi(P) != O
-  f2 x2, y2;
-  keep_ld<S>(x2, keep);
-  keep_ld<S>(y2, keep + 28 * S);
   f2 cx, cy, px, py;
   cx.c0 = cst(PSI_CX28_0); cx.c1 = cst(PSI_CX28_1);
   cy.c0 = cst(PSI_CY28_0); cy.c1 = cst(PSI_CY28_1);
-  f2 cj = x2; neg_raw(cj.c1, x2.c1, K4P); norm(cj.c1);   // conj(x2) < 4
-  mul2x(px, cj, cx, K4P);        // < 2
-  cj = y2; neg_raw(cj.c1, y2.c1, K4P); norm(cj.c1);
-  mul2x(py, cj, cy, K4P);        // < 2
+  {
+    f2 x2, cj; ld_coord(x2, p.x);
+    cj = x2; neg_raw(cj.c1, x2.c1, K4P); norm(cj.c1);   // conj(x2) < 4
+    mul2x(px, cj, cx, K4P);      // < 2
+  }
+  {
+    f2 y2, cj; ld_coord(y2, p.y);
+    cj = y2; neg_raw(cj.c1, y2.c1, K4P); norm(cj.c1);
+    mul2x(py, cj, cy, K4P);      // < 2
+  }
   f2 Z2, Z3, lx, ly;
   sqr2(Z2, Z, K8P);              // < (2, 4)
   mul2x(Z3, Z2, Z, K8P);         // 4 * 4 + 4 * 8 = 48;  < 2

@@ -196,6 +196,24 @@ SSB_INL bool eq(const f& a, const f& b) { f d; sub(d, a, b, K64P); return is_zer
 SSB_INL f cst(const uint32_t* c) { f r; for (int i = 0; i < 14; ++i) r.l[i] = c[i]; return r; }
 // the engine's Montgomery form (R = 2^384) -> this one (R = 2^392): value * 2^400 / 2^392, < 2p
 SSB_INL void from_engine(f& r, const fp& a) { f t; from32(t, a.l); mul(r, t, cst(C_2_400)); }
+// the same conversion without a product: the 12 x 32-bit limbs (a value < p) re-sliced 8 bits up
+// (value * 2^8 < 2^389), then folded below 2p
+SSB_INL void from_engine_shift(f& r, const fp& a) {
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const int b = 28 * k - 8;
+    uint32_t v;
+    if (b < 0) {
+      v = a.l[0] << 8;
+    } else {
+      const int i = b >> 5, s = b & 31;
+      v = a.l[i] >> s;
+      if (s > 4 && i + 1 < 12) v |= a.l[i + 1] << (32 - s);
+    }
+    r.l[k] = v & M28;
+  }
+  fold(r, r);
+}
 // ... and back, fully reduced: (x 2^392) 2^384 / 2^392 = x 2^384, canonical
 SSB_INL void to_engine(fp& r, const f& a) { f t; mul(t, a, cst(C_2_384)); f c; canon(c, t); to32(r.l, c); }
 

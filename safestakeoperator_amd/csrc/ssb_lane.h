@@ -142,24 +142,7 @@ SSB_INL void lv_norm(lv& x) {
   x.l[13] += c;
 }
 // the engine's form a 2^384 (< p) -> a 2^392 (< 2p): the 12 x 32-bit limbs re-sliced 8 bits up, folded
-SSB_INL lv lv_in(const fp& a) {
-  lv r;
-#pragma unroll
-  for (int k = 0; k < 14; ++k) {
-    const int b = 28 * k - 8;
-    uint32_t v;
-    if (b < 0) {
-      v = a.l[0] << 8;
-    } else {
-      const int i = b >> 5, s = b & 31;
-      v = a.l[i] >> s;
-      if (s > 4 && i + 1 < 12) v |= a.l[i + 1] << (32 - s);
-    }
-    r.l[k] = v & r28::M28;
-  }
-  r28::fold(r, r);
-  return r;
-}
+SSB_INL lv lv_in(const fp& a) { lv r; r28::from_engine_shift(r, a); return r; }
 // ... and back: x 2^-8 by one 8-bit Montgomery step ((x + m p) / 2^8, < 1.01 p), then canonical
 SSB_INL fp lv_out(const lv& x) {
   const uint32_t m = (x.l[0] * r28::P28_INV) & 0xffu;
