@@ -4,6 +4,7 @@
 // per-share kernels -- overlap on the device although the slot has a single stream
 // (ssb_k_fused.hip).  The stand-alone kernels (ssb_k_msm.hip, ssb_k_hash.hip) wrap the same bodies.
 #pragma once
+#include <type_traits>
 #include "ssb_kernels.h"
 #include "ssb_lane_ops.h"
 
@@ -74,6 +75,23 @@ SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t ba
         const uint32_t en = ent[x], i = en >> 4;
         if (flags[i] & FLAG_CANDIDATE) jac_madd_at(acc, pow + ((size_t)pidx[i] * PKPOW_W + (en & 15u)));
       }
+#if defined(SSB_MSM_R28)
+    } else if constexpr (std::is_same<F, fp2>::value) {
+      // (experiment knob, SSB_VARIANT_DEFS=-DSSB_MSM_R28) G2 in the reduced radix (ssb_f28.h pt2_madd),
+      // the accumulator's X / Y parked in the block's tree LDS while an addition's products run (the
+      // tree below starts after every lane's loop).  A/B on one box (gpurun_out/r06k): the bucket
+      // launch 2.10 -> 2.05 ms mean, 20 steps 13.9-14.0 -> 14.3-14.4 M, 1,000 steps 17.7 -> 17.3-17.4 M
+      // -- the launch is bound by its G1 side and the point loads, not by the G2 products: not default
+      r28::pt2 a;
+      r28::pt2_set_inf(a);
+      r28::keep_t* keep = (r28::keep_t*)(uint32_t*)sh + lane;
+      static_assert(64 * sizeof(jac<F>) >= sizeof(uint32_t) * r28::KEEP_WORDS * 64, "keep in the tree's LDS");
+      for (uint32_t x = s + j; x < e; x += J) {
+        const uint32_t i = ent[x];
+        if (flags[i] & FLAG_CANDIDATE) r28::pt2_madd<64>(a, pts[i], keep);
+      }
+      r28::pt2_to_engine(acc, a);
+#endif
     } else {
       for (uint32_t x = s + j; x < e; x += J) {
         const uint32_t i = ent[x];
@@ -81,6 +99,7 @@ SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t ba
       }
     }
   }
+  __syncthreads();   // (every lane's loop, and its parked words, are done before the tree's LDS use)
   for (int h = J >> 1; h >= 1; h >>= 1) {
     sh[lane] = acc;
     __syncthreads();

@@ -190,5 +190,103 @@ template <int S> SSB_INL bool g2_in_subgroup_keep(const g2_aff& p, keep_t* keep)
 SSB_INL bool g2_in_subgroup(const g2_aff& p) { uint32_t k[KEEP_WORDS]; return g2_in_subgroup_keep<1>(p, k); }
 #endif
 
+// ---- complete G2 additions for the MSM sums (the bucket sums of k_msm_bucket2, ssb_blocks.h; pt2_add
+// is host-tested for the window sums, which stay in the engine's form: inlined into their chains the
+// reduced-radix additions spilled ~3 KB per lane at 256 architectural registers) ----
+// A Jacobian point with an explicit infinity flag (a lazily reduced Z is not cheaply compared with 0);
+// coordinates bounded as in the subgroup chain: X < 12p, Y < 2p, Z < 4p.  Every input, including
+// equal and opposite points, gives the exact sum (the formulas' exceptional cases are branches).
+struct pt2 { f2 x, y, z; bool inf; };
+SSB_INL void pt2_set_inf(pt2& a) { a.inf = true; }
+SSB_INL void pt2_from_aff(pt2& a, const g2_aff& p) {
+  a.inf = p.inf != 0;
+  ld_coord(a.x, p.x); ld_coord(a.y, p.y);
+  a.z.c0 = cst(ONE28);
+  for (int i = 0; i < 14; ++i) a.z.c1.l[i] = 0u;
+}
+// the engine's Jacobian point (12 x 32-bit, z == 0 at infinity) in and out
+SSB_INL void pt2_from_engine(pt2& a, const g2_jac& p) {
+  a.inf = jac_is_inf(p);
+  from_engine_shift(a.x.c0, p.x.c0); from_engine_shift(a.x.c1, p.x.c1);
+  from_engine_shift(a.y.c0, p.y.c0); from_engine_shift(a.y.c1, p.y.c1);
+  from_engine_shift(a.z.c0, p.z.c0); from_engine_shift(a.z.c1, p.z.c1);
+}
+SSB_INL void pt2_to_engine(g2_jac& r, const pt2& a) {
+  if (a.inf) { jac_set_inf(r); return; }
+  f2 x = a.x, z = a.z;
+  fold2(x, x); fold2(z, z);      // (X < 12p, Z < 4p: below 2p for the conversion)
+  to_engine_shift(r.x.c0, x.c0); to_engine_shift(r.x.c1, x.c1);
+  to_engine_shift(r.y.c0, a.y.c0); to_engine_shift(r.y.c1, a.y.c1);
+  to_engine_shift(r.z.c0, z.c0); to_engine_shift(r.z.c1, z.c1);
+}
+SSB_INL void pt2_dbl(pt2& a) {
+  if (!a.inf) g2_dbl(a.x, a.y, a.z);   // (Y = 0 has no G2 point: the doubling never meets infinity)
+}
+// a += P, P affine (engine form in global memory, read at its uses), X1 / Y1 parked in `keep` while
+// the products run (as the subgroup chain's g2_madd); H == 0: 2P when the points are equal, else O
+template <int S> SSB_INL void pt2_madd(pt2& a, const g2_aff& p, keep_t* keep) {
+  if (p.inf) return;
+  if (a.inf) { pt2_from_aff(a, p); return; }
+  keep_st<S>(keep, a.x);
+  keep_st<S>(keep + 28 * S, a.y);
+  f2 Z1Z1, U2, S2, H;
+  sqr2(Z1Z1, a.z, K8P);          // Z1 < 4: 2 * 4 * 12 = 96;  < (2, 4)
+  { f2 x2; ld_coord(x2, p.x); mul2x(U2, x2, Z1Z1, K8P); }                  // 2 * 2 + 2 * 8 = 20;  < 2
+  { f2 y2, t; ld_coord(y2, p.y); mul2x(t, y2, a.z, K8P); mul2x(S2, t, Z1Z1, K8P); }   // < 2
+  { f2 X; keep_ld<S>(X, keep); sub2(H, U2, X, K16P); }                     // X1 < 12: H < 18
+  f2 rr; { f2 Y; keep_ld<S>(Y, keep + 28 * S); sub2(rr, S2, Y, K4P); }    // Y1 < 2: < 6
+  if (is_zero2(H)) {
+    if (is_zero2(rr)) { pt2_from_aff(a, p); g2_dbl(a.x, a.y, a.z); }      // acc == P
+    else a.inf = true;                                                     // acc == -P
+    return;
+  }
+  f2 Z3; mul2x(Z3, a.z, H, K32P);  // 4 * 18 + 4 * 32 = 200;  < 2
+  dbl2(Z3, Z3);                  // < 4
+  dbl2(rr, rr);                  // < 12
+  f2 I, J;
+  { f2 HH; sqr2(HH, H, K32P); dbl2(I, HH); dbl2(I, I); }                   // 2 * 18 * 50 = 1800;  I < 16
+  mul2x(J, H, I, K32P);          // 18 * 16 + 18 * 32 = 864;  < 2
+  f2 V; { f2 X; keep_ld<S>(X, keep); mul2x(V, X, I, K32P); }               // 12 * 16 + 12 * 32 = 576;  < 2
+  f2 X3; sqr2(X3, rr, K16P);     // 2 * 12 * 28 = 672;  < (2, 4)
+  { f2 jv; dbl2(jv, V); add2(jv, jv, J); sub2(X3, X3, jv, K8P); }          // jv < 6: X3 < 12
+  f2 Y3; { f2 w; sub2(w, V, X3, K16P); mul2x(Y3, rr, w, K32P); }           // w < 18; 12 * 18 + 12 * 32 = 600;  < 2
+  { f2 Y, yj; keep_ld<S>(Y, keep + 28 * S); mul2x(yj, Y, J, K4P); dbl2(yj, yj); sub2(Y3, Y3, yj, K8P); }   // < 10
+  fold2(Y3, Y3);                 // < 2
+  a.x = X3; a.y = Y3; a.z = Z3;
+}
+// a += b (add-2007-bl), both Jacobian
+SSB_INL void pt2_add(pt2& a, const pt2& b) {
+  if (b.inf) return;
+  if (a.inf) { a = b; return; }
+  f2 Z1Z1, Z2Z2, U1, U2, S1, S2, H, rr;
+  sqr2(Z1Z1, a.z, K8P);          // Z < 4: 2 * 4 * 12 = 96;  < (2, 4)
+  sqr2(Z2Z2, b.z, K8P);
+  mul2x(U1, a.x, Z2Z2, K8P);     // 12 * 2 + 12 * 8 = 120, 12 * 4 + 12 * 2 = 72;  < 2
+  mul2x(U2, b.x, Z1Z1, K8P);
+  { f2 t; mul2x(t, a.y, b.z, K8P); mul2x(S1, t, Z2Z2, K8P); }              // 2 * 4 + 2 * 8 = 24; 2 * 2 + 2 * 8 = 20;  < 2
+  { f2 t; mul2x(t, b.y, a.z, K8P); mul2x(S2, t, Z1Z1, K8P); }
+  sub2(H, U2, U1, K4P);          // < 6
+  sub2(rr, S2, S1, K4P);         // < 6
+  if (is_zero2(H)) {
+    if (is_zero2(rr)) g2_dbl(a.x, a.y, a.z);   // a == b
+    else a.inf = true;                         // a == -b
+    return;
+  }
+  dbl2(rr, rr);                  // < 12
+  f2 I; dbl2(I, H); sqr2(I, I, K16P);                                       // 2H < 12: 2 * 12 * 28 = 672;  < (2, 4)
+  f2 J; mul2x(J, H, I, K8P);     // 6 * 2 + 6 * 8 = 60, 6 * 4 + 6 * 2 = 36;  < 2
+  f2 V; mul2x(V, U1, I, K8P);    // < 2
+  f2 X3; sqr2(X3, rr, K16P);     // 2 * 12 * 28 = 672;  < (2, 4)
+  { f2 jv; dbl2(jv, V); add2(jv, jv, J); sub2(X3, X3, jv, K8P); }          // jv < 6: X3 < 12
+  f2 Y3; { f2 w; sub2(w, V, X3, K16P); mul2x(Y3, rr, w, K32P); }           // w < 18: 600;  < 2
+  { f2 sj; mul2x(sj, S1, J, K4P); dbl2(sj, sj); sub2(Y3, Y3, sj, K8P); }   // 2 * 2 + 2 * 4 = 12; sj < 4: Y3 < 10
+  fold2(Y3, Y3);                 // < 2
+  f2 Z3;
+  { f2 zs; add2(zs, a.z, b.z); sqr2(zs, zs, K16P);                          // < 8: 2 * 8 * 24 = 384;  < (2, 4)
+    sub2(zs, zs, Z1Z1, K8P); sub2(zs, zs, Z2Z2, K8P);                       // < 20
+    mul2x(Z3, zs, H, K8P); }     // 20 * 6 + 20 * 8 = 280, 20 * 6 + 20 * 6 = 240;  < 2
+  a.x = X3; a.y = Y3; a.z = Z3;
+}
+
 }  // namespace r28
 }  // namespace ssb

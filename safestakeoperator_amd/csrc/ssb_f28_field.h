@@ -214,6 +214,24 @@ SSB_INL void from_engine_shift(f& r, const fp& a) {
   }
   fold(r, r);
 }
+// ... and back without a product: x 2^-8 by one 8-bit Montgomery step ((x + m p) / 2^8 < 1.01 p for a
+// normalized x < 2p), then the canonical residue, re-sliced into 12 x 32-bit limbs
+SSB_INL void to_engine_shift(fp& r, const f& x) {
+  const uint32_t m = (x.l[0] * P28_INV) & 0xffu;
+  uint32_t z[14];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    c += (uint64_t)m * P28[i] + x.l[i];
+    z[i] = i < 13 ? (uint32_t)c & M28 : (uint32_t)c;
+    c >>= 28;
+  }
+  f y;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) y.l[i] = ((z[i] >> 8) | (i < 13 ? z[i + 1] << 20 : 0u)) & (i < 13 ? M28 : ~0u);
+  f cn; canon(cn, y);
+  to32(r.l, cn);
+}
 // ... and back, fully reduced: (x 2^392) 2^384 / 2^392 = x 2^384, canonical
 SSB_INL void to_engine(fp& r, const f& a) { f t; mul(t, a, cst(C_2_384)); f c; canon(c, t); to32(r.l, c); }
 

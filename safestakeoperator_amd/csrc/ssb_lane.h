@@ -144,23 +144,7 @@ SSB_INL void lv_norm(lv& x) {
 // the engine's form a 2^384 (< p) -> a 2^392 (< 2p): the 12 x 32-bit limbs re-sliced 8 bits up, folded
 SSB_INL lv lv_in(const fp& a) { lv r; r28::from_engine_shift(r, a); return r; }
 // ... and back: x 2^-8 by one 8-bit Montgomery step ((x + m p) / 2^8, < 1.01 p), then canonical
-SSB_INL fp lv_out(const lv& x) {
-  const uint32_t m = (x.l[0] * r28::P28_INV) & 0xffu;
-  uint32_t z[14];
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    c += (uint64_t)m * r28::P28[i] + x.l[i];
-    z[i] = i < 13 ? (uint32_t)c & r28::M28 : (uint32_t)c;
-    c >>= 28;
-  }
-  lv y;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) y.l[i] = ((z[i] >> 8) | (i < 13 ? z[i + 1] << 20 : 0u)) & (i < 13 ? r28::M28 : ~0u);
-  lv cn; r28::canon(cn, y);
-  fp r; r28::to32(r.l, cn);
-  return r;
-}
+SSB_INL fp lv_out(const lv& x) { fp r; r28::to_engine_shift(r, x); return r; }
 SSB_INL bool lv_is_zero(const lv& x) { return r28::is_zero(x); }
 // -x (< 2p)
 SSB_INL void lv_neg(lv& x) {

@@ -488,6 +488,58 @@ int main() {
         n += 2; bad += !same(w1, g1v); bad += !same(w2, g2v);
       }
       printf("%d %d\n", n - bad, n);
+    } else if (cmd == "pt28") {  // pt28 <trials>: the MSM's reduced-radix complete additions vs the engine's
+      int trials; is >> trials;
+      int bad = 0, n = 0;
+      auto eqp = [](const g2_jac& a, const g2_jac& b) {   // the same point (affine compare)
+        g2_aff x, y; jac_to_aff(x, a); jac_to_aff(y, b);
+        return x.inf == y.inf && (x.inf || (fp2_eq(x.x, y.x) && fp2_eq(x.y, y.y)));
+      };
+      uint32_t keep[r28::KEEP_WORDS];
+      for (int tr = 0; tr < trials; ++tr) {
+        uint8_t m[32] = {0}; m[0] = (uint8_t)tr; m[1] = (uint8_t)(tr >> 8); m[2] = 0x51;
+        g2_aff P, Q; hash_to_g2(P, m, (const uint8_t*)DST, (int)strlen(DST));
+        m[3] = 1; hash_to_g2(Q, m, (const uint8_t*)DST, (int)strlen(DST));
+        g2_jac A; jac_from_aff(A, P); jac_dbl(A, A); jac_add_aff(A, A, Q);   // Z != 1
+        g2_aff Aa; jac_to_aff(Aa, A);
+        g2_aff nAa = Aa; fp2_neg(nAa.y, nAa.y);
+        g2_aff infa = Q; infa.inf = 1;
+        g2_jac I; jac_set_inf(I);
+        g2_jac B; jac_from_aff(B, Q); jac_dbl(B, B); jac_dbl(B, B);          // another Z != 1
+        g2_jac nA = A; fp2_neg(nA.y, A.y);
+        // madd: random, acc == P (doubling), acc == -P (infinity), acc at infinity, P at infinity; chained
+        const g2_jac accs[5] = {A, A, A, I, A};
+        const g2_aff qs[5] = {Q, Aa, nAa, Q, infa};
+        for (int c = 0; c < 5; ++c) {
+          g2_jac want; jac_add_aff_inl(want, accs[c], qs[c]);
+          r28::pt2 a; r28::pt2_from_engine(a, accs[c]);
+          r28::pt2_madd<1>(a, qs[c], keep);
+          g2_jac got; r28::pt2_to_engine(got, a);
+          ++n; bad += !eqp(want, got);
+        }
+        { r28::pt2 a; r28::pt2_set_inf(a); g2_jac want; jac_set_inf(want);
+          for (int k = 0; k < 9; ++k) { const g2_aff& q = (k % 3 == 2) ? nAa : (k & 1 ? Q : P);
+            r28::pt2_madd<1>(a, q, keep); jac_add_aff_inl(want, want, q); }
+          g2_jac got; r28::pt2_to_engine(got, a); ++n; bad += !eqp(want, got); }
+        // add: random, a == b (doubling), a == -b, either at infinity; dbl
+        const g2_jac xs[5] = {A, A, A, I, A}, ys[5] = {B, A, nA, B, I};
+        for (int c = 0; c < 5; ++c) {
+          g2_jac want; jac_add_inl(want, xs[c], ys[c]);
+          r28::pt2 a, b; r28::pt2_from_engine(a, xs[c]); r28::pt2_from_engine(b, ys[c]);
+          r28::pt2_add(a, b);
+          g2_jac got; r28::pt2_to_engine(got, a);
+          ++n; bad += !eqp(want, got);
+        }
+        { g2_jac want; jac_dbl(want, B); r28::pt2 a; r28::pt2_from_engine(a, B); r28::pt2_dbl(a);
+          g2_jac got; r28::pt2_to_engine(got, a); ++n; bad += !eqp(want, got); }
+        // a running window sum in both forms (the window kernel's S / U recurrences)
+        { r28::pt2 S, U, o; r28::pt2_set_inf(S); r28::pt2_set_inf(U); g2_jac Se, Ue; jac_set_inf(Se); jac_set_inf(Ue);
+          const g2_jac bk[4] = {A, B, I, nA};
+          for (int e = 3; e >= 0; --e) { r28::pt2_from_engine(o, bk[e]); r28::pt2_add(S, o); r28::pt2_add(U, S);
+            jac_add_inl(Se, Se, bk[e]); jac_add_inl(Ue, Ue, Se); }
+          g2_jac got; r28::pt2_to_engine(got, U); ++n; bad += !eqp(Ue, got); }
+      }
+      printf("%d %d\n", n - bad, n);
     } else if (cmd == "lafin") {  // lafin <trials>: accumulator engine (reduced radix) vs repeated modular add/sub
       int trials; is >> trials;
       uint64_t st = 0x9E3779B97F4A7C15ull;

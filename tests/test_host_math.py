@@ -229,3 +229,12 @@ def test_reduced_radix_subgroup_check(host_exe):
     agree, tot, nin, nout, aok, an = map(int, _run(host_exe, ["sg28 200"])[0].split())
     assert agree == tot == 1001 and nin > 500 and nout == 400
     assert aok == an == 6000
+
+
+def test_reduced_radix_msm_additions(host_exe):
+    """The G2 MSM's reduced-radix complete additions (ssb_f28.h pt2_madd / pt2_add / pt2_dbl: the
+    bucket and window sums of k_msm_bucket2 / k_msm_window2) give the engine's points for random
+    inputs, equal points (doubling), opposite points (infinity), infinity on either side, a chained
+    bucket sum and a window recurrence."""
+    ok, n = _run(host_exe, ["pt28 40"])[0].split()
+    assert ok == n and int(n) == 40 * 13
