@@ -277,6 +277,12 @@ int main() {
         // a value near the bounds: A + 64 p, folded
         r28::f Big; for (int k = 0; k < 14; ++k) Big.l[k] = A.l[k] + r28::K64P[k]; r28::norm(Big);
         aok += fp_eq(back(Big), a); ++an;
+        // the squaring (cross products once, doubled) == the product a a; and at the top of its range:
+        // a 2p - 1 operand (limbs of 2p - 1, normalized)
+        fp sq; fp_mul(sq, a, a);
+        r28::sqr(R, A); aok += fp_eq(back(R), sq); ++an;
+        r28::f T2; r28::add(T2, r28::cst(r28::P28), r28::cst(r28::P28)); T2.l[0] -= 1;   // 2p - 1
+        r28::f S1, S2; r28::sqr(S1, T2); r28::mul(S2, T2, T2); aok += fp_eq(back(S1), back(S2)); ++an;
       }
       printf("%d %d %d %d %d %d\n", agree, tot, nin, nout, aok, an);
     } else if (cmd == "invtest") {  // invtest N -> "<ok> <n>": fp_inv (safegcd) == Fermat, a * a^-1 == 1

@@ -224,11 +224,12 @@ def test_reduced_radix_subgroup_check(host_exe):
     """The 14 x 28-bit reduced-radix G2 membership test (ssb_f28.h, the per-share subgroup kernels'
     form since round 6) gives the engine's answer (g2_in_subgroup_inl) on infinity, hash_to_G2
     outputs, their negations and multiples (in G2) and raw isogeny images and their sums with G2
-    points (on E2, not in G2); and its products, two-product sums and fold / canon equal the
-    engine's arithmetic on 2,000 random triples, including values next to the 64p bound."""
+    points (on E2, not in G2); and its products, two-product sums, squarings (the square roots'
+    powers) and fold / canon equal the engine's arithmetic on 2,000 random triples, including values
+    next to the 64p bound and a 2p - 1 operand."""
     agree, tot, nin, nout, aok, an = map(int, _run(host_exe, ["sg28 200"])[0].split())
     assert agree == tot == 1001 and nin > 500 and nout == 400
-    assert aok == an == 6000
+    assert aok == an == 10000
 
 
 def test_reduced_radix_msm_additions(host_exe):
