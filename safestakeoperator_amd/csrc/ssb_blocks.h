@@ -71,6 +71,17 @@ SSB_INL void msm_bucket_block(uint32_t bid, jac<F>* sh, uint32_t nb, uint32_t ba
     // software-pipelined loop, two points live, held 256 VGPRs + 165 AGPRs = one wave per SIMD;
     // C2 at 20 steps 11.2 -> 12.1 M partial sigs/s)
     if (pow) {
+#if defined(SSB_MSM_R28)
+      if constexpr (std::is_same<F, fp>::value) {   // (experiment knob) G1 in the reduced radix
+        r28::pt1 a;
+        a.inf = true;
+        for (uint32_t x = s + j; x < e; x += J) {
+          const uint32_t en = ent[x], i = en >> 4;
+          if (flags[i] & FLAG_CANDIDATE) r28::pt1_madd(a, pow[(size_t)pidx[i] * PKPOW_W + (en & 15u)]);
+        }
+        r28::pt1_to_engine(acc, a);
+      } else
+#endif
       for (uint32_t x = s + j; x < e; x += J) {
         const uint32_t en = ent[x], i = en >> 4;
         if (flags[i] & FLAG_CANDIDATE) jac_madd_at(acc, pow + ((size_t)pidx[i] * PKPOW_W + (en & 15u)));

@@ -288,5 +288,75 @@ SSB_INL void pt2_add(pt2& a, const pt2& b) {
   a.x = X3; a.y = Y3; a.z = Z3;
 }
 
+
+// ---- the same for G1 (E: y^2 = x^3 + 4 over Fp), for the merged G1 MSM's bucket sums ----
+// coordinates X < 12p, Y < 2p, Z < 4p as for G2; every formula's bound next to it
+struct pt1 { f x, y, z; bool inf; };
+SSB_INL void pt1_from_aff(pt1& a, const g1_aff& p) {
+  a.inf = p.inf != 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  __asm__ __volatile__("" ::: "memory");
+#endif
+  from_engine_shift(a.x, p.x); from_engine_shift(a.y, p.y);
+  a.z = cst(ONE28);
+}
+SSB_INL void pt1_to_engine(g1_jac& r, const pt1& a) {
+  if (a.inf) { jac_set_inf(r); return; }
+  f x, z; fold(x, a.x); fold(z, a.z);
+  to_engine_shift(r.x, x); to_engine_shift(r.y, a.y); to_engine_shift(r.z, z);
+}
+// dbl-2009-l over Fp (a = 0); (Y = 0 has no point of G1's order: never infinity)
+SSB_INL void g1_dbl28(f& X, f& Y, f& Z) {
+  f A, B, C, t, D, E, F, X3, Y3, Z3;
+  sqr(A, X);                     // X < 12: 144;  < 2
+  sqr(B, Y);                     // < 2
+  sqr(C, B);                     // < 2
+  add(t, X, B); sqr(t, t);       // < 14: 196;  < 2
+  dbl_sub_sub(D, t, A, C, KK8P); // 2 (t + 8p - A - C) < 20
+  fold(D, D);                    // < 2
+  mul_small(E, A, 3);            // < 6
+  sqr(F, E);                     // 36;  < 2
+  sub_dbl(X3, F, D, KK8P);       // F + 8p - 2D < 10
+  { f w; sub(w, D, X3, K16P); mul(Y3, E, w); }                             // w < 18: 6 * 18 = 108;  < 2
+  { f c8; mul_small(c8, C, 8); sub(Y3, Y3, c8, K32P); fold(Y3, Y3); }     // c8 < 16: < 34, folded < 2
+  { f y2; add_raw(y2, Y, Y); mul(Z3, y2, Z); }                             // 4 * 4 = 16;  < 2
+  X = X3; Y = Y3; Z = Z3;
+}
+// a += P (madd-2007-bl), P affine (engine form in global memory); complete like pt2_madd
+SSB_INL void pt1_madd(pt1& a, const g1_aff& p) {
+  if (p.inf) return;
+  if (a.inf) { pt1_from_aff(a, p); return; }
+  f Z1Z1, U2, S2, H, rr;
+  sqr(Z1Z1, a.z);                // Z1 < 4: 16;  < 2
+  {
+    f x2, y2;
+#if defined(__HIP_DEVICE_COMPILE__)
+    __asm__ __volatile__("" ::: "memory");
+#endif
+    from_engine_shift(x2, p.x); from_engine_shift(y2, p.y);               // < 2
+    mul(U2, x2, Z1Z1);           // < 2
+    f t; mul(t, y2, a.z); mul(S2, t, Z1Z1);                                // 8, 4;  < 2
+  }
+  sub(H, U2, a.x, K16P);         // X1 < 12: < 18
+  sub(rr, S2, a.y, K4P);         // Y1 < 2: < 6
+  if (is_zero(H)) {
+    if (is_zero(rr)) { pt1_from_aff(a, p); g1_dbl28(a.x, a.y, a.z); }     // a == P
+    else a.inf = true;                                                     // a == -P
+    return;
+  }
+  f Z3; mul(Z3, a.z, H); dbl(Z3, Z3);                                      // 4 * 18 = 72;  < 2, doubled < 4
+  dbl(rr, rr);                   // < 12
+  f I, J, V;
+  { f HH; sqr(HH, H); dbl(I, HH); dbl(I, I); }                             // 324;  I < 8
+  mul(J, H, I);                  // 18 * 8 = 144;  < 2
+  mul(V, a.x, I);                // 12 * 8 = 96;  < 2
+  f X3; sqr(X3, rr);             // 144;  < 2
+  { f jv; dbl(jv, V); add(jv, jv, J); sub(X3, X3, jv, K8P); }              // jv < 6: X3 < 10
+  f Y3; { f w; sub(w, V, X3, K16P); mul(Y3, rr, w); }                      // w < 18: 12 * 18 = 216;  < 2
+  { f yj; mul(yj, a.y, J); dbl(yj, yj); sub(Y3, Y3, yj, K8P); }            // 2 * 2;  yj < 4: < 10
+  fold(Y3, Y3);                  // < 2
+  a.x = X3; a.y = Y3; a.z = Z3;
+}
+
 }  // namespace r28
 }  // namespace ssb

@@ -538,6 +538,25 @@ int main() {
         }
         { g2_jac want; jac_dbl(want, B); r28::pt2 a; r28::pt2_from_engine(a, B); r28::pt2_dbl(a);
           g2_jac got; r28::pt2_to_engine(got, a); ++n; bad += !eqp(want, got); }
+        // G1: the merged MSM's bucket additions (pt1_madd): random, a == P, a == -P, a at infinity, chained
+        { g1_aff g = g1_neg_generator(); fp_neg(g.y, g.y);
+          g1_jac B1; jac_from_aff(B1, g); for (int k = 0; k <= tr % 5 + 1; ++k) jac_dbl(B1, B1);   // Z != 1
+          g1_aff Ba; jac_to_aff(Ba, B1); g1_aff nBa = Ba; fp_neg(nBa.y, Ba.y);
+          g1_jac I1; jac_set_inf(I1);
+          const g1_jac as1[4] = {B1, B1, B1, I1}; const g1_aff qs1[4] = {g, Ba, nBa, g};
+          auto eq1 = [](const g1_jac& a, const g1_jac& b) { g1_aff x, y; jac_to_aff(x, a); jac_to_aff(y, b);
+                                                         return x.inf == y.inf && (x.inf || (fp_eq(x.x, y.x) && fp_eq(x.y, y.y))); };
+          for (int c = 0; c < 4; ++c) {
+            g1_jac want; jac_add_aff_inl(want, as1[c], qs1[c]);
+            r28::pt1 a; a.inf = jac_is_inf(as1[c]);
+            r28::from_engine_shift(a.x, as1[c].x); r28::from_engine_shift(a.y, as1[c].y); r28::from_engine_shift(a.z, as1[c].z);
+            r28::pt1_madd(a, qs1[c]);
+            g1_jac got; r28::pt1_to_engine(got, a); ++n; bad += !eq1(want, got);
+          }
+          r28::pt1 a; a.inf = true; g1_jac want; jac_set_inf(want);
+          for (int k = 0; k < 7; ++k) { const g1_aff& q = (k % 3 == 2) ? nBa : (k & 1 ? g : Ba);
+            r28::pt1_madd(a, q); jac_add_aff_inl(want, want, q); }
+          g1_jac got; r28::pt1_to_engine(got, a); ++n; bad += !eq1(want, got); }
         // a running window sum in both forms (the window kernel's S / U recurrences)
         { r28::pt2 S, U, o; r28::pt2_set_inf(S); r28::pt2_set_inf(U); g2_jac Se, Ue; jac_set_inf(Se); jac_set_inf(Ue);
           const g2_jac bk[4] = {A, B, I, nA};

@@ -236,6 +236,7 @@ def test_reduced_radix_msm_additions(host_exe):
     """The G2 MSM's reduced-radix complete additions (ssb_f28.h pt2_madd / pt2_add / pt2_dbl: the
     bucket and window sums of k_msm_bucket2 / k_msm_window2) give the engine's points for random
     inputs, equal points (doubling), opposite points (infinity), infinity on either side, a chained
-    bucket sum and a window recurrence."""
+    bucket sum and a window recurrence; and the G1 form (pt1_madd, the merged G1 MSM's buckets) the
+    same way."""
     ok, n = _run(host_exe, ["pt28 40"])[0].split()
-    assert ok == n and int(n) == 40 * 13
+    assert ok == n and int(n) == 40 * 18
