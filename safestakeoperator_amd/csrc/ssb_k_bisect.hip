@@ -906,7 +906,9 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
       const uint32_t* list = perm + kstart[key];
       quarter_sum_to<fp2>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, sig_aff, (int)q, gX2 + 4 * key + q);
       quarter_sum_to<fp>(L.u.b, list, gn, flags, FLAG_CANDIDATE, k64, pk_aff, (int)q, gX1 + 4 * key + q);
+#ifndef SSB_TRACE_NO_LOOP   // (experiment: the fault bisection of round 6)
       SSB_TRACE(TR_EX_ITEM);
+#endif
       __threadfence();
       __syncthreads();
       if (lane_ == 0) L.last = atomicAdd(&cursor[key], 1u) == kstart[key] + gn + 3u ? 1u : 0u;
@@ -923,9 +925,13 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
       if (!m) continue;   // uniform
       group_combine(L, gX2 + 4 * key, gX1 + 4 * key);
       __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
+#ifndef SSB_TRACE_NO_LOOP   // (experiment: the fault bisection of round 6)
       SSB_TRACE(TR_EX_GCOMB);
+#endif
       ex_group_check(L, list, gn, m, flags, H[key / NB], verdict);
+#ifndef SSB_TRACE_NO_LOOP   // (experiment: the fault bisection of round 6)
       SSB_TRACE(TR_EX_GCHECK);
+#endif
     }
     return;
   }
