@@ -244,6 +244,176 @@ __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* _
   }
 }
 
+// ---- latency configuration (one batch in flight: ssb_set_pipeline_depth(1), one-stream slots) ----
+// With a single batch on the device nothing competes for the CUs the window launch leaves idle, so
+// the G2 window sums run as 8-lane programs (lp_g2_add: 6 product rounds per addition on a group of
+// 8 lanes, against 43 dependent Fp products on one lane), 16 groups per window in one 128-lane
+// block, and the cofactor clearing rides in the bucket launch instead of the window launch.  Under
+// load (depth > 1) the same forms measured slower -- four-wave, LDS-heavy blocks waiting for a CU
+// with room -- so the pipelined path keeps the single-lane window block.
+constexpr int WL_NT = 128;
+constexpr int WL_G = lane::G2_ADD_G, WL_NG = WL_NT / WL_G, WL_NC = 6;
+constexpr int WL_S = lane::G2_ADD_SCRATCH > lane::G2_DBL_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G2_DBL_SCRATCH;
+constexpr int WL_U = WL_S + WL_NC, WL_O = WL_U + WL_NC, WL_X = WL_O + WL_NC, WL_Y = WL_X + WL_NC, WL_T = WL_Y + WL_NC,
+              WL_GS = WL_T + WL_NC;
+constexpr size_t WL_SLOTS_LDS = (lane::LP_NCODE_CONST + WL_NG * WL_GS) * sizeof(lane::lslot);
+static_assert(WL_SLOTS_LDS >= 64 * sizeof(g2_jac), "the exact redo's tree LDS aliases the lane slots");
+struct wl_flags { uint32_t flg[WL_NG], has[WL_NG], exc_any; };
+// One G2 window sum_d d B_d on WL_NG groups: group t owns the m = 2^c / WL_NG consecutive buckets
+// [t m, (t + 1) m):  S_t = sum_e B_{tm+e}, U_t = sum_e e B_{tm+e} (running sums), a suffix scan of S
+// over the groups, U_t += [m] suffix_t (t >= 1), a tree of U over the groups.  Operands at infinity
+// (empty buckets and their sums) are tracked per group; an exceptional addition (equal or opposite
+// points) makes the caller redo the window with the complete single-lane formulas.  Output:
+// the affine pair (W_w, [2^(c w)](-g1)) of the multi-pairing, as msm_window_block writes it; returns
+// true (uniformly, nothing written) when the window must be redone exactly.
+SSB_INL bool msm_window_lane_block(uint32_t bid, lane::lslot* lds, wl_flags& F, int c, const g2_jac* __restrict__ bsum,
+                                   g2_aff* __restrict__ out_q, g1_aff* __restrict__ out_p, const g1_aff* __restrict__ negg1_pow) {
+  using namespace ssb::lane;
+  const int t = threadIdx.x / WL_G, role = threadIdx.x % WL_G;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + t * WL_GS, 0, 0, 0, (lu32*)&F.flg[t], role};
+  if (threadIdx.x == 0) F.exc_any = 0u;
+  lp_init_consts(g);
+  // Window 0 holds odd digits only (the RLC scalars are odd): its even buckets are all empty, and the
+  // running sums over them would add a point to itself.  It runs over the odd buckets B'_j = B_{2j+1}
+  // instead -- sum_d d B_d = 2 sum_j j B'_j + sum_j B'_j -- the plain sum being the scan's suffix_0.
+  const bool odd = bid == 0;
+  const int m = (1 << c) / (odd ? 2 * WL_NG : WL_NG);
+  const g2_jac* bk = bsum + ((size_t)bid << c) + (odd ? 1 : 0);
+  const int st = odd ? 2 : 1;   // bucket stride
+  lfp* base = (lfp*)lds + LP_NCODE_CONST;
+  auto load = [&](int slot, const g2_jac& p) { if (role < WL_NC) lp_put(g.s + slot + role, lv_in(((const fp*)&p)[role])); };
+  auto copy = [&](int dst, int src) { if (role < WL_NC) g.s[dst + role] = g.s[src + role]; };
+  // Every program call is made by every group (the programs synchronise the block); a group whose
+  // operand is infinity -- an empty bucket (window 0's even digits: the RLC scalars are odd), or a
+  // sum of them -- keeps or takes the other operand instead of the program's result, so the lane
+  // checks only fire on equal or opposite points (then the caller redoes the window exactly).
+  uint32_t exc = 0;
+  // acc <- acc + o (o at slot `os`, at infinity when oinf), through WL_Y
+  auto acc_add = [&](int acc, bool& ainf, int os, bool oinf, bool use) {
+    uint32_t e2 = 0;
+    g2_add(g, acc, os, WL_Y, e2);
+    if (use && !oinf) {
+      if (ainf) copy(acc, os);
+      else { exc |= e2; copy(acc, WL_Y); }
+      ainf = false;
+    }
+    __syncthreads();
+  };
+  bool sinf = jac_is_inf(bk[st * (t * m + m - 1)]), uinf = sinf;
+  load(WL_S, bk[st * (t * m + m - 1)]);
+  load(WL_U, bk[st * (t * m + m - 1)]);
+  for (int e = m - 2; e >= 0; --e) {
+    // (group 0's bucket e = 0 is digit 0: never filled, of weight 0 in U_0, and S_0 feeds no suffix;
+    // in the odd form it is B_1, of weight 0 in the j-sum and part of the plain sum)
+    const bool binf = (!odd && t == 0 && e == 0) || jac_is_inf(bk[st * (t * m + e)]);
+    load(WL_O, bk[st * (t * m + e)]);
+    __syncthreads();
+    acc_add(WL_S, sinf, WL_O, binf, true);
+    if (e >= 1) acc_add(WL_U, uinf, WL_S, sinf, true);
+  }
+  // suffix scan: S_t <- sum_{t' >= t} S_t'
+  for (int off = 1; off < WL_NG; off <<= 1) {
+    copy(WL_X, WL_S);
+    if (role == 0) F.has[t] = sinf ? 0u : 1u;
+    __syncthreads();
+    const bool act = t + off < WL_NG;
+    const int src = act ? t + off : t;
+    if (role < WL_NC) base[t * WL_GS + WL_O + role] = base[src * WL_GS + WL_X + role];
+    const bool oinf = !F.has[src];
+    __syncthreads();
+    acc_add(WL_S, sinf, WL_O, oinf, act);
+  }
+  const bool tinf = sinf;   // (group 0: the plain sum of the odd form)
+  copy(WL_T, WL_S);
+  // U_t += [m] S_t for t >= 1 (group 0's suffix carries weight 0)
+  for (int q = m; q > 1; q >>= 1) g2_dbl(g, WL_S, WL_S);
+  acc_add(WL_U, uinf, WL_S, sinf, t >= 1);
+  // tree over the groups
+  for (int h = WL_NG / 2; h >= 1; h >>= 1) {
+    copy(WL_X, WL_U);
+    if (role == 0) F.has[t] = uinf ? 0u : 1u;
+    __syncthreads();
+    const bool act = t < h;
+    const int src = act ? t + h : t;
+    if (role < WL_NC) base[t * WL_GS + WL_O + role] = base[src * WL_GS + WL_X + role];
+    const bool oinf = !F.has[src];
+    __syncthreads();
+    acc_add(WL_U, uinf, WL_O, oinf, act);
+  }
+  if (odd) {   // group 0: 2 U' + sum_j B'_j
+    g2_dbl(g, WL_U, WL_U);
+    bool ui = uinf;
+    acc_add(WL_U, ui, WL_T, tinf, t == 0);
+    uinf = ui;
+  }
+  if (exc && role == 0) atomicOr(&F.exc_any, 1u);
+  __syncthreads();
+  if (F.exc_any) return true;   // uniform: the caller redoes the window exactly
+  if (threadIdx.x == 0) {
+    g2_jac r;
+    if (uinf) jac_set_inf(r);
+    else for (int i = 0; i < WL_NC; ++i) ((fp*)&r)[i] = lv_out(lp_get(g.s + WL_U + i));
+    g2_aff a;
+    jac_to_aff(a, r);
+    out_q[bid] = a;
+    out_p[bid] = negg1_pow[c * bid];
+  }
+  return false;
+}
+
+__global__ void __launch_bounds__(WL_NT) k_msm_window2_lat(uint32_t nblk2, int c2, const g2_jac* __restrict__ b2,
+                                                         g2_aff* __restrict__ pair_q, g1_aff* __restrict__ pair_p,
+                                                         const g1_aff* __restrict__ negg1_pow, const g1_jac* __restrict__ b1,
+                                                         window2_tail tl) {
+  __shared__ lane::lslot lds[WL_SLOTS_LDS / sizeof(lane::lslot)];
+  __shared__ wl_flags F;
+  SSB_TRACE_T0();
+  if (blockIdx.x < nblk2) {
+    const bool redo = msm_window_lane_block(blockIdx.x, lds, F, c2, b2, pair_q, pair_p, negg1_pow);
+    SSB_TRACE(TR_W2_G2);
+    if (redo) {   // (the slots are dead: the exact form's tree LDS aliases them)
+      __syncthreads();
+      msm_window_block<fp2>(blockIdx.x, (g2_jac*)lds, c2, b2, (g2_jac*)nullptr, pair_q, pair_p, negg1_pow,
+                            (const uint32_t*)nullptr, (const g2_jac*)nullptr);
+      SSB_TRACE(TR_W2_HORNER);
+    }
+    return;
+  }
+  const int r = (int)(blockIdx.x - nblk2) * WL_NT + (int)threadIdx.x;   // the merged G1 side: one reduce per root
+  if (r < tl.ngroups1) msm_root_lane(r, b1, tl.root_sum);
+  SSB_TRACE(TR_W2_G1);
+}
+// The bucket sums with the cofactor clearing riding along (latency configuration): blocks
+// [nblk2 + nblk1, + (n + 7) / 8) clear eight roots each; the last of them writes every root's affine
+// H(root).  No waves-per-EU bound: the bucket bodies may take a whole SIMD's registers here (the
+// launch's ~750 waves fit the 1,024 SIMDs of an idle chip) and the lane programs keep the register
+// budget the window launch gives them.
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, 64))) k_msm_bucket2_clr(
+    uint32_t nblk2, uint32_t nblk1, msm_bucket_args a2, msm_bucket_args a1, const uint32_t* __restrict__ flags,
+    const g2_aff* __restrict__ sig, const g1_aff* __restrict__ pk, g2_jac* __restrict__ b2, g1_jac* __restrict__ b1,
+    g1_pre_args pre, h2c_fuse h, uint32_t* __restrict__ tickets) {
+  constexpr size_t LDS = H2C_CLEAR_LDS > 64 * sizeof(g2_jac) ? H2C_CLEAR_LDS : 64 * sizeof(g2_jac);
+  __shared__ __attribute__((aligned(16))) char lds[LDS];
+  __shared__ uint32_t last;
+  SSB_TRACE_T0();
+  if (blockIdx.x < nblk2) {
+    msm_bucket_block<fp2>(blockIdx.x, (g2_jac*)lds, a2.nb, a2.base, a2.lj, a2.order, a2.start, a2.cnt, a2.ent, flags, sig, b2);
+    return;
+  }
+  if (blockIdx.x < nblk2 + nblk1) {
+    msm_bucket_block<fp>(blockIdx.x - nblk2, (g1_jac*)lds, a1.nb, a1.base, a1.lj, a1.order, a1.start, a1.cnt, a1.ent, flags,
+                         pk, b1, pre.pow, pre.pidx);
+    return;
+  }
+  h2c_clear_block(blockIdx.x - nblk2 - nblk1, (lane::lslot*)lds, h.n, h.q, h.hj, h.exc);
+  SSB_TRACE(TR_W2_CLEAR);
+  if (last_block(&tickets[2], (uint32_t)(h.n + 7) / 8, &last)) {
+    for (uint32_t b = 0; b * 64 < (uint32_t)h.n; ++b) h2c_affine_block(b, h.n, h.q, h.hj, h.exc, h.exact_all, h.out);
+    if (threadIdx.x == 0) tickets[2] = 0u;
+    SSB_TRACE(TR_W2_AFFINE);
+  }
+}
+
 // ---- per-group Horner over the windows (G1 roots): out[g] = sum_w 2^(c w) W_{g,w}, affine ----
 __global__ void SSB_LB(64) k_msm_horner(int ngroups, int c, int W, const g1_jac* __restrict__ wsum,
                                                    g1_aff* __restrict__ out, const uint32_t* __restrict__ redo) {
@@ -390,13 +560,25 @@ void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
               g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw, int n_roots, g2_aff* H, uint32_t* tickets,
-              const g1_aff* pk_pow, const uint32_t* pk_index) {
+              const g1_aff* pk_pow, const uint32_t* pk_index, bool lat) {
   const h2c_fuse h = fuse_of(hw, n_roots, H);
   const uint32_t nb2 = msm_nbuckets(c2), nb1 = msm_nbuckets(c1);
   const g1_pre_args pre{c1.merged ? pk_pow : nullptr, c1.merged ? pk_index : nullptr};
   const uint32_t nblk2 = (nb2 + (64u >> lj2) - 1) / (64u >> lj2), nblk1 = (nb1 + (64u >> lj1) - 1) / (64u >> lj1);
   const uint32_t nbc = h.n ? (uint32_t)(h.n + 7) / 8 : 0u, nba = h.n ? (uint32_t)(h.n + 63) / 64 : 0u;
   const msm_bucket_args a2{nb2, c2.base, lj2, order, start, cnt, ent}, a1{nb1, c1.base, lj1, order, start, cnt, ent};
+  // latency configuration (one batch in flight): the clearing beside the bucket sums, the G2 window
+  // sums as lane programs (>= 2 buckets per lane group, window 0's odd ones included), the merged G1
+  // side's per-root reduce beside them
+  if (lat && tickets && h.n && c1.merged && c2.ngroups == 1 && (1u << c2.c) >= 4u * (uint32_t)WL_NG) {
+    hipLaunchKernelGGL(k_msm_bucket2_clr, dim3(nblk2 + nblk1 + nbc), dim3(64), 0, st, nblk2, nblk1, a2, a1, flags, sig, pk, b2,
+                       b1, pre, h, tickets);
+    const window2_tail tl{tickets, (int)c1.ngroups, (int)c1.W, root_sum, 1};
+    const uint32_t nw2 = c2.W, nbr = (c1.ngroups + WL_NT - 1) / WL_NT;
+    hipLaunchKernelGGL(k_msm_window2_lat, dim3(nw2 + nbr), dim3(WL_NT), 0, st, nw2, (int)c2.c, (const g2_jac*)b2, pair_q, pair_p,
+                       negg1_pow, (const g1_jac*)b1, tl);
+    return;
+  }
   hipLaunchKernelGGL(k_msm_bucket2, dim3(nblk2 + nblk1), dim3(64), 0, st, nblk2, a2, a1, flags, sig, pk, b2, b1, pre);
   const uint32_t nw2 = c2.ngroups * c2.W, nw1 = c1.ngroups * c1.W;
   const uint32_t nbw1 = c1.merged ? (c1.ngroups + 63) / 64 : (nw1 + 63) / 64;

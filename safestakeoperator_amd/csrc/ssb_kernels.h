@@ -234,7 +234,9 @@ void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int
               const uint32_t* start, const uint32_t* cnt, const uint32_t* ent, const uint32_t* flags, const g2_aff* sig,
               const g1_aff* pk, g2_jac* b2, g1_jac* b1, g2_aff* pair_q, g1_aff* pair_p, const g1_aff* negg1_pow,
               g1_jac* wsum1, g1_aff* root_sum, const h2c_ws* hw = nullptr, int n_roots = 0, g2_aff* H = nullptr,
-              uint32_t* tickets = nullptr, const g1_aff* pk_pow = nullptr, const uint32_t* pk_index = nullptr);
+              uint32_t* tickets = nullptr, const g1_aff* pk_pow = nullptr, const uint32_t* pk_index = nullptr,
+              bool lat = false);
+// (lat: one batch in flight -- the latency forms of the bucket and window launches, ssb_k_msm.hip)
 // (c1.merged: the G1 side reads the cached keys' precomputed bases pk_pow[pk_index[share] * PKPOW_W + window])
 // (with tickets: the G1 Horner and the affine H(root) run in the window launch's last G1-window /
 // last clearing block instead of a launch of their own)

@@ -417,6 +417,13 @@ bool fallback_per_share() {
 // batches one at a time, ~0.7 ms apart, once the pairing chains of all slots ended together).  The
 // three-stream latency configuration runs them on the context's spec / tail streams.
 bool post_on_slot(const ssb_slot* s) { return s->shared; }
+// One batch in flight on the context (ssb_set_pipeline_depth(1)): the MSM launches take their latency
+// forms (lane-program G2 window sums, the cofactor clearing beside the bucket sums; ssb_k_msm.hip).
+// SSB_MSM_LAT=0 keeps the pipelined forms (tests compare both).
+bool latency_forms(const ssb_ctx* ctx) {
+  static const bool off = [] { const char* e = getenv("SSB_MSM_LAT"); return e && e[0] == '0'; }();
+  return ctx->nslots == 1 && !off;
+}
 // g1_pre: the public keys come from the cache, which holds their precomputed bases (ctx->pkc_pow):
 // the G1 side is one merged 4-bit MSM per root (msm_cfg::merged)
 msm_plan plan_msm(size_t n, size_t n_roots, bool g1_pre = false) {
@@ -650,7 +657,8 @@ int run_verify(ssb_ctx* ctx, const verify_ws& w, size_t n, size_t n_roots, const
     if (P.g1.merged && !(fuse_sort && d_pk_index && ctx->pkc_pow)) { ctx->err = "internal: merged G1 MSM off the fused cached path"; return SSB_EINVAL; }
     launch::msm_both(st, P.g2, P.lj2, P.g1, P.lj1, w.order, w.start, w.cur, w.ent, w.flags, w.sig_aff, w.pk_aff, w.b2, w.b1,
                      w.H + n_roots, w.pair_p + n_roots, ctx->negg1_pow, w.w1, w.pair_p, fuse_hash ? &hw : nullptr,
-                     (int)n_roots, w.H, fuse_sort ? w.tickets : nullptr, (const g1_aff*)ctx->pkc_pow, d_pk_index);
+                     (int)n_roots, w.H, fuse_sort ? w.tickets : nullptr, (const g1_aff*)ctx->pkc_pow, d_pk_index,
+                     latency_forms(ctx));
   } else {
   if (s1 != st) SSB_HIP(hipStreamWaitEvent(s1, ctx->cur->ev_dec, 0));
   if (P.g1_msm) {

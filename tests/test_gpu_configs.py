@@ -237,9 +237,10 @@ def test_twenty_slots_every_batch_in_fallback(engine):
         assert (out[st == 0] == o_out[o_st == 0]).all()
 
 
-def _cached_one_stream(engine, wl, V, t, n, slots=2):
+def _cached_one_stream(engine, wl, V, t, n, slots=2, batches=None):
     """ssb_threshold_aggregate_batch_cached_dev on one-stream slots (bench.py's timed path: keys from
-    the decoded-key cache, the fused launches): (out96, status, err, verdicts)."""
+    the decoded-key cache, the fused launches), `batches` (default: one per slot) batches of the same
+    inputs: [(out96, status, err, verdicts)]."""
     import ctypes
     import torch
     lib = engine._lib
@@ -259,7 +260,7 @@ def _cached_one_stream(engine, wl, V, t, n, slots=2):
     assert lib.ssb_set_pipeline_depth(engine.handle, slots) == 0, lib.ssb_last_error(engine.handle)
     try:
         runs = []
-        for k in range(slots):
+        for k in range(batches or slots):
             out = torch.zeros((V, 96), dtype=torch.uint8, device=dev)
             st = torch.zeros((V,), dtype=torch.int32, device=dev)
             err = torch.zeros((V, 2), dtype=torch.int64, device=dev)
@@ -292,6 +293,27 @@ def test_c2_cached_one_stream_matches_c_oracle(engine, monkeypatch, g1, rate):
     V, t, n, R = 4096, 3, 4, 64
     wl = bench.make_workload(engine, V, t, n, R, rank=3, invalid_rate=rate)
     runs = _cached_one_stream(engine, wl, V, t, n)
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
+    for out, st, err, ver in runs:
+        assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
+        assert (st == o_st).all() and (err.astype(np.uint64) == o_err.astype(np.uint64)).all()
+        ok = st == 0
+        assert (out[ok] == o_out[ok]).all()
+        _check_against_truth(wl, V, t, n, out, st, err, ver)
+
+
+@pytest.mark.parametrize("rate", [0.0, 0.01, 0.95], ids=["valid", "invalid_1pct", "invalid_95pct"])
+def test_c2_cached_depth1_latency_forms(engine, rate):
+    """One batch in flight (ssb_set_pipeline_depth(1), one-stream slots, bench.py's batch_latency_ms):
+    the MSM launches take their latency forms -- the G2 window sums as 8-lane programs in 128-lane
+    blocks (k_msm_window2_lat), the cofactor clearing and the affine H(root) beside the bucket sums
+    (k_msm_bucket2_clr).  At 95% invalid shares most buckets are empty, so the lane programs meet
+    infinity and the windows are redone exactly in the same block.  Three batches on the one slot
+    (the clearing's completion ticket must come back zeroed).  Every verdict, status and combined
+    signature == the C oracle on the same bytes."""
+    V, t, n, R = 4096, 3, 4, 64
+    wl = bench.make_workload(engine, V, t, n, R, rank=5, invalid_rate=rate)
+    runs = _cached_one_stream(engine, wl, V, t, n, slots=1, batches=3)
     o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
     for out, st, err, ver in runs:
         assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
