@@ -1,27 +1,29 @@
-"""Kernel stats (name, calls, total/avg/min/max ns, percent) from a rocprofv3 rocpd SQLite db,
-in the same columns as rocprofv3's --stats kernel_stats.csv.
-
-    python bench_tools/rocpd_stats.py gpurun_out/<tag>/prof/<file>.db > profiles/<name>.csv
-"""
+"""Kernel statistics (rocprofv3 --stats layout: Name, Calls, TotalDurationNs, AverageNs, Percentage,
+MinNs, MaxNs) from a rocprofv3 rocpd database (run_results.db), for ROCm builds whose --stats output
+is the database only.   python bench_tools/rocpd_stats.py <run_results.db> <out.csv> [grid]"""
 import csv
 import sqlite3
 import sys
 
 
-def stats(db):
-    c = sqlite3.connect(db)
-    rows = c.execute("select name, count(*), sum(end - start), min(end - start), max(end - start) "
-                     "from kernels group by name").fetchall()
-    tot = sum(r[2] for r in rows) or 1
-    out = []
-    for name, n, s, lo, hi in sorted(rows, key=lambda r: -r[2]):
-        short = name.replace("(anonymous namespace)::", "").split("(")[0]
-        out.append([short, n, s, s / n, 100.0 * s / tot, lo, hi])
-    return out
+def main(db_path, out_path, by_grid=False):
+    db = sqlite3.connect(db_path)
+    rows = db.execute("select name, grid_x, duration from kernels").fetchall()
+    agg = {}
+    for name, grid, dur in rows:
+        short = name.split("(")[0]
+        key = (short, grid) if by_grid else short
+        a = agg.setdefault(key, [0, 0, None, 0])
+        a[0] += 1; a[1] += dur; a[2] = dur if a[2] is None else min(a[2], dur); a[3] = max(a[3], dur)
+    total = sum(a[1] for a in agg.values()) or 1
+    with open(out_path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"] + (["Grid"] if by_grid else []))
+        for key, a in sorted(agg.items(), key=lambda x: -x[1][1]):
+            name = key[0] if by_grid else key
+            row = [name, a[0], a[1], round(a[1] / a[0], 1), round(100.0 * a[1] / total, 2), a[2], a[3]]
+            w.writerow(row + ([key[1]] if by_grid else []))
 
 
 if __name__ == "__main__":
-    w = csv.writer(sys.stdout)
-    w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
-    for r in stats(sys.argv[1]):
-        w.writerow([r[0], r[1], r[2], "%.1f" % r[3], "%.2f" % r[4], r[5], r[6]])
+    main(sys.argv[1], sys.argv[2], len(sys.argv) > 3)
