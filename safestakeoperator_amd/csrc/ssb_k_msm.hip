@@ -247,18 +247,23 @@ __global__ void SSB_LB(64) k_msm_window2(uint32_t nblk2, int c2, const g2_jac* _
 // ---- latency configuration (one batch in flight: ssb_set_pipeline_depth(1), one-stream slots) ----
 // With a single batch on the device nothing competes for the CUs the window launch leaves idle, so
 // the G2 window sums run as 8-lane programs (lp_g2_add: 6 product rounds per addition on a group of
-// 8 lanes, against 43 dependent Fp products on one lane), 16 groups per window in one 128-lane
-// block, and the cofactor clearing rides in the bucket launch instead of the window launch.  Under
+// 8 lanes, against 43 dependent Fp products on one lane), 32 groups per window in one 256-lane
+// block, the G1 side's per-root reduce likewise (4-lane groups, lp_g1_add), and the cofactor
+// clearing rides in the bucket launch instead of the window launch.  Under
 // load (depth > 1) the same forms measured slower -- four-wave, LDS-heavy blocks waiting for a CU
 // with room -- so the pipelined path keeps the single-lane window block.
-constexpr int WL_NT = 128;
+constexpr int WL_NT = 256;
 constexpr int WL_G = lane::G2_ADD_G, WL_NG = WL_NT / WL_G, WL_NC = 6;
 constexpr int WL_S = lane::G2_ADD_SCRATCH > lane::G2_DBL_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G2_DBL_SCRATCH;
 constexpr int WL_U = WL_S + WL_NC, WL_O = WL_U + WL_NC, WL_X = WL_O + WL_NC, WL_Y = WL_X + WL_NC, WL_T = WL_Y + WL_NC,
               WL_GS = WL_T + WL_NC;
 constexpr size_t WL_SLOTS_LDS = (lane::LP_NCODE_CONST + WL_NG * WL_GS) * sizeof(lane::lslot);
 static_assert(WL_SLOTS_LDS >= 64 * sizeof(g2_jac), "the exact redo's tree LDS aliases the lane slots");
-struct wl_flags { uint32_t flg[WL_NG], has[WL_NG], exc_any; };
+// the merged G1 side's per-root reduce in the same launch: one group of 4 lanes per root (lp_g1_add)
+constexpr int RL_G = lane::G1_ADD_G, RL_NG = WL_NT / RL_G, RL_NC = 3;
+constexpr int RL_S = lane::G1_ADD_SCRATCH, RL_U = RL_S + RL_NC, RL_O = RL_U + RL_NC, RL_Y = RL_O + RL_NC, RL_GS = RL_Y + RL_NC;
+static_assert((lane::LP_NCODE_CONST + RL_NG * RL_GS) * sizeof(lane::lslot) <= WL_SLOTS_LDS, "root reduce slots");
+struct wl_flags { uint32_t flg[RL_NG > WL_NG ? RL_NG : WL_NG], has[WL_NG], exc_any; };
 // One G2 window sum_d d B_d on WL_NG groups: group t owns the m = 2^c / WL_NG consecutive buckets
 // [t m, (t + 1) m):  S_t = sum_e B_{tm+e}, U_t = sum_e e B_{tm+e} (running sums), a suffix scan of S
 // over the groups, U_t += [m] suffix_t (t >= 1), a tree of U over the groups.  Operands at infinity
@@ -361,6 +366,50 @@ SSB_INL bool msm_window_lane_block(uint32_t bid, lane::lslot* lds, wl_flags& F, 
   return false;
 }
 
+// root_sum[r] = sum_{d=1}^{15} d B_{r,d} (msm_root_lane's running sums) on a group of RL_G lanes per
+// root, RL_NG roots per block; operands at infinity tracked per group, a root whose additions met
+// equal or opposite points is redone on one lane (msm_root_lane, no barriers).
+SSB_INL void msm_root_lane_block(uint32_t bid, lane::lslot* lds, wl_flags& F, int ngroups, const g1_jac* __restrict__ b1,
+                                 g1_aff* __restrict__ out) {
+  using namespace ssb::lane;
+  const int t = threadIdx.x / RL_G, role = threadIdx.x % RL_G;
+  const int r = (int)bid * RL_NG + t;
+  const bool act = r < ngroups;
+  grp g{(lfp*)lds, (lfp*)lds + LP_NCODE_CONST + t * RL_GS, 0, 0, 0, (lu32*)&F.flg[t], role};
+  lp_init_consts(g);
+  const g1_jac* bk = b1 + ((size_t)(act ? r : 0) << 4);
+  auto load = [&](int slot, const g1_jac& p) { if (role < RL_NC) lp_put(g.s + slot + role, lv_in(((const fp*)&p)[role])); };
+  auto copy = [&](int dst, int src) { if (role < RL_NC) g.s[dst + role] = g.s[src + role]; };
+  uint32_t exc = 0;
+  auto acc_add = [&](int acc, bool& ainf, int os, bool oinf) {
+    uint32_t e2 = 0;
+    g1_add(g, acc, os, RL_Y, e2);
+    if (!oinf) {
+      if (ainf) copy(acc, os);
+      else { exc |= e2; copy(acc, RL_Y); }
+      ainf = false;
+    }
+    __syncthreads();
+  };
+  bool sinf = jac_is_inf(bk[15]), uinf = sinf;
+  load(RL_S, bk[15]);
+  load(RL_U, bk[15]);
+  for (int d = 14; d >= 1; --d) {
+    const bool binf = jac_is_inf(bk[d]);
+    load(RL_O, bk[d]);
+    __syncthreads();
+    acc_add(RL_S, sinf, RL_O, binf);
+    acc_add(RL_U, uinf, RL_S, sinf);
+  }
+  if (!act || role != 0) return;
+  if (exc) { msm_root_lane(r, b1, out); return; }
+  g1_jac j;
+  if (uinf) jac_set_inf(j);
+  else for (int i = 0; i < RL_NC; ++i) ((fp*)&j)[i] = lv_out(lp_get(g.s + RL_U + i));
+  g1_aff a;
+  jac_to_aff(a, j);
+  out[r] = a;
+}
 __global__ void __launch_bounds__(WL_NT) k_msm_window2_lat(uint32_t nblk2, int c2, const g2_jac* __restrict__ b2,
                                                          g2_aff* __restrict__ pair_q, g1_aff* __restrict__ pair_p,
                                                          const g1_aff* __restrict__ negg1_pow, const g1_jac* __restrict__ b1,
@@ -379,8 +428,7 @@ __global__ void __launch_bounds__(WL_NT) k_msm_window2_lat(uint32_t nblk2, int c
     }
     return;
   }
-  const int r = (int)(blockIdx.x - nblk2) * WL_NT + (int)threadIdx.x;   // the merged G1 side: one reduce per root
-  if (r < tl.ngroups1) msm_root_lane(r, b1, tl.root_sum);
+  msm_root_lane_block(blockIdx.x - nblk2, lds, F, tl.ngroups1, b1, tl.root_sum);   // the merged G1 side
   SSB_TRACE(TR_W2_G1);
 }
 // The bucket sums with the cofactor clearing riding along (latency configuration): blocks
@@ -574,7 +622,7 @@ void msm_both(hipStream_t st, const msm_cfg& c2, int lj2, const msm_cfg& c1, int
     hipLaunchKernelGGL(k_msm_bucket2_clr, dim3(nblk2 + nblk1 + nbc), dim3(64), 0, st, nblk2, nblk1, a2, a1, flags, sig, pk, b2,
                        b1, pre, h, tickets);
     const window2_tail tl{tickets, (int)c1.ngroups, (int)c1.W, root_sum, 1};
-    const uint32_t nw2 = c2.W, nbr = (c1.ngroups + WL_NT - 1) / WL_NT;
+    const uint32_t nw2 = c2.W, nbr = (c1.ngroups + RL_NG - 1) / RL_NG;
     hipLaunchKernelGGL(k_msm_window2_lat, dim3(nw2 + nbr), dim3(WL_NT), 0, st, nw2, (int)c2.c, (const g2_jac*)b2, pair_q, pair_p,
                        negg1_pow, (const g1_jac*)b1, tl);
     return;
