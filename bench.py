@@ -236,7 +236,7 @@ def make_workload(engine, V, t, n, n_roots, rank, invalid_rate=0.0, invalid_coun
     for i in bad:
         valid[i] = 0
     return dict(roots=roots, sigs=b"".join(sigs), pks=b"".join(pks), ids=ids, job_root=jr, master=master,
-                share_sigs=sigs, share_pks=pks, valid=valid, n_bad=len(bad))
+                share_sigs=sigs, share_pks=pks, valid=valid, n_bad=len(bad), share_sk=share_sk, sign_root=sign_root)
 
 
 def cpu_model():

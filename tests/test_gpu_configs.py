@@ -109,6 +109,46 @@ def test_c2_one_stream_slots_match_c_oracle(engine, rate):
         lib.ssb_set_slot_streams(engine.handle, 3)
 
 
+def _oracle_signed(wl, threads=THREADS):
+    """The workload's shares signed, and their keys derived, by the C oracle alone (bls_c.sign,
+    bls_c.sk_to_pk: 64-bit-limb restatement, pinned by the Ethereum `sign` KAT and RFC 9380), from the
+    same share secrets and signing roots -- inputs independent of the engine's own signer."""
+    from concurrent.futures import ThreadPoolExecutor   # (ctypes calls release the GIL)
+    sks = [k.to_bytes(32, "big") for k in wl["share_sk"]]
+    with ThreadPoolExecutor(threads) as ex:
+        sigs = list(ex.map(lambda a: bls_c.sign(a[0], wl["roots"][a[1]]), zip(sks, wl["sign_root"]), chunksize=256))
+        pks = list(ex.map(bls_c.sk_to_pk, sks, chunksize=256))
+    return sigs, pks
+
+
+@pytest.mark.parametrize("pattern", ["valid", "invalid_1pct", "bad_operator"])
+def test_c2_full_size_oracle_signed_inputs(engine, pattern):
+    """Full C2 (4,096 x 3-of-4, 64 roots, 16,384 shares) on inputs the C ORACLE signed: the engine's
+    batched signer and key derivation == the oracle's bytes for every share, and the engine's batch
+    (every verdict, status, error and combined signature) == the oracle's scan on those bytes; every
+    combined signature == bls_c.sign(master secret, root), i.e. the validator's own signature
+    (tests/test_generic_threshold.rs:26-35 at full size)."""
+    V, t, n, R = 4096, 3, 4, 64
+    kw = {"invalid_rate": 0.01} if pattern == "invalid_1pct" else {"bad_operator": 2} if pattern == "bad_operator" else {}
+    wl = bench.make_workload(engine, V, t, n, R, rank=5, **kw)
+    sigs, pks = _oracle_signed(wl)
+    assert sigs == wl["share_sigs"] and pks == wl["share_pks"]
+    wl = dict(wl, sigs=b"".join(sigs), pks=b"".join(pks))
+    out, st, err, ver = _agg(engine, wl, V, t, n)
+    o_out, o_st, o_err, o_ver = _c_oracle(wl, list(range(V)), t, n)
+    assert (ver == o_ver[:V * n]).all(), np.nonzero(ver != o_ver[:V * n])[0][:20]
+    assert (st == o_st).all() and (err == o_err).all()
+    ok = np.nonzero(st == 0)[0]
+    assert (out[ok] == o_out[ok]).all()
+    _check_against_truth(wl, V, t, n, out, st, err, ver)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(THREADS) as ex:
+        master = list(ex.map(lambda v: bls_c.sign(int(wl["master"][v]).to_bytes(32, "big"), wl["roots"][wl["job_root"][v]]),
+                             ok.tolist(), chunksize=128))
+    assert [bytes(out[v]) for v in ok.tolist()] == master
+    assert len(ok) == V if pattern != "invalid_1pct" else len(ok) > V - 100
+
+
 def _verify_cached_dev(engine, cache_pk48, pk_index, sigs96, root_idx, roots, seed=None):
     import torch
     lib = engine._lib
