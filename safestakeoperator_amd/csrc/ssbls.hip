@@ -421,8 +421,9 @@ bool post_on_slot(const ssb_slot* s) { return s->shared; }
 // forms (lane-program G2 window sums, the cofactor clearing beside the bucket sums; ssb_k_msm.hip).
 // SSB_MSM_LAT=0 keeps the pipelined forms (tests compare both).
 bool latency_forms(const ssb_ctx* ctx) {
-  static const bool off = [] { const char* e = getenv("SSB_MSM_LAT"); return e && e[0] == '0'; }();
-  return ctx->nslots == 1 && !off;
+  // SSB_MSM_LAT: "0" never, "a" at every pipeline depth (experiment), unset: one slot only
+  static const int mode = [] { const char* e = getenv("SSB_MSM_LAT"); return !e ? 1 : e[0] == '0' ? 0 : e[0] == 'a' ? 2 : 1; }();
+  return mode == 2 || (mode == 1 && ctx->nslots == 1);
 }
 // g1_pre: the public keys come from the cache, which holds their precomputed bases (ctx->pkc_pow):
 // the G1 side is one merged 4-bit MSM per root (msm_cfg::merged)
