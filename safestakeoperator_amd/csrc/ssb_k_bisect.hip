@@ -900,23 +900,26 @@ SSB_FN void bk_mul_keys(lane::grp& g, const fp12* __restrict__ fkey, uint32_t b,
     }
   }
 }
-// The bucket's last key's block: X_{b,q} = sum over the bucket's keys of their G2 quarter q sums
-// (lane-strided, shuffle tree) into *out; one call per quarter from the kernel (one function for
-// all four held long branches that overwrite the return address: build guard long_branch_clobbers)
-SSB_FN void bk_x_quarter(int q, uint32_t b, uint32_t NB, int n_roots, const uint32_t* __restrict__ kcnt,
-                         const g2_jac* __restrict__ X2, g2_jac* __restrict__ out) {
+// The bucket's last key's block: X_{b,q} = sum over the bucket's keys of their G2 quarter sums
+// (lane-strided, shuffle tree) into Xb[q]
+SSB_FN void bk_x_quarters(uint32_t b, uint32_t NB, int n_roots, const uint32_t* __restrict__ kcnt,
+                          const g2_jac* __restrict__ X2, g2_jac* __restrict__ Xb) {
   const int lane_ = threadIdx.x;
-  g2_jac acc;
-  jac_set_inf(acc);
-  for (int r = lane_; r < n_roots; r += 64) {
-    const uint32_t key = (uint32_t)r * NB + b;
-    if (kcnt[key]) { const g2_jac o = X2[4 * key + q]; jac_add(acc, acc, o); }
+  for (int q = 0; q < 4; ++q) {
+    g2_jac acc;
+    jac_set_inf(acc);
+    for (int r = lane_; r < n_roots; r += 64) {
+      const uint32_t key = (uint32_t)r * NB + b;
+      if (kcnt[key]) { const g2_jac o = X2[4 * key + q]; jac_add_inl(acc, acc, o); }
+    }
+    for (int h = 32; h >= 1; h >>= 1) {
+      const g2_jac o = shfl_down_pt(acc, h);
+      if (lane_ < h) jac_add_inl(acc, acc, o);
+    }
+    if (lane_ == 0) Xb[q] = acc;
   }
-  for (int h = 32; h >= 1; h >>= 1) {
-    const g2_jac o = shfl_down_pt(acc, h);
-    if (lane_ < h) jac_add(acc, acc, o);
-  }
-  if (lane_ == 0) *out = acc;
+  __threadfence();
+  __syncthreads();
 }
 // X_b (the G2 Horner of the quarters) into L.sQ, -g1 into L.sP; then ex_pair_lds
 SSB_FN void bk_x_point(ex_lds& L, const g2_jac* __restrict__ Xb) {
@@ -1061,9 +1064,7 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
         __syncthreads();
         if (!L.last) continue;
         __threadfence();
-        for (int q2 = 0; q2 < 4; ++q2) bk_x_quarter(q2, b, NB, n_roots, kcnt, gX2, Xb + 4 * b + q2);
-        __threadfence();
-        __syncthreads();
+        bk_x_quarters(b, NB, n_roots, kcnt, gX2, Xb + 4 * b);
         bk_x_point(L, Xb + 4 * b);
         ex_pair_lds(L);
         if (bk_check(L, fkey, b, NB, n_roots, kcnt)) bk_verdicts(b, NB, n_roots, kcnt, kstart, perm, flags, verdict);
