@@ -86,16 +86,11 @@ SSB_INL void fb_prep_block(int n, const fb_prep_args& a) {
   if (t == 0) {
     uint32_t acc = 0;
     uint32_t m = 0;
-    uint32_t bk[16] = {};   // non-empty keys per operator-id bucket (NB <= 16)
     for (int k = 0; k < K; ++k) {
       ks[k] = acc; cursor[k] = acc; acc += kc[k];
-      if (a.klist && kc[k]) { a.klist[m++] = (uint32_t)k; ++bk[k % NB]; }
+      if (a.klist && kc[k]) a.klist[m++] = (uint32_t)k;
     }
-    if (a.klist) {
-      a.klist[K] = m;   // (the group-test items: four per listed key)
-      // the bucket-wide group tests (k_fb_excl, bucket mode): per bucket a completion ticket and its key count
-      for (int b = 0; b < NB; ++b) { a.klist[K + 1 + b] = 0u; a.klist[K + 1 + NB + b] = bk[b]; }
-    }
+    if (a.klist) a.klist[K] = m;   // (the group-test items: four per listed key)
   }
   __syncthreads();
   if (NB > 1)
@@ -842,125 +837,6 @@ SSB_FN void ex_group_check(ex_lds& L, const uint32_t* __restrict__ list, uint32_
     }
   __syncthreads();
 }
-// ---- bucket mode of the group tests (SSB_FB_BUCKET=1) ----
-// One RLC check per operator-id BUCKET across every root instead of one per (root, bucket) key:
-//     FE( prod_r m(S1_{r,b}, H(r)) * m(-g1, X_b) ) == 1,
-// S1_{r,b} = sum k_i pk_i over key (r, b)'s candidates (the G1 Horner of its four quarter sums) and
-// X_b = sum_r sum_q 2^16q X2_{(r,b),q} over the bucket's keys (one G2 Horner per bucket, not per key).
-// A passing bucket decides its candidates valid (the batch's own scalars: soundness 2^-63); a failing
-// one leaves them to k_fb_root's deduction from the committee relations and k_fb_single's checks.
-// With ids 1..4 in four buckets, a faulty operator costs 4 final exponentiations instead of 256.
-// (Each step below is called from the kernel, not from a wrapper: a callable function that keeps
-// values live across a heavy callee saves callee-saved registers in its frame, and frames add up
-// along the call chain -- the first form, with one wrapper per step, took the kernel's private
-// segment from 1,968 to 2,508 B.)
-// The last item of a key: S1 (the G1 Horner of its quarters) into L.sP, H(r) into L.sQ (S1 at
-// infinity without candidates: its Miller value is 1); then ex_pair_lds and bk_store_value.
-SSB_FN void bk_key_g1(ex_lds& L, const g1_jac* __restrict__ X1, const g2_aff& h, uint32_t m) {
-  using namespace ssb::lane;
-  constexpr int S0 = lane::G2_ADD_SCRATCH > lane::G1_ADD_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G1_ADD_SCRATCH;
-  {
-    grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, (int)threadIdx.x};
-    lp_init_consts(g);
-    __syncthreads();
-  }
-  if (m) {   // uniform
-    if (gc_horner_g1(L, X1, S0, S0 + 3)) gc_exact_g1(L, X1);
-    else gc_store_g1(L, S0);
-  } else if (threadIdx.x == 0) {
-    g1_aff P;
-    P.inf = true;
-    L.sP = P;
-  }
-  if (threadIdx.x == 0) L.sQ = h;
-  __syncthreads();
-}
-SSB_FN void bk_store_value(ex_lds& L, fp12* __restrict__ out) {
-  if (threadIdx.x < 12) ((fp*)out)[threadIdx.x] = lane::slot_out(L.u.s[lane::LP_NCODE_CONST + BS_S0 + threadIdx.x]);
-}
-// ACC *= prod of the bucket's key values fkey[r NB + b] (empty keys and values equal to 1 skipped)
-SSB_FN void bk_mul_keys(lane::grp& g, const fp12* __restrict__ fkey, uint32_t b, uint32_t NB, int n_roots,
-                        const uint32_t* __restrict__ kcnt, int ACC, int IN) {
-  using namespace ssb::lane;
-  const int lane_ = threadIdx.x;
-  const fp one = fp_one();
-  for (int base = 0; base < n_roots; base += 64) {
-    bool keep = false;
-    const int r = base + lane_;
-    if (r < n_roots && kcnt[(uint32_t)r * NB + b]) {
-      const fp* v = (const fp*)&fkey[(uint32_t)r * NB + b];
-      keep = !fp_eq(v[0], one);
-      for (int k = 1; k < 12 && !keep; ++k) keep = !fp_is_zero(v[k]);
-    }
-    for (uint64_t m = __ballot(keep); m; m &= m - 1) {   // uniform
-      const uint32_t key = (uint32_t)(base + __builtin_ctzll(m)) * NB + b;
-      if (lane_ < 12) lp_put(g.s + IN + lane_, lv_in(((const fp*)&fkey[key])[lane_]));
-      __syncthreads();
-      f12_mul(g, ACC, IN, ACC);
-    }
-  }
-}
-// The bucket's last key's block: X_{b,q} = sum over the bucket's keys of their G2 quarter sums
-// (lane-strided, shuffle tree) into Xb[q]
-SSB_FN void bk_x_quarters(uint32_t b, uint32_t NB, int n_roots, const uint32_t* __restrict__ kcnt,
-                          const g2_jac* __restrict__ X2, g2_jac* __restrict__ Xb) {
-  const int lane_ = threadIdx.x;
-  for (int q = 0; q < 4; ++q) {
-    g2_jac acc;
-    jac_set_inf(acc);
-    for (int r = lane_; r < n_roots; r += 64) {
-      const uint32_t key = (uint32_t)r * NB + b;
-      if (kcnt[key]) { const g2_jac o = X2[4 * key + q]; jac_add_inl(acc, acc, o); }
-    }
-    for (int h = 32; h >= 1; h >>= 1) {
-      const g2_jac o = shfl_down_pt(acc, h);
-      if (lane_ < h) jac_add_inl(acc, acc, o);
-    }
-    if (lane_ == 0) Xb[q] = acc;
-  }
-  __threadfence();
-  __syncthreads();
-}
-// X_b (the G2 Horner of the quarters) into L.sQ, -g1 into L.sP; then ex_pair_lds
-SSB_FN void bk_x_point(ex_lds& L, const g2_jac* __restrict__ Xb) {
-  using namespace ssb::lane;
-  constexpr int S0 = lane::G2_ADD_SCRATCH > lane::G1_ADD_SCRATCH ? lane::G2_ADD_SCRATCH : lane::G1_ADD_SCRATCH;
-  {
-    grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, (int)threadIdx.x};
-    lp_init_consts(g);
-    __syncthreads();
-  }
-  if (gc_horner_g2(L, Xb, S0, S0 + 6)) gc_exact_g2(L, Xb);   // uniform
-  else gc_store_g2(L, S0);
-  if (threadIdx.x == 0) L.sP = g1_neg_generator();
-  __syncthreads();
-}
-// m(-g1, X_b) (in the slots from BS_S0) times the keys' values, the final exponentiation == 1
-SSB_FN bool bk_check(ex_lds& L, const fp12* __restrict__ fkey, uint32_t b, uint32_t NB, int n_roots,
-                     const uint32_t* __restrict__ kcnt) {
-  using namespace ssb::lane;
-  grp g{(lfp*)L.u.s, (lfp*)L.u.s + LP_NCODE_CONST, 0, 0, 0, (lu32*)&L.flg, (int)threadIdx.x};
-  const int F1 = BS_S0, B = F1 + 24, BP = B + 12, TMP = BP + 4;
-  bk_mul_keys(g, fkey, b, NB, n_roots, kcnt, F1, F1 + 12);
-  f12_final_exp(g, F1, TMP);
-  return f12_slots_one(g, F1);
-}
-// a passing bucket: its candidates valid
-SSB_FN void bk_verdicts(uint32_t b, uint32_t NB, int n_roots, const uint32_t* __restrict__ kcnt,
-                        const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ perm, uint32_t* __restrict__ flags,
-                        uint8_t* __restrict__ verdict) {
-  for (int r = 0; r < n_roots; ++r) {
-    const uint32_t key = (uint32_t)r * NB + b, gn = kcnt[key];
-    const uint32_t* list = perm + kstart[key];
-    for (uint32_t x = threadIdx.x; x < gn; x += 64) {
-      const uint32_t s = list[x];
-      if (!(flags[s] & FLAG_CANDIDATE)) continue;
-      verdict[s] = 1;
-      atomicOr(&flags[s], (uint32_t)FLAG_DECIDED);
-    }
-  }
-}
-
 // The committee stage's checks, after k_fb_rlc's consistency pass listed the suspects (nS of them):
 //   nS <= FB_SUSPECT_MAX -- the EXCLUSION check, the batch check without the suspects:
 //       FE( ftot * prod_r m(-E_r, H(r)) * m(g1, X) ) == 1,
@@ -986,7 +862,7 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
                                      const uint32_t* __restrict__ kcnt, const uint32_t* __restrict__ kstart,
                                      uint32_t* __restrict__ cursor, g2_jac* __restrict__ gX2, g1_jac* __restrict__ gX1,
                                      const g1_aff* __restrict__ negg1_pow, uint32_t* __restrict__ rtk,
-                                     const uint32_t* __restrict__ klist, uint32_t bmode) {
+                                     const uint32_t* __restrict__ klist) {
   if (*ok) return;   // uniform: the batch passed
   SSB_TRACE_T0();
   const uint32_t ns = *nS;
@@ -1009,15 +885,8 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
     // wave through LDS (L.item, outside the union the item's bucket lists reuse), and is checked
     // against `items` before any item-indexed access; the counter overshoots by one fetch per block,
     // harmlessly (nothing reads it past `items`).
-    const uint32_t K = (uint32_t)n_roots * NB;
-    const uint32_t items = 4u * klist[K];
+    const uint32_t items = 4u * klist[n_roots * NB];
     uint32_t* ictr = xtk + 1;
-    // bucket mode (NB > 1): the keys' Miller values, then the buckets' X quarters, after the key quarter sums
-    const bool bk = bmode && NB > 1;
-    fp12* fkey = (fp12*)(gX2 + 4 * K);
-    g2_jac* Xb = (g2_jac*)(fkey + K);
-    uint32_t* btk = (uint32_t*)klist + K + 1;
-    const uint32_t* bkeys = klist + K + 1 + NB;
     for (;;) {
       if (lane_ == 0) L.item = atomicAdd(ictr, 1u);
       __syncthreads();
@@ -1053,25 +922,6 @@ __global__ void SSB_LB2(64) k_fb_excl(int n_roots, const uint32_t* __restrict__ 
       if (nc) atomicAdd(&L.ncand, nc);
       __syncthreads();
       const uint32_t m = L.ncand;
-      if (bk) {   // uniform
-        const uint32_t b = key % NB;
-        bk_key_g1(L, gX1 + 4 * key, H[key / NB], m);
-        ex_pair_lds(L);
-        bk_store_value(L, fkey + key);
-        __threadfence();
-        __syncthreads();
-        if (lane_ == 0) L.last = atomicAdd(&btk[b], 1u) == bkeys[b] - 1u ? 1u : 0u;
-        __syncthreads();
-        if (!L.last) continue;
-        __threadfence();
-        bk_x_quarters(b, NB, n_roots, kcnt, gX2, Xb + 4 * b);
-        bk_x_point(L, Xb + 4 * b);
-        ex_pair_lds(L);
-        if (bk_check(L, fkey, b, NB, n_roots, kcnt)) bk_verdicts(b, NB, n_roots, kcnt, kstart, perm, flags, verdict);
-        __syncthreads();
-        if (lane_ == 0) btk[b] = 0u;
-        continue;
-      }
       if (!m) continue;   // uniform
       group_combine(L, gX2 + 4 * key, gX1 + 4 * key);
       __syncthreads();   // (the bucket lists are dead: the LDS becomes the lane programs' slots)
@@ -1264,11 +1114,6 @@ __global__ void SSB_LB(LV_THREADS) k_fb_level(int l, int L, int lb, int n_roots,
 
 namespace launch {
 
-// SSB_FB_BUCKET=1: the group tests' bucket mode (one check per operator-id bucket across the roots)
-bool fb_bucket_mode() {
-  static const bool on = [] { const char* e = getenv("SSB_FB_BUCKET"); return e && e[0] == '1'; }();
-  return on;
-}
 // log2 of the tree's branching factor: 16-ary (round 1 measured 16 against 4: one invalid share per
 // C2 batch costs 3 tested levels instead of 5)
 int fallback_log2_branch() { return 4; }
@@ -1303,7 +1148,7 @@ void fallback_bisect(hipStream_t st, int n, int n_roots, const rlc_key& key, con
                        (const uint32_t*)fw.nS, (const uint32_t*)fw.slist, (const uint32_t*)fw.start, (const uint32_t*)fw.cnt,
                        (const uint32_t*)fw.perm, flags, share_root, (const uint64_t*)fw.k64, sig, pk, H,
                        fw.ftot, fw.fex, fw.X, fw.xtk, fw.xok, verdict, (const uint32_t*)fw.kcnt, (const uint32_t*)fw.kstart,
-                       fw.cursor, fw.rsig, fw.rpk, fw.negg1_pow, fw.rtk, (const uint32_t*)fw.klist, fb_bucket_mode() ? 1u : 0u);
+                       fw.cursor, fw.rsig, fw.rpk, fw.negg1_pow, fw.rtk, (const uint32_t*)fw.klist);
   hipLaunchKernelGGL(k_fb_root, dim3(4 * (unsigned)n_roots), dim3(64), 0, st, L, n_roots, ok, (const uint32_t*)fw.start,
                      (const uint32_t*)fw.cnt, (const uint32_t*)fw.perm, (const uint32_t*)fw.gst, (const uint32_t*)flags,
                      (const uint64_t*)fw.k64, sig, froot, fw.X, fw.rtk, fw.gv0, fw.nfail, verdict, n, xok,

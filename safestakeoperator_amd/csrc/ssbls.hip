@@ -488,11 +488,7 @@ inline uint32_t ntk_words(size_t np) { return 4 + 1 + (uint32_t)((np + 7) / 8) +
 
 // the tree's per-share products rsig / rpk; the committee stage's group-test mode (k_fb_excl) keeps
 // its four quarter sums per (root, id bucket) key in the same buffers
-// (+ the bucket mode's per-key Miller values and per-bucket X quarters behind them)
-inline size_t fb_prod_slots(size_t n, size_t n_roots) {
-  const size_t K = launch::fb_keys(n_roots);
-  return std::max(n, 4 * K + (K * sizeof(fp12) + sizeof(g2_jac) - 1) / sizeof(g2_jac) + 4 * 16 + 1);
-}
+inline size_t fb_prod_slots(size_t n, size_t n_roots) { return std::max(n, 4 * launch::fb_keys(n_roots)); }
 // the fallback's quarter sums: k_fb_root's four per root, k_fb_excl's four per part of X
 inline size_t fb_x_slots(size_t n_roots) { return std::max(4 * n_roots, (size_t)(4 * launch::EX_X_PARTS)); }
 size_t verify_ws_bytes(size_t n, size_t n_roots) {
@@ -509,7 +505,7 @@ size_t verify_ws_bytes(size_t n, size_t n_roots) {
          align_up((size_t)launch::fallback_levels(n) * (n_roots + 1) * 4) + 2 * align_up(n + n_roots) +
          align_up(n * 8) + align_up(fb_x_slots(n_roots) * sizeof(g2_jac)) + align_up(n_roots * 4) + align_up(4) +
          align_up(n * 4) + align_up(4) + align_up((size_t)launch::ex_pairs((int)n_roots) * sizeof(fp12)) + align_up(ntk_words(np) * 4) +
-         3 * align_up(launch::fb_keys(n_roots) * 4) + align_up((launch::fb_keys(n_roots) + 1 + 2 * 16) * 4);
+         3 * align_up(launch::fb_keys(n_roots) * 4) + align_up((launch::fb_keys(n_roots) + 1) * 4);
 }
 
 verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) {
@@ -539,7 +535,7 @@ verify_ws carve_verify(carve& c, size_t n, size_t n_roots, bool g1_pre = false) 
   w.k64 = c.take<uint64_t>(n); w.fbX = c.take<g2_jac>(fb_x_slots(n_roots)); w.rtk = c.take<uint32_t>(n_roots); w.nfail = c.take<uint32_t>(1);
   w.slist = c.take<uint32_t>(n); w.xok = c.take<uint32_t>(1); w.fex = c.take<fp12>((size_t)launch::ex_pairs((int)n_roots));
   w.kcnt = c.take<uint32_t>(launch::fb_keys(n_roots)); w.kstart = c.take<uint32_t>(launch::fb_keys(n_roots));
-  w.klist = c.take<uint32_t>(launch::fb_keys(n_roots) + 1 + 2 * 16);   // + the buckets' tickets and key counts
+  w.klist = c.take<uint32_t>(launch::fb_keys(n_roots) + 1);
   w.npairs = n_roots + w.plan.g2.W;
   return w;
 }
